@@ -1,0 +1,204 @@
+"""Generate golden vectors by running the REFERENCE implementation.
+
+Run in the build container only (it imports /root/reference, which does not
+exist on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py
+
+Outputs small .npz fixtures next to this script: inputs plus the reference's
+outputs.  They are data (inputs and expected outputs), not reference source.
+
+* simca_<name>.npz  — SIMCA fit on X_fit (one class, or three classes for
+  'multi') for every type × t2lim × qlim combination: per-fit arrays once
+  (xmean, eigs_all, P, invcovT, T, T2, Q, the second-PCA loadings P2 that the
+  reference predicts with) and per-combination limits, T2red/Qred on the fit
+  set, predictions and transform() outputs on X_test.
+* cv_<name>.npz      — cross_validate_simca_grid records (spec/sens/eff per LV).
+* qhf.npz            — vae_model.compute_q_h_f on a fixed batch.
+
+np.random.seed is set before every fit: the reference's second PCA(k) draws
+from NumPy's global RNG (SURVEY.md §8c caveat 1).
+"""
+from __future__ import annotations
+
+import contextlib
+import io
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("OCM_REFERENCE", "/root/reference")
+
+sys.path.insert(0, REF)
+sys.path.insert(0, REPO)  # for oracle.synth_spectra (data generator only)
+
+from oracle.simca_oracle import synth_spectra  # noqa: E402
+
+TYPES = ["sim", "alt", "ci", "dd"]
+T2LIMS = ["Fdist", "Fdistrig", "chi2", "perc", "chi2pom"]
+QLIMS = ["jm", "chi2box", "perc", "chi2pom"]
+
+
+def _combos():
+    for ty in TYPES:
+        if ty == "dd":  # 'dd' forces chi2pom for both limits (utils/SIMCA.py:42-48)
+            yield ty, "chi2pom", "chi2pom"
+            continue
+        for t2 in T2LIMS:
+            for ql in QLIMS:
+                yield ty, t2, ql
+
+
+def make_simca(name, X_fit, y_fit, X_test, y_test, n_components, model_class):
+    from utils import SIMCA  # reference
+
+    out = {"X_fit": X_fit, "y_fit": y_fit, "X_test": X_test, "y_test": y_test}
+    combos = list(_combos())
+    out["combos"] = np.array(["|".join(c) for c in combos])
+    per_fit_done = False
+    lim = {"T2_limit": [], "Q_limit": [], "D_limit": [], "t2dof": [], "t2scfact": [], "qdof": [], "qscfact": []}
+    preds = []
+    classes = None
+    for ty, t2, ql in combos:
+        np.random.seed(7)
+        est = SIMCA(n_components=n_components, model_class=model_class, type=ty, t2lim=t2, qlim=ql,
+                    verbose=False)
+        with contextlib.redirect_stdout(io.StringIO()):
+            est.fit(X_fit, y_fit)
+            pr = est.predict(X_test)
+            trans = est.transform(X_test)
+        classes = list(est.model_class)
+        if not per_fit_done:
+            for ci, cls in enumerate(classes):
+                m = est._model[cls]
+                for key in ("xmean", "eigs_all", "P", "invcovT", "T", "T2", "Q"):
+                    out[f"c{ci}_{key}"] = np.asarray(m[key])
+                out[f"c{ci}_P2"] = np.asarray(m["pca_model"].components_)
+                out[f"c{ci}_mean2"] = np.asarray(m["pca_model"].mean_)
+                out[f"c{ci}_k"] = np.int64(m["n_components"])
+                out[f"c{ci}_n"] = np.int64(m["n_samples"])
+            out["classes"] = np.array(classes)
+            per_fit_done = True
+        for key in lim:
+            vals = []
+            for cls in classes:
+                m = est._model[cls]
+                if key in ("T2_limit", "Q_limit", "D_limit"):
+                    vals.append(float(m[key]))
+            if key == "t2dof":
+                vals = [float(getattr(est, "_t2dof", np.nan))]
+            elif key == "t2scfact":
+                vals = [float(getattr(est, "_t2scfact", np.nan))]
+            elif key == "qdof":
+                vals = [float(getattr(est, "_qdof", np.nan))]
+            elif key == "qscfact":
+                vals = [float(getattr(est, "_qscfact", np.nan))]
+            lim[key].append(vals)
+        preds.append(pr.astype(np.uint8))
+        if "tr_T2" not in out:  # transform() output: the LAST class, loadings P2
+            out["tr_T2"] = np.asarray(trans[0], np.float64)
+            out["tr_Q"] = np.asarray(trans[2])
+        # T2red/Qred are T2/limit (or dof-scaled for dd): keep one class-0 row per combo as a check
+        out.setdefault("_t2red0", []).append(float(np.asarray(est._model[classes[0]]["T2red"])[0]))
+        out.setdefault("_qred0", []).append(float(np.asarray(est._model[classes[0]]["Qred"])[0]))
+    for key, vals in lim.items():
+        out[key] = np.array(vals, dtype=np.float64)
+    out["pred"] = np.stack(preds)
+    out["t2red0"] = np.array(out.pop("_t2red0"))
+    out["qred0"] = np.array(out.pop("_qred0"))
+    # metrics of the default combo against y_test for the first class
+    est = SIMCA(n_components=n_components, model_class=model_class, verbose=False)
+    np.random.seed(7)
+    with contextlib.redirect_stdout(io.StringIO()):
+        est.fit(X_fit, y_fit)
+        est.predict(X_test, y_true=y_test)
+    out["metrics_json"] = np.array(json.dumps(
+        {str(c): {k: float(v) for k, v in est.metrics[c].items()} for c in est.metrics}))
+    np.savez_compressed(os.path.join(HERE, f"simca_{name}.npz"), **out)
+    print(name, "combos", len(combos), "classes", classes)
+
+
+def make_cv(name, X, y, n_splits, LV_min, LV_max, param_grid):
+    from utils import SIMCA, cross_validate_simca_grid, ClasswiseKFoldWithExternalVal
+
+    np.random.seed(11)
+    cv = ClasswiseKFoldWithExternalVal(n_splits=n_splits, cls_label=0)
+    with contextlib.redirect_stdout(io.StringIO()):
+        res = cross_validate_simca_grid(SIMCA(verbose=False), X, y, cv, LV_min=LV_min, LV_max=LV_max,
+                                        param_grid=param_grid, print_summary=False, store_predictions=True)
+    recs = res["results"]
+    out = {
+        "X": X, "y": y, "n_splits": np.int64(n_splits), "LV_min": np.int64(LV_min), "LV_max": np.int64(LV_max),
+        "param_grid_json": np.array(json.dumps(param_grid)),
+        "params_json": np.array(json.dumps([r["params"] for r in recs])),
+        "LV": np.array([r["LV"] for r in recs], dtype=np.int64),
+        "spec": np.array([r["spec"] for r in recs]),
+        "sens": np.array([r["sens"] for r in recs]),
+        "eff": np.array([r["eff"] for r in recs]),
+        "pred": np.stack([b["prediction"] for b in res["by_combo"]]).astype(np.uint8),
+        "best_LV": np.int64(res["best_LV"]),
+        "best_score": np.float64(res["best_score"]),
+    }
+    splits = list(cv.split(X, y))
+    out["split_train"] = np.array([len(a) for a, _ in splits])
+    out["split_test_first"] = np.array([b[0] for _, b in splits])
+    np.savez_compressed(os.path.join(HERE, f"cv_{name}.npz"), **out)
+    print("cv", name, "records", len(recs), "best LV", res["best_LV"])
+
+
+def make_qhf():
+    import torch
+    from vae_model import compute_q_h_f
+
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(256, 96, generator=g) + 2.0
+    x_rec = x + 0.1 * torch.randn(256, 96, generator=g)
+    z = torch.randn(256, 8, generator=g) @ torch.randn(8, 8, generator=g)
+    q, h, f, qc, hc, fc = compute_q_h_f(x, x_rec, z)
+    np.savez_compressed(os.path.join(HERE, "qhf.npz"), x=x.numpy(), x_rec=x_rec.numpy(), z=z.numpy(),
+                        q=q.numpy(), h=h.numpy(), f=f.numpy(), crit=np.array([qc, hc, fc], dtype=np.float64))
+    print("qhf done")
+
+
+def main():
+    # A: one class, spectral gap at k, wavelength-correlated bands.
+    # The last 100 rows carry the out-of-class band; fit on the first 1200.
+    Xa_all = synth_spectra(1600, 96, 4, rank=12, seed=1234, outlier_frac=100 / 1600)
+    Xa, Xa_t = Xa_all[:1200], Xa_all[1200:]
+    ya = np.zeros(1200, dtype=np.int64)
+    ya_t = np.concatenate([np.zeros(300, np.int64), np.ones(100, np.int64)])
+    make_simca("a", Xa, ya, Xa_t, ya_t, 4, 0)
+
+    # B: nuts-like plumbing stand-in (p=256, k=10).
+    Xb_all = synth_spectra(1700, 256, 10, rank=24, seed=99, outlier_frac=100 / 1700)
+    Xb, Xb_t = Xb_all[:1500], Xb_all[1500:]
+    yb = np.zeros(1500, dtype=np.int64)
+    yb_t = np.concatenate([np.zeros(100, np.int64), np.ones(100, np.int64)])
+    make_simca("b", Xb, yb, Xb_t, yb_t, 10, 0)
+
+    # M: three classes, per-class n_components, model_class=None.
+    parts, labels = [], []
+    for c in range(3):
+        parts.append(synth_spectra(300, 64, 3, rank=8, seed=500 + c) + 0.5 * c)
+        labels.append(np.full(300, c, dtype=np.int64))
+    Xm = np.concatenate(parts)
+    ym = np.concatenate(labels)
+    perm = np.random.default_rng(5).permutation(len(ym))
+    Xm, ym = Xm[perm], ym[perm]
+    make_simca("multi", Xm[:750], ym[:750], Xm[750:], ym[750:], [2, 3, 4], None)
+
+    # CV: target class 0 (500 rows) + 100 other-class rows.
+    Xc_all = synth_spectra(600, 64, 4, rank=10, seed=77, outlier_frac=100 / 600)
+    yc = np.concatenate([np.zeros(500, np.int64), np.ones(100, np.int64)])
+    make_cv("a", Xc_all, yc, 5, 2, 6, {})
+    make_cv("grid", Xc_all, yc, 4, 2, 4, {"type": ["alt", "sim"], "qlim": ["jm", "chi2box"]})
+
+    make_qhf()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,150 @@
+"""Pin the CPU oracle against the reference's own outputs (tests/golden/*.npz,
+made by tests/golden/make_golden.py from /root/reference).  CPU only."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import simca_oracle as O
+
+RT_LIM = 1e-5      # limits: scalar F/χ²/JM formulas on eigenvalues
+RT_Q = 1e-4        # Q, T² (SURVEY.md §8c proposed tolerances)
+BAND = 1e-4        # decisions compared outside |dred-Dlim|/Dlim < BAND
+FLOOR = 1e-5       # absolute noise floor for per-row distances, × median(|ref|):
+                   # the reference's float32 scores carry an absolute error ∝ row norm
+
+
+def close(a, b, rtol=RT_Q, floor=FLOOR, **kw):
+    b = np.asarray(b)
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=floor * float(np.median(np.abs(b))), **kw)
+
+
+def _load(golden_dir, name):
+    path = os.path.join(golden_dir, name)
+    if not os.path.exists(path):
+        pytest.skip(f"missing fixture {name}")
+    return dict(np.load(path, allow_pickle=False))
+
+
+@pytest.mark.parametrize("name", ["simca_a.npz", "simca_b.npz", "simca_multi.npz"])
+def test_oracle_fit_arrays(golden_dir, name):
+    g = _load(golden_dir, name)
+    classes = list(g["classes"])
+    ks = [int(g[f"c{i}_k"]) for i in range(len(classes))]
+    nc = ks if len(classes) > 1 else ks[0]
+    est = O.OracleSIMCA(n_components=nc, model_class=None if len(classes) > 1 else int(classes[0]))
+    est.fit(g["X_fit"], g["y_fit"])
+    for i, cls in enumerate(classes):
+        m = est._model[cls]
+        k = ks[i]
+        np.testing.assert_allclose(m["xmean"], g[f"c{i}_xmean"], rtol=1e-5, atol=1e-6)
+        ev = g[f"c{i}_eigs_all"]
+        np.testing.assert_allclose(m["eigs_all"][:k], ev[:k], rtol=1e-5)
+        th_ref = O.tail_thetas(ev, k)
+        np.testing.assert_allclose(m["thetas"], th_ref, rtol=1e-4)
+        # loadings: same sign convention (svd_flip u_based_decision=False)
+        np.testing.assert_allclose(m["P"], g[f"c{i}_P"], atol=2e-4)
+        np.testing.assert_allclose(m["T"], g[f"c{i}_T"], rtol=1e-4, atol=1e-3)
+        ic = g[f"c{i}_invcovT"]  # off-diagonals are float32-SVD noise in the reference
+        np.testing.assert_allclose(m["invcovT"], ic, rtol=1e-4, atol=1e-5 * np.abs(np.diag(ic)).max())
+        close(m["T2"], g[f"c{i}_T2"])
+        close(m["Q"], g[f"c{i}_Q"])
+        assert m["Q"].dtype == g[f"c{i}_Q"].dtype == np.float32
+        assert m["T2"].dtype == np.float64
+
+
+@pytest.mark.parametrize("name", ["simca_a.npz", "simca_b.npz", "simca_multi.npz"])
+def test_oracle_limits_and_decisions(golden_dir, name):
+    g = _load(golden_dir, name)
+    classes = list(g["classes"])
+    ks = [int(g[f"c{i}_k"]) for i in range(len(classes))]
+    nc = ks if len(classes) > 1 else ks[0]
+    mc = None if len(classes) > 1 else int(classes[0])
+    n_checked = 0
+    for ci, combo in enumerate(g["combos"]):
+        ty, t2, ql = str(combo).split("|")
+        est = O.OracleSIMCA(n_components=nc, model_class=mc, type=ty, t2lim=t2, qlim=ql)
+        est.fit(g["X_fit"], g["y_fit"])
+        for j, cls in enumerate(classes):
+            m = est._model[cls]
+            np.testing.assert_allclose(m["T2_limit"], g["T2_limit"][ci][j], rtol=RT_LIM if t2 != "perc" else 1e-4,
+                                       err_msg=f"{combo} T2_limit")
+            np.testing.assert_allclose(m["Q_limit"], g["Q_limit"][ci][j], rtol=1e-4, err_msg=f"{combo} Q_limit")
+            np.testing.assert_allclose(m["D_limit"], g["D_limit"][ci][j], rtol=1e-4, err_msg=f"{combo} D_limit")
+        if ty == "dd":
+            assert est.st.t2dof == g["t2dof"][ci][0] and est.st.qdof == g["qdof"][ci][0]
+        m0 = est._model[classes[0]]
+        np.testing.assert_allclose(m0["T2red"][0], g["t2red0"][ci], rtol=1e-4)
+        np.testing.assert_allclose(m0["Qred"][0], g["qred0"][ci], rtol=1e-4)
+        pred = est.predict(g["X_test"])
+        ref = g["pred"][ci].astype(np.float64)
+        for j, cls in enumerate(classes):
+            d = est.dred(g["X_test"], cls)
+            dl = est._model[cls]["D_limit"]
+            clear = np.abs(d - dl) > BAND * abs(dl)
+            np.testing.assert_array_equal(pred[clear, j], ref[clear, j], err_msg=f"{combo} class {cls}")
+            n_checked += int(clear.sum())
+    assert n_checked > 0
+
+
+@pytest.mark.parametrize("name", ["simca_a.npz", "simca_b.npz", "simca_multi.npz"])
+def test_oracle_transform(golden_dir, name):
+    g = _load(golden_dir, name)
+    classes = list(g["classes"])
+    ks = [int(g[f"c{i}_k"]) for i in range(len(classes))]
+    est = O.OracleSIMCA(n_components=ks if len(classes) > 1 else ks[0],
+                        model_class=None if len(classes) > 1 else int(classes[0]))
+    est.fit(g["X_fit"], g["y_fit"])
+    T2, _, Q, _ = est.transform(g["X_test"])
+    # reference transform() predicts with the randomized PCA(k) loadings (P2);
+    # the oracle with the full-SVD loadings — the same subspace on gapped data.
+    close(T2, g["tr_T2"], rtol=2e-4)
+    close(Q, g["tr_Q"], rtol=2e-4)
+
+
+def test_oracle_metrics(golden_dir):
+    g = _load(golden_dir, "simca_a.npz")
+    est = O.OracleSIMCA(n_components=int(g["c0_k"]), model_class=0)
+    est.fit(g["X_fit"], g["y_fit"])
+    est.predict(g["X_test"], y_true=g["y_test"])
+    ref = json.loads(str(g["metrics_json"]))["0"]
+    got = est.metrics[0]
+    for key in ("TP", "TN", "FP", "FN"):
+        assert got[key] == ref[key]
+    for key in ("sensitivity", "specificity", "accuracy", "efficiency"):
+        np.testing.assert_allclose(got[key], ref[key])
+
+
+@pytest.mark.parametrize("name", ["cv_a.npz", "cv_grid.npz"])
+def test_oracle_cv(golden_dir, name):
+    g = _load(golden_dir, name)
+    grid = json.loads(str(g["param_grid_json"]))
+    from itertools import product
+
+    keys = sorted(grid)
+    combos = [dict(zip(keys, v)) for v in product(*[grid[k] for k in keys])] if grid else [{}]
+    res = O.cross_validate_simca_grid(g["X"], g["y"], 0, int(g["n_splits"]), int(g["LV_min"]), int(g["LV_max"]),
+                                      cfg_grid=combos)
+    assert [r["params"] for r in res["results"]] == json.loads(str(g["params_json"]))
+    np.testing.assert_array_equal([r["LV"] for r in res["results"]], g["LV"])
+    np.testing.assert_allclose([r["spec"] for r in res["results"]], g["spec"], atol=0.5)
+    np.testing.assert_allclose([r["sens"] for r in res["results"]], g["sens"], atol=0.5)
+    assert res["best_LV"] == int(g["best_LV"])
+
+
+def test_oracle_kfold_layout(golden_dir):
+    g = _load(golden_dir, "cv_a.npz")
+    y = g["y"]
+    splits = list(O.classwise_kfold(len(y), np.flatnonzero(y == 0), int(g["n_splits"])))
+    np.testing.assert_array_equal([len(a) for a, _ in splits], g["split_train"])
+    np.testing.assert_array_equal([b[0] for _, b in splits], g["split_test_first"])
+
+
+def test_oracle_qhf(golden_dir):
+    g = _load(golden_dir, "qhf.npz")
+    q, h, f, qc, hc, fc = O.compute_q_h_f(g["x"], g["x_rec"], g["z"])
+    np.testing.assert_allclose(q, g["q"], rtol=1e-4)
+    np.testing.assert_allclose(h, g["h"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(f, g["f"], rtol=1e-4)
+    np.testing.assert_allclose([qc, hc, fc], g["crit"], rtol=1e-4)
