@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Benchmark: spectra/s of SIMCA fit + Q/T² score (BASELINE.json metric).
+
+One step = the full SIMCA hot path on the synthetic 1M×2048 fp32 batch each
+rank holds in HBM, k = 20, type 'alt', t2lim 'Fdist', qlim 'jm' (the driver
+defaults, simca_nuts.py:186): shifted Gram (FP32 MFMA) → [RCCL all-reduce of
+Gram/colsum/n when N > 1] → covariance → top-20 eigenpairs + θ1..θ3 →
+fit-set scoring (T², Q, moments) → limits → predict (fused decision) on the
+same rows.  value = rows of all ranks / max-over-ranks step time
+(weak scaling: rows per GPU fixed).
+
+    python bench.py [--gpus N --steps K --warmup W --rows R --no-cpu]
+
+Prints ONE JSON line (rank 0).  The `roofline` object is for the dominant
+kernel, k_gram: algorithmic FLOP per launch = rows × p(p+1) (symmetric Gram)
+÷ its mean duration, timed live with HIP events around every launch in the
+timed region.  `cpu_baseline` times the oracle's reference-precision path
+(float32 full SVD + randomized PCA(k) + NumPy scoring) on a bounded row
+sample on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ocm-vae-simca_amd"))
+sys.path.insert(0, REPO)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix)
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "spectra/sec SIMCA fit+Q/T² score at 1M×2048"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rows", type=int, default=1_000_000, help="spectra per GPU")
+    ap.add_argument("--p", type=int, default=2048)
+    ap.add_argument("--k", type=int, default=20)
+    ap.add_argument("--cpu-sample", type=int, default=65536, help="rows for the CPU baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def synth_device(n, p, k, seed, device, rank_count=40, noise=0.05):
+    """Synthetic spectra generated in HBM: rank-40 Gaussian-band
+    loadings (shared by all ranks), scores with a gap at k, σ-noise, sloped
+    baseline.  Chunked so temporaries stay small."""
+    import torch
+
+    g = torch.Generator(device=device).manual_seed(1234)  # loadings: same on every rank
+    wl = torch.linspace(0.0, 1.0, p, device=device, dtype=torch.float64)
+    centers = torch.rand(rank_count, generator=g, device=device, dtype=torch.float64) * 0.9 + 0.05
+    widths = torch.rand(rank_count, generator=g, device=device, dtype=torch.float64) * 0.07 + 0.01
+    L = torch.exp(-0.5 * ((wl[None, :] - centers[:, None]) / widths[:, None]) ** 2)
+    L = (L / L.norm(dim=1, keepdim=True)).float()
+    s = torch.cat([torch.linspace(20, 8, k), torch.linspace(2, 0.5, rank_count - k)]).to(device)
+    base = (1.0 + 0.3 * wl).float()
+    X = torch.empty((n, p), dtype=torch.float32, device=device)
+    gr = torch.Generator(device=device).manual_seed(seed)
+    step = 65536
+    for a in range(0, n, step):
+        b = min(n, a + step)
+        S = torch.randn((b - a, rank_count), generator=gr, device=device) * s
+        X[a:b] = S @ L + noise * torch.randn((b - a, p), generator=gr, device=device) + base
+    return X
+
+
+def cpu_baseline(rows, p, k):
+    """Oracle at reference precision on a bounded sample (fit + predict)."""
+    import numpy as np
+
+    from oracle import simca_oracle as O
+
+    try:
+        from threadpoolctl import threadpool_info
+
+        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    X = O.synth_spectra(rows, p, k, rank=40, seed=1234)
+    y = np.zeros(rows, dtype=np.int64)
+    est = O.OracleSIMCA(n_components=k, model_class=0, precision="reference", predict_loadings="randomized")
+    t0 = time.perf_counter()
+    est.fit(X, y, rng=np.random.RandomState(0))
+    est.predict(X)
+    dt = time.perf_counter() - t0
+    return {"value": rows / dt, "unit": "spectra/s", "cores": int(threads), "kind": "port",
+            "sample": f"{rows}x{p} fp32, k={k}, alt/Fdist/jm: float32 full SVD + randomized PCA(k) + "
+                      f"NumPy scores, fit+predict on the same rows ({dt:.2f} s)"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(device)
+
+    from ocm import _lib
+    from ocm.dist import ShardedSIMCA
+
+    n, p, k = args.rows, args.p, args.k
+    X = synth_device(n, p, k, seed=4321 + rank, device=device)
+    pred = torch.empty(n, dtype=torch.float64, device=device)
+    torch.cuda.synchronize()
+
+    def step():
+        model = ShardedSIMCA(n_components=k, type="alt", t2lim="Fdist", qlim="jm").fit(X)
+        model.predict(X, out=pred)
+        return model
+
+    for _ in range(args.warmup):
+        step()
+    ctx = _lib.Context.get(device.index)
+    ctx.read_timing(0)
+    ctx.read_timing(1)
+    ctx.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        model = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ctx.set_timing(False)
+    gram_ms, gram_n = ctx.read_timing(0)
+    score_ms, score_n = ctx.read_timing(1)
+    dt = t1 - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt / args.steps * 1e3
+    value = world * n * args.steps / dt
+
+    gram_avg_s = gram_ms / max(gram_n, 1) / 1e3
+    gram_flop = n * p * (p + 1)  # symmetric Gram, algorithmic
+    achieved = gram_flop / gram_avg_s / 1e12 if gram_avg_s > 0 else 0.0
+    score_avg_s = score_ms / max(score_n, 1) / 1e3
+    score_gbs = n * p * 4 / score_avg_s / 1e9 if score_avg_s > 0 else 0.0
+
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_gram_latest.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    accepted = float(pred.sum().item()) / n
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "spectra/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (rank-40 band spectra + noise, generated in HBM)",
+        "config": {
+            "workload": f"SIMCA fit+score, synthetic {n}x{p} fp32 per GPU, k={k}, type=alt t2lim=Fdist qlim=jm",
+            "rows_per_gpu": n, "p": p, "k": k,
+            "parallelism": f"row shards x{world} (RCCL all-reduce of Gram/colsum/n)",
+        },
+        "roofline": {
+            "kernel": "k_gram (FP32 MFMA shifted Gram)",
+            "bound": "mfma",
+            "achieved": round(achieved, 2),
+            "peak": FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+            "traffic": traffic,
+            "flop_per_launch": gram_flop,
+            "avg_launch_ms": round(gram_avg_s * 1e3, 4),
+            "launches": gram_n,
+        },
+        "score_kernel": {"kernel": "k_score (fused projection/Q/T2)", "bound": "hbm",
+                         "achieved_GBs": round(score_gbs, 1), "peak_GBs": HBM_PEAK_GBS,
+                         "frac": round(score_gbs / HBM_PEAK_GBS, 4), "avg_launch_ms": round(score_avg_s * 1e3, 4),
+                         "launches": score_n, "bytes_per_launch": n * p * 4},
+        "checks": {"accept_rate": round(accepted, 4), "eig_iters": model.fit_.eig_iters,
+                   "T2_limit": model.T2_limit, "Q_limit": model.Q_limit},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_sample, p, k)
+        except Exception as e:  # report, never fail the GPU number
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

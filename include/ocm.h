@@ -1,0 +1,173 @@
+/*
+ * ocm.h — C ABI of libocm.so, the MI355X (gfx950) SIMCA / VAE-SIMCA engine.
+ *
+ * The reference (TEAM-AIOLY/OCM-VAE-SIMCA) is pure Python and has no native
+ * boundary; the boundary its drivers use is the estimator API of
+ * utils/SIMCA.py and utils/CVSIMCA.py.  This header is the
+ * native layer UNDER that API: every entry point replaces one piece of
+ * arithmetic the reference runs through NumPy/SciPy/scikit-learn, cited
+ * per function.  The Python mirror (ocm-vae-simca_amd/utils/SIMCA.py,
+ * .../ocm/_lib.py) binds these with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Arrays marked [dev] are device pointers
+ *    (HBM, e.g. torch tensor data_ptr()); [host] are host pointers.
+ *  - Row-major.  X is n×p float32 with leading dimension ldx (elements).
+ *  - `rows` [dev, nullable]: optional int64 row-index list; when non-NULL
+ *    the r-th processed row is X[rows[r]] (class subsets / CV test sets
+ *    without a gather copy).
+ *  - `stream` is a hipStream_t (NULL = default stream).  Every call is
+ *    stream-ordered; calls that return host values synchronise that stream.
+ *  - Return 0 on success, a negative OCM_ERR_* code on failure;
+ *    ocm_last_error() gives the message (thread-local).
+ */
+#ifndef OCM_H_
+#define OCM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OCM_ABI_VERSION 1
+
+#define OCM_OK 0
+#define OCM_ERR_ARG (-1)         /* invalid argument (maps to ValueError) */
+#define OCM_ERR_HIP (-2)         /* HIP runtime error */
+#define OCM_ERR_NOMEM (-3)       /* device allocation failed */
+#define OCM_ERR_NOCONV (-4)      /* eigensolver hit max_iter (results still written) */
+#define OCM_ERR_UNSUPPORTED (-5) /* shape outside the supported envelope */
+
+/* decision types (utils/SIMCA.py:131-144) */
+#define OCM_TYPE_SIM 0 /* dred = max(t, q)       */
+#define OCM_TYPE_ALT 1 /* dred = sqrt(t² + q²)   */
+#define OCM_TYPE_CI 2  /* dred = t + q           */
+#define OCM_TYPE_DD 3  /* dred = t + q (dof-scaled t, q) */
+
+typedef struct ocm_ctx ocm_ctx;
+
+/* t = T2 * t2_scale, q = Q * q_scale; accept = dred(t, q) < dlim.
+ * Non-dd types: t2_scale = 1/T2_limit, q_scale = 1/Q_limit.
+ * dd: t2_scale = t2dof/t2scfact, q_scale = qdof/qscfact (utils/SIMCA.py:76-81,141-144). */
+typedef struct ocm_decision {
+  int32_t type;
+  int32_t pad_;
+  double t2_scale;
+  double q_scale;
+  double dlim;
+} ocm_decision;
+
+int ocm_abi_version(void);
+const char* ocm_last_error(void);
+int ocm_ctx_create(int device, ocm_ctx** out);
+int ocm_ctx_destroy(ocm_ctx* ctx);
+/* Pre-size the context workspace (bytes) so later calls never allocate
+ * (lets a caller capture the launch sequence in a hipGraph). */
+int ocm_ctx_reserve(ocm_ctx* ctx, size_t bytes);
+
+/* Live kernel timing for benchmarks: while enabled, every launch of a timed
+ * kernel is bracketed by a hipEvent pair on its stream (no synchronisation).
+ * ocm_ctx_read_timing waits for the recorded events, returns the summed
+ * duration (ms) and launch count of kernel `kernel_id`, and clears them. */
+#define OCM_TIMED_KERNELS 2
+#define OCM_KERNEL_GRAM 0  /* k_gram: the FP32-MFMA Gram main kernel */
+#define OCM_KERNEL_SCORE 1 /* k_score: fused projection / Q / T² kernel */
+int ocm_ctx_set_timing(ocm_ctx* ctx, int enable);
+int ocm_ctx_read_timing(ocm_ctx* ctx, int kernel_id, double* total_ms, int64_t* count);
+
+/* Column mean of the first n processed rows, fp64 accumulation.
+ * Replaces sklearn PCA mean_ (sklearn/decomposition/_pca.py:560; called
+ * from utils/SIMCA.py:64-66).  Used with n = a small sample as the Gram
+ * shift, and as the exact mean when needed.  mean_out [dev] p doubles. */
+int ocm_colmean_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                    double* mean_out, void* stream);
+
+/* Per-segment shifted Gram on FP32 MFMA.
+ * Replaces the SVD of the centred class matrix (utils/SIMCA.py:64-66 ->
+ * sklearn _pca.py:569-584 scipy.linalg.svd gesdd): the covariance
+ * eigen-decomposition needs only Σ yᵀy and Σ y with y = x - shift.
+ * Segment s covers processed rows [seg_offsets[s], seg_offsets[s+1]).
+ * G_out [dev] nseg·p·p doubles (full symmetric), colsum_out [dev] nseg·p.
+ * seg_offsets [host] nseg+1 ascending, seg_offsets[0] = 0, last = n.
+ * shift [dev] p floats. */
+int ocm_gram_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                 const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
+                 void* stream);
+
+/* Covariance from a signed combination of segment Grams (CV downdating):
+ *   Gc = Σ_t coef[t]·G[t], sc = Σ_t coef[t]·colsum[t], d = sc/n,
+ *   C = (Gc - n·d·dᵀ)/(n-1), mean = shift + d.
+ * Replaces np.cov / explained_variance_ = S²/(n-1) (_pca.py:584).
+ * G_list/colsum_list/coef [host] arrays of nterm pointers/values; C_out [dev]
+ * p·p doubles; mean_out [dev] p doubles. */
+int ocm_cov_from_gram(ocm_ctx* ctx, const double* const* G_list, const double* const* colsum_list,
+                      const double* coef, int32_t nterm, const float* shift, int64_t n, int32_t p, double* C_out,
+                      double* mean_out, void* stream);
+
+/* Top-k eigenpairs of symmetric C (fp64 subspace iteration + Rayleigh-Ritz,
+ * Jacobi on the projected block) and the tail moments
+ *   theta[m-1] = Σ_{i>k} λ_i^m  (m = 1..3, utils/SIMCA.py:189-191, 203-204, 226-227)
+ * computed from the deflated matrix (I-VVᵀ)C(I-VVᵀ) (traces, no full spectrum).
+ * theta_mode: 0 none, 1 θ1..θ2, 2 θ1..θ3.
+ * evals_out [dev] k (descending), evecs_out [dev] k×p rows = loadings with the
+ * sklearn svd_flip sign (max-|entry| positive, extmath.py:895-953),
+ * theta_out [dev] 3, iters_out [host, nullable].  Returns OCM_ERR_NOCONV if
+ * the residual tolerance was not met within max_iter (outputs still valid). */
+int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
+                 int32_t theta_mode, double* evals_out, double* evecs_out, double* theta_out, int32_t* iters_out,
+                 void* stream);
+
+/* Symmetric pseudo-inverse (eigenvalue cutoff rcond·λmax) of a small d×d
+ * fp64 matrix, d ≤ 64 (np.linalg.pinv(np.cov(...)) at utils/SIMCA.py:69,
+ * VAE_SIMCA.py:247-248, utils/final_vaesimca.py:430-434).  [dev] in/out. */
+int ocm_sym_pinv_f64(ocm_ctx* ctx, const double* A, int32_t d, double rcond, double* out, void* stream);
+
+/* Fused scoring on FP32 MFMA (utils/SIMCA.py:65-71 fit, 104-107 transform,
+ * 127-130 predict):  y = x - mu; t = P·y (k); r = y - Pᵀt; Q = Σ r²;
+ * T2 = tᵀ·A·t.  P [dev] k×p float32 row-major (ldp = p), mu [dev] p floats,
+ * A [dev] k×k doubles.  Outputs (all nullable, [dev]): T_out m×k float32,
+ * T2_out m doubles, Q_out m floats.  If dec != NULL [host] the decision is
+ * fused: accept_out[r·accept_stride] = 1.0/0.0 (float64, the reference's
+ * predictions[:, i] column).  stats_out [dev, nullable] 4 doubles
+ * = {ΣT2, ΣT2², ΣQ, ΣQ²} (chi2pom moments).  k ≤ 64. */
+int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
+                  const float* P, const float* mu, const double* A, int32_t k, float* T_out, double* T2_out,
+                  float* Q_out, const ocm_decision* dec, double* accept_out, int64_t accept_stride,
+                  double* stats_out, void* stream);
+
+/* Reduced distances and decision from stored T2/Q (utils/SIMCA.py:76-81,
+ * 109-114, 131-145).  Outputs nullable [dev]: t2red, qred, dred (m doubles),
+ * accept (m doubles 0/1 at stride accept_stride). */
+int ocm_decide(ocm_ctx* ctx, const double* T2, const float* Q, int64_t m, const ocm_decision* dec,
+               double* t2red_out, double* qred_out, double* dred_out, double* accept_out, int64_t accept_stride,
+               void* stream);
+
+/* q_i = Σ_j (x_ij - xhat_ij)² for a VAE reconstruction (vae_model.py:164,
+ * utils/final_vaesimca.py:425,492).  x, xhat [dev] m×p float32 (ld), q_out
+ * [dev] m floats. */
+int ocm_rowsq_residual_f32(ocm_ctx* ctx, const float* x, const float* xhat, int64_t m, int32_t p, int64_t ld,
+                           float* q_out, void* stream);
+
+/* b[i] = (float)a[i] — loadings / mean handed to the float32 scoring kernel. */
+int ocm_cast_f64_f32(ocm_ctx* ctx, const double* a, int64_t n, float* b, void* stream);
+
+/* np.percentile(v, pct) with linear interpolation (utils/SIMCA.py:160,187;
+ * VAE_SIMCA.py:285,305; utils/final_vaesimca.py:436-437) by radix select.
+ * dtype: 0 = float64, 1 = float32.  v [dev] n values (no NaN);
+ * out [host] 1 double. */
+int ocm_percentile(ocm_ctx* ctx, const void* v, int32_t dtype, int64_t n, double pct, double* out, void* stream);
+
+/* One radix-select pass (for multi-rank percentiles: callers all-reduce the
+ * histogram between passes).  Counts values whose order key matches
+ * `prefix` on the bits above `shift + 8`, binned by the 8 bits at `shift`.
+ * hist_out [dev] 256 uint64 (overwritten). */
+int ocm_radix_hist(ocm_ctx* ctx, const void* v, int32_t dtype, int64_t n, uint64_t prefix, int32_t shift,
+                   uint64_t* hist_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OCM_H_ */

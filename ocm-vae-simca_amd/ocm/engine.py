@@ -1,0 +1,269 @@
+"""Device-side SIMCA engine: the hot path of SURVEY.md §8(a) on libocm.
+
+``fit_class`` = utils/SIMCA.py:62-99 (``_fit_one_class``) and
+``score_class`` = :120-145 (``predict`` for one class), re-planned for one
+MI355X:
+
+    shift  = mean of ≤4096 sample rows        ocm_colmean_f32   (tiny)
+    G, s   = Σ (x-shift)(x-shift)ᵀ, Σ (x-shift) ocm_gram_f32      (FP32 MFMA, 1 HBM pass)
+    C, μ   = (G - n d dᵀ)/(n-1), shift + d      ocm_cov_from_gram
+    λ, P, θ = top-k eigenpairs, tail moments   ocm_eig_topk      (fp64, HBM-resident C)
+    T, T², Q (+ moments)                        ocm_score_f32     (FP32 MFMA, fused)
+    limits                                      host fp64 scalars (ocm/limits.py)
+
+All arrays stay in HBM; only scalars cross to the host.  The second,
+randomized ``PCA(k)`` the reference fits for predict (utils/SIMCA.py:75) is
+not repeated: it estimates the same leading subspace the eigensolver already
+returns exactly (SURVEY.md §8c caveat 1).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import Context, OcmDecision, TYPE_CODES, check, ptr, stream_handle
+
+SHIFT_SAMPLE = 4096
+EIG_TOL = 1e-10
+EIG_MAX_ITER = 3000
+
+
+def require_device():
+    if not torch.cuda.is_available():
+        raise _lib.OcmError("no HIP device visible: the SIMCA engine runs on MI355X (gfx950) only")
+
+
+def as_device_f32(X, device=None) -> torch.Tensor:
+    """Host NumPy / torch input -> contiguous float32 tensor in HBM."""
+    require_device()
+    if isinstance(X, torch.Tensor):
+        t = X
+        if device is None and t.is_cuda:
+            device = t.device
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(X))
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    t = t.to(device=device, dtype=torch.float32, non_blocking=False)
+    if not t.is_contiguous():
+        t = t.contiguous()
+    return t
+
+
+@dataclass
+class ClassFit:
+    """Per-class model state (device tensors + host scalars)."""
+    k: int
+    n: int
+    p: int
+    mean64: torch.Tensor
+    mean32: torch.Tensor
+    evals: torch.Tensor          # (k,) f64
+    P64: torch.Tensor            # (k, p) f64, svd_flip sign convention
+    P32: torch.Tensor            # (k, p) f32 (scoring operand)
+    invcov: torch.Tensor         # (k, k) f64 = pinv(cov(T)) = diag(1/λ)
+    thetas: tuple = (0.0, 0.0, 0.0)
+    evals_host: np.ndarray = None
+    T: torch.Tensor | None = None
+    T2: torch.Tensor | None = None
+    Q: torch.Tensor | None = None
+    T2_stats: tuple = (0.0, 0.0)
+    Q_stats: tuple = (0.0, 0.0)
+    eig_iters: int = 0
+    C: torch.Tensor | None = None
+    extra: dict = field(default_factory=dict)
+
+
+def _stream(dev):
+    return stream_handle(dev)
+
+
+def colmean(X: torch.Tensor, rows: torch.Tensor | None, n: int) -> torch.Tensor:
+    ctx = Context.get(X.device.index)
+    out = torch.empty(X.shape[1], dtype=torch.float64, device=X.device)
+    check(_lib.load().ocm_colmean_f32(ctx.handle, ptr(X), X.stride(0), ptr(rows), n, X.shape[1], ptr(out),
+                                      _stream(X.device)), "ocm_colmean_f32")
+    return out
+
+
+def cast_f32(a: torch.Tensor) -> torch.Tensor:
+    ctx = Context.get(a.device.index)
+    out = torch.empty(a.shape, dtype=torch.float32, device=a.device)
+    check(_lib.load().ocm_cast_f64_f32(ctx.handle, ptr(a), a.numel(), ptr(out), _stream(a.device)),
+          "ocm_cast_f64_f32")
+    return out
+
+
+def gram(X: torch.Tensor, rows: torch.Tensor | None, seg_offsets, shift32: torch.Tensor):
+    """Per-segment shifted Gram (nseg, p, p) f64 and column sums (nseg, p)."""
+    p = X.shape[1]
+    seg = [int(s) for s in seg_offsets]
+    nseg = len(seg) - 1
+    n = seg[-1]
+    G = torch.empty((nseg, p, p), dtype=torch.float64, device=X.device)
+    cs = torch.empty((nseg, p), dtype=torch.float64, device=X.device)
+    arr = (ctypes.c_int64 * len(seg))(*seg)
+    ctx = Context.get(X.device.index)
+    check(_lib.load().ocm_gram_f32(ctx.handle, ptr(X), X.stride(0), ptr(rows), n, p, ptr(shift32), arr, nseg,
+                                   ptr(G), ptr(cs), _stream(X.device)), "ocm_gram_f32")
+    return G, cs
+
+
+def cov_from_gram(terms, shift32: torch.Tensor, n: int):
+    """terms: list of (coef, G (p,p), colsum (p,)) -> (C (p,p) f64, mean (p,) f64)."""
+    p = shift32.shape[0]
+    dev = shift32.device
+    C = torch.empty((p, p), dtype=torch.float64, device=dev)
+    mean = torch.empty(p, dtype=torch.float64, device=dev)
+    nt = len(terms)
+    Gp = (ctypes.c_void_p * nt)(*[t[1].data_ptr() for t in terms])
+    Sp = (ctypes.c_void_p * nt)(*[t[2].data_ptr() for t in terms])
+    cf = (ctypes.c_double * nt)(*[float(t[0]) for t in terms])
+    ctx = Context.get(dev.index)
+    check(_lib.load().ocm_cov_from_gram(ctx.handle, Gp, Sp, cf, nt, ptr(shift32), n, p, ptr(C), ptr(mean),
+                                        _stream(dev)), "ocm_cov_from_gram")
+    return C, mean
+
+
+def eig_topk(C: torch.Tensor, k: int, theta_mode: int, tol=EIG_TOL, max_iter=EIG_MAX_ITER):
+    p = C.shape[0]
+    dev = C.device
+    evals = torch.empty(k, dtype=torch.float64, device=dev)
+    evecs = torch.empty((k, p), dtype=torch.float64, device=dev)
+    theta = torch.zeros(3, dtype=torch.float64, device=dev)
+    iters = ctypes.c_int32(0)
+    ctx = Context.get(dev.index)
+    rc = _lib.load().ocm_eig_topk(ctx.handle, ptr(C), p, k, tol, max_iter, theta_mode, ptr(evals), ptr(evecs),
+                                  ptr(theta), ctypes.byref(iters), _stream(dev))
+    if rc == _lib.OCM_ERR_NOCONV:
+        import warnings
+
+        warnings.warn(f"ocm_eig_topk: not converged to tol={tol} in {max_iter} iterations", RuntimeWarning)
+    else:
+        check(rc, "ocm_eig_topk")
+    return evals, evecs, theta, int(iters.value)
+
+
+def sym_pinv(A: torch.Tensor, rcond=1e-15) -> torch.Tensor:
+    d = A.shape[0]
+    out = torch.empty_like(A)
+    ctx = Context.get(A.device.index)
+    check(_lib.load().ocm_sym_pinv_f64(ctx.handle, ptr(A.contiguous()), d, rcond, ptr(out), _stream(A.device)),
+          "ocm_sym_pinv_f64")
+    return out
+
+
+def make_decision(type_name: str, t2_scale: float, q_scale: float, dlim: float) -> OcmDecision:
+    return OcmDecision(TYPE_CODES[type_name], 0, float(t2_scale), float(q_scale), float(dlim))
+
+
+def score(X: torch.Tensor, rows: torch.Tensor | None, m: int, P32: torch.Tensor, mean32: torch.Tensor,
+          A: torch.Tensor, want_T=False, want_T2=True, want_Q=True, decision: OcmDecision | None = None,
+          accept_out: torch.Tensor | None = None, accept_stride: int = 1, want_stats=False):
+    """Fused scoring (ocm_score_f32).  Returns dict of device tensors."""
+    k, p = P32.shape
+    dev = X.device
+    out = {}
+    T = torch.empty((m, k), dtype=torch.float32, device=dev) if want_T else None
+    T2 = torch.empty(m, dtype=torch.float64, device=dev) if want_T2 else None
+    Q = torch.empty(m, dtype=torch.float32, device=dev) if want_Q else None
+    st = torch.empty(4, dtype=torch.float64, device=dev) if want_stats else None
+    ctx = Context.get(dev.index)
+    dec_p = ctypes.byref(decision) if decision is not None else None
+    check(_lib.load().ocm_score_f32(ctx.handle, ptr(X), X.stride(0), ptr(rows), m, p, ptr(P32), ptr(mean32),
+                                    ptr(A), k, ptr(T), ptr(T2), ptr(Q), dec_p, ptr(accept_out), accept_stride,
+                                    ptr(st), _stream(dev)), "ocm_score_f32")
+    out["T"], out["T2"], out["Q"], out["stats"] = T, T2, Q, st
+    return out
+
+
+def decide(T2: torch.Tensor, Q: torch.Tensor, decision: OcmDecision, want_red=True, want_dred=False,
+           accept_out=None, accept_stride=1):
+    m = T2.shape[0]
+    dev = T2.device
+    t2r = torch.empty(m, dtype=torch.float64, device=dev) if want_red else None
+    qr = torch.empty(m, dtype=torch.float64, device=dev) if want_red else None
+    dr = torch.empty(m, dtype=torch.float64, device=dev) if want_dred else None
+    ctx = Context.get(dev.index)
+    check(_lib.load().ocm_decide(ctx.handle, ptr(T2), ptr(Q), m, ctypes.byref(decision), ptr(t2r), ptr(qr),
+                                 ptr(dr), ptr(accept_out), accept_stride, _stream(dev)), "ocm_decide")
+    return t2r, qr, dr
+
+
+def percentile(v: torch.Tensor, pct: float) -> float:
+    dtype = 0 if v.dtype == torch.float64 else 1
+    if v.dtype not in (torch.float64, torch.float32):
+        raise TypeError("percentile: float32/float64 only")
+    out = ctypes.c_double(0.0)
+    ctx = Context.get(v.device.index)
+    check(_lib.load().ocm_percentile(ctx.handle, ptr(v), dtype, v.numel(), float(pct), ctypes.byref(out),
+                                     _stream(v.device)), "ocm_percentile")
+    return out.value
+
+
+def rowsq_residual(x: torch.Tensor, xhat: torch.Tensor) -> torch.Tensor:
+    m, p = x.shape
+    q = torch.empty(m, dtype=torch.float32, device=x.device)
+    ctx = Context.get(x.device.index)
+    check(_lib.load().ocm_rowsq_residual_f32(ctx.handle, ptr(x), ptr(xhat), m, p, x.stride(0), ptr(q),
+                                             _stream(x.device)), "ocm_rowsq_residual_f32")
+    return q
+
+
+def invcov_from_evals(evals: torch.Tensor, rcond=1e-15) -> torch.Tensor:
+    """pinv(cov(T)) for T = centred scores on the eigenbasis: cov(T) = diag(λ)
+    (utils/SIMCA.py:69 with np.linalg.pinv's rcond=1e-15 cutoff)."""
+    lam = evals.to(torch.float64)
+    cut = rcond * lam.abs().max()
+    inv = torch.where(lam.abs() > cut, 1.0 / lam, torch.zeros_like(lam))
+    return torch.diag(inv)
+
+
+def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_mode: int,
+              want_T=True, keep_C=False, shift32: torch.Tensor | None = None, allreduce=None) -> ClassFit:
+    """Gram → covariance → top-k eigenpairs → fit-set scores for one class.
+
+    ``allreduce`` (optional callable on a list of device tensors) sums the
+    per-rank Gram / column sums / row counts across ranks (RCCL), for row
+    shards of one class spread over GPUs."""
+    p = X.shape[1]
+    if k > p or k < 1:
+        raise ValueError(f"n_components={k} must be in [1, {p}]")
+    if shift32 is None:
+        shift64 = colmean(X, rows, min(n, SHIFT_SAMPLE))
+        shift32 = cast_f32(shift64)
+        if allreduce is not None:
+            allreduce([shift32], op="mean")
+    G, cs = gram(X, rows, [0, n], shift32)
+    n_total = n
+    if allreduce is not None:
+        cnt = torch.tensor([float(n)], dtype=torch.float64, device=X.device)
+        allreduce([G, cs, cnt])
+        n_total = int(round(cnt.item()))
+    if n_total < 2:
+        raise ValueError("SIMCA needs at least 2 samples in a class")
+    C, mean64 = cov_from_gram([(1.0, G[0], cs[0])], shift32, n_total)
+    del G
+    evals, evecs, theta, iters = eig_topk(C, k, theta_mode)
+    P32 = cast_f32(evecs)
+    mean32 = cast_f32(mean64)
+    invcov = invcov_from_evals(evals)
+    sc = score(X, rows, n, P32, mean32, invcov, want_T=want_T, want_stats=True)
+    host = torch.cat([evals, theta, sc["stats"]]).cpu().numpy()
+    ev_h = host[:k]
+    th = tuple(float(v) for v in host[k:k + 3])
+    stats = host[k + 3:]
+    if allreduce is not None:
+        stt = torch.tensor(stats, dtype=torch.float64, device=X.device)
+        allreduce([stt])
+        stats = stt.cpu().numpy()
+    fit = ClassFit(k=k, n=n_total, p=p, mean64=mean64, mean32=mean32, evals=evals, P64=evecs, P32=P32,
+                   invcov=invcov, thetas=th, evals_host=ev_h, T=sc["T"], T2=sc["T2"], Q=sc["Q"],
+                   T2_stats=(stats[0], stats[1]), Q_stats=(stats[2], stats[3]), eig_iters=iters,
+                   C=C if keep_C else None)
+    fit.extra["shift32"] = shift32
+    return fit

@@ -1,0 +1,119 @@
+"""Host-side scalar limits of SIMCA (fp64 SciPy quantiles), computed from the
+device-side moments / percentiles / tail traces.
+
+Mirror of utils/SIMCA.py:156-236 (``_Tlim``, ``_Qlim``, ``_critic_distance``):
+same formulas, same quirks (chi2pom state kept on the estimator and
+overwritten per class; unknown limit names leave the result unbound).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+from scipy import stats
+from scipy.special import erfinv
+
+
+class Moments:
+    """n, Σx, Σx² of a device vector (from the scoring kernel's fused stats)
+    plus a lazy percentile callback (device radix select)."""
+
+    def __init__(self, n, s1, s2, percentile):
+        self.n = int(n)
+        self.s1 = float(s1)
+        self.s2 = float(s2)
+        self._pct = percentile
+
+    @property
+    def mean(self) -> float:
+        return self.s1 / self.n
+
+    def var(self, ddof=1) -> float:
+        if self.n - ddof <= 0:
+            return float("nan")
+        m = self.mean
+        return max(self.s2 - self.n * m * m, 0.0) / (self.n - ddof)
+
+    def percentile(self, pct: float) -> float:
+        return self._pct(pct)
+
+
+def t2_limit(est, T2: Moments, k: int) -> float:
+    """utils/SIMCA.py:156-182."""
+    n = T2.n
+    if est.t2lim == "perc":
+        return T2.percentile(est.t2cl * 100)
+    if est.t2lim == "Fdistrig":
+        F = stats.f.ppf(est.t2cl, k, n - k)
+        return (k / n) * (n ** 2 - 1) / (n - k) * F
+    if est.t2lim == "Fdist":
+        F = stats.f.ppf(est.t2cl, k, n - k)
+        return k * (n - 1) / (n - k) * F
+    if est.t2lim == "chi2":
+        return stats.chi2.ppf(est.t2cl, k)
+    if est.t2lim == "chi2pom":
+        h0 = float(T2.mean)
+        v = float(T2.var(ddof=1)) if n > 1 else 0.0
+        Nh = max(int(np.round(2 * (h0 ** 2) / v)) if v > 0 else 1, 1)
+        est._t2dof = Nh
+        est._t2scfact = h0
+        return h0 * stats.chi2.ppf(est.t2cl, Nh) / Nh
+    raise UnboundLocalError(f"local variable 'T2_limit' referenced before assignment (t2lim={est.t2lim!r})")
+
+
+def q_limit(est, Q: Moments, thetas) -> float:
+    """utils/SIMCA.py:184-217.  ``thetas`` = (θ1, θ2, θ3) of the discarded eigenvalues."""
+    if est.qlim == "perc":
+        return Q.percentile(est.qcl * 100)
+    if est.qlim == "jm":
+        th1, th2, th3 = thetas
+        if th1 == 0:
+            raise UnboundLocalError("local variable 'h0' referenced before assignment (jm limit with theta1 == 0)")
+        h0 = 1 - (2 * th1 * th3) / (3 * th2 ** 2)
+        h0 = max(h0, 0.001)
+        ca = math.sqrt(2) * erfinv(2 * est.qcl - 1)
+        h1 = ca * math.sqrt(2 * th2 * h0 ** 2) / th1
+        h2 = th2 * h0 * (h0 - 1) / (th1 ** 2)
+        return th1 * (h1 + 1 + h2) ** (1 / h0)
+    if est.qlim == "chi2box":
+        th1, th2, _ = thetas
+        g = th2 / th1
+        Ng = (th1 ** 2) / th2
+        print("here we are")  # reference prints these (utils/SIMCA.py:207-208)
+        print(th1, th2, g, Ng)
+        return g * stats.chi2.ppf(est.qcl, Ng)
+    if est.qlim == "chi2pom":
+        v0 = np.float64(Q.mean)
+        Nv = max(round(2 * (v0 ** 2) / np.float64(Q.var(ddof=1))), 1)
+        est._qdof = Nv
+        est._qscfact = float(v0)
+        return float(v0 * stats.chi2.ppf(est.qcl, Nv) / Nv)
+    raise UnboundLocalError(f"local variable 'Q_limit' referenced before assignment (qlim={est.qlim!r})")
+
+
+def critic_distance(est, T2_limit, Q_limit, thetas, k: int):
+    """utils/SIMCA.py:219-236."""
+    if est.type == "sim":
+        return 1
+    if est.type == "alt":
+        return np.sqrt(2)
+    if est.type == "ci":
+        th1, th2, _ = thetas
+        tr1 = (k / T2_limit) + (th1 / Q_limit)
+        tr2 = (k / T2_limit ** 2) + (th2 / Q_limit ** 2)
+        gd = tr2 / tr1
+        hd = tr1 ** 2 / tr2
+        return gd * stats.chi2.ppf(est.dcl, hd)
+    if est.type == "dd":
+        return stats.chi2.ppf(est.dcl, est._t2dof + est._qdof)
+    raise UnboundLocalError(f"local variable 'dlim' referenced before assignment (type={est.type!r})")
+
+
+def theta_mode_for(est) -> int:
+    """Which tail moments the configured limits need: jm → θ1..θ3,
+    chi2box / ci → θ1..θ2, otherwise none."""
+    if est.qlim == "jm":
+        return 2
+    if est.qlim == "chi2box" or est.type == "ci":
+        return 1
+    return 0

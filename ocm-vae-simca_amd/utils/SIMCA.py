@@ -1,0 +1,354 @@
+"""Drop-in ``SIMCA`` estimator backed by the MI355X engine (libocm.so).
+
+Same class name, constructor keywords, attributes, ``_model`` keys, return
+types and quirks as the reference estimator (TEAM-AIOLY/OCM-VAE-SIMCA
+``utils/SIMCA.py:12-381``), so drivers such as ``simca_nuts.py``
+(``from utils import SIMCA`` … ``.fit`` / ``.predict`` / ``.transform`` /
+``._model[cls]['D_limit']``) run unchanged.  The arithmetic runs on the GPU
+through ``ocm.engine`` (Gram on FP32 MFMA, fp64 eigensolver, fused
+projection/Q/T² scoring); only the scalar limits are evaluated on the host.
+
+Inputs may be NumPy arrays (copied to HBM; results come back as NumPy, like
+the reference) or CUDA torch tensors (device-resident; ``predict`` then
+returns a device tensor and ``_model`` arrays are materialised lazily).
+
+Documented deviations:
+* predict/transform use the exact top-k loadings of the covariance; the
+  reference re-estimates them with a randomized ``PCA(k)`` (utils/SIMCA.py:75)
+  which agrees on the same subspace to its own randomised tolerance;
+* ``_model[cls]['pca_model']`` is an engine-backed facade with the sklearn
+  PCA attributes drivers read (``components_``, ``mean_``, ``transform``,
+  ``inverse_transform``);
+* ``eigs_all`` holds the leading k eigenvalues from the HIP eigensolver and,
+  on first access only, the rest of the spectrum (a diagnostic no limit uses;
+  the θ moments come from device traces).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+from sklearn.base import BaseEstimator, ClassifierMixin
+
+from ocm import engine, limits
+
+__all__ = ["SIMCA"]
+
+
+class _Lazy:
+    __slots__ = ("fn",)
+
+    def __init__(self, fn):
+        self.fn = fn
+
+
+class ModelDict(dict):
+    """``_model[cls]`` — a dict whose large arrays are copied out of HBM on
+    first access (the timed path never pays for host copies)."""
+
+    def __getitem__(self, key):
+        v = dict.__getitem__(self, key)
+        if isinstance(v, _Lazy):
+            v = v.fn()
+            dict.__setitem__(self, key, v)
+        return v
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def values(self):
+        return [self[k] for k in self]
+
+    def items(self):
+        return [(k, self[k]) for k in self]
+
+    def __repr__(self):
+        return "{" + ", ".join(f"{k!r}: {self[k]!r}" for k in self) + "}"
+
+
+class EnginePCA:
+    """sklearn-PCA-shaped view of one class model (what ``pca_model`` exposes)."""
+
+    def __init__(self, fit: engine.ClassFit, out_dtype):
+        self._fit = fit
+        self._dt = out_dtype
+        self.n_components = fit.k
+        self.n_components_ = fit.k
+        self.n_features_in_ = fit.p
+
+    @property
+    def components_(self):
+        return self._fit.P64.cpu().numpy().astype(self._dt)
+
+    @property
+    def mean_(self):
+        return self._fit.mean64.cpu().numpy().astype(self._dt)
+
+    @property
+    def explained_variance_(self):
+        return self._fit.evals_host.astype(self._dt)
+
+    def transform(self, X):
+        Xd = engine.as_device_f32(X)
+        out = engine.score(Xd, None, Xd.shape[0], self._fit.P32, self._fit.mean32, self._fit.invcov,
+                           want_T=True, want_T2=False, want_Q=False)
+        T = out["T"]
+        return T if isinstance(X, torch.Tensor) else T.cpu().numpy().astype(self._dt)
+
+    def inverse_transform(self, T):
+        # T·P + μ (sklearn/decomposition/_base.py:197); facade utility, not on the hot path
+        Td = T if isinstance(T, torch.Tensor) else torch.from_numpy(np.asarray(T))
+        Td = Td.to(self._fit.P64.device, torch.float64)
+        Xr = Td @ self._fit.P64 + self._fit.mean64
+        return Xr if isinstance(T, torch.Tensor) else Xr.cpu().numpy().astype(self._dt)
+
+
+def _np(t, dtype=None):
+    a = t.detach().cpu().numpy()
+    return a.astype(dtype) if dtype is not None and a.dtype != dtype else a
+
+
+class SIMCA(BaseEstimator, ClassifierMixin):
+    def __init__(self, n_components=2, model_class=None, type: str = "alt", t2lim="Fdist", t2cl=0.95, qlim="jm",
+                 qcl=0.95, dcl=0.95, maxPC=20, criteria="compl", verbose=True):
+        self.n_components = n_components
+        self.model_class = model_class
+        self.type = type
+        self.t2lim = t2lim
+        self.t2cl = t2cl
+        self.qlim = qlim
+        self.qcl = qcl
+        self.criteria = criteria
+        self.dcl = dcl
+        self.maxPC = maxPC
+        self.metrics = {}
+        self.verbose = verbose
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, X, classes):
+        """utils/SIMCA.py:27-59 (same parameter normalisation and quirks)."""
+        if self.model_class is None:
+            self.model_class = np.unique(_host_labels(classes))
+        elif isinstance(self.model_class, (int, np.integer)):
+            self.model_class = [self.model_class]
+        if not isinstance(self.n_components, list):
+            self.n_components = [self.n_components]
+        if len(self.n_components) == 1:
+            self.n_components = [self.n_components[0]] * len(self.model_class)
+        elif len(self.n_components) != len(self.model_class):
+            raise ValueError("n_components length must match number of classes")
+        if self.type == "dd" and self.t2lim != "chi2pom":
+            print("t2lim set as chi2pom")
+            self.t2lim = "chi2pom"
+        if self.type == "dd" and self.qlim != "chi2pom":
+            print("qlim set as chi2pom")
+            self.qlim = "chi2pom"
+
+        self._out_dtype = _out_dtype(X)
+        Xd = engine.as_device_f32(X)
+        lab = _device_labels(classes, Xd.device)
+        self._model = {}
+        self._fits = {}
+        for i, cls in enumerate(self.model_class):
+            mask = lab == int(cls)
+            n = int(mask.sum().item())
+            rows = None if n == Xd.shape[0] else torch.nonzero(mask).flatten()
+            self._model[cls] = self._fit_one_class(Xd, rows, n, int(self.n_components[i]))
+            self._fits[cls] = self._model[cls]._fit
+        self.n_features_in_ = X.shape[1]
+        self.is_fitted_ = True
+        return self
+
+    def _fit_one_class(self, Xd, rows, n, k):
+        """utils/SIMCA.py:62-99 on the device."""
+        fit = engine.fit_class(Xd, rows, n, k, limits.theta_mode_for(self), want_T=True, keep_C=True)
+        T2m = limits.Moments(n, *fit.T2_stats, lambda pct: engine.percentile(fit.T2, pct))
+        Qm = limits.Moments(n, *fit.Q_stats, lambda pct: engine.percentile(fit.Q, pct))
+        T2_limit = limits.t2_limit(self, T2m, k)
+        Q_limit = limits.q_limit(self, Qm, fit.thetas)
+        D_limit = limits.critic_distance(self, T2_limit, Q_limit, fit.thetas, k)
+        dec = self._decision(T2_limit, Q_limit, D_limit)
+        dt = self._out_dtype
+        red = {}
+
+        def reds():
+            if not red:
+                t2r, qr, _ = engine.decide(fit.T2, fit.Q, dec)
+                red["t2"], red["q"] = _np(t2r), _np(qr)
+            return red
+
+        md = ModelDict()
+        md._fit = fit
+        md.update({
+            "pca_model": EnginePCA(fit, dt),
+            "n_components": k,
+            "xmean": _Lazy(lambda: _np(fit.mean64, dt)),
+            "invcovT": _Lazy(lambda: _np(fit.invcov)),
+            "eigs_all": _Lazy(lambda: _all_eigs(fit, n)),
+            "T": _Lazy(lambda: _np(fit.T, dt)),
+            "P": _Lazy(lambda: _np(fit.P64, dt)),
+            "T2": _Lazy(lambda: _np(fit.T2)),
+            "Q": _Lazy(lambda: _np(fit.Q, dt)),
+            "T2red": _Lazy(lambda: reds()["t2"]),
+            "Qred": _Lazy(lambda: reds()["q"]),
+            "T2_limit": T2_limit,
+            "Q_limit": Q_limit,
+            "D_limit": D_limit,
+            "n_samples": n,
+        })
+        return md
+
+    def _decision(self, T2_limit, Q_limit, D_limit):
+        if self.type == "dd":
+            return engine.make_decision("dd", self._t2dof / self._t2scfact, self._qdof / self._qscfact, D_limit)
+        if self.type not in ("sim", "alt", "ci"):
+            raise UnboundLocalError(f"local variable 'dred' referenced before assignment (type={self.type!r})")
+        return engine.make_decision(self.type, 1.0 / T2_limit, 1.0 / Q_limit, D_limit)
+
+    # ------------------------------------------------------------ transform
+    def transform(self, X):
+        """utils/SIMCA.py:101-117 — (T2, T2red, Q, Qred) of the LAST class."""
+        Xd = engine.as_device_f32(X)
+        cls = self.model_class[-1]
+        fit = self._fits[cls]
+        m = self._model[cls]
+        out = engine.score(Xd, None, Xd.shape[0], fit.P32, fit.mean32, fit.invcov)
+        dec = self._decision(m["T2_limit"], m["Q_limit"], m["D_limit"])
+        t2r, qr, _ = engine.decide(out["T2"], out["Q"], dec)
+        if isinstance(X, torch.Tensor):
+            return out["T2"], t2r, out["Q"], qr
+        return _np(out["T2"]), _np(t2r), _np(out["Q"], self._out_dtype), _np(qr)
+
+    # -------------------------------------------------------------- predict
+    def predict(self, X, y_true=None):
+        """utils/SIMCA.py:120-154 — (m, C) float64 of 0/1, decision fused in the scoring kernel."""
+        Xd = engine.as_device_f32(X)
+        m = Xd.shape[0]
+        C = len(self.model_class)
+        pred = torch.zeros((m, C), dtype=torch.float64, device=Xd.device)
+        for i, cls in enumerate(self.model_class):
+            fit = self._fits[cls]
+            info = self._model[cls]
+            dec = self._decision(info["T2_limit"], info["Q_limit"], info["D_limit"])
+            acc = pred[:, i:] if C > 1 else pred
+            engine.score(Xd, None, m, fit.P32, fit.mean32, fit.invcov, want_T2=False, want_Q=False,
+                         decision=dec, accept_out=acc, accept_stride=C)
+        out = pred if isinstance(X, torch.Tensor) else pred.cpu().numpy()
+        if y_true is not None:
+            yt = _host_labels(y_true)
+            ph = out.cpu().numpy() if isinstance(out, torch.Tensor) else out
+            for i, cls in enumerate(self.model_class):
+                self.metrics[cls] = self._metrics_simca_conformity(yt, ph[:, i], cls)
+                if self.verbose:
+                    mt = self.metrics[cls]
+                    print(f"Sample class {cls} = {np.sum(yt == cls)}")
+                    print(f"Confusion Matrix for class {cls}:\nTP: {mt['TP']}, TN: {mt['TN']}, FP: {mt['FP']}, FN: {mt['FN']}")
+                    print(f"Class {cls} - Sensitivity: {mt['sensitivity']}, Specificity: {mt['specificity']:.4f}, "
+                          f"Accuracy: {mt['accuracy']:.4f}, Efficiency: {mt['efficiency']:.4f}")
+        return out
+
+    # -------------------------------------------------------------- metrics
+    def _metrics_simca_conformity(self, y_true, y_pred, class_index):
+        """utils/SIMCA.py:238-266 (NumPy broadcasting semantics kept)."""
+        y_true = _host_labels(y_true)
+        y_pred = y_pred.cpu().numpy() if isinstance(y_pred, torch.Tensor) else np.asarray(y_pred)
+        true_class = (y_true == class_index).astype(int)
+        TP = np.sum((y_pred == 1) & (true_class == 1))
+        TN = np.sum((y_pred == 0) & (true_class == 0))
+        FP = np.sum((y_pred == 1) & (true_class == 0))
+        FN = np.sum((y_pred == 0) & (true_class == 1))
+        with np.errstate(divide="ignore", invalid="ignore"):
+            sensitivity = TP / (TP + FN) * 100
+            specificity = TN / (TN + FP) * 100
+            accuracy = (TP + TN) / (TP + TN + FP + FN) * 100
+            efficiency = np.sqrt(sensitivity * specificity)
+        return {"sensitivity": sensitivity, "specificity": specificity, "accuracy": accuracy,
+                "efficiency": efficiency, "TP": TP, "TN": TN, "FP": FP, "FN": FN}
+
+    def score(self, X, y):
+        """utils/SIMCA.py:268-278 — returns specificity (2-D y_pred, list class index, as the reference)."""
+        y_pred = self.predict(X, y_true=y)
+        metrics = self._metrics_simca_conformity(y, y_pred, self.model_class)
+        return metrics["specificity"]
+
+    # ------------------------------------------------------------ plotting
+    def toplotT2Q(self, X, y_test):
+        """T²red–Qred scatter with the decision curve (utils/SIMCA.py:280-307); host plotting glue."""
+        import matplotlib.pyplot as plt
+
+        for cls in self._model:
+            T2, T2red, Q, Qred = self.transform(X)
+            Dlim = self._model[cls]["D_limit"]
+            a = np.arange(0, Dlim + 0.0001, 0.0001)
+            curve = np.sqrt(np.maximum(Dlim ** 2 - a ** 2, 0))
+            plt.figure(figsize=(6, 6))
+            sc = plt.scatter(T2red, Qred, c=y_test, cmap="viridis", s=40, edgecolor="k", linewidth=0.5, alpha=0.7)
+            plt.plot(a, curve, "b-", lw=2, label=f"Confine classe {cls}")
+            plt.xlabel(r"$T^2_{red}$")
+            plt.ylabel(r"$Q_{red}$")
+            plt.legend(*sc.legend_elements(), title="Class")
+            plt.title(rf"$T^2$ vs $Q$  Classe {cls}")
+            plt.grid(True, alpha=0.3)
+            plt.xlim(left=0)
+            plt.ylim(bottom=0)
+            plt.tight_layout()
+            plt.show()
+            return plt
+
+    def toplotT2Q_iterative(self, X, y_test):
+        """Plotly version (utils/SIMCA.py:310-381); host plotting glue."""
+        import plotly.graph_objects as go
+
+        figs = []
+        y_color = np.asarray(y_test).astype(str)
+        for cls in self._model:
+            T2, T2red, Q, Qred = self.transform(X)
+            Dlim = float(self._model[cls]["D_limit"])
+            a = np.linspace(0, Dlim, 1200)
+            curve = np.sqrt(np.maximum(Dlim ** 2 - a ** 2, 0.0))
+            x_max = max(np.max(T2red), Dlim) * 1.05 if len(T2red) else Dlim * 1.05
+            y_max = max(np.max(Qred), Dlim) * 1.05 if len(Qred) else Dlim * 1.05
+            fig = go.Figure()
+            for c in np.unique(y_color):
+                mask = y_color == c
+                if np.any(mask):
+                    fig.add_trace(go.Scatter(x=T2red[mask], y=Qred[mask], mode="markers",
+                                             marker=dict(size=7, line=dict(width=0.7, color="black")),
+                                             name=f"Class {c}", showlegend=True, visible=True))
+            fig.add_trace(go.Scatter(x=a, y=curve, mode="lines", name="Decision Limit",
+                                     line=dict(color="blue", width=3), opacity=1.0))
+            fig.update_layout(width=600, height=600, xaxis_title="T<sup>2</sup><sub>red</sub>",
+                              yaxis_title="Q</sup><sub>red</sub>")
+            fig.update_xaxes(range=[0, x_max], zeroline=True)
+            fig.update_yaxes(range=[0, y_max], zeroline=True)
+            figs.append(fig)
+        return figs[0] if len(figs) == 1 else figs
+
+
+def _out_dtype(X):
+    if isinstance(X, torch.Tensor):
+        return np.float64 if X.dtype == torch.float64 else np.float32
+    return np.float64 if np.asarray(X).dtype == np.float64 else np.float32
+
+
+def _host_labels(y):
+    if isinstance(y, torch.Tensor):
+        return y.detach().cpu().numpy()
+    return np.asarray(y)
+
+
+def _device_labels(y, device):
+    if isinstance(y, torch.Tensor):
+        return y.to(device=device, dtype=torch.int64)
+    return torch.from_numpy(np.asarray(y).astype(np.int64)).to(device)
+
+
+def _all_eigs(fit: engine.ClassFit, n: int):
+    """Full explained-variance spectrum (min(n, p) values, descending): the
+    leading k from the HIP eigensolver, the rest from the HBM-resident
+    covariance on first access (diagnostic only)."""
+    r = min(n, fit.p)
+    if fit.C is None:
+        return fit.evals_host.copy()
+    full = torch.linalg.eigvalsh(fit.C).flip(0)[:r].cpu().numpy()
+    full[: fit.k] = fit.evals_host
+    return full

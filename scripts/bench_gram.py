@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""A/B the Gram kernel variants in ONE process (interleaved rounds), on the
+bench workload (1M×2048 fp32 in HBM).  Prints TFLOP/s (symmetric count) per
+variant and the max relative difference of G between variants."""
+import argparse
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "ocm-vae-simca_amd"))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1_000_000)
+    ap.add_argument("--p", type=int, default=2048)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="acc64:0,f32:8192,f32:4096,f32:16384")
+    args = ap.parse_args()
+    import torch
+
+    from bench import synth_device
+    from ocm import engine
+    from ocm._lib import Context
+
+    dev = torch.device("cuda", 0)
+    X = synth_device(args.rows, args.p, 20, seed=7, device=dev)
+    shift = engine.cast_f32(engine.colmean(X, None, 4096))
+    ctx = Context.get(0)
+    variants = [v.split(":") for v in args.variants.split(",")]
+    res = {v[0] + ":" + v[1]: [] for v in variants}
+    Gs = {}
+    flop = args.rows * args.p * (args.p + 1)
+    for r in range(args.rounds):
+        for name, chunk in variants:
+            os.environ["OCM_GRAM_VARIANT"] = name
+            os.environ["OCM_GRAM_CHUNK"] = chunk
+            engine.gram(X, None, [0, args.rows], shift)  # warm (workspace)
+            torch.cuda.synchronize()
+            ctx.read_timing(0)
+            ctx.set_timing(True)
+            G, cs = engine.gram(X, None, [0, args.rows], shift)
+            ctx.set_timing(False)
+            ms, cnt = ctx.read_timing(0)
+            res[name + ":" + chunk].append(flop / (ms / 1e3) / 1e12)
+            if r == 0:
+                Gs[name + ":" + chunk] = G[0].clone()
+    ref = next(iter(Gs.values()))
+    for key, vals in res.items():
+        d = ((Gs[key] - ref).abs().max() / ref.abs().max()).item()
+        print(f"{key:16s} TFLOP/s median {sorted(vals)[len(vals)//2]:7.2f}  all {[round(v,1) for v in vals]}  "
+              f"maxrel vs first {d:.2e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

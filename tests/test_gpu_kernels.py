@@ -1,0 +1,187 @@
+"""Kernel-level parity on the GPU: every libocm entry point against the CPU
+oracle / a float64 NumPy reference of the same op, on seeded inputs."""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from ocm import engine
+
+    return engine
+
+
+def _dev(a):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.parametrize("n,p", [(5000, 300), (777, 128), (4100, 96), (3000, 1000)])
+def test_gram_matches_fp64(eng, n, p):
+    rng = np.random.default_rng(n + p)
+    X = (rng.standard_normal((n, p)) * rng.uniform(0.1, 3, p) + 2.0).astype(np.float32)
+    Xd = _dev(X)
+    shift = _dev(X[:17].mean(0).astype(np.float32))
+    G, cs = eng.gram(Xd, None, [0, n], shift)
+    Y = X.astype(np.float64) - shift.cpu().numpy().astype(np.float64)
+    Gref = Y.T @ Y
+    np.testing.assert_allclose(G[0].cpu().numpy(), Gref, rtol=2e-6, atol=2e-6 * np.abs(Gref).max())
+    np.testing.assert_allclose(cs[0].cpu().numpy(), Y.sum(0), rtol=1e-6, atol=1e-6 * np.abs(Y).sum(0).max())
+
+
+def test_gram_segments_and_rows(eng):
+    import torch
+
+    rng = np.random.default_rng(3)
+    n, p = 6000, 200
+    X = rng.standard_normal((n, p)).astype(np.float32)
+    rows = np.sort(rng.choice(n, 4500, replace=False))
+    seg = [0, 1000, 1000, 2600, 4500]  # includes an empty segment
+    Xd = _dev(X)
+    shift = torch.zeros(p, dtype=torch.float32, device="cuda")
+    G, cs = eng.gram(Xd, _dev(rows.astype(np.int64)), seg, shift)
+    Xs = X[rows].astype(np.float64)
+    for s in range(len(seg) - 1):
+        Y = Xs[seg[s]:seg[s + 1]]
+        ref = Y.T @ Y
+        np.testing.assert_allclose(G[s].cpu().numpy(), ref, rtol=2e-6, atol=2e-6 * max(np.abs(ref).max(), 1))
+        np.testing.assert_allclose(cs[s].cpu().numpy(), Y.sum(0), rtol=1e-6, atol=1e-7 * np.abs(Y).sum(0).max())
+
+
+def test_cov_and_mean(eng):
+    from oracle.simca_oracle import synth_spectra
+
+    X = synth_spectra(4000, 300, 8, rank=20, seed=5)
+    Xd = _dev(X)
+    shift = eng.cast_f32(eng.colmean(Xd, None, 64))
+    G, cs = eng.gram(Xd, None, [0, 4000], shift)
+    C, mean = eng.cov_from_gram([(1.0, G[0], cs[0])], shift, 4000)
+    Xf = X.astype(np.float64)
+    # y = x − shift is formed in float32 (≤ 6e-8·|y| per element) before the f64
+    # sums; the reference's own float32 mean (sklearn) is no better than 1e-7
+    np.testing.assert_allclose(mean.cpu().numpy(), Xf.mean(0), rtol=0, atol=2e-7)
+    Cref = np.cov(Xf, rowvar=False)
+    np.testing.assert_allclose(C.cpu().numpy(), Cref, rtol=1e-5, atol=1e-6 * np.abs(Cref).max())
+
+
+@pytest.mark.parametrize("p,k", [(300, 8), (256, 20), (48, 5), (1000, 12)])
+def test_eig_topk_and_thetas(eng, p, k):
+    rng = np.random.default_rng(p * 31 + k)
+    # spectrum with a gap at k and a long tail
+    lam = np.concatenate([np.linspace(50, 10, k), np.geomspace(1.0, 1e-3, p - k)])
+    Qm, _ = np.linalg.qr(rng.standard_normal((p, p)))
+    C = (Qm * lam) @ Qm.T
+    C = 0.5 * (C + C.T)
+    Cd = _dev(C)
+    evals, evecs, theta, iters = eng.eig_topk(Cd, k, 2)
+    w, V = np.linalg.eigh(C)
+    w, V = w[::-1], V[:, ::-1]
+    np.testing.assert_allclose(evals.cpu().numpy(), w[:k], rtol=1e-10)
+    P = evecs.cpu().numpy()
+    for i in range(k):
+        v = V[:, i] * np.sign(V[np.argmax(np.abs(V[:, i])), i])
+        np.testing.assert_allclose(P[i], v, atol=1e-7)
+    tail = w[k:]
+    np.testing.assert_allclose(theta.cpu().numpy(), [tail.sum(), (tail ** 2).sum(), (tail ** 3).sum()],
+                               rtol=1e-8)
+
+
+def test_eig_no_gap_converges(eng):
+    rng = np.random.default_rng(9)
+    p, k = 512, 10
+    A = rng.standard_normal((2000, p))
+    C = np.cov(A, rowvar=False)
+    evals, evecs, theta, iters = eng.eig_topk(_dev(C), k, 2)
+    w = np.linalg.eigvalsh(C)[::-1]
+    np.testing.assert_allclose(evals.cpu().numpy(), w[:k], rtol=1e-8)
+    tail = w[k:]
+    np.testing.assert_allclose(theta.cpu().numpy()[:2], [tail.sum(), (tail ** 2).sum()], rtol=1e-8)
+
+
+@pytest.mark.parametrize("k", [4, 20, 40])
+def test_score_matches_oracle(eng, k):
+    import torch
+    from oracle.simca_oracle import project_scores, synth_spectra
+
+    n, p = 3000, 520
+    X = synth_spectra(n, p, min(k, 20), rank=max(k + 5, 30), seed=k, outlier_frac=0.1)
+    Xf = X.astype(np.float64)
+    mean = Xf.mean(0)
+    w, V = np.linalg.eigh(np.cov(Xf, rowvar=False))
+    P = V[:, ::-1][:, :k].T.copy()
+    lam = w[::-1][:k]
+    A = np.diag(1 / lam)
+    T_ref, T2_ref, Q_ref = project_scores(X, P, mean, A)
+    out = eng.score(_dev(X), None, n, _dev(P.astype(np.float32)), _dev(mean.astype(np.float32)), _dev(A),
+                    want_T=True, want_stats=True)
+    np.testing.assert_allclose(out["T"].cpu().numpy(), T_ref, rtol=1e-4, atol=1e-4 * np.abs(T_ref).max())
+    np.testing.assert_allclose(out["T2"].cpu().numpy(), T2_ref, rtol=2e-5, atol=1e-6 * np.median(T2_ref))
+    np.testing.assert_allclose(out["Q"].cpu().numpy(), Q_ref, rtol=2e-5, atol=1e-6 * np.median(Q_ref))
+    st = out["stats"].cpu().numpy()
+    np.testing.assert_allclose(st, [T2_ref.sum(), (T2_ref ** 2).sum(), Q_ref.astype(np.float64).sum(),
+                                    (Q_ref.astype(np.float64) ** 2).sum()], rtol=1e-6)
+    # row-index path (gather) and fused decision
+    rows = np.arange(n - 1, -1, -3)
+    acc = torch.zeros((len(rows), 2), dtype=torch.float64, device="cuda")
+    dec = eng.make_decision("alt", 1 / np.percentile(T2_ref, 90), 1 / np.percentile(Q_ref, 90), np.sqrt(2))
+    out2 = eng.score(_dev(X), _dev(rows.astype(np.int64)), len(rows), _dev(P.astype(np.float32)),
+                     _dev(mean.astype(np.float32)), _dev(A), decision=dec, accept_out=acc[:, 1:], accept_stride=2)
+    np.testing.assert_allclose(out2["Q"].cpu().numpy(), Q_ref[rows], rtol=2e-5, atol=1e-6 * np.median(Q_ref))
+    d = np.sqrt((T2_ref[rows] * dec.t2_scale) ** 2 + (Q_ref[rows].astype(np.float64) * dec.q_scale) ** 2)
+    clear = np.abs(d - np.sqrt(2)) > 1e-4
+    np.testing.assert_array_equal(acc[:, 1].cpu().numpy()[clear], (d < np.sqrt(2))[clear].astype(float))
+    assert np.all(acc[:, 0].cpu().numpy() == 0)
+
+
+def test_decide_types(eng):
+    import torch
+
+    rng = np.random.default_rng(1)
+    m = 1000
+    T2 = rng.gamma(3, 1, m)
+    Q = rng.gamma(5, 1, m).astype(np.float32)
+    for ty in ["sim", "alt", "ci", "dd"]:
+        dec = eng.make_decision(ty, 0.3, 0.2, 1.3)
+        acc = torch.zeros(m, dtype=torch.float64, device="cuda")
+        t2r, qr, dr = eng.decide(_dev(T2), _dev(Q), dec, want_dred=True, accept_out=acc)
+        t, q = T2 * 0.3, Q.astype(np.float64) * 0.2
+        ref = {"sim": np.maximum(t, q), "alt": np.sqrt(t * t + q * q), "ci": t + q, "dd": t + q}[ty]
+        np.testing.assert_allclose(dr.cpu().numpy(), ref, rtol=1e-14)
+        np.testing.assert_array_equal(acc.cpu().numpy(), (ref < 1.3).astype(float))
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 1000, 100003])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_percentile(eng, n, dtype):
+    rng = np.random.default_rng(n)
+    v = (rng.standard_normal(n) * 10).astype(dtype)
+    v[: n // 3] = np.abs(v[: n // 3])  # mixed signs, duplicates below
+    if n > 10:
+        v[5:9] = v[4]
+    for pct in [0, 5, 50, 95, 99.9, 100]:
+        got = eng.percentile(_dev(v), pct)
+        # numpy evaluates the interpolation in the array dtype; so does ocm_percentile
+        np.testing.assert_allclose(got, np.percentile(v, pct), rtol=1e-7 if dtype == np.float32 else 1e-15)
+
+
+def test_sym_pinv(eng):
+    rng = np.random.default_rng(2)
+    for d in [3, 17, 32, 64]:
+        B = rng.standard_normal((d + 5, d))
+        A = B.T @ B
+        np.testing.assert_allclose(eng.sym_pinv(_dev(A)).cpu().numpy(), np.linalg.pinv(A), rtol=1e-8, atol=1e-10)
+    A = np.diag([3.0, 2.0, 0.0])  # rank-deficient -> pseudo-inverse
+    np.testing.assert_allclose(eng.sym_pinv(_dev(A)).cpu().numpy(), np.linalg.pinv(A), atol=1e-14)
+
+
+def test_rowsq_residual(eng):
+    rng = np.random.default_rng(4)
+    x = rng.standard_normal((777, 333)).astype(np.float32)
+    xh = x + 0.01 * rng.standard_normal(x.shape).astype(np.float32)
+    q = eng.rowsq_residual(_dev(x), _dev(xh)).cpu().numpy()
+    np.testing.assert_allclose(q, ((x.astype(np.float64) - xh) ** 2).sum(1), rtol=1e-6)
