@@ -5,15 +5,17 @@
 // dense contraction over the spectra rows.
 //
 // Layout: X row-major n×p float32 (spectra × wavelengths).  A workgroup owns
-// one 128×128 tile (ti ≤ tj) of G = Σ yᵀy (y = x - shift) over one chunk of
-// rows; it streams 32-row × 128-column panels of the two column blocks
-// through double-buffered LDS (coalesced 512-B row segments, shift
-// subtracted on the way in) and accumulates with v_mfma_f32_32x32x2_f32
-// (exact f32 FMA chain).  Every 1024 rows the f32 accumulators are flushed
-// into f64 registers, so long chunks keep ≈1e-7 relative error; chunk
-// partials are summed in f64 by a second kernel.  Diagonal tiles also
-// accumulate the column sums.  Workgroup ids are remapped so that all tiles
-// of one row chunk run on one XCD and share its L2.
+// one GT×GT tile (ti ≤ tj, upper triangle only) of G = Σ yᵀy (y = x − shift)
+// over one chunk of rows; it streams BK-row panels of the two column blocks
+// through double-buffered LDS (coalesced row segments, shift subtracted on
+// the way in) and accumulates with v_mfma_f32_32x32x2_f32 (exact f32 FMA
+// chain).  Waves tile the output 2 (M) × GT/64 (N), each wave GT/2 × 64 =
+// (GT/64) × 2 MFMA tiles.  Chunk partials (f32, ≤ 8192 rows each ≈ 6e-8·√L
+// relative) are summed in f64 by a second kernel.  Diagonal tiles also
+// accumulate the column sums (f64).  Workgroup ids are remapped so that
+// consecutive tiles of one row chunk land on one XCD and share its L2.
+//   GT = 256 (default): 8 waves, BK = 16, 64 KiB LDS, 128 accumulators/lane.
+//   GT = 128:           4 waves, BK = 32, 64 KiB LDS,  64 accumulators/lane.
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -22,10 +24,6 @@
 
 namespace {
 
-constexpr int GT = 128;       // output tile edge
-constexpr int GBK = 32;       // rows per LDS stage
-constexpr int GTHREADS = 256; // 4 waves, 2×2 of 64×64
-constexpr int GFLUSH = 32;    // stages per f32 -> f64 flush (1024 rows)
 constexpr int MAXSEG = 32;
 
 struct SegTable {
@@ -44,30 +42,27 @@ __device__ __forceinline__ void tile_coords(int t, int nt, int& ti, int& tj) {
   tj = ti + t;
 }
 
-template <bool VEC>
-__device__ __forceinline__ f32x4 load_row4(const float* __restrict__ X, int64_t ldx, int64_t srow, int col, int p) {
-  f32x4 v = {0.f, 0.f, 0.f, 0.f};
-  const float* src = X + srow * ldx + col;
-  if (VEC && col + 3 < p) {
-    v = *reinterpret_cast<const f32x4*>(src);
-  } else {
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (col + e < p) v[e] = src[e];
-  }
-  return v;
-}
+template <int GT, int BK_>
+struct GramCfg {
+  static constexpr int BK = BK_;                        // rows per LDS stage
+  static constexpr int WN = GT / 64;                    // waves along N
+  static constexpr int THREADS = 2 * WN * 64;           // 2 × WN waves
+  static constexpr int MT = GT / 64;                    // 32-row MFMA tiles per wave (M = GT/2)
+  static constexpr int C4 = GT / 4;                     // float4 per panel row
+  static constexpr int RSTEP = THREADS / C4;            // rows per loader pass
+  static constexpr int LPP = BK / RSTEP;                // loader passes per panel
+};
 
-// ACC64: flush the f32 MFMA accumulators into f64 registers every GFLUSH
-// stages (long chunks, 1 wave/SIMD); otherwise f32 over the whole (short)
-// chunk and f32 partials (≤ 256 registers → 2 workgroups per CU).
-template <bool VEC, bool ACC64, typename PT>
-__global__ __launch_bounds__(GTHREADS, ACC64 ? 1 : 2) void k_gram(const float* __restrict__ X, int64_t ldx,
-                                                       const int64_t* __restrict__ rows, int p,
-                                                       const float* __restrict__ shift, SegTable st, int nt,
-                                                       int ntiles, int total_wg, PT* __restrict__ part,
-                                                       double* __restrict__ colpart) {
-  __shared__ __attribute__((aligned(16))) float lds[2][2][GBK][GT];  // [buf][A/B][row][col] 64 KiB
+constexpr int GATHER_MAX_CHUNK = 2048;  // rows per chunk when a row-index list is used
+
+template <int GT, int BK_, bool VEC, bool GATHER>
+__global__ __launch_bounds__(GT * 2, 2) void k_gram(
+    const float* __restrict__ X, int64_t ldx, const int64_t* __restrict__ rows, int p, const float* __restrict__ shift,
+    SegTable st, int nt, int ntiles, int total_wg, float* __restrict__ part, double* __restrict__ colpart) {
+  using Cfg = GramCfg<GT, BK_>;
+  constexpr int BK = Cfg::BK, MT = Cfg::MT, LPP = Cfg::LPP, RSTEP = Cfg::RSTEP;
+  __shared__ __attribute__((aligned(16))) float lds[2][2][BK][GT];  // [buf][A/B][row][col]
+  __shared__ int64_t ridx[GATHER ? GATHER_MAX_CHUNK : 1];           // chunk's row indices
 
   // XCD-aware bijective remap: blocks b ≡ x (mod 8) share an XCD; give each
   // XCD a contiguous range of logical ids (chunk-major, tile-minor).
@@ -85,15 +80,21 @@ __global__ __launch_bounds__(GTHREADS, ACC64 ? 1 : 2) void k_gram(const float* _
   while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
   const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
   const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
-  const int nstage = (int)((r1 - r0 + GBK - 1) / GBK);
+  const int nstage = (int)((r1 - r0 + BK - 1) / BK);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
+  if (GATHER) {
+    // stage the chunk's row indices in LDS so that X loads never wait on an
+    // index load (vmcnt is in-order: it would drain the prefetch as well)
+    for (int64_t g = r0 + tid; g < r1; g += Cfg::THREADS) ridx[g - r0] = rows[g];
+    __syncthreads();
+  }
   const int l31 = lane & 31, h = lane >> 5;
 
-  // loader mapping: 32 float4 per 128-col row segment, 8 rows per pass
-  const int c4 = tid & 31, rr = tid >> 5;
+  // loader: C4 float4 per panel row, RSTEP rows per pass, LPP passes
+  const int c4 = tid % Cfg::C4, rr = tid / Cfg::C4;
   f32x4 shA, shB;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -102,125 +103,134 @@ __global__ __launch_bounds__(GTHREADS, ACC64 ? 1 : 2) void k_gram(const float* _
     shB[e] = cb < p ? shift[cb] : 0.f;
   }
 
-  f32x4 ra[4], rb[4];
+  f32x4 ra[LPP], rb[LPP];
   double csum64[4] = {0.0, 0.0, 0.0, 0.0};
 
+  // Branch-free prefetch: addresses are clamped into valid memory and the
+  // loads are left in flight; the shift subtraction and the row / column
+  // masks are applied in sstore (after the MFMAs), so no load is waited on
+  // before the compute that should hide it.
+  const int colA = I + 4 * c4, colB = J + 4 * c4;
+  // VEC requires p % 4 == 0: a float4 is then entirely inside or outside [0, p)
+  const bool inA = colA < p, inB = colB < p;
+  const float* baseA = X + (inA ? colA : 0);
+  const float* baseB = X + (inB ? colB : 0);
   auto gload = [&](int stage) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t g = r0 + (int64_t)stage * GBK + rr + 8 * j;
-      f32x4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
-      if (g < r1) {
-        const int64_t srow = rows ? rows[g] : g;
-        va = load_row4<VEC>(X, ldx, srow, I + 4 * c4, p) - shA;
-        if (!diag) vb = load_row4<VEC>(X, ldx, srow, J + 4 * c4, p) - shB;
-        // padded columns must stay exactly zero
+    for (int j = 0; j < LPP; ++j) {
+      int64_t g = r0 + (int64_t)stage * BK + rr + RSTEP * j;
+      g = g < r1 ? g : r1 - 1;
+      const int64_t srow = GATHER ? ridx[g - r0] : g;
+      // B is loaded unconditionally (a diagonal tile re-reads A's line from
+      // L1): a conditional load would force register moves that wait on it
+      if (VEC) {
+        ra[j] = *reinterpret_cast<const f32x4*>(baseA + srow * ldx);
+        rb[j] = *reinterpret_cast<const f32x4*>(baseB + srow * ldx);
+      } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          if (I + 4 * c4 + e >= p) va[e] = 0.f;
-          if (J + 4 * c4 + e >= p) vb[e] = 0.f;
+          ra[j][e] = X[srow * ldx + min(colA + e, p - 1)];
+          rb[j][e] = X[srow * ldx + min(colB + e, p - 1)];
         }
       }
-      ra[j] = va;
-      rb[j] = vb;
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int stage, int buf) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      *reinterpret_cast<f32x4*>(&lds[buf][0][rr + 8 * j][4 * c4]) = ra[j];
-      if (!diag) *reinterpret_cast<f32x4*>(&lds[buf][1][rr + 8 * j][4 * c4]) = rb[j];
+    for (int j = 0; j < LPP; ++j) {
+      const int64_t g = r0 + (int64_t)stage * BK + rr + RSTEP * j;
+      const bool rv = g < r1;
+      f32x4 va, vb;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        va[e] = (rv && colA + e < p) ? ra[j][e] - shA[e] : 0.f;
+        vb[e] = (rv && colB + e < p) ? rb[j][e] - shB[e] : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(&lds[buf][0][rr + RSTEP * j][4 * c4]) = va;
+      if (!diag) *reinterpret_cast<f32x4*>(&lds[buf][1][rr + RSTEP * j][4 * c4]) = vb;
       if (diag) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) csum64[e] += (double)ra[j][e];
+        for (int e = 0; e < 4; ++e) csum64[e] += (double)va[e];
       }
     }
   };
+  (void)inB;
 
-  f32x16 acc[2][2];
-  double acc64[2][2][ACC64 ? 16 : 1];
+  f32x16 acc[MT][2];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < MT; ++a)
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
-#pragma unroll
-      for (int r = 0; r < (ACC64 ? 16 : 1); ++r) acc64[a][c][r] = 0.0;
-    }
 
   if (nstage > 0) {
     gload(0);
-    sstore(0);
+    sstore(0, 0);
   }
   __syncthreads();
   const int bsel = diag ? 0 : 1;
+  // In a diagonal tile, waves whose whole sub-block lies strictly below the
+  // diagonal (row start ≥ col end) only help stage data: G is symmetric and
+  // the reduce kernel mirrors the upper half.
+  const bool idle = diag && (wm * (GT / 2) >= (wn + 1) * 64);
   int cur = 0;
   for (int stg = 0; stg < nstage; ++stg) {
     if (stg + 1 < nstage) gload(stg + 1);
     const float* As = &lds[cur][0][0][0];
     const float* Bs = &lds[cur][bsel][0][0];
 #pragma unroll
-    for (int kk = 0; kk < GBK / 2; ++kk) {
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      if (idle) break;
       const int krow = (2 * kk + h) * GT;
-      const float a0 = As[krow + wm * 64 + l31];
-      const float a1 = As[krow + wm * 64 + 32 + l31];
-      const float b0 = Bs[krow + wn * 64 + l31];
-      const float b1 = Bs[krow + wn * 64 + 32 + l31];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      float av[MT], bv[2];
+#pragma unroll
+      for (int a = 0; a < MT; ++a) av[a] = As[krow + wm * (GT / 2) + a * 32 + l31];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) bv[c] = Bs[krow + wn * 64 + c * 32 + l31];
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[c], acc[a][c], 0, 0, 0);
     }
-    if (stg + 1 < nstage) sstore(cur ^ 1);
+    if (stg + 1 < nstage) sstore(stg + 1, cur ^ 1);
     __syncthreads();
     cur ^= 1;
-    if (ACC64 && ((stg + 1) % GFLUSH == 0 || stg + 1 == nstage)) {
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            acc64[a][c][ACC64 ? r : 0] += (double)acc[a][c][r];
-            acc[a][c][r] = 0.f;
-          }
-    }
   }
 
-  // partial tile out: [chunk][tile][GT][GT]
-  PT* out = part + ((size_t)chunk * ntiles + tile) * (GT * GT);
+  // partial tile out: [chunk][tile][GT][GT] float
+  float* out = part + ((size_t)chunk * ntiles + tile) * (GT * GT);
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < MT; ++a)
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int row = wm * (GT / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int col = wn * 64 + c * 32 + l31;
-        out[row * GT + col] = ACC64 ? (PT)acc64[a][c][ACC64 ? r : 0] : (PT)acc[a][c][r];
+        out[row * GT + col] = acc[a][c][r];
       }
 
   if (diag) {
-    // reduce the 8 row groups of each column through LDS (reuse stage buffer)
+    // reduce the RSTEP row groups of each column through LDS (reuse stage buffer)
     __syncthreads();
-    double* red = reinterpret_cast<double*>(&lds[0][0][0][0]);  // [8][128]
+    double* red = reinterpret_cast<double*>(&lds[0][0][0][0]);  // [RSTEP][GT]
 #pragma unroll
     for (int e = 0; e < 4; ++e) red[rr * GT + 4 * c4 + e] = csum64[e];
     __syncthreads();
-    if (tid < GT) {
+    for (int c = tid; c < GT; c += Cfg::THREADS) {
       double v = 0.0;
 #pragma unroll
-      for (int g = 0; g < 8; ++g) v += red[g * GT + tid];
-      colpart[((size_t)chunk * nt + ti) * GT + tid] = v;
+      for (int g = 0; g < RSTEP; ++g) v += red[g * GT + c];
+      colpart[((size_t)chunk * nt + ti) * GT + c] = v;
     }
   }
 }
 
 // Sum chunk partials of one segment into G (full symmetric) and colsum.
-template <typename PT>
-__global__ void k_gram_reduce(const PT* __restrict__ part, const double* __restrict__ colpart, int nt,
-                              int ntiles, int p, int c0, int c1, double* __restrict__ G, double* __restrict__ colsum) {
+template <int GT>
+__global__ void k_gram_reduce(const float* __restrict__ part, const double* __restrict__ colpart, int nt, int ntiles,
+                              int p, int c0, int c1, double* __restrict__ G, double* __restrict__ colsum) {
   const int tile = blockIdx.y;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;  // element in tile
   int ti, tj;
@@ -228,11 +238,13 @@ __global__ void k_gram_reduce(const PT* __restrict__ part, const double* __restr
   if (e < GT * GT) {
     const int i = e / GT, j = e % GT;
     const int gi = ti * GT + i, gj = tj * GT + j;
-    double v = 0.0;
-    for (int c = c0; c < c1; ++c) v += (double)part[((size_t)c * ntiles + tile) * (GT * GT) + e];
-    if (gi < p && gj < p) {
+    // diagonal tiles: only the upper triangle is valid (k_gram skips the
+    // strictly-lower wave blocks); mirror it
+    if (gi < p && gj < p && !(ti == tj && i > j)) {
+      double v = 0.0;
+      for (int c = c0; c < c1; ++c) v += (double)part[((size_t)c * ntiles + tile) * (GT * GT) + e];
       G[(size_t)gi * p + gj] = v;
-      if (ti != tj) G[(size_t)gj * p + gi] = v;
+      if (gi != gj) G[(size_t)gj * p + gi] = v;
     }
   }
   if (ti == tj && e < GT) {
@@ -296,6 +308,77 @@ __global__ void k_cov(CovTerms tm, const double* __restrict__ dvec, int p, doubl
   C[e] = (g - n * dvec[i] * dvec[j]) / (n - 1.0);
 }
 
+template <int GT, int BK>
+int gram_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+              const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
+              hipStream_t st, int64_t chunk_rows) {
+  using Cfg = GramCfg<GT, BK>;
+  const int nt = (p + GT - 1) / GT;
+  const int ntiles = nt * (nt + 1) / 2;
+  const bool vec = (ldx % 4 == 0) && (p % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+  if (rows) chunk_rows = std::min<int64_t>(chunk_rows, GATHER_MAX_CHUNK);
+  chunk_rows = (int64_t)ocm::align_up((size_t)chunk_rows, Cfg::BK);
+
+  // total chunks over all segments (an empty segment owns 0 chunks)
+  std::vector<int32_t> cprefix(nseg + 1, 0);
+  for (int s = 0; s < nseg; ++s) {
+    const int64_t len = seg_offsets[s + 1] - seg_offsets[s];
+    cprefix[s + 1] = cprefix[s] + (int32_t)((len + chunk_rows - 1) / chunk_rows);
+  }
+  const int64_t nchunks = cprefix[nseg];
+  const size_t part_elems = (size_t)nchunks * ntiles * GT * GT;
+  const size_t col_elems = (size_t)nchunks * nt * GT;
+  void* wsp = ocm::workspace(ctx, part_elems * sizeof(float) + col_elems * sizeof(double) + 4096, st);
+  if (!wsp) return OCM_ERR_NOMEM;
+  ocm::Carve cv{static_cast<char*>(wsp)};
+  float* part = cv.take<float>(part_elems);
+  double* colpart = cv.take<double>(col_elems);
+
+  // launch in groups of ≤ MAXSEG segments; chunk ids are global
+  for (int s0 = 0; s0 < nseg; s0 += MAXSEG) {
+    const int s1 = std::min(nseg, s0 + MAXSEG);
+    SegTable tab{};
+    tab.nseg = s1 - s0;
+    tab.chunk_rows = (int32_t)chunk_rows;
+    for (int s = s0; s <= s1; ++s) {
+      tab.begin[s - s0] = seg_offsets[s];
+      tab.cprefix[s - s0] = cprefix[s] - cprefix[s0];
+    }
+    const int64_t gchunks = cprefix[s1] - cprefix[s0];
+    if (gchunks == 0) continue;
+    const int64_t total = gchunks * ntiles;
+    OCM_REQUIRE(total < (1LL << 31), "ocm_gram_f32: too many workgroups");
+    float* pg = part + (size_t)cprefix[s0] * ntiles * GT * GT;
+    double* col_g = colpart + (size_t)cprefix[s0] * nt * GT;
+    ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
+    dim3 grid((unsigned)total), blk(Cfg::THREADS);
+#define OCM_GRAM_LAUNCH(V_, G_)                                                                                    \
+  hipLaunchKernelGGL((k_gram<GT, BK, V_, G_>), grid, blk, 0, st, X, ldx, rows, p, shift, tab, nt, ntiles, (int)total, \
+                     pg, col_g)
+    if (rows) {
+      if (vec) OCM_GRAM_LAUNCH(true, true); else OCM_GRAM_LAUNCH(false, true);
+    } else {
+      if (vec) OCM_GRAM_LAUNCH(true, false); else OCM_GRAM_LAUNCH(false, false);
+    }
+#undef OCM_GRAM_LAUNCH
+    OCM_CHECK_LAUNCH("k_gram");
+  }
+  for (int s = 0; s < nseg; ++s) {
+    double* Gs = G_out + (size_t)s * p * p;
+    double* cs = colsum_out + (size_t)s * p;
+    if (cprefix[s + 1] == cprefix[s]) {
+      OCM_HIP(hipMemsetAsync(Gs, 0, (size_t)p * p * sizeof(double), st));
+      OCM_HIP(hipMemsetAsync(cs, 0, (size_t)p * sizeof(double), st));
+      continue;
+    }
+    dim3 g((GT * GT + 255) / 256, ntiles);
+    hipLaunchKernelGGL(k_gram_reduce<GT>, g, dim3(256), 0, st, part, colpart, nt, ntiles, p, cprefix[s],
+                       cprefix[s + 1], Gs, cs);
+    OCM_CHECK_LAUNCH("k_gram_reduce");
+  }
+  return OCM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -328,100 +411,22 @@ int ocm_gram_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows,
   for (int s = 0; s < nseg; ++s)
     OCM_REQUIRE(seg_offsets[s + 1] >= seg_offsets[s], "ocm_gram_f32: seg_offsets not ascending");
   hipStream_t st = (hipStream_t)stream;
-  const int nt = (p + GT - 1) / GT;
-  const int ntiles = nt * (nt + 1) / 2;
-  const bool vec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
-
-  // Variant: "acc64" (f64 flush, long chunks) or "f32" (short chunks, f32
-  // partials, 2 WG/CU).  OCM_GRAM_VARIANT / OCM_GRAM_CHUNK override (A/B).
-  bool acc64 = false;
-  int64_t chunk_rows = 0;
-  if (const char* e = std::getenv("OCM_GRAM_VARIANT")) acc64 = std::string(e) == "acc64";
-  if (const char* e = std::getenv("OCM_GRAM_CHUNK")) chunk_rows = std::atoll(e);
-  if (chunk_rows <= 0) {
-    if (acc64) {
-      // enough workgroups to fill 256 CUs several times, ≥ 2048 rows
-      const int64_t target_wg = (int64_t)ctx->num_cus * 8;
-      const int64_t want_chunks = std::max<int64_t>(1, target_wg / ntiles);
-      chunk_rows = std::max<int64_t>(2048, (n + want_chunks - 1) / want_chunks);
-    } else {
-      chunk_rows = 8192;  // f32 accumulation length (≈ 6e-8·√8192 relative per partial)
-    }
-  }
-  chunk_rows = (int64_t)ocm::align_up((size_t)chunk_rows, GBK);
-  if (chunk_rows > (1 << 30)) chunk_rows = 1 << 30;
-
-  // total chunks over all segments (an empty segment owns 0 chunks)
-  std::vector<int32_t> cprefix(nseg + 1, 0);
-  for (int s = 0; s < nseg; ++s) {
-    const int64_t len = seg_offsets[s + 1] - seg_offsets[s];
-    cprefix[s + 1] = cprefix[s] + (int32_t)((len + chunk_rows - 1) / chunk_rows);
-  }
-  const int64_t nchunks = cprefix[nseg];
-  const size_t part_elems = (size_t)nchunks * ntiles * GT * GT;
-  const size_t col_elems = (size_t)nchunks * nt * GT;
-  const size_t pbytes = acc64 ? sizeof(double) : sizeof(float);
-  void* wsp = ocm::workspace(ctx, part_elems * pbytes + col_elems * sizeof(double) + 4096, st);
-  if (!wsp) return OCM_ERR_NOMEM;
-  ocm::Carve cv{static_cast<char*>(wsp)};
-  void* part = acc64 ? (void*)cv.take<double>(part_elems) : (void*)cv.take<float>(part_elems);
-  double* colpart = cv.take<double>(col_elems);
-
-  // launch in groups of ≤ MAXSEG segments; chunk ids are global
-  for (int s0 = 0; s0 < nseg; s0 += MAXSEG) {
-    const int s1 = std::min(nseg, s0 + MAXSEG);
-    SegTable tab{};
-    tab.nseg = s1 - s0;
-    tab.chunk_rows = (int32_t)chunk_rows;
-    for (int s = s0; s <= s1; ++s) {
-      tab.begin[s - s0] = seg_offsets[s];
-      tab.cprefix[s - s0] = cprefix[s] - cprefix[s0];
-    }
-    const int64_t gchunks = cprefix[s1] - cprefix[s0];
-    if (gchunks == 0) continue;
-    const int64_t total = gchunks * ntiles;
-    OCM_REQUIRE(total < (1LL << 31), "ocm_gram_f32: too many workgroups");
-    const size_t poff = (size_t)cprefix[s0] * ntiles * GT * GT;
-    double* col_g = colpart + (size_t)cprefix[s0] * nt * GT;
-    ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
-    dim3 grid((unsigned)total), blk(GTHREADS);
-    if (acc64) {
-      double* pg = static_cast<double*>(part) + poff;
-      if (vec)
-        hipLaunchKernelGGL((k_gram<true, true, double>), grid, blk, 0, st, X, ldx, rows, p, shift, tab, nt, ntiles,
-                           (int)total, pg, col_g);
-      else
-        hipLaunchKernelGGL((k_gram<false, true, double>), grid, blk, 0, st, X, ldx, rows, p, shift, tab, nt, ntiles,
-                           (int)total, pg, col_g);
-    } else {
-      float* pg = static_cast<float*>(part) + poff;
-      if (vec)
-        hipLaunchKernelGGL((k_gram<true, false, float>), grid, blk, 0, st, X, ldx, rows, p, shift, tab, nt, ntiles,
-                           (int)total, pg, col_g);
-      else
-        hipLaunchKernelGGL((k_gram<false, false, float>), grid, blk, 0, st, X, ldx, rows, p, shift, tab, nt, ntiles,
-                           (int)total, pg, col_g);
-    }
-    OCM_CHECK_LAUNCH("k_gram");
-  }
-  for (int s = 0; s < nseg; ++s) {
-    double* Gs = G_out + (size_t)s * p * p;
-    double* cs = colsum_out + (size_t)s * p;
-    if (cprefix[s + 1] == cprefix[s]) {
-      OCM_HIP(hipMemsetAsync(Gs, 0, (size_t)p * p * sizeof(double), st));
-      OCM_HIP(hipMemsetAsync(cs, 0, (size_t)p * sizeof(double), st));
-      continue;
-    }
-    dim3 g((GT * GT + 255) / 256, ntiles);
-    if (acc64)
-      hipLaunchKernelGGL(k_gram_reduce<double>, g, dim3(256), 0, st, static_cast<const double*>(part), colpart, nt,
-                         ntiles, p, cprefix[s], cprefix[s + 1], Gs, cs);
-    else
-      hipLaunchKernelGGL(k_gram_reduce<float>, g, dim3(256), 0, st, static_cast<const float*>(part), colpart, nt,
-                         ntiles, p, cprefix[s], cprefix[s + 1], Gs, cs);
-    OCM_CHECK_LAUNCH("k_gram_reduce");
-  }
-  return OCM_OK;
+  // Tile: 256 when p fills at least one 256 block, else 128 (less padding).
+  // OCM_GRAM_TILE / OCM_GRAM_CHUNK override for A/B runs.
+  int tile = p > 128 ? 256 : 128;
+  int bk = 32;
+  // f32 accumulation length per partial: short chunks keep the tiles of one
+  // chunk co-resident on an XCD (L2 reuse) and the tail short; the partial
+  // buffer is capped at 512 chunks (≈4.7 GB for p = 2048).
+  int64_t chunk_rows = std::max<int64_t>(2048, (n + 511) / 512);
+  if (const char* e = std::getenv("OCM_GRAM_TILE")) tile = std::atoi(e) == 128 ? 128 : 256;
+  if (const char* e = std::getenv("OCM_GRAM_BK")) bk = std::atoi(e) == 16 ? 16 : 32;
+  if (const char* e = std::getenv("OCM_GRAM_CHUNK")) chunk_rows = std::max<int64_t>(64, std::atoll(e));
+  if (tile == 256 && bk == 32)
+    return gram_impl<256, 32>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows);
+  if (tile == 256)
+    return gram_impl<256, 16>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows);
+  return gram_impl<128, 32>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows);
 }
 
 int ocm_cov_from_gram(ocm_ctx* ctx, const double* const* G_list, const double* const* colsum_list,

@@ -66,76 +66,55 @@ __global__ __launch_bounds__(256) void k_score(const float* __restrict__ X, int6
   // loaders: D chunk — lane → (row = 4j + lane/16, col4 = (lane%16)*4), j < 8
   const int dcol = (lane & 15) * 4, drow = lane >> 4;
   int64_t srow[8];
-  bool rvalid[8];
+  unsigned rmask = 0;  // bit j: row j of this lane's loader set is real
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int64_t g = row0 + 4 * j + drow;
-    rvalid[j] = g < m;
-    srow[j] = rvalid[j] ? (rows ? rows[g] : g) : 0;
+    const bool ok = g < m;
+    rmask |= ok ? (1u << j) : 0u;
+    const int64_t gc = ok ? g : m - 1;  // clamp: always a valid address
+    srow[j] = rows ? rows[gc] : gc;
   }
   // P chunk — thread → (comp = e/16, col4 = (e%16)*4), e = tid + 256·i
   constexpr int PV = KP * SC / 4 / 256;  // float4 per thread (2 or 4)
 
-  f32x4 rd[8], rp[PV];
+  // Branch-free prefetch (clamped addresses, loads left in flight); the mean
+  // subtraction and the row / column / component masks are applied in
+  // sstore, after the MFMAs that hide the loads.
+  f32x4 rd[8], rp[PV], rmu;
+  auto ld4 = [&](const float* base, int col) -> f32x4 {
+    if (VEC) return *reinterpret_cast<const f32x4*>(base + (col < p ? col : 0));
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = base[min(col + e, p - 1)];
+    return v;
+  };
   auto gload = [&](int c0) {
-    f32x4 mu4 = {0.f, 0.f, 0.f, 0.f};
+    rmu = ld4(mu, c0 + dcol);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) mu4[e] = (c0 + dcol + e < p) ? mu[c0 + dcol + e] : 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (rvalid[j]) {
-        const float* src = X + srow[j] * ldx + c0 + dcol;
-        if (VEC && c0 + dcol + 3 < p) {
-          v = *reinterpret_cast<const f32x4*>(src);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (c0 + dcol + e < p) v[e] = src[e];
-        }
-        v -= mu4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (c0 + dcol + e >= p) v[e] = 0.f;
-      }
-      rd[j] = v;
-    }
+    for (int j = 0; j < 8; ++j) rd[j] = ld4(X + srow[j] * ldx, c0 + dcol);
 #pragma unroll
     for (int i = 0; i < PV; ++i) {
       const int e = tid + 256 * i;
       const int comp = e >> 4, col = (e & 15) * 4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (comp < k) {
-        const float* src = P + (int64_t)comp * p + c0 + col;
-        if (VEC && c0 + col + 3 < p) {
-          v = *reinterpret_cast<const f32x4*>(src);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (c0 + col + q < p) v[q] = src[q];
-        }
-      }
-      rp[i] = v;
+      rp[i] = ld4(P + (int64_t)min(comp, k - 1) * p, c0 + col);
     }
   };
-  auto sstore = [&]() {
+  auto sstore = [&](int c0) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float* d = Dw + (4 * j + drow) * (SC + 1) + dcol;
-      d[0] = rd[j][0];
-      d[1] = rd[j][1];
-      d[2] = rd[j][2];
-      d[3] = rd[j][3];
+      const bool rv = (rmask >> j) & 1u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] = (rv && c0 + dcol + e < p) ? rd[j][e] - rmu[e] : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < PV; ++i) {
       const int e = tid + 256 * i;
       const int comp = e >> 4, col = (e & 15) * 4;
       float* d = Ps + comp * (SC + 1) + col;
-      d[0] = rp[i][0];
-      d[1] = rp[i][1];
-      d[2] = rp[i][2];
-      d[3] = rp[i][3];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q] = (comp < k && c0 + col + q < p) ? rp[i][q] : 0.f;
     }
   };
 
@@ -154,7 +133,7 @@ __global__ __launch_bounds__(256) void k_score(const float* __restrict__ X, int6
   gload(0);
   for (int c = 0; c < nchunk; ++c) {
     __syncthreads();  // previous chunk's LDS reads are done
-    sstore();
+    sstore(c * SC);
     __syncthreads();
     if (c + 1 < nchunk) gload((c + 1) * SC);
 #pragma unroll
@@ -186,7 +165,7 @@ __global__ __launch_bounds__(256) void k_score(const float* __restrict__ X, int6
   gload(0);
   for (int c = 0; c < nchunk; ++c) {
     __syncthreads();
-    sstore();
+    sstore(c * SC);
     __syncthreads();
     if (c + 1 < nchunk) gload((c + 1) * SC);
     float qc = 0.f;

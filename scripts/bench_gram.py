@@ -17,7 +17,7 @@ def main():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--p", type=int, default=2048)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="acc64:0,f32:8192,f32:4096,f32:16384")
+    ap.add_argument("--variants", default="256x32:2048,256x32:1024,256x32:4096,128x32:2048")
     args = ap.parse_args()
     import torch
 
@@ -35,7 +35,7 @@ def main():
     flop = args.rows * args.p * (args.p + 1)
     for r in range(args.rounds):
         for name, chunk in variants:
-            os.environ["OCM_GRAM_VARIANT"] = name
+            os.environ["OCM_GRAM_TILE"], os.environ["OCM_GRAM_BK"] = name.split("x")
             os.environ["OCM_GRAM_CHUNK"] = chunk
             engine.gram(X, None, [0, args.rows], shift)  # warm (workspace)
             torch.cuda.synchronize()
