@@ -124,16 +124,19 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
  * VAE_SIMCA.py:247-248, utils/final_vaesimca.py:430-434).  [dev] in/out. */
 int ocm_sym_pinv_f64(ocm_ctx* ctx, const double* A, int32_t d, double rcond, double* out, void* stream);
 
-/* Fused scoring on FP32 MFMA (utils/SIMCA.py:65-71 fit, 104-107 transform,
- * 127-130 predict):  y = x - mu; t = P·y (k); r = y - Pᵀt; Q = Σ r²;
- * T2 = tᵀ·A·t.  P [dev] k×p float32 row-major (ldp = p), mu [dev] p floats,
- * A [dev] k×k doubles.  Outputs (all nullable, [dev]): T_out m×k float32,
+/* Fused scoring of float32 spectra (utils/SIMCA.py:65-71 fit, 104-107
+ * transform, 127-130 predict):  y = x - mu; t = P·y (k); Q = ‖y − Pᵀt‖²;
+ * T2 = tᵀ·A·t.  Default kernel: FP32 MFMA projection + explicit residual
+ * (two register-streamed sweeps); alternative FP64-MFMA single pass with
+ * Q = ‖y‖² − ‖t‖².  P [dev] k×p float64 row-major with orthonormal rows
+ * (ldp = p), mu [dev] p doubles, A [dev] k×k doubles.
+ * Outputs (all nullable, [dev]): T_out m×k float32,
  * T2_out m doubles, Q_out m floats.  If dec != NULL [host] the decision is
  * fused: accept_out[r·accept_stride] = 1.0/0.0 (float64, the reference's
  * predictions[:, i] column).  stats_out [dev, nullable] 4 doubles
  * = {ΣT2, ΣT2², ΣQ, ΣQ²} (chi2pom moments).  k ≤ 64. */
 int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
-                  const float* P, const float* mu, const double* A, int32_t k, float* T_out, double* T2_out,
+                  const double* P, const double* mu, const double* A, int32_t k, float* T_out, double* T2_out,
                   float* Q_out, const ocm_decision* dec, double* accept_out, int64_t accept_stride,
                   double* stats_out, void* stream);
 

@@ -5,17 +5,22 @@
 // (predict + decision), sklearn/decomposition/_base.py:147-153,197
 // (transform / inverse_transform), vae_model.py:164.
 //
-// Layout: a wave owns 32 spectra; a workgroup (4 waves) 128 spectra.  The
-// row tile streams through LDS in 64-wavelength chunks (coalesced 256-B row
-// segments, mean subtracted on the way in) next to the matching 64-column
-// slice of the loadings P.  Two sweeps over the chunks:
+// Three kernels share one epilogue (T², Q, fused decision, moments):
+//   k_score_direct (default)  f32 MFMA, each wave streams its 32 rows from
+//       HBM straight into operand registers; loadings/mean in LDS blocks.
+//   k_score                   f32 MFMA, row tiles staged through LDS.
+//   k_score_f64               one pass, f64 MFMA, Q = ‖d‖² − ‖t‖².
+// The f32 kernels run two sweeps over the row's columns:
 //   sweep 1  Tᵀ (comps × rows) += P_chunk · D_chunkᵀ        v_mfma_f32_32x32x2_f32
 //   sweep 2  Rᵀ (cols × rows)   = P_chunkᵀ · Tᵀ → r = d − R, q += r²
 // Sweep 2 feeds the sweep-1 accumulator registers straight back as the B
 // operand (its column is already on the lane), so T never leaves registers.
 // Q is the explicit residual (first-order insensitive to error in t, unlike
-// the ‖d‖² − ‖t‖² identity).  T is flushed to f64 every chunk.  The second
-// sweep re-reads the tile, served from L2/Infinity Cache.
+// the ‖d‖² − ‖t‖² identity, which f32 accumulation cannot afford).  T is
+// flushed to f64 every chunk.
+#include <cstdlib>
+#include <string>
+
 #include "ocm_internal.h"
 
 namespace {
@@ -36,6 +41,74 @@ __device__ __forceinline__ double dred_of(int type, double t, double q) {
     case OCM_TYPE_SIM: return fmax(t, q);
     case OCM_TYPE_ALT: return sqrt(t * t + q * q);
     default: return t + q;  // ci, dd
+  }
+}
+
+// Shared epilogue: T rows gathered through LDS (f64), T² = tᵀ A t, Q, fused
+// decision, per-workgroup moment partials.  accT64 holds Tᵀ in the 32×32 MFMA
+// accumulator layout: comp = 32t + (r&3) + 8(r>>2) + 4h, row = lane & 31.
+template <int KT, int NW>
+__device__ __forceinline__ void score_epilogue(double* tls, double* sred, const double (&accT64)[KT][16], double q64,
+                                               int64_t row0, int64_t m, int k, int a_diag,
+                                               const double* __restrict__ A, float* __restrict__ T_out,
+                                               double* __restrict__ T2_out, float* __restrict__ Q_out, DecArgs dec,
+                                               double* __restrict__ acc_out, int64_t acc_stride,
+                                               double* __restrict__ stat_part) {
+  constexpr int KP = KT * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  __syncthreads();
+  double* Tt = tls + wave * 32 * (KP + 1);
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int comp = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      Tt[l31 * (KP + 1) + comp] = accT64[t][r];
+    }
+  __syncthreads();
+  const int64_t grow = row0 + l31;
+  const bool own = (h == 0) && (grow < m);
+  double T2 = 0.0, Q = q64;
+  if (own) {
+    const double* trow = Tt + l31 * (KP + 1);
+    if (a_diag) {
+      for (int a = 0; a < k; ++a) T2 += trow[a] * trow[a] * A[a * k + a];
+    } else {
+      for (int a = 0; a < k; ++a) {
+        double s = 0.0;
+        for (int b = 0; b < k; ++b) s += A[a * k + b] * trow[b];
+        T2 += trow[a] * s;
+      }
+    }
+    if (T_out)
+      for (int a = 0; a < k; ++a) T_out[grow * k + a] = (float)trow[a];
+    if (T2_out) T2_out[grow] = T2;
+    if (Q_out) Q_out[grow] = (float)Q;
+    if (dec.enabled) {
+      const double dr = dred_of(dec.type, T2 * dec.t2_scale, (double)(float)Q * dec.q_scale);
+      acc_out[grow * acc_stride] = dr < dec.dlim ? 1.0 : 0.0;
+    }
+  }
+  if (stat_part) {
+    const double qf = (double)(float)Q;
+    double s0 = own ? T2 : 0.0, s1 = own ? T2 * T2 : 0.0, s2 = own ? qf : 0.0, s3 = own ? qf * qf : 0.0;
+    s0 = wave_sum_f64(s0);
+    s1 = wave_sum_f64(s1);
+    s2 = wave_sum_f64(s2);
+    s3 = wave_sum_f64(s3);
+    if (lane == 0) {
+      sred[wave * 4 + 0] = s0;
+      sred[wave * 4 + 1] = s1;
+      sred[wave * 4 + 2] = s2;
+      sred[wave * 4 + 3] = s3;
+    }
+    __syncthreads();
+    if (tid < 4) {
+      double v = 0.0;
+      for (int w = 0; w < NW; ++w) v += sred[w * 4 + tid];
+      stat_part[(int64_t)blockIdx.x * 4 + tid] = v;
+    }
   }
 }
 
@@ -193,57 +266,342 @@ __global__ __launch_bounds__(256) void k_score(const float* __restrict__ X, int6
   }
   q64 += __shfl_xor(q64, 32, 64);
 
-  // ---- epilogue: gather T rows through LDS (f64), T², decision, stats ------
-  __syncthreads();
-  double* Tt = reinterpret_cast<double*>(smem) + wave * SR * (KP + 1);
+  score_epilogue<KT, SW>(reinterpret_cast<double*>(smem), &sred[0][0], accT64, q64, row0, m, k, a_diag, A, T_out,
+                         T2_out, Q_out, dec, acc_out, acc_stride, stat_part);
+}
+
+// ---------------------------------------------------------------------------
+// k_score_direct — the default scoring kernel.  Every wave streams its own
+// 32 rows from HBM straight into MFMA operand registers (double-buffered,
+// two named register sets, loop unrolled by 2); the loadings and the mean
+// are staged per workgroup in LDS in 256-column blocks (one barrier pair per
+// block, i.e. per 8 MFMA chunks), so waves never wait on each other inside a
+// block.  The K order is permuted so that lane (row = lane&31, half h) reads
+// contiguous 16-B pieces of its row: in a 32-column chunk, MFMA step 4i+e
+// uses column 8i + 4h + e (i, e < 4) for the data (B) and loadings (A) alike.
+// ---------------------------------------------------------------------------
+constexpr int PB = 256;  // columns per LDS loadings block
+
+template <int KT, bool VEC>
+__global__ __launch_bounds__(256, 2) void k_score_direct(const float* __restrict__ X, int64_t ldx,
+                                                         const int64_t* __restrict__ rows, int64_t m, int p,
+                                                         const float* __restrict__ P, const float* __restrict__ mu,
+                                                         const double* __restrict__ A, int k, int a_diag,
+                                                         float* __restrict__ T_out, double* __restrict__ T2_out,
+                                                         float* __restrict__ Q_out, DecArgs dec,
+                                                         double* __restrict__ acc_out, int64_t acc_stride,
+                                                         double* __restrict__ stat_part) {
+  constexpr int KP = KT * 32;
+  constexpr int PS = PB + 4;  // padded LDS row: conflict-free ds_read_b128 across comps
+  constexpr int MAIN_F = KP * PS + PB;
+  constexpr int EPI_F = SW * SR * (KP + 1) * 2;
+  __shared__ __attribute__((aligned(16))) float smem[MAIN_F > EPI_F ? MAIN_F : EPI_F];
+  __shared__ double sred[SW * 4];
+  float* Pl = smem;             // [KP][PS]
+  float* Ml = smem + KP * PS;   // [PB]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  const int64_t row0 = (int64_t)blockIdx.x * SROWS + wave * SR;
+  const int64_t grow = row0 + l31;
+  const float rowmask = grow < m ? 1.f : 0.f;
+  const int64_t gcl = grow < m ? grow : m - 1;
+  const float* xrow = X + (rows ? rows[gcl] : gcl) * ldx;
+
+  auto ld4 = [&](const float* base, int col) -> f32x4 {
+    if (VEC) return *reinterpret_cast<const f32x4*>(base + (col < p ? col : 0));
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = base[min(col + e, p - 1)];
+    return v;
+  };
+  // stage loadings / mean columns [b0, b0+PB) into LDS (zero outside k, p)
+  auto stage = [&](int b0) {
+    __syncthreads();  // previous block fully consumed
+    for (int e = tid; e < KP * (PB / 4); e += 256) {
+      const int comp = e / (PB / 4), c4 = (e % (PB / 4)) * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (comp < k) v = ld4(P + (int64_t)comp * p, b0 + c4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (b0 + c4 + q >= p) v[q] = 0.f;
+      *reinterpret_cast<f32x4*>(&Pl[comp * PS + c4]) = v;
+    }
+    for (int c = tid; c < PB; c += 256) Ml[c] = b0 + c < p ? mu[b0 + c] : 0.f;
+    __syncthreads();
+  };
+
+  f32x16 accT[KT];
+  double accT64[KT][16];
 #pragma unroll
   for (int t = 0; t < KT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int comp = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      Tt[l31 * (KP + 1) + comp] = accT64[t][r];
+      accT[t][r] = 0.f;
+      accT64[t][r] = 0.0;
     }
+
+  // ---- sweep 1: Tᵀ = P · Dᵀ, 32-column chunks ---------------------------------
+  // data set for one chunk: d[i] = x[8i + 4h .. +3]
+  struct S1 {
+    f32x4 d[4];
+  };
+  auto load1 = [&](S1& S, int c0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) S.d[i] = ld4(xrow, c0 + 8 * i + 4 * h);
+  };
+  auto comp1 = [&](const S1& S, int c0, int b0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int lc = c0 - b0 + 8 * i + 4 * h;  // column within the LDS block
+      const f32x4 u = *reinterpret_cast<const f32x4*>(&Ml[lc]);
+      f32x4 w[KT];
+#pragma unroll
+      for (int t = 0; t < KT; ++t) w[t] = *reinterpret_cast<const f32x4*>(&Pl[(t * 32 + l31) * PS + lc]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // padded columns have u = 0 and w = 0, so only the row mask is needed
+        const float b = (S.d[i][e] - u[e]) * rowmask;
+#pragma unroll
+        for (int t = 0; t < KT; ++t) accT[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[t][e], b, accT[t], 0, 0, 0);
+      }
+    }
+  };
+  for (int b0 = 0; b0 < p; b0 += PB) {
+    stage(b0);
+    const int bend = min(b0 + PB, p);
+    S1 SA, SB;
+    load1(SA, b0);
+    for (int c0 = b0; c0 < bend; c0 += 64) {
+      load1(SB, c0 + 32);
+      comp1(SA, c0, b0);
+      if (c0 + 64 < bend) load1(SA, c0 + 64);
+      if (c0 + 32 < bend) comp1(SB, c0 + 32, b0);
+    }
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        accT64[t][r] += (double)accT[t][r];
+        accT[t][r] = 0.f;
+      }
+  }
+
+  // T back to f32 as the sweep-2 B operand
+  f32x16 accTf[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accTf[t][r] = (float)accT64[t][r];
+
+  // ---- sweep 2: Rᵀ = Pᵀ · Tᵀ per 32-column chunk, Q = Σ (d − R)² -------------
+  // step r consumes comps κ_r + 4h (κ_r = (r&3) + 8(r>>2)); for k ≤ 24 the
+  // trailing steps hold only zero loadings and are skipped.
+  const int nsteps = KT == 1 ? (k > 24 ? 16 : (k > 16 ? 12 : (k > 8 ? 8 : 4))) : 16;
+  double q64 = 0.0;
+  auto comp2 = [&](const S1& S, int c0, int b0) {
+    f32x16 accR;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accR[r] = 0.f;
+    const int lcol = c0 - b0 + l31;
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (KT == 1 && r >= nsteps) break;
+        const int comp = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        accR = __builtin_amdgcn_mfma_f32_32x32x2f32(Pl[comp * PS + lcol], accTf[t][r], accR, 0, 0, 0);
+      }
+    float qc = 0.f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      // accR register 4g+e holds column 8g + 4h + e of the chunk (row lane&31)
+      const int col = c0 + 8 * g + 4 * h;
+      const f32x4 u = *reinterpret_cast<const f32x4*>(&Ml[col - b0]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float cm = col + e < p ? 1.f : 0.f;  // clamped loads beyond p carry data
+        const float r = ((S.d[g][e] - u[e]) - accR[4 * g + e]) * cm;
+        qc += r * r;
+      }
+    }
+    q64 += (double)(qc * rowmask);
+  };
+  // same per-lane column pieces as sweep 1 (8g + 4h), so load1 is reused
+  for (int b0 = 0; b0 < p; b0 += PB) {
+    stage(b0);
+    const int bend = min(b0 + PB, p);
+    S1 SA, SB;
+    load1(SA, b0);
+    for (int c0 = b0; c0 < bend; c0 += 64) {
+      load1(SB, c0 + 32);
+      comp2(SA, c0, b0);
+      if (c0 + 64 < bend) load1(SA, c0 + 64);
+      if (c0 + 32 < bend) comp2(SB, c0 + 32, b0);
+    }
+  }
+  q64 += __shfl_xor(q64, 32, 64);
+
+  score_epilogue<KT, SW>(reinterpret_cast<double*>(smem), sred, accT64, q64, row0, m, k, a_diag, A, T_out, T2_out,
+                         Q_out, dec, acc_out, acc_stride, stat_part);
+}
+
+// ---------------------------------------------------------------------------
+// k_score_f64 — single-pass scoring on FP64 MFMA (v_mfma_f64_16x16x4_f64).
+// d = (double)x − μ is exact; t = P·d accumulates in f64 (≈1e-15 relative),
+// so the orthogonal distance can use the norm identity Q = ‖d‖² − ‖t‖²
+// (P has orthonormal rows) with no catastrophic loss — X is read ONCE (the
+// f32 kernels need a second, explicit-residual sweep).  A wave owns 16 rows;
+// lane (row = lane&15, q = lane>>4) streams columns 16q … 16q+15 of every
+// 64-column chunk of its row (K order permuted identically for P and d).
+// Loadings (f64) and mean (f64) are staged per workgroup in 256-column LDS
+// blocks.  KT16 = number of 16-component MFMA tiles (k ≤ 16·KT16).
+// ---------------------------------------------------------------------------
+typedef double f64x4_t __attribute__((ext_vector_type(4)));
+constexpr int FR = 16;  // rows per wave
+constexpr int FPB = 256;
+
+template <int KT16, bool VEC>
+__global__ __launch_bounds__(256, 2) void k_score_f64(const float* __restrict__ X, int64_t ldx,
+                                                      const int64_t* __restrict__ rows, int64_t m, int p,
+                                                      const double* __restrict__ P, const double* __restrict__ mu,
+                                                      const double* __restrict__ A, int k, int a_diag,
+                                                      float* __restrict__ T_out, double* __restrict__ T2_out,
+                                                      float* __restrict__ Q_out, DecArgs dec,
+                                                      double* __restrict__ acc_out, int64_t acc_stride,
+                                                      double* __restrict__ stat_part) {
+  constexpr int KP = 16 * KT16;
+  constexpr int PS = FPB + 1;  // odd stride (doubles): conflict-free ds_read_b64 across comps and q
+  constexpr int MAIN_D = KP * PS + FPB;
+  constexpr int EPI_D = SW * FR * (KP + 1);
+  __shared__ double smem[MAIN_D > EPI_D ? MAIN_D : EPI_D];
+  __shared__ double sred[SW * 4];
+  double* Pl = smem;
+  double* Ml = smem + KP * PS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j16 = lane & 15, q = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * (SW * FR) + wave * FR;
+  const int64_t grow = row0 + j16;
+  const double rowmask = grow < m ? 1.0 : 0.0;
+  const int64_t gcl = grow < m ? grow : m - 1;
+  const float* xrow = X + (rows ? rows[gcl] : gcl) * ldx;
+
+  auto ld4 = [&](int col) -> f32x4 {
+    if (VEC) return *reinterpret_cast<const f32x4*>(xrow + (col < p ? col : 0));
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = xrow[min(col + e, p - 1)];
+    return v;
+  };
+  auto stage = [&](int b0) {
+    __syncthreads();
+    for (int e = tid; e < KP * FPB; e += 256) {
+      const int comp = e / FPB, c = e % FPB;
+      Pl[comp * PS + c] = (comp < k && b0 + c < p) ? P[(int64_t)comp * p + b0 + c] : 0.0;
+    }
+    for (int c = tid; c < FPB; c += 256) Ml[c] = b0 + c < p ? mu[b0 + c] : 0.0;
+    __syncthreads();
+  };
+
+  f64x4_t acc[KT16];
+#pragma unroll
+  for (int t = 0; t < KT16; ++t) acc[t] = (f64x4_t){0.0, 0.0, 0.0, 0.0};
+  double dsq = 0.0;
+
+  struct SD {
+    f32x4 d[4];
+  };
+  auto load = [&](SD& S, int c0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) S.d[i] = ld4(c0 + 16 * q + 4 * i);
+  };
+  auto comp = [&](const SD& S, int c0, int b0) {
+    const int lc = c0 - b0 + 16 * q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int s = 4 * i + e;
+        // padded columns: μ = 0 and P = 0 there; the mask keeps ‖d‖² clean
+        const double cm = (c0 + 16 * q + s < p) ? rowmask : 0.0;
+        const double dv = ((double)S.d[i][e] - Ml[lc + s]) * cm;
+        dsq = fma(dv, dv, dsq);
+#pragma unroll
+        for (int t = 0; t < KT16; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(Pl[(t * 16 + j16) * PS + lc + s], dv, acc[t], 0, 0, 0);
+      }
+  };
+  for (int b0 = 0; b0 < p; b0 += FPB) {
+    stage(b0);
+    const int bend = min(b0 + FPB, p);
+    SD SA, SB;
+    load(SA, b0);
+    for (int c0 = b0; c0 < bend; c0 += 128) {
+      load(SB, c0 + 64);
+      comp(SA, c0, b0);
+      if (c0 + 128 < bend) load(SA, c0 + 128);
+      if (c0 + 64 < bend) comp(SB, c0 + 64, b0);
+    }
+  }
+
+  // acc[t][r] = t_{16t + q + 4r} of row (lane & 15); rows shared by lanes j, j+16, j+32, j+48
+  double tsq = 0.0;
+#pragma unroll
+  for (int t = 0; t < KT16; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tsq += acc[t][r] * acc[t][r];
+  tsq += __shfl_xor(tsq, 16, 64);
+  tsq += __shfl_xor(tsq, 32, 64);
+  dsq += __shfl_xor(dsq, 16, 64);
+  dsq += __shfl_xor(dsq, 32, 64);
+  const double Qv = fmax(dsq - tsq, 0.0);
+
+  // gather t rows through LDS (f64) for T², T_out
   __syncthreads();
-  const int64_t grow = row0 + l31;
-  const bool own = (h == 0) && (grow < m);
-  double T2 = 0.0, Q = q64;
+  double* Tt = smem + wave * FR * (KP + 1);
+#pragma unroll
+  for (int t = 0; t < KT16; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Tt[j16 * (KP + 1) + 16 * t + q + 4 * r] = acc[t][r];
+  __syncthreads();
+  const bool own = (q == 0) && (grow < m);
+  double T2 = 0.0;
   if (own) {
-    const double* trow = Tt + l31 * (KP + 1);
+    const double* trow = Tt + j16 * (KP + 1);
     if (a_diag) {
       for (int a = 0; a < k; ++a) T2 += trow[a] * trow[a] * A[a * k + a];
     } else {
       for (int a = 0; a < k; ++a) {
-        double s = 0.0;
-        for (int b = 0; b < k; ++b) s += A[a * k + b] * trow[b];
-        T2 += trow[a] * s;
+        double sacc = 0.0;
+        for (int b = 0; b < k; ++b) sacc += A[a * k + b] * trow[b];
+        T2 += trow[a] * sacc;
       }
     }
     if (T_out)
       for (int a = 0; a < k; ++a) T_out[grow * k + a] = (float)trow[a];
     if (T2_out) T2_out[grow] = T2;
-    if (Q_out) Q_out[grow] = (float)Q;
+    if (Q_out) Q_out[grow] = (float)Qv;
     if (dec.enabled) {
-      const double dr = dred_of(dec.type, T2 * dec.t2_scale, (double)(float)Q * dec.q_scale);
+      const double dr = dred_of(dec.type, T2 * dec.t2_scale, (double)(float)Qv * dec.q_scale);
       acc_out[grow * acc_stride] = dr < dec.dlim ? 1.0 : 0.0;
     }
   }
   if (stat_part) {
-    const double qf = (double)(float)Q;
+    const double qf = (double)(float)Qv;
     double s0 = own ? T2 : 0.0, s1 = own ? T2 * T2 : 0.0, s2 = own ? qf : 0.0, s3 = own ? qf * qf : 0.0;
     s0 = wave_sum_f64(s0);
     s1 = wave_sum_f64(s1);
     s2 = wave_sum_f64(s2);
     s3 = wave_sum_f64(s3);
     if (lane == 0) {
-      sred[wave][0] = s0;
-      sred[wave][1] = s1;
-      sred[wave][2] = s2;
-      sred[wave][3] = s3;
+      sred[wave * 4 + 0] = s0;
+      sred[wave * 4 + 1] = s1;
+      sred[wave * 4 + 2] = s2;
+      sred[wave * 4 + 3] = s3;
     }
     __syncthreads();
     if (tid < 4) {
       double v = 0.0;
-      for (int w = 0; w < SW; ++w) v += sred[w][tid];
+      for (int w = 0; w < SW; ++w) v += sred[w * 4 + tid];
       stat_part[(int64_t)blockIdx.x * 4 + tid] = v;
     }
   }
@@ -297,7 +655,7 @@ __global__ void k_cast_f64_f32(const double* __restrict__ a, int64_t n, float* _
 extern "C" {
 
 int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
-                  const float* P, const float* mu, const double* A, int32_t k, float* T_out, double* T2_out,
+                  const double* P, const double* mu, const double* A, int32_t k, float* T_out, double* T2_out,
                   float* Q_out, const ocm_decision* dec, double* accept_out, int64_t accept_stride,
                   double* stats_out, void* stream) {
   OCM_REQUIRE(ctx && X && P && mu && A, "ocm_score_f32: NULL argument");
@@ -309,12 +667,35 @@ int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
     if (stats_out) OCM_HIP(hipMemsetAsync(stats_out, 0, 4 * sizeof(double), st));
     return OCM_OK;
   }
-  const int64_t nblk = (m + SROWS - 1) / SROWS;
+  // variant: "direct" (f32 MFMA, two register-streamed sweeps; default),
+  // "f64" (single pass, FP64 MFMA, norm identity) or "lds" (f32, LDS tiles);
+  // OCM_SCORE_VARIANT overrides for A/B runs.  Measured on MI355X at
+  // 1M×2048, k=20: direct 3.61 ms, lds 4.08 ms, f64 4.25 ms (profiles/).
+  int variant = 1;
+  if (const char* e = std::getenv("OCM_SCORE_VARIANT")) {
+    const std::string v(e);
+    variant = v == "f64" ? 0 : (v == "lds" ? 2 : 1);
+  }
+  const int64_t rows_per_blk = variant == 0 ? (int64_t)SW * FR : (int64_t)SROWS;
+  const int64_t nblk = (m + rows_per_blk - 1) / rows_per_blk;
   OCM_REQUIRE(nblk < (1LL << 31), "ocm_score_f32: too many rows");
-  double* part = nullptr;
-  if (stats_out) {
-    part = static_cast<double*>(ocm::workspace(ctx, (size_t)nblk * 4 * sizeof(double), st));
-    if (!part) return OCM_ERR_NOMEM;
+  const size_t part_bytes = stats_out ? (size_t)nblk * 4 * sizeof(double) : 0;
+  const size_t cast_bytes = variant ? ((size_t)k * p + p) * sizeof(float) + 512 : 0;
+  void* w = ocm::workspace(ctx, part_bytes + cast_bytes + 1024, st);
+  if (!w) return OCM_ERR_NOMEM;
+  ocm::Carve cv{static_cast<char*>(w)};
+  double* part = stats_out ? cv.take<double>((size_t)nblk * 4) : nullptr;
+  const float* P32 = nullptr;
+  const float* mu32 = nullptr;
+  if (variant) {  // f32 kernels take f32 loadings / mean
+    float* pc = cv.take<float>((size_t)k * p);
+    float* mc = cv.take<float>(p);
+    hipLaunchKernelGGL(k_cast_f64_f32, dim3((unsigned)(((int64_t)k * p + 255) / 256)), dim3(256), 0, st, P,
+                       (int64_t)k * p, pc);
+    hipLaunchKernelGGL(k_cast_f64_f32, dim3((p + 255) / 256), dim3(256), 0, st, mu, (int64_t)p, mc);
+    OCM_CHECK_LAUNCH("k_cast_f64_f32");
+    P32 = pc;
+    mu32 = mc;
   }
   const int a_diag = 0;  // general k×k quadratic form (k² FMAs per row are negligible)
   DecArgs d{};
@@ -325,19 +706,33 @@ int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
     d.q_scale = dec->q_scale;
     d.dlim = dec->dlim;
   }
-  const bool vec = (ldx % 4 == 0) && (p % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0) &&
-                   ((reinterpret_cast<uintptr_t>(P) & 15) == 0);
+  const bool vec = (ldx % 4 == 0) && (p % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
   dim3 g((unsigned)nblk);
   {
     ocm::TimedRegion tr(ctx, OCM_KERNEL_SCORE, st);
-#define OCM_SCORE_LAUNCH(KT_, V_)                                                                              \
-  hipLaunchKernelGGL((k_score<KT_, V_>), g, dim3(256), 0, st, X, ldx, rows, m, p, P, mu, A, k, a_diag, T_out, \
+#define OCM_SCORE_LAUNCH(K_, KT_, V_, PP_, MU_)                                                             \
+  hipLaunchKernelGGL((K_<KT_, V_>), g, dim3(256), 0, st, X, ldx, rows, m, p, PP_, MU_, A, k, a_diag, T_out, \
                      T2_out, Q_out, d, accept_out, accept_stride, part)
-    if (k <= 32) {
-      if (vec) OCM_SCORE_LAUNCH(1, true); else OCM_SCORE_LAUNCH(1, false);
+#define OCM_SCORE_KT(K_, KTA_, KTB_, COND_, PP_, MU_)                                         \
+  if (COND_) {                                                                               \
+    if (vec) OCM_SCORE_LAUNCH(K_, KTA_, true, PP_, MU_); else OCM_SCORE_LAUNCH(K_, KTA_, false, PP_, MU_); \
+  } else {                                                                                   \
+    if (vec) OCM_SCORE_LAUNCH(K_, KTB_, true, PP_, MU_); else OCM_SCORE_LAUNCH(K_, KTB_, false, PP_, MU_); \
+  }
+    if (variant == 0) {
+      if (k <= 16) {
+        OCM_SCORE_KT(k_score_f64, 1, 2, true, P, mu)
+      } else if (k <= 32) {
+        OCM_SCORE_KT(k_score_f64, 2, 2, true, P, mu)
+      } else {
+        OCM_SCORE_KT(k_score_f64, 3, 4, k <= 48, P, mu)
+      }
+    } else if (variant == 1) {
+      OCM_SCORE_KT(k_score_direct, 1, 2, k <= 32, P32, mu32)
     } else {
-      if (vec) OCM_SCORE_LAUNCH(2, true); else OCM_SCORE_LAUNCH(2, false);
+      OCM_SCORE_KT(k_score, 1, 2, k <= 32, P32, mu32)
     }
+#undef OCM_SCORE_KT
 #undef OCM_SCORE_LAUNCH
   }
   OCM_CHECK_LAUNCH("k_score");

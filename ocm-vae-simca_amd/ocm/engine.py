@@ -8,7 +8,7 @@ MI355X:
     G, s   = Σ (x-shift)(x-shift)ᵀ, Σ (x-shift) ocm_gram_f32      (FP32 MFMA, 1 HBM pass)
     C, μ   = (G - n d dᵀ)/(n-1), shift + d      ocm_cov_from_gram
     λ, P, θ = top-k eigenpairs, tail moments   ocm_eig_topk      (fp64, HBM-resident C)
-    T, T², Q (+ moments)                        ocm_score_f32     (FP32 MFMA, fused)
+    T, T², Q (+ moments)                        ocm_score_f32     (FP64 MFMA, one pass, fused)
     limits                                      host fp64 scalars (ocm/limits.py)
 
 All arrays stay in HBM; only scalars cross to the host.  The second,
@@ -61,10 +61,8 @@ class ClassFit:
     n: int
     p: int
     mean64: torch.Tensor
-    mean32: torch.Tensor
     evals: torch.Tensor          # (k,) f64
-    P64: torch.Tensor            # (k, p) f64, svd_flip sign convention
-    P32: torch.Tensor            # (k, p) f32 (scoring operand)
+    P64: torch.Tensor            # (k, p) f64, svd_flip sign convention (scoring operand)
     invcov: torch.Tensor         # (k, k) f64 = pinv(cov(T)) = diag(1/λ)
     thetas: tuple = (0.0, 0.0, 0.0)
     evals_host: np.ndarray = None
@@ -161,11 +159,12 @@ def make_decision(type_name: str, t2_scale: float, q_scale: float, dlim: float) 
     return OcmDecision(TYPE_CODES[type_name], 0, float(t2_scale), float(q_scale), float(dlim))
 
 
-def score(X: torch.Tensor, rows: torch.Tensor | None, m: int, P32: torch.Tensor, mean32: torch.Tensor,
+def score(X: torch.Tensor, rows: torch.Tensor | None, m: int, P64: torch.Tensor, mean64: torch.Tensor,
           A: torch.Tensor, want_T=False, want_T2=True, want_Q=True, decision: OcmDecision | None = None,
           accept_out: torch.Tensor | None = None, accept_stride: int = 1, want_stats=False):
-    """Fused scoring (ocm_score_f32).  Returns dict of device tensors."""
-    k, p = P32.shape
+    """Fused scoring (ocm_score_f32): P64 (k, p) f64 orthonormal rows, mean64 (p,) f64.
+    Returns dict of device tensors."""
+    k, p = P64.shape
     dev = X.device
     out = {}
     T = torch.empty((m, k), dtype=torch.float32, device=dev) if want_T else None
@@ -174,7 +173,7 @@ def score(X: torch.Tensor, rows: torch.Tensor | None, m: int, P32: torch.Tensor,
     st = torch.empty(4, dtype=torch.float64, device=dev) if want_stats else None
     ctx = Context.get(dev.index)
     dec_p = ctypes.byref(decision) if decision is not None else None
-    check(_lib.load().ocm_score_f32(ctx.handle, ptr(X), X.stride(0), ptr(rows), m, p, ptr(P32), ptr(mean32),
+    check(_lib.load().ocm_score_f32(ctx.handle, ptr(X), X.stride(0), ptr(rows), m, p, ptr(P64), ptr(mean64),
                                     ptr(A), k, ptr(T), ptr(T2), ptr(Q), dec_p, ptr(accept_out), accept_stride,
                                     ptr(st), _stream(dev)), "ocm_score_f32")
     out["T"], out["T2"], out["Q"], out["stats"] = T, T2, Q, st
@@ -249,10 +248,8 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
     C, mean64 = cov_from_gram([(1.0, G[0], cs[0])], shift32, n_total)
     del G
     evals, evecs, theta, iters = eig_topk(C, k, theta_mode)
-    P32 = cast_f32(evecs)
-    mean32 = cast_f32(mean64)
     invcov = invcov_from_evals(evals)
-    sc = score(X, rows, n, P32, mean32, invcov, want_T=want_T, want_stats=True)
+    sc = score(X, rows, n, evecs, mean64, invcov, want_T=want_T, want_stats=True)
     host = torch.cat([evals, theta, sc["stats"]]).cpu().numpy()
     ev_h = host[:k]
     th = tuple(float(v) for v in host[k:k + 3])
@@ -261,8 +258,7 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
         stt = torch.tensor(stats, dtype=torch.float64, device=X.device)
         allreduce([stt])
         stats = stt.cpu().numpy()
-    fit = ClassFit(k=k, n=n_total, p=p, mean64=mean64, mean32=mean32, evals=evals, P64=evecs, P32=P32,
-                   invcov=invcov, thetas=th, evals_host=ev_h, T=sc["T"], T2=sc["T2"], Q=sc["Q"],
+    fit = ClassFit(k=k, n=n_total, p=p, mean64=mean64, evals=evals, P64=evecs, invcov=invcov, thetas=th, evals_host=ev_h, T=sc["T"], T2=sc["T2"], Q=sc["Q"],
                    T2_stats=(stats[0], stats[1]), Q_stats=(stats[2], stats[3]), eig_iters=iters,
                    C=C if keep_C else None)
     fit.extra["shift32"] = shift32

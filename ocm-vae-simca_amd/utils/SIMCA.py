@@ -89,7 +89,7 @@ class EnginePCA:
 
     def transform(self, X):
         Xd = engine.as_device_f32(X)
-        out = engine.score(Xd, None, Xd.shape[0], self._fit.P32, self._fit.mean32, self._fit.invcov,
+        out = engine.score(Xd, None, Xd.shape[0], self._fit.P64, self._fit.mean64, self._fit.invcov,
                            want_T=True, want_T2=False, want_Q=False)
         T = out["T"]
         return T if isinstance(X, torch.Tensor) else T.cpu().numpy().astype(self._dt)
@@ -211,7 +211,7 @@ class SIMCA(BaseEstimator, ClassifierMixin):
         cls = self.model_class[-1]
         fit = self._fits[cls]
         m = self._model[cls]
-        out = engine.score(Xd, None, Xd.shape[0], fit.P32, fit.mean32, fit.invcov)
+        out = engine.score(Xd, None, Xd.shape[0], fit.P64, fit.mean64, fit.invcov)
         dec = self._decision(m["T2_limit"], m["Q_limit"], m["D_limit"])
         t2r, qr, _ = engine.decide(out["T2"], out["Q"], dec)
         if isinstance(X, torch.Tensor):
@@ -230,7 +230,7 @@ class SIMCA(BaseEstimator, ClassifierMixin):
             info = self._model[cls]
             dec = self._decision(info["T2_limit"], info["Q_limit"], info["D_limit"])
             acc = pred[:, i:] if C > 1 else pred
-            engine.score(Xd, None, m, fit.P32, fit.mean32, fit.invcov, want_T2=False, want_Q=False,
+            engine.score(Xd, None, m, fit.P64, fit.mean64, fit.invcov, want_T2=False, want_Q=False,
                          decision=dec, accept_out=acc, accept_stride=C)
         out = pred if isinstance(X, torch.Tensor) else pred.cpu().numpy()
         if y_true is not None:

@@ -117,8 +117,7 @@ def test_score_matches_oracle(eng, k):
     lam = w[::-1][:k]
     A = np.diag(1 / lam)
     T_ref, T2_ref, Q_ref = project_scores(X, P, mean, A)
-    out = eng.score(_dev(X), None, n, _dev(P.astype(np.float32)), _dev(mean.astype(np.float32)), _dev(A),
-                    want_T=True, want_stats=True)
+    out = eng.score(_dev(X), None, n, _dev(P), _dev(mean), _dev(A), want_T=True, want_stats=True)
     np.testing.assert_allclose(out["T"].cpu().numpy(), T_ref, rtol=1e-4, atol=1e-4 * np.abs(T_ref).max())
     np.testing.assert_allclose(out["T2"].cpu().numpy(), T2_ref, rtol=2e-5, atol=1e-6 * np.median(T2_ref))
     np.testing.assert_allclose(out["Q"].cpu().numpy(), Q_ref, rtol=2e-5, atol=1e-6 * np.median(Q_ref))
@@ -129,8 +128,8 @@ def test_score_matches_oracle(eng, k):
     rows = np.arange(n - 1, -1, -3)
     acc = torch.zeros((len(rows), 2), dtype=torch.float64, device="cuda")
     dec = eng.make_decision("alt", 1 / np.percentile(T2_ref, 90), 1 / np.percentile(Q_ref, 90), np.sqrt(2))
-    out2 = eng.score(_dev(X), _dev(rows.astype(np.int64)), len(rows), _dev(P.astype(np.float32)),
-                     _dev(mean.astype(np.float32)), _dev(A), decision=dec, accept_out=acc[:, 1:], accept_stride=2)
+    out2 = eng.score(_dev(X), _dev(rows.astype(np.int64)), len(rows), _dev(P), _dev(mean), _dev(A),
+                     decision=dec, accept_out=acc[:, 1:], accept_stride=2)
     np.testing.assert_allclose(out2["Q"].cpu().numpy(), Q_ref[rows], rtol=2e-5, atol=1e-6 * np.median(Q_ref))
     d = np.sqrt((T2_ref[rows] * dec.t2_scale) ** 2 + (Q_ref[rows].astype(np.float64) * dec.q_scale) ** 2)
     clear = np.abs(d - np.sqrt(2)) > 1e-4
