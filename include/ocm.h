@@ -169,6 +169,47 @@ int ocm_percentile(ocm_ctx* ctx, const void* v, int32_t dtype, int64_t n, double
 int ocm_radix_hist(ocm_ctx* ctx, const void* v, int32_t dtype, int64_t n, uint64_t prefix, int32_t shift,
                    uint64_t* hist_out, void* stream);
 
+/* ---- class-wise cross-validation fold engine (utils/CVSIMCA.py:103-269) ----
+ * One Gram pass gives every fold's Gram (segments), train Gram = total − fold;
+ * one eigensolve per fold at LV_max; each LV ≤ LV_max reuses it through
+ *   T²_LV = Σ_{j<LV} t_j²/λ_j,   Q_LV = Q_{LVmax} + Σ_{LV≤j<LVmax} t_j².   */
+
+/* G_out = Σ_t coef[t]·G_list[t] (p×p), colsum_out = Σ_t coef[t]·colsum_list[t]
+ * (either output nullable; colsum_list nullable).  G_out may alias G_list[0]
+ * only.  G_list/colsum_list/coef [host] arrays of nterm device pointers/values. */
+int ocm_gram_combine(ocm_ctx* ctx, const double* const* G_list, const double* const* colsum_list,
+                     const double* coef, int32_t nterm, int32_t p, double* G_out, double* colsum_out, void* stream);
+
+/* Per-LV T² and Q of m rows from their LV_max scores (training rows of a fold:
+ * the perc / chi2pom limit statistics, utils/SIMCA.py:157-159, 172-181, 186-187,
+ * 211-216).  T [dev] m×k float32 (from ocm_score_f32, k = LV_max), Q [dev] m
+ * float32, inv_evals [dev] k doubles (diag of invcovT), lvs [host] nlv values
+ * in [1, k].  Outputs nullable [dev]: T2_out nlv×m doubles, Q_out nlv×m floats,
+ * stats_out nlv×4 doubles {ΣT², ΣT²², ΣQ, ΣQ²}.  k, nlv ≤ 64. */
+int ocm_cv_prefix(ocm_ctx* ctx, const float* T, int64_t m, int32_t k, const float* Q, const double* inv_evals,
+                  const int32_t* lvs, int32_t nlv, double* T2_out, float* Q_out, double* stats_out, void* stream);
+
+/* One decision configuration of the CV sweep: LV components, a decision
+ * type and its scales / critical distance (as ocm_decision). */
+typedef struct ocm_cv_config {
+  int32_t lv;
+  int32_t type;
+  double t2_scale;
+  double q_scale;
+  double dlim;
+} ocm_cv_config;
+#define OCM_CV_MAXCFG 1024
+
+/* Confusion counts of every configuration over the test rows of a fold
+ * (utils/CVSIMCA.py:186-199 → utils/SIMCA.py:238-266): rows < m_split are the
+ * held-out target rows, the rest the other-class rows.  positive [dev] m
+ * bytes (y_true == class_index).  counts_out [dev] ncfg×2×4 uint64
+ * {TP, TN, FP, FN} per (config, part).  accept_out [dev, nullable] ncfg×m
+ * doubles 0/1 (pooled predictions).  cfg [host]. */
+int ocm_cv_counts(ocm_ctx* ctx, const float* T, int64_t m, int32_t k, const float* Q, const double* inv_evals,
+                  const uint8_t* positive, int64_t m_split, const ocm_cv_config* cfg, int32_t ncfg,
+                  uint64_t* counts_out, double* accept_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

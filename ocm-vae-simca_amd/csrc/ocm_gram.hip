@@ -228,25 +228,52 @@ __global__ __launch_bounds__(GT * 2, 2) void k_gram(
 }
 
 // Sum chunk partials of one segment into G (full symmetric) and colsum.
+// Each thread owns 4 consecutive tile elements (one float4 per chunk) and
+// keeps 4 chunks' loads in flight (independent partial sums, fixed order).
 template <int GT>
-__global__ void k_gram_reduce(const float* __restrict__ part, const double* __restrict__ colpart, int nt, int ntiles,
-                              int p, int c0, int c1, double* __restrict__ G, double* __restrict__ colsum) {
+__global__ __launch_bounds__(256) void k_gram_reduce(const float* __restrict__ part,
+                                                     const double* __restrict__ colpart, int nt, int ntiles, int p,
+                                                     int c0, int c1, double* __restrict__ G,
+                                                     double* __restrict__ colsum) {
   const int tile = blockIdx.y;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // element in tile
+  const int e4 = blockIdx.x * blockDim.x + threadIdx.x;  // float4 index in tile
   int ti, tj;
   tile_coords(tile, nt, ti, tj);
-  if (e < GT * GT) {
-    const int i = e / GT, j = e % GT;
-    const int gi = ti * GT + i, gj = tj * GT + j;
-    // diagonal tiles: only the upper triangle is valid (k_gram skips the
-    // strictly-lower wave blocks); mirror it
-    if (gi < p && gj < p && !(ti == tj && i > j)) {
-      double v = 0.0;
-      for (int c = c0; c < c1; ++c) v += (double)part[((size_t)c * ntiles + tile) * (GT * GT) + e];
-      G[(size_t)gi * p + gj] = v;
-      if (gi != gj) G[(size_t)gj * p + gi] = v;
+  if (e4 < GT * GT / 4) {
+    const size_t stride = (size_t)ntiles * (GT * GT) / 4;
+    const f32x4* src = reinterpret_cast<const f32x4*>(part) + (size_t)tile * (GT * GT) / 4 + e4;
+    double s[4][4] = {};
+    int c = c0;
+    for (; c + 4 <= c1; c += 4) {
+      f32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = src[(size_t)(c + u) * stride];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[u][q] += (double)v[u][q];
+    }
+    for (; c < c1; ++c) {
+      const f32x4 v = src[(size_t)c * stride];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s[0][q] += (double)v[q];
+    }
+    const int e = 4 * e4;
+    const int i = e / GT, j0 = e % GT;
+    const int gi = ti * GT + i;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = j0 + q, gj = tj * GT + j;
+      // diagonal tiles: only the upper triangle is valid (k_gram skips the
+      // strictly-lower wave blocks); mirror it
+      if (gi < p && gj < p && !(ti == tj && i > j)) {
+        const double v = (s[0][q] + s[1][q]) + (s[2][q] + s[3][q]);
+        G[(size_t)gi * p + gj] = v;
+        if (gi != gj) G[(size_t)gj * p + gi] = v;
+      }
     }
   }
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (ti == tj && e < GT) {
     const int gi = ti * GT + e;
     double v = 0.0;
@@ -371,7 +398,7 @@ int gram_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, in
       OCM_HIP(hipMemsetAsync(cs, 0, (size_t)p * sizeof(double), st));
       continue;
     }
-    dim3 g((GT * GT + 255) / 256, ntiles);
+    dim3 g((GT * GT / 4 + 255) / 256, ntiles);
     hipLaunchKernelGGL(k_gram_reduce<GT>, g, dim3(256), 0, st, part, colpart, nt, ntiles, p, cprefix[s],
                        cprefix[s + 1], Gs, cs);
     OCM_CHECK_LAUNCH("k_gram_reduce");

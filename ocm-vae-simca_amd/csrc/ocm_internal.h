@@ -73,6 +73,16 @@ struct Carve {
   }
 };
 
+// Reduced distance of a decision rule (utils/SIMCA.py:131-144):
+// sim max(t, q), alt √(t²+q²), ci / dd t + q.
+__device__ __forceinline__ double dred_of(int type, double t, double q) {
+  switch (type) {
+    case OCM_TYPE_SIM: return fmax(t, q);
+    case OCM_TYPE_ALT: return sqrt(t * t + q * q);
+    default: return t + q;  // ci, dd
+  }
+}
+
 }  // namespace ocm
 
 #define OCM_HIP(call)                                                                       \

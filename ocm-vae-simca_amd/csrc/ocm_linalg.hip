@@ -26,7 +26,10 @@ namespace {
 // ---------------------------------------------------------------------------
 // fp64 MFMA GEMM  D = A·B  (row-major, NN), 64×64 tile, BK = 16.
 // MODE 0: store (split-K: z-slice writes its own partial plane)
-// MODE 1: trace epilogue  part[wg] = Σ_{tile} (A·B)_{ij} · E_{ij}
+// MODE 1: trace epilogue  part[wg] = w · Σ_{tile} (A·B)_{ij} · E_{ij}; A·B
+//         and E symmetric: the grid is the upper triangle of tiles
+//         (blockIdx.x linear), off-diagonal tiles weighted 2
+// MODE 2: rank update  D = E − A·B, part[2wg..] = {Σ diag D, Σ D²}
 // ---------------------------------------------------------------------------
 constexpr int DT = 64, DBK = 16, DPAD = 16;
 
@@ -37,10 +40,23 @@ __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int
                                                double* __restrict__ part) {
   __shared__ double As[DBK][DT + DPAD];
   __shared__ double Bs[DBK][DT + DPAD];
-  __shared__ double red[4];
+  __shared__ double red[8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.x * DT, n0 = blockIdx.y * DT;
+  int bx = blockIdx.x, by = blockIdx.y;
+  double wtile = 1.0;
+  if (MODE == 1) {  // linear upper-triangle index -> (bx <= by)
+    const int nt = (N + DT - 1) / DT;
+    int rem = blockIdx.x;
+    bx = 0;
+    while (rem >= nt - bx) {
+      rem -= nt - bx;
+      ++bx;
+    }
+    by = bx + rem;
+    wtile = bx == by ? 1.0 : 2.0;
+  }
+  const int m0 = bx * DT, n0 = by * DT;
   const int kb = blockIdx.z * kper, ke = min(K, kb + kper);
   f64x4 acc[2][2];
 #pragma unroll
@@ -73,7 +89,7 @@ __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int
     }
     __syncthreads();
   }
-  double tr = 0.0;
+  double tr = 0.0, fro = 0.0;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -84,17 +100,35 @@ __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int
         const int row = m0 + wm * 32 + a * 16 + (lane >> 4) + 4 * r;
         const int col = n0 + wn * 32 + b * 16 + (lane & 15);
         if (row < M && col < N) {
-          if (MODE == 0)
+          if (MODE == 0) {
             D[(int64_t)blockIdx.z * M * ldd + (int64_t)row * ldd + col] = acc[a][b][r];
-          else
+          } else if (MODE == 1) {
             tr += acc[a][b][r] * E[(int64_t)row * lde + col];
+          } else {
+            const double v = E[(int64_t)row * lde + col] - acc[a][b][r];
+            D[(int64_t)row * ldd + col] = v;
+            fro += v * v;
+            if (row == col) tr += v;
+          }
         }
       }
-  if (MODE == 1) {
+  if (MODE >= 1) {
     tr = wave_sum_f64(tr);
-    if (lane == 0) red[wave] = tr;
+    if (MODE == 2) fro = wave_sum_f64(fro);
+    if (lane == 0) {
+      red[wave] = tr;
+      red[4 + wave] = fro;
+    }
     __syncthreads();
-    if (tid == 0) part[blockIdx.y * gridDim.x + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+    if (tid == 0) {
+      if (MODE == 1) {
+        part[blockIdx.x] = wtile * ((red[0] + red[1]) + (red[2] + red[3]));
+      } else {
+        const int wg = blockIdx.y * gridDim.x + blockIdx.x;
+        part[2 * wg] = (red[0] + red[1]) + (red[2] + red[3]);
+        part[2 * wg + 1] = (red[4] + red[5]) + (red[6] + red[7]);
+      }
+    }
   }
 }
 
@@ -108,11 +142,14 @@ __global__ void k_sum_planes(const double* __restrict__ P, int nz, int64_t plane
 }
 
 // ordered sum of n partials into out[0] (single wave, deterministic)
-__global__ void k_sum_partials(const double* __restrict__ part, int n, double* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_sum_partials(const double* __restrict__ part, int n, double* __restrict__ out) {
+  __shared__ double red[4];
   double v = 0.0;
-  for (int i = threadIdx.x; i < n; i += 64) v += part[i];
+  for (int i = threadIdx.x; i < n; i += 256) v += part[i];
   v = wave_sum_f64(v);
-  if (threadIdx.x == 0) *out = v;
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // partial  S = Aᵀ B  for tall row-major A, B (p×b, ld = b): block = 64 rows
@@ -145,18 +182,22 @@ __global__ __launch_bounds__(256) void k_atb_part(const double* __restrict__ A, 
 // ---------------------------------------------------------------------------
 constexpr int JMAX = 64;
 
-__global__ __launch_bounds__(256) void k_jacobi(const double* __restrict__ Ain, int n_in, int max_sweeps,
-                                                double* __restrict__ evals, double* __restrict__ Zout,
-                                                int* __restrict__ sweeps_out) {
+// NF > 0: compile-time padded size (index arithmetic folds); NT threads
+// (64 = one wave: the per-round barriers reduce to LDS waits).
+template <int NF, int NT>
+__global__ __launch_bounds__(NT) void k_jacobi(const double* __restrict__ Ain, int n_in, int max_sweeps,
+                                               double* __restrict__ evals, double* __restrict__ Zout,
+                                               int* __restrict__ sweeps_out) {
+  constexpr int NW = NT / 64;
   __shared__ double A[JMAX][JMAX + 1];
   __shared__ double Z[JMAX][JMAX + 1];
   __shared__ double rc[JMAX], rs[JMAX];
   __shared__ int pp[JMAX / 2], qq[JMAX / 2];
-  __shared__ double wsum[8];
+  __shared__ double wsum[2 * NW];
   __shared__ int done;
-  const int n = (n_in + 1) & ~1;
+  const int n = NF > 0 ? NF : (n_in + 1) & ~1;
   const int tid = threadIdx.x;
-  for (int e = tid; e < n * n; e += 256) {
+  for (int e = tid; e < n * n; e += NT) {
     const int i = e / n, j = e % n;
     A[i][j] = (i < n_in && j < n_in) ? 0.5 * (Ain[i * n_in + j] + Ain[j * n_in + i]) : 0.0;
     Z[i][j] = (i == j) ? 1.0 : 0.0;
@@ -167,7 +208,7 @@ __global__ __launch_bounds__(256) void k_jacobi(const double* __restrict__ Ain, 
   for (; sweep < max_sweeps; ++sweep) {
     // convergence test: off(A)² ≤ (1e-15)² · Σ diag²  (relative to the scale of A)
     double off = 0.0, dg = 0.0;
-    for (int e = tid; e < n * n; e += 256) {
+    for (int e = tid; e < n * n; e += NT) {
       const int i = e / n, j = e % n;
       const double v = A[i][j] * A[i][j];
       if (i == j) dg += v; else off += v;
@@ -176,12 +217,15 @@ __global__ __launch_bounds__(256) void k_jacobi(const double* __restrict__ Ain, 
     dg = wave_sum_f64(dg);
     if ((tid & 63) == 0) {
       wsum[tid >> 6] = off;
-      wsum[4 + (tid >> 6)] = dg;
+      wsum[NW + (tid >> 6)] = dg;
     }
     __syncthreads();
     if (tid == 0) {
-      const double o = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-      const double d = wsum[4] + wsum[5] + wsum[6] + wsum[7];
+      double o = 0.0, d = 0.0;
+      for (int w = 0; w < NW; ++w) {
+        o += wsum[w];
+        d += wsum[NW + w];
+      }
       done = (o <= 1e-30 * d) || (o == 0.0);
     }
     __syncthreads();
@@ -207,7 +251,7 @@ __global__ __launch_bounds__(256) void k_jacobi(const double* __restrict__ Ain, 
       }
       __syncthreads();
       // rows:  A ← Jᵀ A
-      for (int e = tid; e < half * n; e += 256) {
+      for (int e = tid; e < half * n; e += NT) {
         const int k = e / n, j = e % n;
         const int p = pp[k], q = qq[k];
         const double c = rc[k], s = rs[k];
@@ -217,7 +261,7 @@ __global__ __launch_bounds__(256) void k_jacobi(const double* __restrict__ Ain, 
       }
       __syncthreads();
       // columns: A ← A J, Z ← Z J
-      for (int e = tid; e < half * n; e += 256) {
+      for (int e = tid; e < half * n; e += NT) {
         const int i = e / half, k = e % half;
         const int p = pp[k], q = qq[k];
         const double c = rc[k], s = rs[k];
@@ -232,7 +276,7 @@ __global__ __launch_bounds__(256) void k_jacobi(const double* __restrict__ Ain, 
     }
   }
   // sort descending (stable): rank by value then index
-  for (int i = tid; i < n_in; i += 256) {
+  for (int i = tid; i < n_in; i += NT) {
     const double li = A[i][i];
     int rank = 0;
     for (int j = 0; j < n_in; ++j) {
@@ -241,6 +285,140 @@ __global__ __launch_bounds__(256) void k_jacobi(const double* __restrict__ Ain, 
     }
     evals[rank] = li;
     for (int r = 0; r < n_in; ++r) Zout[r * n_in + rank] = Z[r][i];
+  }
+  if (tid == 0 && sweeps_out) *sweeps_out = sweep;
+}
+
+// ---------------------------------------------------------------------------
+// Block-parallel Jacobi (NF = 32/48/64, compile-time).  Parallel ordering in
+// storage: rotation pair k always occupies slots (2k, 2k+1); after each round
+// the contents move to the round-robin tournament's next slots (a fixed
+// permutation `jdest`), written into a ping-pong buffer.  One thread updates a
+// whole 2×2 block with both the row and the column rotation (and writes the
+// mirrored block), so a round is: rotations → barrier → block update →
+// barrier.  Slot order is irrelevant for the output (sorted at the end).
+// ---------------------------------------------------------------------------
+template <int NF>
+__device__ __forceinline__ int jdest(int s) {
+  // slot -> tournament position; position t shifts to t-1 (1 -> NF-1, 0 fixed)
+  const int t = (s & 1) ? NF - 1 - (s >> 1) : (s >> 1);
+  const int t2 = t == 0 ? 0 : (t == 1 ? NF - 1 : t - 1);
+  return t2 < NF / 2 ? 2 * t2 : 2 * (NF - 1 - t2) + 1;
+}
+
+template <int NF>
+__global__ __launch_bounds__(256) void k_jacobi_blk(const double* __restrict__ Ain, int max_sweeps,
+                                                    double* __restrict__ evals, double* __restrict__ Zout,
+                                                    int* __restrict__ sweeps_out) {
+  constexpr int H = NF / 2, NB = H * (H + 1) / 2, LD = NF + 1;
+  __shared__ double A[2][NF][LD];
+  __shared__ double Z[2][NF][LD];
+  __shared__ double rc[H], rs[H];
+  __shared__ unsigned char bk[NB], bl[NB];
+  __shared__ double wsum[8];
+  __shared__ int done;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < NF * NF; e += 256) {
+    const int i = e / NF, j = e % NF;
+    A[0][i][j] = 0.5 * (Ain[i * NF + j] + Ain[j * NF + i]);
+    Z[0][i][j] = (i == j) ? 1.0 : 0.0;
+  }
+  if (tid == 0) {
+    int b = 0;
+    for (int k = 0; k < H; ++k)
+      for (int l = k; l < H; ++l) {
+        bk[b] = (unsigned char)k;
+        bl[b] = (unsigned char)l;
+        ++b;
+      }
+  }
+  __syncthreads();
+  int cur = 0, sweep = 0;
+  for (; sweep < max_sweeps; ++sweep) {
+    double off = 0.0, dg = 0.0;
+    for (int e = tid; e < NF * NF; e += 256) {
+      const int i = e / NF, j = e % NF;
+      const double v = A[cur][i][j] * A[cur][i][j];
+      if (i == j) dg += v; else off += v;
+    }
+    off = wave_sum_f64(off);
+    dg = wave_sum_f64(dg);
+    if ((tid & 63) == 0) {
+      wsum[tid >> 6] = off;
+      wsum[4 + (tid >> 6)] = dg;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const double o = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+      const double d = (wsum[4] + wsum[5]) + (wsum[6] + wsum[7]);
+      done = (o <= 1e-30 * d) || (o == 0.0);
+    }
+    __syncthreads();
+    if (done) break;
+    for (int round = 0; round < NF - 1; ++round) {
+      if (tid < H) {
+        const double app = A[cur][2 * tid][2 * tid], aqq = A[cur][2 * tid + 1][2 * tid + 1];
+        const double apq = A[cur][2 * tid][2 * tid + 1];
+        double c = 1.0, sn = 0.0;
+        if (apq != 0.0) {
+          const double theta = (aqq - app) / (2.0 * apq);
+          const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+          c = 1.0 / sqrt(t * t + 1.0);
+          sn = t * c;
+        }
+        rc[tid] = c;
+        rs[tid] = sn;
+      }
+      __syncthreads();
+      const int nx = cur ^ 1;
+      for (int b = tid; b < NB; b += 256) {
+        const int k = bk[b], l = bl[b];
+        const double ck = rc[k], sk = rs[k], cl = rc[l], sl = rs[l];
+        const int p = 2 * k, q = 2 * k + 1, u = 2 * l, v = 2 * l + 1;
+        const double a00 = A[cur][p][u], a01 = A[cur][p][v], a10 = A[cur][q][u], a11 = A[cur][q][v];
+        // rows (pair k): B = Jkᵀ A
+        const double b00 = ck * a00 - sk * a10, b01 = ck * a01 - sk * a11;
+        const double b10 = sk * a00 + ck * a10, b11 = sk * a01 + ck * a11;
+        // columns (pair l): B Jl
+        double o00 = cl * b00 - sl * b01, o01 = sl * b00 + cl * b01;
+        double o10 = cl * b10 - sl * b11, o11 = sl * b10 + cl * b11;
+        if (k == l) {  // the rotated pair: exact zero off-diagonal
+          o01 = 0.0;
+          o10 = 0.0;
+        }
+        const int dp = jdest<NF>(p), dq = jdest<NF>(q), du = jdest<NF>(u), dv = jdest<NF>(v);
+        A[nx][dp][du] = o00;
+        A[nx][dp][dv] = o01;
+        A[nx][dq][du] = o10;
+        A[nx][dq][dv] = o11;
+        if (k != l) {
+          A[nx][du][dp] = o00;
+          A[nx][dv][dp] = o01;
+          A[nx][du][dq] = o10;
+          A[nx][dv][dq] = o11;
+        }
+      }
+      // Z ← Z J (columns = slots; rows = coordinates, not permuted)
+      for (int e = tid; e < NF * H; e += 256) {
+        const int r = e / H, l = e % H;
+        const double cl = rc[l], sl = rs[l];
+        const double zp = Z[cur][r][2 * l], zq = Z[cur][r][2 * l + 1];
+        Z[nx][r][jdest<NF>(2 * l)] = cl * zp - sl * zq;
+        Z[nx][r][jdest<NF>(2 * l + 1)] = sl * zp + cl * zq;
+      }
+      __syncthreads();
+      cur = nx;
+    }
+  }
+  for (int i = tid; i < NF; i += 256) {
+    const double li = A[cur][i][i];
+    int rank = 0;
+    for (int j = 0; j < NF; ++j) {
+      const double lj = A[cur][j][j];
+      rank += (lj > li) || (lj == li && j < i);
+    }
+    evals[rank] = li;
+    for (int r = 0; r < NF; ++r) Zout[r * NF + rank] = Z[cur][r][i];
   }
   if (tid == 0 && sweeps_out) *sweeps_out = sweep;
 }
@@ -405,49 +583,40 @@ __global__ __launch_bounds__(256) void k_extract_signfix(const double* __restric
   for (int j = threadIdx.x; j < p; j += 256) evecs[(int64_t)i * p + j] = sg * V[(int64_t)j * b + i];
 }
 
-// C⊥ = C − V Mᵀ − M Vᵀ + N Vᵀ  (V, M = C V, N = V H; first k columns of the
-// p×b row-major blocks), plus per-block partials of tr C⊥ and ‖C⊥‖²_F.
-__global__ __launch_bounds__(256) void k_deflate(const double* __restrict__ C, const double* __restrict__ V,
-                                                 const double* __restrict__ M, const double* __restrict__ Nm, int p,
-                                                 int b, int k, double* __restrict__ Ct, double* __restrict__ part) {
-  __shared__ double red[8];
+// Operands of the deflation update C⊥ = C − U·Wt (one fp64-MFMA GEMM):
+//   C⊥ = C − V_k M_kᵀ − M_k V_kᵀ + N_k V_kᵀ = C − [V_k | M_k − N_k]·[M_k | V_k]ᵀ
+// with V the Ritz basis, M = C V, N = V_k H_k (first k columns of p×b blocks).
+// U p×2k row-major, Wt 2k×p row-major.
+__global__ __launch_bounds__(256) void k_deflate_operands(const double* __restrict__ V, const double* __restrict__ M,
+                                                          const double* __restrict__ Nm, int p, int b, int k,
+                                                          double* __restrict__ U, double* __restrict__ Wt) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  double tr = 0.0, fro = 0.0;
-  if (e < (int64_t)p * p) {
-    const int i = (int)(e / p), j = (int)(e % p);
-    double v = C[e];
-    for (int l = 0; l < k; ++l) {
-      const double vi = V[(int64_t)i * b + l], vj = V[(int64_t)j * b + l];
-      v -= vi * M[(int64_t)j * b + l] + M[(int64_t)i * b + l] * vj - Nm[(int64_t)i * b + l] * vj;
-    }
-    Ct[e] = v;
-    fro = v * v;
-    if (i == j) tr = v;
-  }
-  tr = wave_sum_f64(tr);
-  fro = wave_sum_f64(fro);
-  if ((threadIdx.x & 63) == 0) {
-    red[threadIdx.x >> 6] = tr;
-    red[4 + (threadIdx.x >> 6)] = fro;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-    part[2 * blockIdx.x + 1] = red[4] + red[5] + red[6] + red[7];
-  }
+  if (e >= (int64_t)p * k) return;
+  const int i = (int)(e / k), l = (int)(e % k);
+  const double v = V[(int64_t)i * b + l], m = M[(int64_t)i * b + l], nn = Nm[(int64_t)i * b + l];
+  U[(int64_t)i * 2 * k + l] = v;
+  U[(int64_t)i * 2 * k + k + l] = m - nn;
+  Wt[(int64_t)l * p + i] = m;
+  Wt[(int64_t)(k + l) * p + i] = v;
 }
 
-__global__ void k_sum_pairs(const double* __restrict__ part, int n, double* __restrict__ out2) {
+__global__ __launch_bounds__(256) void k_sum_pairs(const double* __restrict__ part, int n, double* __restrict__ out2) {
+  __shared__ double red[8];
   double a = 0.0, b = 0.0;
-  for (int i = threadIdx.x; i < n; i += 64) {
+  for (int i = threadIdx.x; i < n; i += 256) {
     a += part[2 * i];
     b += part[2 * i + 1];
   }
   a = wave_sum_f64(a);
   b = wave_sum_f64(b);
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = a;
+    red[4 + (threadIdx.x >> 6)] = b;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    out2[0] = a;
-    out2[1] = b;
+    out2[0] = (red[0] + red[1]) + (red[2] + red[3]);
+    out2[1] = (red[4] + red[5]) + (red[6] + red[7]);
   }
 }
 
@@ -524,6 +693,21 @@ int dgemm(const double* A, int64_t lda, const double* B, int64_t ldb, double* D,
   return OCM_OK;
 }
 
+int jacobi(const double* A, int n, int max_sweeps, double* ev, double* Z, hipStream_t st) {
+  if (n == 32)
+    hipLaunchKernelGGL(k_jacobi_blk<32>, dim3(1), dim3(256), 0, st, A, max_sweeps, ev, Z, nullptr);
+  else if (n == 48)
+    hipLaunchKernelGGL(k_jacobi_blk<48>, dim3(1), dim3(256), 0, st, A, max_sweeps, ev, Z, nullptr);
+  else if (n == 64)
+    hipLaunchKernelGGL(k_jacobi_blk<64>, dim3(1), dim3(256), 0, st, A, max_sweeps, ev, Z, nullptr);
+  else if (n <= 32)
+    hipLaunchKernelGGL((k_jacobi<0, 64>), dim3(1), dim3(64), 0, st, A, n, max_sweeps, ev, Z, nullptr);
+  else
+    hipLaunchKernelGGL((k_jacobi<0, 256>), dim3(1), dim3(256), 0, st, A, n, max_sweeps, ev, Z, nullptr);
+  OCM_CHECK_LAUNCH("k_jacobi");
+  return OCM_OK;
+}
+
 int atb(const double* A, const double* B, int p, int b, double* out, double* part, hipStream_t st) {
   const int nblk = (p + 63) / 64;
   hipLaunchKernelGGL(k_atb_part, dim3(nblk), dim3(256), 0, st, A, B, p, b, part);
@@ -567,8 +751,8 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
     ocm::Carve cv{static_cast<char*>(w)};
     double* ev = cv.take<double>(p);
     double* Z = cv.take<double>((size_t)p * p);
-    hipLaunchKernelGGL(k_jacobi, dim3(1), dim3(256), 0, st, C, p, 60, ev, Z, nullptr);
-    OCM_CHECK_LAUNCH("k_jacobi");
+    int rc = jacobi(C, p, 60, ev, Z, st);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_small_finish, dim3(1), dim3(64), 0, st, ev, Z, p, k, evals_out, evecs_out,
                        theta_mode ? theta_out : nullptr);
     OCM_CHECK_LAUNCH("k_small_finish");
@@ -587,10 +771,10 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
   const int ksplit = std::max(1, std::min(16, (int)(256 / std::max(1, ((p + 63) / 64) * ((b + 63) / 64)))));
   const size_t pb = (size_t)p * b, bb = (size_t)b * b;
   const int nblk = (p + 63) / 64;
-  const size_t def_blocks = ((size_t)p * p + 255) / 256;
+  const size_t def_blocks = (size_t)((p + DT - 1) / DT) * ((p + DT - 1) / DT);  // deflate GEMM tiles
   const size_t trace_wgs = (size_t)((p + DT - 1) / DT) * ((p + DT - 1) / DT);
   size_t need = (6 * pb + 6 * bb + (size_t)ksplit * pb + (size_t)nblk * bb + 4 * b + 64) * sizeof(double);
-  if (theta_mode) need += ((size_t)p * p + 2 * def_blocks + trace_wgs + 8) * sizeof(double);
+  if (theta_mode) need += ((size_t)p * p + 4 * (size_t)k * p + 2 * def_blocks + trace_wgs + 8) * sizeof(double);
   void* w = ocm::workspace(ctx, need + 16 * 256, st);
   if (!w) return OCM_ERR_NOMEM;
   ocm::Carve cv{static_cast<char*>(w)};
@@ -638,8 +822,8 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
     if (rc) return rc;
     rc = atb(V, W, p, b, H, apart, st);  // H = Vᵀ W
     if (rc) return rc;
-    hipLaunchKernelGGL(k_jacobi, dim3(1), dim3(256), 0, st, H, b, 40, theta, Z, nullptr);
-    OCM_CHECK_LAUNCH("k_jacobi");
+    rc = jacobi(H, b, 40, theta, Z, st);
+    if (rc) return rc;
     rc = dgemm(V, b, Z, b, T1, b, p, b, b, 1, nullptr, st);  // Ritz vectors
     if (rc) return rc;
     rc = dgemm(W, b, Z, b, T2, b, p, b, b, 1, nullptr, st);  // C · Ritz vectors
@@ -659,6 +843,7 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
       converged = true;
       break;
     }
+    if (it == max_iter) break;  // keep V, W, theta consistent for the outputs
     // next basis: orth(C · Ritz vectors)
     OCM_HIP(hipMemcpyAsync(T1, W, pb * sizeof(double), hipMemcpyDeviceToDevice, st));
     rc = orth(T1, V, 1000 + it);
@@ -674,26 +859,32 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
     // H_k = V_kᵀ (C V_k): the projected block; N = V H restricted to k columns
     rc = atb(V, W, p, b, H, apart, st);
     if (rc) return rc;
-    // zero H outside the leading k×k block so N = V_k H_k
-    std::vector<double> mask;  // (done on device: cheap kernel-free trick via dgemm with masked H)
-    (void)mask;
-    rc = dgemm(V, b, H, b, Nm, b, p, b, b, 1, nullptr, st);
+    // N = V_k H_k (K = k: only the leading k Ritz directions are deflated)
+    rc = dgemm(V, b, H, b, Nm, b, p, b, k, 1, nullptr, st);
     if (rc) return rc;
     double* Ct = cv.take<double>((size_t)p * p);
     double* dpart = cv.take<double>(2 * def_blocks);
     double* tpart = cv.take<double>(trace_wgs);
     double* tr2 = cv.take<double>(2);
-    hipLaunchKernelGGL(k_deflate, dim3((unsigned)def_blocks), dim3(256), 0, st, C, V, W, Nm, p, b, k, Ct, dpart);
-    OCM_CHECK_LAUNCH("k_deflate");
-    hipLaunchKernelGGL(k_sum_pairs, dim3(1), dim3(64), 0, st, dpart, (int)def_blocks, tr2);
+    double* U = cv.take<double>((size_t)2 * k * p);
+    double* Wt = cv.take<double>((size_t)2 * k * p);
+    hipLaunchKernelGGL(k_deflate_operands, dim3((unsigned)(((size_t)p * k + 255) / 256)), dim3(256), 0, st, V, W,
+                       Nm, p, b, k, U, Wt);
+    OCM_CHECK_LAUNCH("k_deflate_operands");
+    const dim3 gd((p + DT - 1) / DT, (p + DT - 1) / DT, 1);
+    hipLaunchKernelGGL(k_dgemm<2>, gd, dim3(256), 0, st, U, (int64_t)(2 * k), Wt, (int64_t)p, Ct, (int64_t)p, p, p,
+                       2 * k, 2 * k, C, (int64_t)p, dpart);
+    OCM_CHECK_LAUNCH("k_dgemm deflate");
+    hipLaunchKernelGGL(k_sum_pairs, dim3(1), dim3(256), 0, st, dpart, (int)(gd.x * gd.y), tr2);
     OCM_CHECK_LAUNCH("k_sum_pairs");
     OCM_HIP(hipMemcpyAsync(theta_out, tr2, 2 * sizeof(double), hipMemcpyDeviceToDevice, st));
     if (theta_mode >= 2) {
-      dim3 g((p + DT - 1) / DT, (p + DT - 1) / DT, 1);
+      const int nt = (p + DT - 1) / DT;
+      dim3 g((unsigned)(nt * (nt + 1) / 2), 1, 1);
       hipLaunchKernelGGL(k_dgemm<1>, g, dim3(256), 0, st, Ct, (int64_t)p, Ct, (int64_t)p, nullptr, 0, p, p, p, p, Ct,
                          (int64_t)p, tpart);
       OCM_CHECK_LAUNCH("k_dgemm trace");
-      hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(64), 0, st, tpart, (int)trace_wgs, theta_out + 2);
+      hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, tpart, (int)g.x, theta_out + 2);
       OCM_CHECK_LAUNCH("k_sum_partials");
     } else {
       OCM_HIP(hipMemsetAsync(theta_out + 2, 0, sizeof(double), st));
@@ -711,8 +902,8 @@ int ocm_sym_pinv_f64(ocm_ctx* ctx, const double* A, int32_t d, double rcond, dou
   ocm::Carve cv{static_cast<char*>(w)};
   double* ev = cv.take<double>(d);
   double* Z = cv.take<double>((size_t)d * d);
-  hipLaunchKernelGGL(k_jacobi, dim3(1), dim3(256), 0, st, A, d, 60, ev, Z, nullptr);
-  OCM_CHECK_LAUNCH("k_jacobi");
+  const int rc = jacobi(A, d, 60, ev, Z, st);
+  if (rc) return rc;
   hipLaunchKernelGGL(k_pinv_from_eig, dim3((d * d + 255) / 256), dim3(256), 0, st, ev, Z, d,
                      rcond > 0 ? rcond : 1e-15, out);
   OCM_CHECK_LAUNCH("k_pinv_from_eig");

@@ -36,13 +36,7 @@ struct DecArgs {
   double t2_scale, q_scale, dlim;
 };
 
-__device__ __forceinline__ double dred_of(int type, double t, double q) {
-  switch (type) {
-    case OCM_TYPE_SIM: return fmax(t, q);
-    case OCM_TYPE_ALT: return sqrt(t * t + q * q);
-    default: return t + q;  // ci, dd
-  }
-}
+using ocm::dred_of;
 
 // Shared epilogue: T rows gathered through LDS (f64), T² = tᵀ A t, Q, fused
 // decision, per-workgroup moment partials.  accT64 holds Tᵀ in the 32×32 MFMA

@@ -35,6 +35,13 @@ class OcmDecision(ctypes.Structure):
     _fields_ = [("type", c_i32), ("pad_", c_i32), ("t2_scale", c_f64), ("q_scale", c_f64), ("dlim", c_f64)]
 
 
+class OcmCvConfig(ctypes.Structure):
+    _fields_ = [("lv", c_i32), ("type", c_i32), ("t2_scale", c_f64), ("q_scale", c_f64), ("dlim", c_f64)]
+
+
+OCM_CV_MAXCFG = 1024
+
+
 class OcmError(RuntimeError):
     pass
 
@@ -70,6 +77,12 @@ SIGNATURES = {
     "ocm_cast_f64_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_void_p]),
     "ocm_percentile": (c_i32, [c_void_p, c_void_p, c_i32, c_i64, c_f64, ctypes.POINTER(c_f64), c_void_p]),
     "ocm_radix_hist": (c_i32, [c_void_p, c_void_p, c_i32, c_i64, ctypes.c_uint64, c_i32, c_void_p, c_void_p]),
+    "ocm_gram_combine": (c_i32, [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p),
+                                 ctypes.POINTER(c_f64), c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
+    "ocm_cv_prefix": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_void_p, c_void_p, ctypes.POINTER(c_i32), c_i32,
+                              c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ocm_cv_counts": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_void_p, c_i64,
+                              ctypes.POINTER(OcmCvConfig), c_i32, c_void_p, c_void_p, c_void_p]),
 }
 
 _lib = None

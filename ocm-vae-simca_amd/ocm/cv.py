@@ -1,5 +1,371 @@
-"""Fold engine for class-wise SIMCA cross-validation (filled in below)."""
+"""Fold engine for class-wise SIMCA cross-validation (C3).
+
+Replaces the per-(combo, LV, fold) refit loop of utils/CVSIMCA.py:145-222
+for this package's SIMCA under a ``ClasswiseKFoldWithExternalVal`` split:
+
+* one segmented Gram pass over the target-class rows, segments = folds
+  (``ocm_gram_f32``); fold f trains on Gram(total) − Gram(f) (fp64
+  downdating, ``ocm_cov_from_gram`` with coefficients +1/−1);
+* one eigensolve per fold at LV_max; every LV in the sweep is a prefix of it
+  (the LV-component PCA of the same class matrix is the leading LV of the
+  same decomposition, utils/SIMCA.py:64-70); the tail moments θ for LV are
+  θ(LV_max) plus the eigenvalues LV..LV_max−1;
+* each fold's test rows (held-out fold ∪ all other-class rows,
+  utils/CVSIMCA.py:77-80) are scored ONCE at LV_max by row index
+  (``ocm_score_f32``); ``ocm_cv_counts`` turns those scores into confusion
+  counts for every (param combo, LV) decision at once;
+* training-row statistics (``perc`` / ``chi2pom`` limits) come from one more
+  scoring of the fold's training rows and ``ocm_cv_prefix``.
+
+Aggregation is the reference's: spec = mean over folds of TN/(TN+FP)·100
+(:195-203), sens from the pooled prediction vector, where target rows carry
+their own fold's prediction and other-class rows the LAST fold's
+(:190, 205-207), eff = √(sens·spec) (:208).
+
+Multi-GPU (``group`` given): each rank holds a contiguous row block of X
+(``row_offset``) and the full label vector.  Per-fold Grams are summed by one
+RCCL all-reduce, fold f's eigensolve runs on rank f mod W and its model is
+broadcast, every rank scores its own rows, and the confusion counts and
+training moments are all-reduced.  Same code path at W = 1 without
+collectives.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import engine, limits
+
+__all__ = ["grid", "cv_grid", "FoldModels"]
+
+
+class _Spec:
+    """The limit-relevant configuration of one param combo (SIMCA kwargs)."""
+
+    def __init__(self, params: dict):
+        self.type = params.get("type", "alt")
+        self.t2lim = params.get("t2lim", "Fdist")
+        self.t2cl = params.get("t2cl", 0.95)
+        self.qlim = params.get("qlim", "jm")
+        self.qcl = params.get("qcl", 0.95)
+        self.dcl = params.get("dcl", 0.95)
+        if self.type == "dd":  # utils/SIMCA.py:42-48
+            self.t2lim = "chi2pom"
+            self.qlim = "chi2pom"
+
+    def needs_train_stats(self) -> bool:
+        return self.t2lim in ("perc", "chi2pom") or self.qlim in ("perc", "chi2pom")
+
+    def needs_percentile(self) -> bool:
+        return self.t2lim == "perc" or self.qlim == "perc"
+
+
+def _applicable(base_est, X, y, cv, lv_values, param_grid):
+    """The fold engine covers this package's SIMCA (not wrapped in a Pipeline),
+    a ClasswiseKFoldWithExternalVal split, an LV sweep, and a single target
+    label whose model_class is that label (or None)."""
+    from sklearn.model_selection import ParameterGrid
+    from utils.CVSIMCA import ClasswiseKFoldWithExternalVal
+    from utils.SIMCA import SIMCA
+
+    if type(base_est) is not SIMCA or not isinstance(cv, ClasswiseKFoldWithExternalVal):
+        return None
+    if lv_values is None or len(lv_values) == 0 or y is None:
+        return None
+    y = np.asarray(y)
+    cls_idx = cv.target_indices(X, y)
+    labels = np.unique(y[cls_idx])
+    if labels.size != 1:
+        return None
+    tl = labels[0]
+    combos = list(ParameterGrid(param_grid))
+    base = base_est.get_params()
+    for combo in combos:
+        params = dict(base, **combo)
+        mc = params.get("model_class")
+        if mc is not None and not np.array_equal(np.ravel(np.asarray(mc)), np.asarray([tl])):
+            return None
+    if max(lv_values) > 64 or min(lv_values) < 1:
+        return None
+    return cls_idx, tl, combos, base
 
 
 def grid(base_est, X, y, cv, lv_values, param_grid, class_index, store_predictions):
-    return None, None
+    """utils/CVSIMCA.py drop-in hook: (records, by_combo), or (None, None)
+    when the fold engine does not cover the configuration."""
+    app = _applicable(base_est, X, y, cv, lv_values, param_grid)
+    if app is None:
+        return None, None
+    cls_idx, tl, combos, base = app
+    if class_index is None:
+        # the reference reads simca.model_class after fit: the list [label]
+        class_index = [tl]
+    y = np.asarray(y)
+    folds = [cls_idx[test_rel] for _, test_rel in cv.kf.split(cls_idx)]
+    return cv_grid(X, y, folds, cls_idx, lv_values, combos, base, class_index, store_predictions)
+
+
+class FoldModels:
+    """Per-fold eigen-models at LV_max (device tensors on every rank)."""
+
+    def __init__(self):
+        self.evals = []     # (LVmax,) f64 device
+        self.evecs = []     # (LVmax, p) f64 device
+        self.mean = []      # (p,) f64 device
+        self.inv = []       # (LVmax,) f64 device: diag of invcovT
+        self.evals_h = []   # host numpy
+        self.theta_h = []   # host (3,) tail moments at LVmax
+        self.n_train = []
+
+
+def _inv_evals(evals: torch.Tensor, rcond=1e-15) -> torch.Tensor:
+    cut = rcond * evals.abs().max()
+    return torch.where(evals.abs() > cut, 1.0 / evals, torch.zeros_like(evals))
+
+
+def _thetas_for(lv, lvmax, evals_h, theta_h):
+    """θ_m(LV) = Σ_{i>LV} λ_i^m = θ_m(LVmax) + Σ_{LV≤i<LVmax} λ_i^m."""
+    tail = evals_h[lv:lvmax]
+    return (float(theta_h[0] + np.sum(tail)), float(theta_h[1] + np.sum(tail ** 2)),
+            float(theta_h[2] + np.sum(tail ** 3)))
+
+
+def _local(idx: np.ndarray, lo: int, hi: int) -> np.ndarray:
+    """Global row indices in [lo, hi) → local indices."""
+    sel = idx[(idx >= lo) & (idx < hi)]
+    return (sel - lo).astype(np.int64)
+
+
+def _rates(TP, TN, FP, FN):
+    """utils/SIMCA.py:246-250 on int64 counts (NaN on an empty denominator)."""
+    TP, TN, FP, FN = (np.int64(v) for v in (TP, TN, FP, FN))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        sens = TP / (TP + FN) * 100
+        spec = TN / (TN + FP) * 100
+    return sens, spec
+
+
+def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, store_predictions,
+            row_offset=0, group=None):
+    """The fold engine.  X: this rank's rows (host array or device tensor) =
+    global rows [row_offset, row_offset + len(X)); y, folds, cls_idx: global.
+    Returns (records, by_combo) in the reference's record order."""
+    Xd = engine.as_device_f32(X)
+    dev = Xd.device
+    n_loc, p = Xd.shape
+    lo, hi = row_offset, row_offset + n_loc
+    y = np.asarray(y)
+    n_glob = y.shape[0]
+    distributed = group is not None or (dist.is_available() and dist.is_initialized()
+                                        and dist.get_world_size() > 1)
+    W = dist.get_world_size(group) if distributed else 1
+    R = dist.get_rank(group) if distributed else 0
+    K = len(folds)
+    lvs = sorted(set(int(v) for v in lv_values))
+    lvmax = lvs[-1]
+    if lvmax > p:
+        raise ValueError(f"n_components={lvmax} must be in [1, {p}]")
+    specs = [_Spec(dict(base_params, **c)) for c in combos]
+    theta_mode = max(limits.theta_mode_for(s) for s in specs)
+    need_train = any(s.needs_train_stats() for s in specs)
+    need_pct = any(s.needs_percentile() for s in specs)
+    others = np.setdiff1d(np.arange(n_glob), cls_idx)
+    positive_glob = (y == np.asarray(class_index)) if np.ndim(class_index) else (y == class_index)
+    positive_glob = np.asarray(positive_glob, dtype=bool).reshape(n_glob)
+    n_target = int(cls_idx.size)
+
+    # ---- pass 1: per-fold Grams of the target rows (one HBM pass) ----
+    loc_folds = [_local(f, lo, hi) for f in folds]
+    order = np.concatenate(loc_folds) if loc_folds else np.zeros(0, np.int64)
+    seg = np.concatenate([[0], np.cumsum([f.size for f in loc_folds])]).astype(np.int64)
+    rows_t = torch.from_numpy(order).to(dev)
+    if order.size:
+        shift64 = engine.colmean(Xd, rows_t, min(int(order.size), engine.SHIFT_SAMPLE))
+    else:
+        shift64 = torch.zeros(p, dtype=torch.float64, device=dev)
+    if distributed:
+        has = torch.tensor([1.0 if order.size else 0.0], dtype=torch.float64, device=dev)
+        shift64 = shift64 * has
+        dist.all_reduce(shift64, group=group)
+        dist.all_reduce(has, group=group)
+        shift64 /= has
+    shift32 = engine.cast_f32(shift64)
+    if order.size:
+        G, cs = engine.gram(Xd, rows_t, seg, shift32)
+    else:
+        G = torch.zeros((K, p, p), dtype=torch.float64, device=dev)
+        cs = torch.zeros((K, p), dtype=torch.float64, device=dev)
+    if distributed:
+        dist.all_reduce(G, group=group)
+        dist.all_reduce(cs, group=group)
+    Gt = torch.empty((p, p), dtype=torch.float64, device=dev)
+    cst = torch.empty(p, dtype=torch.float64, device=dev)
+    engine.gram_combine([(1.0, G[f], cs[f]) for f in range(K)], Gt, cst)
+
+    # ---- per-fold eigen-models (fold f on rank f mod W, then broadcast) ----
+    models = FoldModels()
+    for f in range(K):
+        n_tr = n_target - int(folds[f].size)
+        if n_tr < 2:
+            raise ValueError("SIMCA needs at least 2 samples in a class")
+        pack = torch.empty(lvmax + 3 + p + lvmax * p, dtype=torch.float64, device=dev)
+        if f % W == R:
+            C, mean = engine.cov_from_gram([(1.0, Gt, cst), (-1.0, G[f], cs[f])], shift32, n_tr)
+            evals, evecs, theta, _ = engine.eig_topk(C, lvmax, theta_mode)
+            del C
+            pack[:lvmax] = evals
+            pack[lvmax:lvmax + 3] = theta
+            pack[lvmax + 3:lvmax + 3 + p] = mean
+            pack[lvmax + 3 + p:] = evecs.reshape(-1)
+        if distributed:
+            dist.broadcast(pack, src=dist.get_global_rank(group, f % W) if group is not None else f % W,
+                           group=group)
+        evals = pack[:lvmax]
+        models.evals.append(evals)
+        models.mean.append(pack[lvmax + 3:lvmax + 3 + p])
+        models.evecs.append(pack[lvmax + 3 + p:].view(lvmax, p))
+        models.inv.append(_inv_evals(evals))
+        host = pack[:lvmax + 3].cpu().numpy()
+        models.evals_h.append(host[:lvmax])
+        models.theta_h.append(host[lvmax:lvmax + 3])
+        models.n_train.append(n_tr)
+    del G, cs, Gt
+
+    # ---- per-fold scoring, limits, counts ----
+    ncfg = len(combos) * len(lvs)
+    counts = np.zeros((K, ncfg, 2, 4), dtype=np.int64)
+    preds_fold = [] if store_predictions else None
+    others_loc = _local(others, lo, hi)
+    F_cache = {}
+    for f in range(K):
+        mean, evecs, inv = models.mean[f], models.evecs[f], models.inv[f]
+        A = torch.diag(inv)
+        n_tr = models.n_train[f]
+        # training-row statistics per LV (perc / chi2pom limits)
+        tr_stats = None
+        tr_arrays = None
+        if need_train:
+            tr_loc = np.concatenate([loc_folds[g] for g in range(K) if g != f]) if K > 1 else np.zeros(0, np.int64)
+            if tr_loc.size:
+                rows = torch.from_numpy(tr_loc).to(dev)
+                sc = engine.score(Xd, rows, int(tr_loc.size), evecs, mean, A, want_T=True, want_T2=False,
+                                  want_Q=True)
+                T2a, Qa, st = engine.cv_prefix(sc["T"], sc["Q"], inv, lvs, want_T2=need_pct, want_Q=need_pct,
+                                               want_stats=True)
+                del sc
+            else:
+                T2a = torch.zeros((len(lvs), 0), dtype=torch.float64, device=dev) if need_pct else None
+                Qa = torch.zeros((len(lvs), 0), dtype=torch.float32, device=dev) if need_pct else None
+                st = torch.zeros((len(lvs), 4), dtype=torch.float64, device=dev)
+            if distributed:
+                dist.all_reduce(st, group=group)
+            tr_stats = st.cpu().numpy()
+            tr_arrays = (T2a, Qa)
+
+        # limits → decision configs (host fp64, utils/SIMCA.py:156-236)
+        configs = []
+        for s in specs:
+            for li, lv in enumerate(lvs):
+                th = _thetas_for(lv, lvmax, models.evals_h[f], models.theta_h[f])
+                if tr_stats is not None:
+                    T2a, Qa = tr_arrays
+                    s1 = tr_stats[li]
+                    T2m = limits.Moments(n_tr, s1[0], s1[1], _pct_fn(T2a, li, n_tr, group, distributed))
+                    Qm = limits.Moments(n_tr, s1[2], s1[3], _pct_fn(Qa, li, n_tr, group, distributed))
+                else:
+                    T2m = Qm = limits.Moments(n_tr, 0.0, 0.0, None)
+                key = (s.t2lim, s.t2cl, lv, n_tr)
+                if s.t2lim in ("Fdist", "Fdistrig", "chi2") and key in F_cache:
+                    t2l = F_cache[key]
+                else:
+                    t2l = limits.t2_limit(s, T2m, lv)
+                    if s.t2lim in ("Fdist", "Fdistrig", "chi2"):
+                        F_cache[key] = t2l
+                ql = limits.q_limit(s, Qm, th)
+                dl = limits.critic_distance(s, t2l, ql, th, lv)
+                if s.type == "dd":
+                    configs.append((lv, "dd", s._t2dof / s._t2scfact, s._qdof / s._qscfact, float(dl)))
+                else:
+                    configs.append((lv, s.type, 1.0 / t2l, 1.0 / ql, float(dl)))
+
+        # held-out fold ∪ other-class rows, scored once at LV_max
+        fold_loc = loc_folds[f]
+        test_loc = np.concatenate([fold_loc, others_loc])
+        m = int(test_loc.size)
+        if m:
+            rows = torch.from_numpy(test_loc).to(dev)
+            pos = torch.from_numpy(positive_glob[test_loc + lo].astype(np.uint8)).to(dev)
+            sc = engine.score(Xd, rows, m, evecs, mean, A, want_T=True, want_T2=False, want_Q=True)
+            cnt, acc = engine.cv_counts(sc["T"], sc["Q"], inv, pos, int(fold_loc.size), configs,
+                                        want_accept=store_predictions)
+            del sc
+        else:
+            cnt = torch.zeros((ncfg, 2, 4), dtype=torch.int64, device=dev)
+            acc = torch.zeros((ncfg, 0), dtype=torch.float64, device=dev) if store_predictions else None
+        if distributed:
+            dist.all_reduce(cnt, group=group)
+        counts[f] = cnt.cpu().numpy()
+        if store_predictions:
+            preds_fold.append((test_loc + lo, acc.cpu().numpy()))
+
+    # ---- aggregation (utils/CVSIMCA.py:190-222) ----
+    records, by_combo = [], []
+    if store_predictions and distributed:
+        preds_fold = _gather_predictions(preds_fold, group)
+    for ci_, combo in enumerate(combos):
+        for li, lv in enumerate(lvs):
+            c = ci_ * len(lvs) + li
+            step_spec = np.zeros(K, dtype=float)
+            for f in range(K):
+                tot = counts[f, c, 0] + counts[f, c, 1]
+                step_spec[f] = _rates(*tot)[1]
+            pooled = counts[:, c, 0].sum(axis=0) + counts[K - 1, c, 1]
+            sens = float(_rates(*pooled)[0])
+            spec = float(np.mean(step_spec))
+            records.append({"params": combo.copy(), "LV": lv, "spec": spec, "sens": sens,
+                            "eff": float(np.sqrt(sens * spec))})
+            if store_predictions:
+                pred_vec = np.zeros(n_glob, dtype=float)
+                for f in range(K):
+                    idx, acc = preds_fold[f]
+                    pred_vec[idx] = acc[c]
+                by_combo.append({"params": combo.copy(), "LV": lv, "prediction": pred_vec})
+    # keep the reference's record order: combos outer, LV in the given order
+    if list(lv_values) != lvs:
+        order = {lv: i for i, lv in enumerate(lvs)}
+        per = len(lvs)
+        recs, bys = [], []
+        for ci_ in range(len(combos)):
+            for lv in lv_values:
+                recs.append(records[ci_ * per + order[int(lv)]])
+                if store_predictions:
+                    bys.append(by_combo[ci_ * per + order[int(lv)]])
+        records, by_combo = recs, bys
+    return records, by_combo
+
+
+def _pct_fn(arr, li, n, group, distributed):
+    if arr is None:
+        return None
+
+    def pct(q):
+        v = arr[li]
+        if distributed:
+            from .dist import percentile_sharded
+
+            return percentile_sharded(v, q, n, group)
+        return engine.percentile(v, q)
+
+    return pct
+
+
+def _gather_predictions(preds_fold, group):
+    """All ranks' (global row index, accept) pairs per fold → every rank."""
+    W = dist.get_world_size(group)
+    out = []
+    for idx, acc in preds_fold:
+        got = [None] * W
+        dist.all_gather_object(got, (idx, acc), group=group)
+        out.append((np.concatenate([g[0] for g in got]), np.concatenate([g[1] for g in got], axis=1)))
+    return out

@@ -8,7 +8,7 @@ MI355X:
     G, s   = Σ (x-shift)(x-shift)ᵀ, Σ (x-shift) ocm_gram_f32      (FP32 MFMA, 1 HBM pass)
     C, μ   = (G - n d dᵀ)/(n-1), shift + d      ocm_cov_from_gram
     λ, P, θ = top-k eigenpairs, tail moments   ocm_eig_topk      (fp64, HBM-resident C)
-    T, T², Q (+ moments)                        ocm_score_f32     (FP64 MFMA, one pass, fused)
+    T, T², Q (+ moments, fused decision)        ocm_score_f32     (FP32 MFMA projection, 2 register-streamed sweeps)
     limits                                      host fp64 scalars (ocm/limits.py)
 
 All arrays stay in HBM; only scalars cross to the host.  The second,
@@ -202,6 +202,50 @@ def percentile(v: torch.Tensor, pct: float) -> float:
     check(_lib.load().ocm_percentile(ctx.handle, ptr(v), dtype, v.numel(), float(pct), ctypes.byref(out),
                                      _stream(v.device)), "ocm_percentile")
     return out.value
+
+
+def gram_combine(terms, G_out: torch.Tensor | None, cs_out: torch.Tensor | None):
+    """G_out = Σ coef·G, cs_out = Σ coef·colsum over terms [(coef, G, colsum)]."""
+    nt = len(terms)
+    dev = terms[0][1].device
+    p = terms[0][1].shape[-1]
+    Gp = (ctypes.c_void_p * nt)(*[t[1].data_ptr() for t in terms])
+    Sp = (ctypes.c_void_p * nt)(*[t[2].data_ptr() for t in terms])
+    cf = (ctypes.c_double * nt)(*[float(t[0]) for t in terms])
+    check(_lib.load().ocm_gram_combine(Context.get(dev.index).handle, Gp, Sp, cf, nt, p, ptr(G_out), ptr(cs_out),
+                                       _stream(dev)), "ocm_gram_combine")
+
+
+def cv_prefix(T: torch.Tensor, Q: torch.Tensor, inv_evals: torch.Tensor, lvs, want_T2=False, want_Q=False,
+              want_stats=True):
+    """Per-LV T² / Q of rows scored at LV_max (+ moments {ΣT², ΣT²², ΣQ, ΣQ²} per LV)."""
+    m, k = T.shape
+    dev = T.device
+    nlv = len(lvs)
+    T2o = torch.empty((nlv, m), dtype=torch.float64, device=dev) if want_T2 else None
+    Qo = torch.empty((nlv, m), dtype=torch.float32, device=dev) if want_Q else None
+    st = torch.empty((nlv, 4), dtype=torch.float64, device=dev) if want_stats else None
+    arr = (ctypes.c_int32 * nlv)(*[int(v) for v in lvs])
+    check(_lib.load().ocm_cv_prefix(Context.get(dev.index).handle, ptr(T), m, k, ptr(Q), ptr(inv_evals), arr, nlv,
+                                    ptr(T2o), ptr(Qo), ptr(st), _stream(dev)), "ocm_cv_prefix")
+    return T2o, Qo, st
+
+
+def cv_counts(T: torch.Tensor, Q: torch.Tensor, inv_evals: torch.Tensor, positive: torch.Tensor, m_split: int,
+              configs, want_accept=False):
+    """Confusion counts (ncfg, 2, 4) uint64-as-int64 {TP, TN, FP, FN} for rows [0, m_split) and
+    [m_split, m); configs = [(lv, type_name, t2_scale, q_scale, dlim)]."""
+    m, k = T.shape
+    dev = T.device
+    nc = len(configs)
+    counts = torch.empty((nc, 2, 4), dtype=torch.int64, device=dev)
+    acc = torch.empty((nc, m), dtype=torch.float64, device=dev) if want_accept else None
+    arr = (_lib.OcmCvConfig * nc)(*[_lib.OcmCvConfig(int(lv), TYPE_CODES[ty], float(a), float(b), float(d))
+                                    for (lv, ty, a, b, d) in configs])
+    check(_lib.load().ocm_cv_counts(Context.get(dev.index).handle, ptr(T), m, k, ptr(Q), ptr(inv_evals),
+                                    ptr(positive), int(m_split), arr, nc, ptr(counts), ptr(acc), _stream(dev)),
+          "ocm_cv_counts")
+    return counts, acc
 
 
 def rowsq_residual(x: torch.Tensor, xhat: torch.Tensor) -> torch.Tensor:
