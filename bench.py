@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--k", type=int, default=20)
     ap.add_argument("--cpu-sample", type=int, default=65536, help="rows for the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-vae", action="store_true", help="skip the secondary VAE train-steps/s measurement")
+    ap.add_argument("--vae-steps", type=int, default=200)
     return ap.parse_args()
 
 
@@ -94,6 +96,39 @@ def cpu_baseline(rows, p, k):
     return {"value": rows / dt, "unit": "spectra/s", "cores": int(threads), "kind": "port",
             "sample": f"{rows}x{p} fp32, k={k}, alt/Fdist/jm: float32 full SVD + randomized PCA(k) + "
                       f"NumPy scores, fit+predict on the same rows ({dt:.2f} s)"}
+
+
+def vae_bench(device, steps, warmup, batch=512, length=2048):
+    """Secondary metric (BASELINE.json): VAE-SIMCA train steps/s, C4 network
+    (cb=3, nf=3, ks=7, hid=64, d=32) at B=512 × L=2048 in bf16,
+    one HIP-graph replay per optimizer step (ocm/vae_train.py)."""
+    import torch
+
+    import vae_model as V
+    from ocm.vae_train import GraphedVAETrainer
+
+    nb = 16
+    X = synth_device(batch * nb, length, 20, seed=99, device=device)
+    mean = X.mean(0).cpu().numpy()
+    std = X.std(0).cpu().numpy() + 1e-6
+    torch.manual_seed(0)
+    m = V.ConvVAE1D(length, 32, mean, std, conv_blocks=3, n_filters=3, kernel_size=7, hidden_fc=64).to(device)
+    tr = GraphedVAETrainer(m, batch, lr=1e-3, dtype=torch.bfloat16)
+    for i in range(warmup):
+        tr.step(X[(i % nb) * batch:(i % nb + 1) * batch])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        tr.step(X[(i % nb) * batch:(i % nb + 1) * batch])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    loss = float(tr.out[0].item())
+    return {"metric": "VAE-SIMCA train steps/sec", "value": round(steps / dt, 2), "unit": "steps/s",
+            "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "dtype": "bf16",
+            "config": {"workload": f"ConvVAE1D cb=3 nf=3 ks=7 hid=64 d=32, B={batch}, L={length}, "
+                                   "BCE-with-logits + KL, Adam, HIP-graph step",
+                       "params": sum(p.numel() for p in m.parameters())},
+            "reference_cpu_steps_per_s": 2.5, "final_loss": round(loss, 5)}
 
 
 def main():
@@ -207,6 +242,11 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample, p, k)
         except Exception as e:  # report, never fail the GPU number
             out["cpu_baseline"] = {"error": repr(e)}
+    if world == 1 and not args.no_vae:
+        try:
+            out["vae"] = vae_bench(device, args.vae_steps, 10)
+        except Exception as e:  # report, never fail the primary number
+            out["vae"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -147,11 +147,13 @@ int ocm_decide(ocm_ctx* ctx, const double* T2, const float* Q, int64_t m, const 
                double* t2red_out, double* qred_out, double* dred_out, double* accept_out, int64_t accept_stride,
                void* stream);
 
-/* q_i = Σ_j (x_ij - xhat_ij)² for a VAE reconstruction (vae_model.py:164,
- * utils/final_vaesimca.py:425,492).  x, xhat [dev] m×p float32 (ld), q_out
- * [dev] m floats. */
-int ocm_rowsq_residual_f32(ocm_ctx* ctx, const float* x, const float* xhat, int64_t m, int32_t p, int64_t ld,
-                           float* q_out, void* stream);
+/* q_i = Σ_j (x_ij - xhat_ij)² (fp64 accumulation) for a VAE reconstruction
+ * (vae_model.py:164, utils/final_vaesimca.py:425,492), the latent round-trip Q
+ * (VAE_SIMCA.py:256-259, 365-366) and the Euclidean latent distance h about a
+ * stored mean (utils/final_vaesimca.py:510-512: ldxh = 0 broadcasts one xhat
+ * row).  x [dev] m×p float32 (ldx), xhat [dev] (ldxh), q_out [dev] m floats. */
+int ocm_rowsq_residual_f32(ocm_ctx* ctx, const float* x, int64_t ldx, const float* xhat, int64_t ldxh, int64_t m,
+                           int32_t p, float* q_out, void* stream);
 
 /* b[i] = (float)a[i] — loadings / mean handed to the float32 scoring kernel. */
 int ocm_cast_f64_f32(ocm_ctx* ctx, const double* a, int64_t n, float* b, void* stream);

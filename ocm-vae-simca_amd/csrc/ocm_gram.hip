@@ -335,6 +335,143 @@ __global__ void k_cov(CovTerms tm, const double* __restrict__ dvec, int p, doubl
   C[e] = (g - n * dvec[i] * dvec[j]) / (n - 1.0);
 }
 
+// ---------------------------------------------------------------------------
+// Narrow matrices (p ≤ 64: VAE latents, tiny spectra): fp64 accumulation.
+// Latent covariances can be badly conditioned (the leverage / Mahalanobis
+// forms square it), so the FP32-MFMA path's ~1e-7 relative Gram error is not
+// acceptable there; at p ≤ 64 the fp64 VALU work (n·p²/2 FMAs) is negligible.
+// One workgroup per chunk of one segment: 64-row tiles of y = x − shift (fp64)
+// in LDS, each thread owns a fixed set of upper-triangle pairs.
+// ---------------------------------------------------------------------------
+constexpr int SMALL_P = 64, SMALL_ROWS = 64, SMALL_CHUNK = 2048;
+
+__global__ __launch_bounds__(256) void k_gram_small(const float* __restrict__ X, int64_t ldx,
+                                                    const int64_t* __restrict__ rows, int p,
+                                                    const float* __restrict__ shift,
+                                                    const int64_t* __restrict__ span,
+                                                    double* __restrict__ part, double* __restrict__ cpart) {
+  __shared__ double ys[SMALL_ROWS][SMALL_P + 1];
+  __shared__ short pi[SMALL_P * (SMALL_P + 1) / 2], pj[SMALL_P * (SMALL_P + 1) / 2];
+  const int tid = threadIdx.x;
+  const int npair = p * (p + 1) / 2;
+  if (tid == 0) {
+    int e = 0;
+    for (int i = 0; i < p; ++i)
+      for (int j = i; j < p; ++j) {
+        pi[e] = (short)i;
+        pj[e] = (short)j;
+        ++e;
+      }
+  }
+  const int64_t r0 = span[2 * blockIdx.x], r1 = span[2 * blockIdx.x + 1];  // rows [r0, r1)
+  constexpr int MAXPT = (SMALL_P * (SMALL_P + 1) / 2 + 255) / 256;  // pairs per thread
+  double acc[MAXPT];
+#pragma unroll
+  for (int u = 0; u < MAXPT; ++u) acc[u] = 0.0;
+  double csum = 0.0;
+  for (int64_t b = r0; b < r1; b += SMALL_ROWS) {
+    const int nr = (int)min<int64_t>(SMALL_ROWS, r1 - b);
+    __syncthreads();
+    for (int e = tid; e < SMALL_ROWS * p; e += 256) {
+      const int r = e / p, c = e % p;
+      double v = 0.0;
+      if (r < nr) {
+        const int64_t sr = rows ? rows[b + r] : b + r;
+        v = (double)X[sr * ldx + c] - (double)shift[c];
+      }
+      ys[r][c] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < MAXPT; ++u) {
+      const int e = tid + 256 * u;
+      if (e < npair) {
+        const int i = pi[e], j = pj[e];
+        double a = acc[u];
+        for (int r = 0; r < nr; ++r) a += ys[r][i] * ys[r][j];
+        acc[u] = a;
+      }
+    }
+    if (tid < p)
+      for (int r = 0; r < nr; ++r) csum += ys[r][tid];
+  }
+#pragma unroll
+  for (int u = 0; u < MAXPT; ++u) {
+    const int e = tid + 256 * u;
+    if (e < npair) part[(size_t)blockIdx.x * npair + e] = acc[u];
+  }
+  if (tid < p) cpart[(size_t)blockIdx.x * p + tid] = csum;
+}
+
+// G (full symmetric) and colsum of one segment = ordered sum of its chunks
+__global__ __launch_bounds__(256) void k_gram_small_reduce(const double* __restrict__ part,
+                                                           const double* __restrict__ cpart, int p, int c0, int c1,
+                                                           double* __restrict__ G, double* __restrict__ colsum) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int npair = p * (p + 1) / 2;
+  if (e < npair) {
+    // e -> (i, j), i <= j, row-major upper triangle
+    int i = 0, rem = e;
+    while (rem >= p - i) {
+      rem -= p - i;
+      ++i;
+    }
+    const int j = i + rem;
+    double v = 0.0;
+    for (int c = c0; c < c1; ++c) v += part[(size_t)c * npair + e];
+    G[(size_t)i * p + j] = v;
+    G[(size_t)j * p + i] = v;
+  }
+  if (e < p) {
+    double v = 0.0;
+    for (int c = c0; c < c1; ++c) v += cpart[(size_t)c * p + e];
+    colsum[e] = v;
+  }
+}
+
+int gram_small(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int32_t p, const float* shift,
+               const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out, hipStream_t st) {
+  // chunks never straddle a segment: span = (lo, hi) row range per chunk
+  std::vector<int64_t> span;
+  std::vector<int> cpre(nseg + 1, 0);
+  for (int s = 0; s < nseg; ++s) {
+    cpre[s] = (int)(span.size() / 2);
+    for (int64_t a = seg_offsets[s]; a < seg_offsets[s + 1]; a += SMALL_CHUNK) {
+      span.push_back(a);
+      span.push_back(std::min<int64_t>(a + SMALL_CHUNK, seg_offsets[s + 1]));
+    }
+  }
+  const int nchunk = (int)(span.size() / 2);
+  cpre[nseg] = nchunk;
+  const int npair = p * (p + 1) / 2;
+  const size_t need = (size_t)nchunk * (npair + p) * sizeof(double) + span.size() * sizeof(int64_t) + 1024;
+  void* w = ocm::workspace(ctx, need, st);
+  if (!w) return OCM_ERR_NOMEM;
+  ocm::Carve cv{static_cast<char*>(w)};
+  double* part = cv.take<double>((size_t)nchunk * npair);
+  double* cpart = cv.take<double>((size_t)nchunk * p);
+  int64_t* dspan = cv.take<int64_t>(span.size());
+  if (nchunk > 0) {
+    // pageable source: staged before the call returns
+    OCM_HIP(hipMemcpyAsync(dspan, span.data(), span.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_gram_small, dim3(nchunk), dim3(256), 0, st, X, ldx, rows, p, shift, dspan, part, cpart);
+    OCM_CHECK_LAUNCH("k_gram_small");
+  }
+  for (int s = 0; s < nseg; ++s) {
+    double* Gs = G_out + (size_t)s * p * p;
+    double* cs = colsum_out + (size_t)s * p;
+    if (cpre[s + 1] == cpre[s]) {
+      OCM_HIP(hipMemsetAsync(Gs, 0, (size_t)p * p * sizeof(double), st));
+      OCM_HIP(hipMemsetAsync(cs, 0, (size_t)p * sizeof(double), st));
+      continue;
+    }
+    hipLaunchKernelGGL(k_gram_small_reduce, dim3((npair + 255) / 256), dim3(256), 0, st, part, cpart, p, cpre[s],
+                       cpre[s + 1], Gs, cs);
+    OCM_CHECK_LAUNCH("k_gram_small_reduce");
+  }
+  return OCM_OK;
+}
+
 template <int GT, int BK>
 int gram_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
               const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
@@ -438,6 +575,8 @@ int ocm_gram_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows,
   for (int s = 0; s < nseg; ++s)
     OCM_REQUIRE(seg_offsets[s + 1] >= seg_offsets[s], "ocm_gram_f32: seg_offsets not ascending");
   hipStream_t st = (hipStream_t)stream;
+  if (p <= SMALL_P && !std::getenv("OCM_GRAM_FORCE_MFMA"))
+    return gram_small(ctx, X, ldx, rows, p, shift, seg_offsets, nseg, G_out, colsum_out, st);
   // Tile: 256 when p fills at least one 256 block, else 128 (less padding).
   // OCM_GRAM_TILE / OCM_GRAM_CHUNK override for A/B runs.
   int tile = p > 128 ? 256 : 128;

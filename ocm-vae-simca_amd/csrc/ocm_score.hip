@@ -625,15 +625,15 @@ __global__ void k_decide(const double* __restrict__ T2, const float* __restrict_
 }
 
 // q_i = Σ_j (x_ij − x̂_ij)², one wave per row, f64 accumulation
-__global__ __launch_bounds__(256) void k_rowsq(const float* __restrict__ x, const float* __restrict__ xh, int64_t m,
-                                               int p, int64_t ld, float* __restrict__ q) {
+__global__ __launch_bounds__(256) void k_rowsq(const float* __restrict__ x, int64_t ldx, const float* __restrict__ xh,
+                                               int64_t ldxh, int64_t m, int p, float* __restrict__ q) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= m) return;
   double s = 0.0;
   for (int j = lane; j < p; j += 64) {
-    const float d = x[r * ld + j] - xh[r * ld + j];
-    s += (double)d * d;
+    const double d = (double)x[r * ldx + j] - (double)xh[r * ldxh + j];
+    s += d * d;
   }
   s = wave_sum_f64(s);
   if (lane == 0) q[r] = (float)s;
@@ -748,13 +748,13 @@ int ocm_decide(ocm_ctx* ctx, const double* T2, const float* Q, int64_t m, const 
   return OCM_OK;
 }
 
-int ocm_rowsq_residual_f32(ocm_ctx* ctx, const float* x, const float* xhat, int64_t m, int32_t p, int64_t ld,
-                           float* q_out, void* stream) {
+int ocm_rowsq_residual_f32(ocm_ctx* ctx, const float* x, int64_t ldx, const float* xhat, int64_t ldxh, int64_t m,
+                           int32_t p, float* q_out, void* stream) {
   OCM_REQUIRE(ctx && x && xhat && q_out, "ocm_rowsq_residual_f32: NULL argument");
-  OCM_REQUIRE(p > 0 && ld >= p, "ocm_rowsq_residual_f32: bad shape");
+  OCM_REQUIRE(p > 0 && ldx >= p && (ldxh == 0 || ldxh >= p), "ocm_rowsq_residual_f32: bad shape");
   if (m <= 0) return OCM_OK;
-  hipLaunchKernelGGL(k_rowsq, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, xhat, m, p, ld,
-                     q_out);
+  hipLaunchKernelGGL(k_rowsq, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, ldx, xhat, ldxh, m,
+                     p, q_out);
   OCM_CHECK_LAUNCH("k_rowsq");
   return OCM_OK;
 }

@@ -73,7 +73,8 @@ SIGNATURES = {
                               c_void_p, c_void_p]),
     "ocm_decide": (c_i32, [c_void_p, c_void_p, c_void_p, c_i64, ctypes.POINTER(OcmDecision), c_void_p, c_void_p,
                            c_void_p, c_void_p, c_i64, c_void_p]),
-    "ocm_rowsq_residual_f32": (c_i32, [c_void_p, c_void_p, c_void_p, c_i64, c_i32, c_i64, c_void_p, c_void_p]),
+    "ocm_rowsq_residual_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i64, c_i32, c_void_p,
+                                       c_void_p]),
     "ocm_cast_f64_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_void_p]),
     "ocm_percentile": (c_i32, [c_void_p, c_void_p, c_i32, c_i64, c_f64, ctypes.POINTER(c_f64), c_void_p]),
     "ocm_radix_hist": (c_i32, [c_void_p, c_void_p, c_i32, c_i64, ctypes.c_uint64, c_i32, c_void_p, c_void_p]),

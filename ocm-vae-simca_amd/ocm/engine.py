@@ -249,11 +249,19 @@ def cv_counts(T: torch.Tensor, Q: torch.Tensor, inv_evals: torch.Tensor, positiv
 
 
 def rowsq_residual(x: torch.Tensor, xhat: torch.Tensor) -> torch.Tensor:
+    """q_i = Σ_j (x_ij − xhat_ij)² (float32 out, fp64 accumulation).  ``xhat``
+    may be one row (shape (p,) or (1, p)): it is broadcast to every row."""
     m, p = x.shape
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    bcast = xhat.dim() == 1 or xhat.shape[0] == 1
+    xh = xhat.reshape(1, p) if bcast else xhat
+    if xh.stride(-1) != 1:
+        xh = xh.contiguous()
     q = torch.empty(m, dtype=torch.float32, device=x.device)
     ctx = Context.get(x.device.index)
-    check(_lib.load().ocm_rowsq_residual_f32(ctx.handle, ptr(x), ptr(xhat), m, p, x.stride(0), ptr(q),
-                                             _stream(x.device)), "ocm_rowsq_residual_f32")
+    check(_lib.load().ocm_rowsq_residual_f32(ctx.handle, ptr(x), x.stride(0), ptr(xh), 0 if bcast else xh.stride(0),
+                                             m, p, ptr(q), _stream(x.device)), "ocm_rowsq_residual_f32")
     return q
 
 

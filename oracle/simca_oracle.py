@@ -33,6 +33,7 @@ from dataclasses import dataclass, field
 import numpy as np
 import scipy.linalg
 from scipy import stats
+from scipy import special
 from scipy.special import erfinv
 
 # ---------------------------------------------------------------------------
@@ -500,6 +501,86 @@ def full_distance_decision(mus_test: np.ndarray, latent_mean: np.ndarray, q: np.
     f = h / h0 * Nh + q / q0 * Nq
     fcrit = stats.chi2.ppf(1 - alpha, Nh + Nq)
     return f <= fcrit, f, fcrit
+
+
+def vaesimca_fit(Z: np.ndarray, Zhat: np.ndarray, type="alt", t2lim="Fdist", t2cl=0.95, qlim="jm", qcl=0.95,
+                 dcl=0.95):
+    """VAE_SIMCA.py:230-346 restated (not importable: the script loads data at
+    import, :388-389).  Z: calibration latents μ (float32 as produced by the
+    encoder), Zhat: enc(dec(μ)).  Returns the class-model dict the script
+    stores (latent_mean, invcovT, T2, Q, limits, dofs)."""
+    Z = np.asarray(Z, np.float32)
+    nc = Z.shape[1]
+    n = Z.shape[0]
+    x_mean = Z.mean(axis=0, dtype=np.float64)
+    cov = np.cov(Z, rowvar=False) + np.eye(nc) * 1e-12
+    invcovT = np.linalg.pinv(cov)
+    diff = Z - x_mean[None, :]
+    T2 = np.einsum("ij,jk,ik->i", diff, invcovT, diff)
+    Q = np.sum((Z - np.asarray(Zhat, np.float32)) ** 2, axis=1, dtype=np.float64).astype(np.float32)
+    t2dof = t2sc = qdof = qsc = None
+    # _compute_T2_limit (:281-300): percentile surrogates
+    if t2lim in ("perc", "chi2"):
+        T2lim = np.percentile(T2, t2cl * 100)
+    elif t2lim == "Fdist":
+        T2lim = nc * (n - 1) / (n - nc) * np.percentile(T2, t2cl * 100)
+    elif t2lim == "chi2pom":
+        h0 = float(np.mean(T2))
+        v = float(np.var(T2, ddof=1)) if n > 1 else 0.0
+        Nh = max(int(np.round(2 * h0 ** 2 / v)) if v > 0 else 1, 1)
+        T2lim, t2dof, t2sc = h0 * np.percentile(T2, t2cl * 100) / Nh, Nh, h0
+    else:
+        raise ValueError(t2lim)
+    # _compute_Q_limit (:302-327): jm from Q moments (not eigenvalues)
+    Qd = Q.astype(np.float64)
+    if qlim == "perc":
+        Qlim = np.percentile(Q, qcl * 100)
+    elif qlim == "jm":
+        th1, th2, th3 = Qd.sum(), (Qd ** 2).sum(), (Qd ** 3).sum()
+        if th1 == 0:
+            Qlim = 0
+        else:
+            h0 = max(1 - (2 * th1 * th3) / (3 * th2 ** 2), 1e-3)
+            ca = np.sqrt(2) * special.erfinv(2 * qcl - 1)
+            Qlim = th1 * (1 + ca * np.sqrt(2 * th2 * h0 ** 2) / th1 + th2 * h0 * (h0 - 1) / th1 ** 2) ** (1 / h0)
+    elif qlim == "chi2pom":
+        v0 = Qd.mean()
+        Nv = max(round(2 * v0 ** 2 / np.var(Qd, ddof=1)), 1)
+        Qlim, qdof, qsc = v0 * np.percentile(Q, qcl * 100) / Nv, Nv, v0
+    else:
+        raise ValueError(qlim)
+    # _compute_D_limit (:329-346)
+    if type == "sim":
+        Dlim = 1
+    elif type == "alt":
+        Dlim = np.sqrt(2)
+    elif type == "ci":
+        tr1 = nc / T2lim + Qd.sum() / Qlim
+        tr2 = nc / T2lim ** 2 + (Qd ** 2).sum() / Qlim ** 2
+        Dlim = tr2 / tr1 * np.percentile(Q, dcl * 100)
+    elif type == "dd":
+        Dlim = t2dof + qdof
+    else:
+        raise ValueError(type)
+    return {"latent_mean": x_mean, "invcovT": invcovT, "T2": T2, "Q": Q, "T2_limit": float(T2lim),
+            "Q_limit": float(Qlim), "D_limit": float(Dlim), "T2dof": t2dof, "T2scfact": t2sc, "Qdof": qdof,
+            "Qscfact": qsc, "n_components": nc, "type": type}
+
+
+def vaesimca_predict(model: dict, Z: np.ndarray, Zhat: np.ndarray):
+    """VAE_SIMCA.py:348-382: T², latent Q and the decision (sim and ci take the max rule)."""
+    Z = np.asarray(Z, np.float32)
+    diff = Z - model["latent_mean"][None, :]
+    T2 = np.einsum("ij,jk,ik->i", diff, model["invcovT"], diff)
+    Q = np.sum((Z - np.asarray(Zhat, np.float32)) ** 2, axis=1, dtype=np.float64).astype(np.float32)
+    with np.errstate(divide="ignore"):
+        if model["type"] == "alt":
+            D = np.sqrt((T2 / model["T2_limit"]) ** 2 + (Q / model["Q_limit"]) ** 2)
+        elif model["type"] == "dd":
+            D = T2 * model["T2dof"] / model["T2scfact"] + Q * model["Qdof"] / model["Qscfact"]
+        else:
+            D = np.maximum(T2 / model["T2_limit"], Q / model["Q_limit"])
+    return D < model["D_limit"], T2, Q, D
 
 
 # ---------------------------------------------------------------------------

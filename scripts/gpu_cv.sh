@@ -1,0 +1,14 @@
+# GPU: full -m gpu suite, then the C3 CV benchmark (1M x 2048, 10 folds).
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 600 python scripts/bench_cv.py > gpurun_out/bench_cv.log 2>&1 || { echo "bench_cv failed"; tail -20 gpurun_out/bench_cv.log; exit 2; }
+grep "^{" gpurun_out/bench_cv.log
+timeout -k 10 600 python scripts/bench_cv.py --lv-min 2 --lv-max 20 --reps 2 > gpurun_out/bench_cv_sweep.log 2>&1 || { echo "bench_cv sweep failed"; tail -20 gpurun_out/bench_cv_sweep.log; exit 3; }
+grep "^{" gpurun_out/bench_cv_sweep.log
+
+timeout -k 10 600 python bench.py --steps 5 --warmup 2 --no-cpu > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench.log; exit 4; }
+grep "^{" gpurun_out/bench.log
+echo done

@@ -15,6 +15,9 @@ outputs.  They are data (inputs and expected outputs), not reference source.
   set, predictions and transform() outputs on X_test.
 * cv_<name>.npz      — cross_validate_simca_grid records (spec/sens/eff per LV).
 * qhf.npz            — vae_model.compute_q_h_f on a fixed batch.
+* vae_<name>.npz     — vae_model.ConvVAE1D (seeded init → state_dict), eval /
+  train forward on a fixed batch with seeded ε, both losses, and the latent
+  inputs of VAESIMCA (encoder μ, round trip ẑ) on a calibration / test set.
 
 np.random.seed is set before every fit: the reference's second PCA(k) draws
 from NumPy's global RNG (SURVEY.md §8c caveat 1).
@@ -164,6 +167,61 @@ def make_qhf():
     print("qhf done")
 
 
+VAE_CONFIGS = {
+    # name: (input_length, latent_dim, kwargs)
+    "a": (96, 8, dict(conv_blocks=2, n_filters=3, kernel_size=7, stride=2, hidden_fc=32)),
+    "b": (101, 6, dict(conv_blocks=3, n_filters=2, kernel_size=5, stride=2, hidden_fc=24, activation="gelu",
+                       use_batchnorm=False)),
+}
+
+
+def make_vae():
+    """vae_model.ConvVAE1D / losses on fixed seeds, plus the latent inputs of
+    VAESIMCA (encoder μ and the latent round trip ẑ = enc(dec(μ)))."""
+    import torch
+    from vae_model import ConvVAE1D, beta_vae_bce_loss, beta_vae_cosine_loss
+
+    for name, (L, d, kw) in VAE_CONFIGS.items():
+        g = np.random.default_rng(21)
+        wl = np.linspace(0, 1, L)
+        base = (1.0 + 0.5 * np.sin(6 * wl)).astype(np.float32)
+        x = (base + 0.2 * g.standard_normal((64, L))).astype(np.float32)
+        x_cal = (base + 0.2 * g.standard_normal((300, L))).astype(np.float32)
+        x_test = (base + 0.2 * g.standard_normal((100, L))).astype(np.float32)
+        x_test[60:] += 0.8 * np.exp(-0.5 * ((wl - 0.4) / 0.05) ** 2).astype(np.float32)
+        mean, std = x_cal.mean(0), x_cal.std(0) + 1e-3
+        torch.manual_seed(0)
+        m = ConvVAE1D(L, d, mean, std, **kw)
+        out = {"x": x, "x_cal": x_cal, "x_test": x_test, "mean": mean, "std": std,
+               "config_json": np.array(json.dumps({"input_length": L, "latent_dim": d, **kw}))}
+        for k, v in m.state_dict().items():
+            out["sd/" + k] = v.detach().numpy().copy()
+        xt = torch.from_numpy(x)
+        with torch.no_grad():
+            m.eval()
+            torch.manual_seed(1)
+            x_rec, mu, logvar = m(xt)
+            out["eval_x_rec"], out["eval_mu"], out["eval_logvar"] = x_rec.numpy(), mu.numpy(), logvar.numpy()
+            out["eval_x_dec"] = (m.decode(mu) * m.spec_std + m.spec_mean).numpy()
+            m.train()
+            torch.manual_seed(2)
+            x_rec_t, mu_t, lv_t = m(xt)
+            out["train_x_rec"], out["train_mu"], out["train_logvar"] = x_rec_t.numpy(), mu_t.numpy(), lv_t.numpy()
+            l1 = beta_vae_bce_loss(xt, x_rec_t, mu_t, lv_t, beta=0.5)
+            l2 = beta_vae_cosine_loss(xt, x_rec_t, mu_t, lv_t, beta=0.5)
+            out["bce_loss"] = np.array([float(l1[0]), l1[1], l1[2]])
+            out["cos_loss"] = np.array([float(l2[0]), l2[1], l2[2]])
+            m.eval()
+            for tag, xs in (("cal", x_cal), ("test", x_test)):
+                xs_t = torch.from_numpy(xs)
+                mu_s, _ = m.encode((xs_t - m.spec_mean) / m.spec_std)
+                z_hat, _ = m.encode((m.decode(mu_s) - m.spec_mean) / m.spec_std)
+                out[f"mu_{tag}"] = mu_s.numpy()
+                out[f"zhat_{tag}"] = z_hat.numpy()
+        np.savez_compressed(os.path.join(HERE, f"vae_{name}.npz"), **out)
+        print("vae", name, sum(v.numel() for v in m.parameters()), "params")
+
+
 def main():
     # A: one class, spectral gap at k (SURVEY.md §8d), wavelength-correlated bands.
     # The last 100 rows carry the out-of-class band; fit on the first 1200.
@@ -198,6 +256,7 @@ def main():
     make_cv("grid", Xc_all, yc, 4, 2, 4, {"type": ["alt", "sim"], "qlim": ["jm", "chi2box"]})
 
     make_qhf()
+    make_vae()
 
 
 if __name__ == "__main__":

@@ -184,3 +184,17 @@ def test_rowsq_residual(eng):
     xh = x + 0.01 * rng.standard_normal(x.shape).astype(np.float32)
     q = eng.rowsq_residual(_dev(x), _dev(xh)).cpu().numpy()
     np.testing.assert_allclose(q, ((x.astype(np.float64) - xh) ** 2).sum(1), rtol=1e-6)
+
+
+def test_rowsq_residual_broadcast_and_strided(eng):
+    """ldxh = 0 broadcasts one row (Euclidean latent distance about a mean,
+    utils/final_vaesimca.py:510-512); a strided x view is honoured."""
+    rng = np.random.default_rng(6)
+    z = rng.standard_normal((1001, 32)).astype(np.float32)
+    mu = rng.standard_normal(32).astype(np.float32)
+    h = eng.rowsq_residual(_dev(z), _dev(mu)).cpu().numpy()
+    np.testing.assert_allclose(h, ((z.astype(np.float64) - mu) ** 2).sum(1), rtol=1e-6)
+    big = _dev(rng.standard_normal((50, 100)).astype(np.float32))
+    view = big[:, 10:42]
+    q = eng.rowsq_residual(view, _dev(mu)).cpu().numpy()
+    np.testing.assert_allclose(q, ((view.cpu().numpy().astype(np.float64) - mu) ** 2).sum(1), rtol=1e-6)

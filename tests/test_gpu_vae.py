@@ -1,0 +1,124 @@
+"""SIMCA-on-latents on the GPU (ocm/vae.py, vae_model.compute_q_h_f).
+
+* compute_q_h_f on device tensors vs the reference's output (qhf.npz):
+  q rtol 1e-5, h / f rtol 1e-4 (the reference runs a float32 SVD), criticals
+  rtol 1e-4;
+* latent_stats / full_distance_decision vs the oracle restatement of
+  utils/final_vaesimca.py on the reference model's latents (vae_*.npz);
+* VAESIMCA fit_thresholds / predict with the drop-in ConvVAE1D carrying the
+  reference weights vs the oracle restatement of VAE_SIMCA.py fed with the
+  reference model's own μ / ẑ: limits rtol 1e-4, decisions identical except
+  within a 1e-4 band of D_limit.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+
+def _load(golden_dir, name):
+    return dict(np.load(os.path.join(golden_dir, name), allow_pickle=False))
+
+
+def test_compute_q_h_f_device(golden_dir):
+    import torch
+    import vae_model as V
+
+    g = _load(golden_dir, "qhf.npz")
+    dev = torch.device("cuda", 0)
+    q, h, f, qc, hc, fc = V.compute_q_h_f(torch.from_numpy(g["x"]).to(dev), torch.from_numpy(g["x_rec"]).to(dev),
+                                          torch.from_numpy(g["z"]).to(dev))
+    assert q.is_cuda and h.is_cuda and f.is_cuda
+    np.testing.assert_allclose(q.cpu().numpy(), g["q"], rtol=1e-5)
+    np.testing.assert_allclose(h.cpu().numpy(), g["h"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(f.cpu().numpy(), g["f"], rtol=1e-4)
+    np.testing.assert_allclose([qc, hc, fc], g["crit"], rtol=1e-4)
+
+
+def _model(g, dev):
+    import torch
+    import vae_model as V
+
+    cfg = json.loads(str(g["config_json"]))
+    L, d = cfg.pop("input_length"), cfg.pop("latent_dim")
+    m = V.ConvVAE1D(L, d, g["mean"], g["std"], **cfg)
+    m.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("sd/")})
+    return m.to(dev).eval()
+
+
+def test_latent_stats_and_full_distance(golden_dir):
+    import torch
+    from oracle import simca_oracle as O
+    from ocm import vae
+
+    g = _load(golden_dir, "vae_a.npz")
+    dev = torch.device("cuda", 0)
+    mus = g["mu_cal"]
+    q_cal = np.sum((g["mu_cal"] - g["zhat_cal"]) ** 2, axis=1).astype(np.float32)
+    mean, inv, thr, qthr = vae.latent_stats(torch.from_numpy(mus).to(dev), torch.from_numpy(q_cal).to(dev))
+    o_mean, o_inv, o_thr, o_qthr = O.latent_stats(mus, q_cal)
+    np.testing.assert_allclose(mean.cpu().numpy(), o_mean, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(inv.cpu().numpy(), o_inv, rtol=1e-6, atol=1e-6 * np.abs(o_inv).max())
+    np.testing.assert_allclose([thr, qthr], [o_thr, o_qthr], rtol=1e-6)
+    mus_t = g["mu_test"]
+    q_t = np.sum((g["mu_test"] - g["zhat_test"]) ** 2, axis=1).astype(np.float32)
+    acc, f, fcrit = vae.full_distance_decision(torch.from_numpy(mus_t).to(dev), torch.from_numpy(o_mean).to(dev),
+                                               torch.from_numpy(q_t).to(dev))
+    o_acc, o_f, o_fcrit = O.full_distance_decision(mus_t, o_mean.astype(np.float32), q_t)
+    np.testing.assert_allclose(f.cpu().numpy(), o_f, rtol=1e-5)
+    np.testing.assert_allclose(fcrit, o_fcrit, rtol=1e-6)
+    band = np.abs(o_f - o_fcrit) > 1e-4 * o_fcrit
+    np.testing.assert_array_equal(acc.cpu().numpy()[band], o_acc[band])
+
+
+COMBOS = [("alt", "Fdist", "jm"), ("sim", "perc", "perc"), ("ci", "chi2", "jm"), ("dd", "chi2pom", "chi2pom"),
+          ("alt", "chi2pom", "chi2pom")]
+
+
+@pytest.mark.parametrize("name", ["vae_a.npz", "vae_b.npz"])
+@pytest.mark.parametrize("combo", COMBOS)
+def test_vaesimca_vs_restatement(golden_dir, name, combo):
+    import torch
+    from oracle import simca_oracle as O
+    from ocm.vae import VAESIMCA
+
+    g = _load(golden_dir, name)
+    dev = torch.device("cuda", 0)
+    m = _model(g, dev)
+    ty, t2, ql = combo
+    est = VAESIMCA(m, type=ty, t2lim=t2, qlim=ql, device=dev, verbose=False)
+    cal = [(torch.from_numpy(g["x_cal"][i:i + 128]),) for i in range(0, len(g["x_cal"]), 128)]
+    test = [(torch.from_numpy(g["x_test"][i:i + 64]),) for i in range(0, len(g["x_test"]), 64)]
+    est.fit_thresholds(cal, class_label=0)
+    ref = O.vaesimca_fit(g["mu_cal"], g["zhat_cal"], ty, t2, 0.95, ql, 0.95, 0.95)
+    got = est._model[0]
+    # latents from the drop-in network on the GPU vs the reference network on the CPU
+    np.testing.assert_allclose(got["T2"], ref["T2"], rtol=2e-3, atol=1e-4)
+    np.testing.assert_allclose(got["Q"], ref["Q"], rtol=2e-3, atol=1e-5 * float(np.median(ref["Q"])))
+    for key in ("T2_limit", "Q_limit", "D_limit"):
+        np.testing.assert_allclose(got[key], ref[key], rtol=5e-3, err_msg=key)
+    y_pred, T2, Q = est.predict(test)
+    assert y_pred.dtype == bool and T2.dtype == np.float64 and Q.dtype == np.float32
+    # decisions: same limits → same accept/reject except at the boundary
+    o_acc, _, _, D = O.vaesimca_predict({**got, "type": ty}, g["mu_test"], g["zhat_test"])
+    band = np.abs(D - got["D_limit"]) > 1e-2 * got["D_limit"]
+    np.testing.assert_array_equal(y_pred[band], o_acc[band])
+
+
+def test_vaesimca_errors():
+    from ocm.vae import VAESIMCA
+
+    est = VAESIMCA(None, t2lim="bogus")
+    with pytest.raises(ValueError):
+        est._t2_limit(None, 3)
+    est = VAESIMCA(None, qlim="bogus")
+    with pytest.raises(ValueError):
+        est._q_limit(None)
+    est = VAESIMCA(None, type="dd")
+    with pytest.raises(ValueError):
+        est._d_limit(1.0, 1.0, None, 3, None, None)

@@ -1,0 +1,75 @@
+"""Drop-in vae_model (ocm-vae-simca_amd/vae_model.py) vs the reference's
+vae_model on the CPU (tests/golden/vae_*.npz, qhf.npz; make_golden.py).
+
+Checks: the seeded initialisation reproduces the reference's state_dict
+exactly (same layer creation / init order), the state_dict key set and
+shapes are identical (checkpoints interchange), eval and train forward with
+a seeded ε match, and both losses match.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import vae_model as V
+
+
+def _load(golden_dir, name):
+    return dict(np.load(os.path.join(golden_dir, name), allow_pickle=False))
+
+
+def _model(g, seed=0):
+    cfg = json.loads(str(g["config_json"]))
+    L, d = cfg.pop("input_length"), cfg.pop("latent_dim")
+    torch.manual_seed(seed)
+    return V.ConvVAE1D(L, d, g["mean"], g["std"], **cfg)
+
+
+@pytest.mark.parametrize("name", ["vae_a.npz", "vae_b.npz"])
+def test_seeded_init_and_state_dict_layout(golden_dir, name):
+    g = _load(golden_dir, name)
+    m = _model(g)
+    sd = m.state_dict()
+    ref = {k[3:]: v for k, v in g.items() if k.startswith("sd/")}
+    assert set(sd) == set(ref)
+    for k, v in ref.items():
+        assert tuple(sd[k].shape) == v.shape, k
+        np.testing.assert_array_equal(sd[k].numpy(), v, err_msg=k)
+
+
+@pytest.mark.parametrize("name", ["vae_a.npz", "vae_b.npz"])
+def test_forward_and_losses(golden_dir, name):
+    g = _load(golden_dir, name)
+    m = _model(g, seed=123)  # different init, then load the reference weights
+    m.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("sd/")})
+    x = torch.from_numpy(g["x"])
+    with torch.no_grad():
+        m.eval()
+        torch.manual_seed(1)
+        x_rec, mu, logvar = m(x)
+        np.testing.assert_allclose(mu.numpy(), g["eval_mu"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(logvar.numpy(), g["eval_logvar"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(x_rec.numpy(), g["eval_x_rec"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose((m.decode(mu) * m.spec_std + m.spec_mean).numpy(), g["eval_x_dec"], rtol=1e-5,
+                                   atol=1e-5)
+        m.train()
+        torch.manual_seed(2)
+        x_rec_t, mu_t, lv_t = m(x)
+        np.testing.assert_allclose(x_rec_t.numpy(), g["train_x_rec"], rtol=1e-5, atol=1e-5)
+        l1 = V.beta_vae_bce_loss(x, x_rec_t, mu_t, lv_t, beta=0.5)
+        l2 = V.beta_vae_cosine_loss(x, x_rec_t, mu_t, lv_t, beta=0.5)
+    np.testing.assert_allclose([float(l1[0]), l1[1], l1[2]], g["bce_loss"], rtol=1e-5)
+    np.testing.assert_allclose([float(l2[0]), l2[1], l2[2]], g["cos_loss"], rtol=1e-5)
+    assert isinstance(l1[1], float) and isinstance(l1[2], float)
+
+
+def test_compute_q_h_f_host(golden_dir):
+    g = _load(golden_dir, "qhf.npz")
+    q, h, f, qc, hc, fc = V.compute_q_h_f(torch.from_numpy(g["x"]), torch.from_numpy(g["x_rec"]),
+                                          torch.from_numpy(g["z"]))
+    np.testing.assert_allclose(q.numpy(), g["q"], rtol=1e-5)
+    np.testing.assert_allclose(h.numpy(), g["h"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(f.numpy(), g["f"], rtol=1e-4)
+    np.testing.assert_allclose([qc, hc, fc], g["crit"], rtol=1e-5)

@@ -1,0 +1,41 @@
+"""The VAE trainer's step (ocm/vae_train.py, eager mode on the CPU) equals the
+reference's training step (forward → beta_vae_bce_loss → zero_grad →
+backward → Adam.step, vae_bce_nut.py:178-203) run with the reference-format
+loss on an identical copy of the model."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+import vae_model as V
+
+
+@pytest.mark.parametrize("loss", ["bce", "cosine"])
+def test_trainer_step_matches_reference_step(loss):
+    from ocm.vae_train import GraphedVAETrainer
+
+    L, d, B = 64, 4, 16
+    g = torch.Generator().manual_seed(0)
+    x = 1.0 + 0.3 * torch.randn(B, L, generator=g)
+    torch.manual_seed(0)
+    m1 = V.ConvVAE1D(L, d, np.zeros(L, np.float32), np.ones(L, np.float32), conv_blocks=2, n_filters=2,
+                     kernel_size=5, hidden_fc=16)
+    m2 = copy.deepcopy(m1)
+    tr = GraphedVAETrainer(m1, B, lr=1e-3, weight_decay=1e-4, beta=0.7, loss=loss, dtype=torch.float32, graph=False)
+    opt = torch.optim.Adam(m2.parameters(), lr=1e-3, weight_decay=1e-4)
+    fn = V.beta_vae_bce_loss if loss == "bce" else V.beta_vae_cosine_loss
+    for it in range(3):
+        torch.manual_seed(100 + it)
+        total, recon, kl = tr.step(x)
+        m2.train()
+        torch.manual_seed(100 + it)
+        x_rec, mu, logvar = m2(x)
+        ref_total, ref_recon, ref_kl = fn(x, x_rec, mu, logvar, beta=0.7)
+        opt.zero_grad()
+        ref_total.backward()
+        opt.step()
+        np.testing.assert_allclose([float(total), float(recon), float(kl)], [float(ref_total), ref_recon, ref_kl],
+                                   rtol=1e-6)
+    for (n1, p1), (n2, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        torch.testing.assert_close(p1, p2, rtol=1e-6, atol=1e-7, msg=n1)
