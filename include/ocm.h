@@ -212,6 +212,18 @@ int ocm_cv_counts(ocm_ctx* ctx, const float* T, int64_t m, int32_t k, const floa
                   const uint8_t* positive, int64_t m_split, const ocm_cv_config* cfg, int32_t ncfg,
                   uint64_t* counts_out, double* accept_out, void* stream);
 
+/* ---- spectral preprocessing ----
+ * SNV x ← (x − mean_row)/(std_row + 1e-8) (np.std ddof 0; simca_nuts.py:47-49,
+ * utils/data_utils.py:57) when snv != 0, then, when window > 0, the
+ * Savitzky–Golay filter scipy.signal.savgol_filter(x, window, polyorder,
+ * deriv, delta, axis=1, mode='interp') (simca_nuts.py:51,
+ * simca_new_cheese.py:37-38) given as taps [host] (window + 2·(window/2)·window
+ * doubles: interior correlation taps, then the left and right edge rows; see
+ * ocm/preprocess.py savgol_taps).  One HBM pass per row.  X, out [dev] m×p
+ * float32 (ldx, ldo; out may not alias X).  window odd ≤ 63, p ≤ 12288. */
+int ocm_snv_savgol_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, int32_t p, int32_t snv,
+                       int32_t window, const double* taps, float* out, int64_t ldo, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

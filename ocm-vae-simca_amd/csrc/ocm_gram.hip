@@ -227,6 +227,175 @@ __global__ __launch_bounds__(GT * 2, 2) void k_gram(
   }
 }
 
+// ---------------------------------------------------------------------------
+// bf16×3 split Gram on bf16 MFMA (v_mfma_f32_32x32x16_bf16, 16× the FP32-MFMA
+// rate).  Every y = x − shift (f32) is split exactly into three bf16 levels
+// y = y1 + y2 + y3 (each RNE; an f32 has 24 significant bits = 3 × 8, so the
+// split is exact); the tile accumulates the six products with
+// level(a) + level(b) ≤ 4 (y1y1, y1y2, y2y1, y1y3, y2y2, y3y1) in f32.  The
+// dropped y2y3 + y3y2 + y3y3 are ≤ ~2⁻²⁴·|y_i||y_j| per term — the size of
+// the f32 rounding of a single product, so the result carries FP32-MFMA
+// accuracy at 16/6 ≈ 2.7× its peak rate.
+// Same work decomposition and partial layout as k_gram<256, ·> (so the same
+// reduce); 16 rows per LDS stage, stored K-major per column (16 bf16 = 32 B
+// per column and level) with the two 16-B halves swapped on bit 3 of the
+// column: the ds_read_b128 fragment reads (lane = column, half = k-octet) and
+// the ds_write_b128 stores are then bank-conflict-free.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int G3T = 256, G3K = 16, G3THREADS = 512;
+
+__device__ __forceinline__ int g3_off(int panel, int lvl, int col, int half) {
+  // bytes within one stage buffer: [panel][lvl][col][32 B], half swizzled
+  return (((panel * 3 + lvl) * G3T + col) << 5) + ((half ^ ((col >> 3) & 1)) << 4);
+}
+
+template <bool GATHER>
+__global__ __launch_bounds__(G3THREADS, 1) void k_gram3(
+    const float* __restrict__ X, int64_t ldx, const int64_t* __restrict__ rows, int p, const float* __restrict__ shift,
+    SegTable st, int nt, int ntiles, int total_wg, float* __restrict__ part, double* __restrict__ colpart) {
+  constexpr int STAGE_BYTES = 2 * 3 * G3T * 32;  // 48 KiB per stage (both panels)
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE_BYTES];
+  __shared__ int64_t ridx[GATHER ? GATHER_MAX_CHUNK : 1];
+  __shared__ double cred[G3T];
+
+  const int b = blockIdx.x;
+  const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
+  const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int chunk = wg / ntiles;
+  const int tile = wg - chunk * ntiles;
+  int ti, tj;
+  tile_coords(tile, nt, ti, tj);
+  const bool diag = (ti == tj);
+  const int I = ti * G3T, J = tj * G3T;
+
+  int s = 0;
+  while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
+  const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
+  const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
+  const int nstage = (int)((r1 - r0 + G3K - 1) / G3K);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;  // 2 (M, 128 rows each) × 4 (N, 64 cols each)
+  if (GATHER) {
+    for (int64_t g = r0 + tid; g < r1; g += G3THREADS) ridx[g - r0] = rows[g];
+    __syncthreads();
+  }
+  // loader: one column, 8 consecutive rows (one k-octet) per thread and panel
+  const int lc = tid & (G3T - 1), lh = tid >> 8;
+  const int colA = I + lc, colB = J + lc;
+  const bool inA = colA < p, inB = colB < p;
+  const float* baseA = X + (inA ? colA : p - 1);
+  const float* baseB = X + (inB ? colB : p - 1);
+  const float shA = inA ? shift[colA] : 0.f, shB = inB ? shift[colB] : 0.f;
+  float ra[8], rb[8];
+  double csum = 0.0;
+
+  auto gload = [&](int stage) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      int64_t g = r0 + (int64_t)stage * G3K + 8 * lh + j;
+      g = g < r1 ? g : r1 - 1;
+      const int64_t srow = GATHER ? ridx[g - r0] : g;
+      ra[j] = baseA[srow * ldx];
+      rb[j] = baseB[srow * ldx];
+    }
+  };
+  auto split_store = [&](const float (&v)[8], float sh, bool incol, int64_t g0, int panel, char* buf, bool acc_cs) {
+    bf16x8 l1, l2, l3;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float y = (incol && g0 + j < r1) ? v[j] - sh : 0.f;
+      if (acc_cs) csum += (double)y;
+      const __bf16 b1 = (__bf16)y;
+      const float e1 = y - (float)b1;
+      const __bf16 b2 = (__bf16)e1;
+      const float e2 = e1 - (float)b2;
+      l1[j] = b1;
+      l2[j] = b2;
+      l3[j] = (__bf16)e2;
+    }
+    *reinterpret_cast<bf16x8*>(buf + g3_off(panel, 0, lc, lh)) = l1;
+    *reinterpret_cast<bf16x8*>(buf + g3_off(panel, 1, lc, lh)) = l2;
+    *reinterpret_cast<bf16x8*>(buf + g3_off(panel, 2, lc, lh)) = l3;
+  };
+  auto sstore = [&](int stage, int bi) {
+    char* buf = lds + bi * STAGE_BYTES;
+    const int64_t g0 = r0 + (int64_t)stage * G3K + 8 * lh;
+    split_store(ra, shA, inA, g0, 0, buf, diag);
+    if (!diag) split_store(rb, shB, inB, g0, 1, buf, false);
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+
+  if (nstage > 0) {
+    gload(0);
+    sstore(0, 0);
+  }
+  __syncthreads();
+  const int bpanel = diag ? 0 : 1;
+  const bool idle = diag && (wm * 128 >= (wn + 1) * 64);
+  const int l31 = lane & 31, h = lane >> 5;
+  int cur = 0;
+  for (int stg = 0; stg < nstage; ++stg) {
+    if (stg + 1 < nstage) gload(stg + 1);
+    if (!idle) {
+      const char* buf = lds + cur * STAGE_BYTES;
+      bf16x8 bv[2][3];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int l = 0; l < 3; ++l)
+          bv[c][l] = *reinterpret_cast<const bf16x8*>(buf + g3_off(bpanel, l, wn * 64 + c * 32 + l31, h));
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        bf16x8 av[3];
+#pragma unroll
+        for (int l = 0; l < 3; ++l)
+          av[l] = *reinterpret_cast<const bf16x8*>(buf + g3_off(0, l, wm * 128 + a * 32 + l31, h));
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          f32x16 t = acc[a][c];
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[c][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[c][1], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[c][2], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[c][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[c][1], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[c][0], t, 0, 0, 0);
+          acc[a][c] = t;
+        }
+      }
+    }
+    if (stg + 1 < nstage) sstore(stg + 1, cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  float* out = part + ((size_t)chunk * ntiles + tile) * (G3T * G3T);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int col = wn * 64 + c * 32 + l31;
+        out[row * G3T + col] = acc[a][c][r];
+      }
+  if (diag) {
+    if (lh == 1) cred[lc] = csum;
+    __syncthreads();
+    if (lh == 0) colpart[((size_t)chunk * nt + ti) * G3T + lc] = csum + cred[lc];
+  }
+}
+
 // Sum chunk partials of one segment into G (full symmetric) and colsum.
 // Each thread owns 4 consecutive tile elements (one float4 per chunk) and
 // keeps 4 chunks' loads in flight (independent partial sums, fixed order).
@@ -475,7 +644,8 @@ int gram_small(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
 template <int GT, int BK>
 int gram_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
               const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
-              hipStream_t st, int64_t chunk_rows) {
+              hipStream_t st, int64_t chunk_rows, bool split3 = false) {
+  if (GT != 256) split3 = false;
   using Cfg = GramCfg<GT, BK>;
   const int nt = (p + GT - 1) / GT;
   const int ntiles = nt * (nt + 1) / 2;
@@ -519,7 +689,14 @@ int gram_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, in
 #define OCM_GRAM_LAUNCH(V_, G_)                                                                                    \
   hipLaunchKernelGGL((k_gram<GT, BK, V_, G_>), grid, blk, 0, st, X, ldx, rows, p, shift, tab, nt, ntiles, (int)total, \
                      pg, col_g)
-    if (rows) {
+    if (split3) {
+      if (rows)
+        hipLaunchKernelGGL(k_gram3<true>, grid, dim3(G3THREADS), 0, st, X, ldx, rows, p, shift, tab, nt, ntiles,
+                           (int)total, pg, col_g);
+      else
+        hipLaunchKernelGGL(k_gram3<false>, grid, dim3(G3THREADS), 0, st, X, ldx, rows, p, shift, tab, nt, ntiles,
+                           (int)total, pg, col_g);
+    } else if (rows) {
       if (vec) OCM_GRAM_LAUNCH(true, true); else OCM_GRAM_LAUNCH(false, true);
     } else {
       if (vec) OCM_GRAM_LAUNCH(true, false); else OCM_GRAM_LAUNCH(false, false);
@@ -588,6 +765,12 @@ int ocm_gram_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows,
   if (const char* e = std::getenv("OCM_GRAM_TILE")) tile = std::atoi(e) == 128 ? 128 : 256;
   if (const char* e = std::getenv("OCM_GRAM_BK")) bk = std::atoi(e) == 16 ? 16 : 32;
   if (const char* e = std::getenv("OCM_GRAM_CHUNK")) chunk_rows = std::max<int64_t>(64, std::atoll(e));
+  // OCM_GRAM_MODE: "f32" (FP32 MFMA) or "bf16x3" (exact 3-level bf16 split on bf16 MFMA)
+  bool split3 = false;
+  if (const char* e = std::getenv("OCM_GRAM_MODE")) split3 = std::string(e) == "bf16x3";
+  if (split3)
+    return gram_impl<256, 32>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows,
+                              true);
   if (tile == 256 && bk == 32)
     return gram_impl<256, 32>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows);
   if (tile == 256)

@@ -82,6 +82,8 @@ SIGNATURES = {
                                  ctypes.POINTER(c_f64), c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
     "ocm_cv_prefix": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_void_p, c_void_p, ctypes.POINTER(c_i32), c_i32,
                               c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ocm_snv_savgol_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_i32, c_i32, c_i32,
+                                   ctypes.POINTER(c_f64), c_void_p, c_i64, c_void_p]),
     "ocm_cv_counts": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_void_p, c_i64,
                               ctypes.POINTER(OcmCvConfig), c_i32, c_void_p, c_void_p, c_void_p]),
 }

@@ -147,8 +147,15 @@ class VAESIMCA:
     @torch.no_grad()
     def fit_thresholds(self, loader, class_label=0):
         self.vae.eval()
-        self.model_class = [class_label]
         Z, Zh = self._latents(loader)
+        self.fit_latents(Z, Zh, class_label)
+
+    def fit_latents(self, Z: torch.Tensor, Zh: torch.Tensor, class_label=0):
+        """The statistics part of ``fit_thresholds`` on given latents μ and
+        round trips ẑ (device or host arrays, (n, d))."""
+        self.model_class = [class_label]
+        Z = engine.as_device_f32(Z)
+        Zh = engine.as_device_f32(Zh, Z.device)
         n, nc = Z.shape
         mean, C = _latent_cov(Z)
         C.diagonal().add_(1e-12)
@@ -221,8 +228,14 @@ class VAESIMCA:
     @torch.no_grad()
     def predict(self, loader):
         self.vae.eval()
-        info = self._model[self.model_class[0]]
         Z, Zh = self._latents(loader)
+        return self.predict_latents(Z, Zh)
+
+    def predict_latents(self, Z: torch.Tensor, Zh: torch.Tensor):
+        """The decision part of ``predict`` on given latents μ / round trips ẑ."""
+        info = self._model[self.model_class[0]]
+        Z = engine.as_device_f32(Z)
+        Zh = engine.as_device_f32(Zh, Z.device)
         T2 = latent_T2(Z, info["_mean_dev"], info["_invcov_dev"])
         Q = engine.rowsq_residual(Z, Zh)
         if self.type == "alt":

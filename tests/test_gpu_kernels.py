@@ -15,6 +15,13 @@ def eng():
     return engine
 
 
+@pytest.fixture(params=["f32", "bf16x3"])
+def gram_mode(request, monkeypatch):
+    """Both Gram kernels: FP32 MFMA and the exact bf16×3 split on bf16 MFMA."""
+    monkeypatch.setenv("OCM_GRAM_MODE", request.param)
+    return request.param
+
+
 def _dev(a):
     import torch
 
@@ -22,7 +29,7 @@ def _dev(a):
 
 
 @pytest.mark.parametrize("n,p", [(5000, 300), (777, 128), (4100, 96), (3000, 1000)])
-def test_gram_matches_fp64(eng, n, p):
+def test_gram_matches_fp64(eng, gram_mode, n, p):
     rng = np.random.default_rng(n + p)
     X = (rng.standard_normal((n, p)) * rng.uniform(0.1, 3, p) + 2.0).astype(np.float32)
     Xd = _dev(X)
@@ -34,7 +41,7 @@ def test_gram_matches_fp64(eng, n, p):
     np.testing.assert_allclose(cs[0].cpu().numpy(), Y.sum(0), rtol=1e-6, atol=1e-6 * np.abs(Y).sum(0).max())
 
 
-def test_gram_segments_and_rows(eng):
+def test_gram_segments_and_rows(eng, gram_mode):
     import torch
 
     rng = np.random.default_rng(3)
@@ -53,7 +60,7 @@ def test_gram_segments_and_rows(eng):
         np.testing.assert_allclose(cs[s].cpu().numpy(), Y.sum(0), rtol=1e-6, atol=1e-7 * np.abs(Y).sum(0).max())
 
 
-def test_cov_and_mean(eng):
+def test_cov_and_mean(eng, gram_mode):
     from oracle.simca_oracle import synth_spectra
 
     X = synth_spectra(4000, 300, 8, rank=20, seed=5)

@@ -93,6 +93,14 @@ def test_limits_and_decisions_all_combos(golden_dir, name):
     assert n_checked > 0
 
 
+@pytest.mark.parametrize("name", ["simca_a.npz", "simca_b.npz"])
+def test_fit_and_limits_with_bf16x3_gram(golden_dir, name, monkeypatch):
+    """The same reference parity with the Gram on the exact bf16×3 split."""
+    monkeypatch.setenv("OCM_GRAM_MODE", "bf16x3")
+    test_fit_arrays_vs_reference(golden_dir, name)
+    test_limits_and_decisions_all_combos(golden_dir, name)
+
+
 @pytest.mark.parametrize("name", ["simca_a.npz", "simca_b.npz", "simca_multi.npz"])
 def test_transform_vs_reference(golden_dir, name):
     g = _load(golden_dir, name)

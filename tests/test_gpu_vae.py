@@ -5,10 +5,12 @@
   rtol 1e-4;
 * latent_stats / full_distance_decision vs the oracle restatement of
   utils/final_vaesimca.py on the reference model's latents (vae_*.npz);
-* VAESIMCA fit_thresholds / predict with the drop-in ConvVAE1D carrying the
-  reference weights vs the oracle restatement of VAE_SIMCA.py fed with the
-  reference model's own μ / ẑ: limits rtol 1e-4, decisions identical except
-  within a 1e-4 band of D_limit.
+* VAESIMCA limits / decisions on the reference network's own latents μ, ẑ
+  (identical inputs) vs the oracle restatement of VAE_SIMCA.py: rtol 1e-5,
+  dofs exact, decisions identical outside a 1e-5 band of D_limit;
+* the network path (drop-in ConvVAE1D with the reference weights on the GPU,
+  fp32 convolutions) reproduces the reference latents to rtol 1e-4 and the
+  limits to 1e-3.
 """
 import json
 import os
@@ -77,37 +79,69 @@ def test_latent_stats_and_full_distance(golden_dir):
 
 
 COMBOS = [("alt", "Fdist", "jm"), ("sim", "perc", "perc"), ("ci", "chi2", "jm"), ("dd", "chi2pom", "chi2pom"),
-          ("alt", "chi2pom", "chi2pom")]
+          ("alt", "chi2pom", "chi2pom"), ("ci", "perc", "chi2pom")]
 
 
 @pytest.mark.parametrize("name", ["vae_a.npz", "vae_b.npz"])
 @pytest.mark.parametrize("combo", COMBOS)
 def test_vaesimca_vs_restatement(golden_dir, name, combo):
+    """Limits and decisions on the reference network's own latents (identical
+    inputs): fp64 paths rtol 1e-6, decisions identical outside a 1e-6 band."""
     import torch
     from oracle import simca_oracle as O
     from ocm.vae import VAESIMCA
 
     g = _load(golden_dir, name)
     dev = torch.device("cuda", 0)
-    m = _model(g, dev)
     ty, t2, ql = combo
-    est = VAESIMCA(m, type=ty, t2lim=t2, qlim=ql, device=dev, verbose=False)
-    cal = [(torch.from_numpy(g["x_cal"][i:i + 128]),) for i in range(0, len(g["x_cal"]), 128)]
-    test = [(torch.from_numpy(g["x_test"][i:i + 64]),) for i in range(0, len(g["x_test"]), 64)]
-    est.fit_thresholds(cal, class_label=0)
+    est = VAESIMCA(None, type=ty, t2lim=t2, qlim=ql, device=dev, verbose=False)
+    est.fit_latents(torch.from_numpy(g["mu_cal"]).to(dev), torch.from_numpy(g["zhat_cal"]).to(dev), 0)
     ref = O.vaesimca_fit(g["mu_cal"], g["zhat_cal"], ty, t2, 0.95, ql, 0.95, 0.95)
     got = est._model[0]
-    # latents from the drop-in network on the GPU vs the reference network on the CPU
-    np.testing.assert_allclose(got["T2"], ref["T2"], rtol=2e-3, atol=1e-4)
-    np.testing.assert_allclose(got["Q"], ref["Q"], rtol=2e-3, atol=1e-5 * float(np.median(ref["Q"])))
+    np.testing.assert_allclose(got["latent_mean"], ref["latent_mean"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(got["T2"], ref["T2"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(got["Q"], ref["Q"], rtol=1e-6)
     for key in ("T2_limit", "Q_limit", "D_limit"):
-        np.testing.assert_allclose(got[key], ref[key], rtol=5e-3, err_msg=key)
-    y_pred, T2, Q = est.predict(test)
+        np.testing.assert_allclose(got[key], ref[key], rtol=1e-5, err_msg=key)
+    for key in ("T2dof", "Qdof"):
+        assert got[key] == ref[key]
+    y_pred, T2, Q = est.predict_latents(torch.from_numpy(g["mu_test"]).to(dev),
+                                        torch.from_numpy(g["zhat_test"]).to(dev))
     assert y_pred.dtype == bool and T2.dtype == np.float64 and Q.dtype == np.float32
-    # decisions: same limits → same accept/reject except at the boundary
-    o_acc, _, _, D = O.vaesimca_predict({**got, "type": ty}, g["mu_test"], g["zhat_test"])
-    band = np.abs(D - got["D_limit"]) > 1e-2 * got["D_limit"]
+    o_acc, _, _, D = O.vaesimca_predict(ref, g["mu_test"], g["zhat_test"])
+    band = np.abs(D - ref["D_limit"]) > 1e-5 * ref["D_limit"]
     np.testing.assert_array_equal(y_pred[band], o_acc[band])
+
+
+@pytest.mark.parametrize("name", ["vae_a.npz", "vae_b.npz"])
+def test_vaesimca_network_path(golden_dir, name):
+    """fit_thresholds / predict through the drop-in network on the GPU (fp32
+    convolutions: TF32 off) vs the reference network's latents on the CPU."""
+    import torch
+    from oracle import simca_oracle as O
+    from ocm.vae import VAESIMCA
+
+    g = _load(golden_dir, name)
+    dev = torch.device("cuda", 0)
+    prev = torch.backends.cudnn.enabled
+    torch.backends.cudnn.enabled = False  # native fp32 convolutions (see scripts/diag_vae_conv.py)
+    try:
+        m = _model(g, dev)
+        with torch.no_grad():
+            xs = torch.from_numpy(g["x_cal"]).to(dev)
+            mu, _ = m.encode((xs - m.spec_mean) / m.spec_std)
+        np.testing.assert_allclose(mu.cpu().numpy(), g["mu_cal"], rtol=1e-4, atol=1e-4 * np.abs(g["mu_cal"]).max())
+        est = VAESIMCA(m, type="alt", t2lim="Fdist", qlim="jm", device=dev, verbose=False)
+        cal = [(torch.from_numpy(g["x_cal"][i:i + 128]),) for i in range(0, len(g["x_cal"]), 128)]
+        test = [(torch.from_numpy(g["x_test"][i:i + 64]),) for i in range(0, len(g["x_test"]), 64)]
+        est.fit_thresholds(cal, class_label=0)
+        ref = O.vaesimca_fit(g["mu_cal"], g["zhat_cal"], "alt", "Fdist", 0.95, "jm", 0.95, 0.95)
+        for key in ("T2_limit", "Q_limit"):
+            np.testing.assert_allclose(est._model[0][key], ref[key], rtol=1e-3, err_msg=key)
+        y_pred, T2, Q = est.predict(test)
+        assert y_pred.shape == (len(g["x_test"]),)
+    finally:
+        torch.backends.cudnn.enabled = prev
 
 
 def test_vaesimca_errors():
