@@ -13,14 +13,11 @@ With world size 1 the same code runs with no collective.
 """
 from __future__ import annotations
 
-import ctypes
-
 import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import _lib, engine, limits
-from ._lib import Context, check, ptr
+from . import engine, limits
 
 
 def make_allreduce(group=None):
@@ -40,37 +37,45 @@ def make_allreduce(group=None):
 
 def percentile_sharded(v: torch.Tensor, pct: float, n_total: int, group=None) -> float:
     """np.percentile(linear) of the concatenation of every rank's ``v`` by a
-    distributed radix select: each pass's 256-bin histogram is all-reduced."""
+    distributed radix select: each pass's 256-bin histogram (ocm_radix_hist)
+    is all-reduced, so every rank walks the same digits.  The interpolation
+    follows NumPy's dtype rules exactly as the single-GPU ocm_percentile does
+    (float32 arithmetic for a float32 array)."""
     allreduce = make_allreduce(group)
     if allreduce is None:
         return engine.percentile(v, pct)
-    dtype = 0 if v.dtype == torch.float64 else 1
-    nbits = 64 if dtype == 0 else 32
-    ctx = Context.get(v.device.index)
-    lib = _lib.load()
-    hist = torch.empty(256, dtype=torch.int64, device=v.device)
+    f32 = v.dtype == torch.float32
+    nbits = 32 if f32 else 64
 
     def kth(rank):
         prefix = 0
         for shift in range(nbits - 8, -1, -8):
-            check(lib.ocm_radix_hist(ctx.handle, ptr(v), dtype, v.numel(), ctypes.c_uint64(prefix), shift, ptr(hist),
-                                     engine._stream(v.device)), "ocm_radix_hist")
+            hist = engine.radix_hist(v, prefix, shift)
             allreduce([hist])
-            h = hist.cpu().numpy()
-            c = np.cumsum(h)
-            d = int(np.searchsorted(c, rank, side="right"))
-            rank -= int(c[d - 1]) if d > 0 else 0
-            prefix |= d << shift
-        return _key_to_value(prefix, dtype)
+            c = np.cumsum(hist.cpu().numpy())
+            dgt = int(np.searchsorted(c, rank, side="right"))
+            rank -= int(c[dgt - 1]) if dgt > 0 else 0
+            prefix |= dgt << shift
+        return _key_to_value(prefix, 1 if f32 else 0)
 
-    q = pct / 100.0
-    vi = (n_total - 1) * q
-    lo = int(np.floor(vi))
-    g = vi - lo
-    a = kth(lo)
-    b = kth(lo + 1) if (g > 0 and lo + 1 < n_total) else a
-    diff = b - a
-    return b - diff * (1 - g) if g >= 0.5 else a + diff * g
+    return _interp(kth, n_total, pct, f32)
+
+
+def _interp(kth, n, pct, f32):
+    """NumPy 2.2 method='linear' (numpy/lib/_function_base_impl.py): q, the
+    virtual index and gamma in the array dtype; _lerp's b-side form for
+    gamma >= 0.5; the top index takes the last order statistic."""
+    ft = np.float32 if f32 else np.float64
+    q = ft(pct) / ft(100)
+    vi = ft(n - 1) * q
+    lo_f = np.floor(vi)
+    top = vi >= ft(n - 1)
+    lo = n - 1 if top else int(lo_f)
+    g = ft(vi - lo_f)
+    a = ft(kth(lo))
+    b = a if top else ft(kth(lo + 1))
+    diff = ft(b - a)
+    return float(ft(b - diff * (ft(1) - g)) if g >= ft(0.5) else ft(a + diff * g))
 
 
 def _key_to_value(key: int, dtype: int) -> float:

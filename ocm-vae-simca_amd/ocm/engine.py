@@ -248,6 +248,20 @@ def cv_counts(T: torch.Tensor, Q: torch.Tensor, inv_evals: torch.Tensor, positiv
     return counts, acc
 
 
+def radix_hist(v: torch.Tensor, prefix: int, shift: int, hist: torch.Tensor | None = None) -> torch.Tensor:
+    """One radix-select pass (ocm_radix_hist): 256-bin counts of the order keys
+    of ``v`` that match ``prefix`` above bit ``shift + 8``, binned by the 8 bits
+    at ``shift``.  int64 tensor on the device."""
+    if v.dtype not in (torch.float64, torch.float32):
+        raise TypeError("radix_hist: float32/float64 only")
+    if hist is None:
+        hist = torch.empty(256, dtype=torch.int64, device=v.device)
+    check(_lib.load().ocm_radix_hist(Context.get(v.device.index).handle, ptr(v), 0 if v.dtype == torch.float64 else 1,
+                                     v.numel(), ctypes.c_uint64(prefix), shift, ptr(hist), _stream(v.device)),
+          "ocm_radix_hist")
+    return hist
+
+
 def rowsq_residual(x: torch.Tensor, xhat: torch.Tensor) -> torch.Tensor:
     """q_i = Σ_j (x_ij − xhat_ij)² (float32 out, fp64 accumulation).  ``xhat``
     may be one row (shape (p,) or (1, p)): it is broadcast to every row."""

@@ -174,6 +174,8 @@ class VAESIMCA:
 
     # -- limits (VAE_SIMCA.py:281-346) -----------------------------------
     def _t2_limit(self, T2, nc):
+        if self.t2lim not in ("perc", "chi2", "Fdist", "chi2pom"):
+            raise ValueError(f"T2 limit type {self.t2lim} not implemented")
         n = T2.numel()
         if self.t2lim in ("perc", "chi2"):
             return engine.percentile(T2, self.t2cl * 100), None, None

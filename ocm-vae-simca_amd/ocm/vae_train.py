@@ -63,15 +63,26 @@ class GraphedVAETrainer:
 
     def _capture(self, warmup):
         self.model.train()
+        # the warm-up steps (allocator, kernel selection, optimizer state
+        # creation) run on the zero batch buffer: snapshot the model and put it
+        # back afterwards, in place, so the first replay is training step 1
+        saved = {k: v.detach().clone() for k, v in self.module.state_dict().items()}
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            for _ in range(warmup):  # allocator / autotuning warm-up outside the graph
+            for _ in range(warmup):
                 self._body()
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = self._body()
+        with torch.no_grad():
+            for k, v in self.module.state_dict().items():
+                v.copy_(saved[k])
+            for st in self.opt.state.values():  # fresh Adam moments and step counters
+                for t in st.values():
+                    if torch.is_tensor(t):
+                        t.zero_()
 
     def step(self, x: torch.Tensor | None = None):
         """Run one training step on ``x`` (copied into the static batch buffer);

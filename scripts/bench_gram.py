@@ -17,7 +17,7 @@ def main():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--p", type=int, default=2048)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="256x32:2048,256x32:1024,256x32:4096,128x32:2048")
+    ap.add_argument("--variants", default="f32:256x32:2048,bf16x3:256x32:2048,bf16x3:256x32:4096,bf16x3:256x32:1024")
     args = ap.parse_args()
     import torch
 
@@ -30,13 +30,15 @@ def main():
     shift = engine.cast_f32(engine.colmean(X, None, 4096))
     ctx = Context.get(0)
     variants = [v.split(":") for v in args.variants.split(",")]
-    res = {v[0] + ":" + v[1]: [] for v in variants}
+    res = {":".join(v): [] for v in variants}
     Gs = {}
     flop = args.rows * args.p * (args.p + 1)
     for r in range(args.rounds):
-        for name, chunk in variants:
+        for mode, name, chunk in variants:
+            os.environ["OCM_GRAM_MODE"] = mode
             os.environ["OCM_GRAM_TILE"], os.environ["OCM_GRAM_BK"] = name.split("x")
             os.environ["OCM_GRAM_CHUNK"] = chunk
+            key = f"{mode}:{name}:{chunk}"
             engine.gram(X, None, [0, args.rows], shift)  # warm (workspace)
             torch.cuda.synchronize()
             ctx.read_timing(0)
@@ -44,13 +46,21 @@ def main():
             G, cs = engine.gram(X, None, [0, args.rows], shift)
             ctx.set_timing(False)
             ms, cnt = ctx.read_timing(0)
-            res[name + ":" + chunk].append(flop / (ms / 1e3) / 1e12)
+            res[key].append(flop / (ms / 1e3) / 1e12)
             if r == 0:
-                Gs[name + ":" + chunk] = G[0].clone()
+                Gs[key] = G[0].clone()
+    # exact reference for the error column: fp64 Gram of a row sample (first 65536 rows)
+    ns = min(args.rows, 65536)
+    Y = (X[:ns].double() - shift.double())
+    Gref = Y.T @ Y
+    for mode in sorted({v[0] for v in variants}):
+        os.environ["OCM_GRAM_MODE"] = mode
+        Gm, _ = engine.gram(X, None, [0, ns], shift)
+        print(f"{mode:8s} sample Gram max rel err vs fp64: {((Gm[0] - Gref).abs().max() / Gref.abs().max()).item():.2e}")
     ref = next(iter(Gs.values()))
     for key, vals in res.items():
         d = ((Gs[key] - ref).abs().max() / ref.abs().max()).item()
-        print(f"{key:16s} TFLOP/s median {sorted(vals)[len(vals)//2]:7.2f}  all {[round(v,1) for v in vals]}  "
+        print(f"{key:24s} TFLOP/s median {sorted(vals)[len(vals)//2]:7.2f}  all {[round(v,1) for v in vals]}  "
               f"maxrel vs first {d:.2e}", flush=True)
 
 

@@ -16,7 +16,7 @@ os.makedirs(prof, exist_ok=True)
 
 
 def short(name):
-    for key in ("k_gram_reduce", "k_gram", "k_score_direct", "k_score"):
+    for key in ("k_gram_reduce", "k_gram3", "k_gram", "k_score_direct", "k_score"):
         if key + "<" in name or key + "(" in name:
             return key
     return name[:60]
@@ -59,7 +59,12 @@ for kname, cs in agg.items():
         rec["wave_cycle_split"] = {k: m[k] / wc for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY") if k in m}
     out[kname] = rec
 json.dump(out, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
-if "k_gram" in out and "hbm_bytes_per_launch" in out["k_gram"]:
-    json.dump({"kernel": "k_gram", "hbm_bytes_per_launch": out["k_gram"]["hbm_bytes_per_launch"], "source": f"{tag}_pmc.json"},
-              open(os.path.join(prof, "pmc_gram_latest.json"), "w"), indent=1)
+latest_path = os.path.join(prof, "pmc_gram_latest.json")
+latest = json.load(open(latest_path)) if os.path.exists(latest_path) else {}
+if "kernel" in latest:  # older single-kernel format
+    latest = {latest["kernel"]: {"hbm_bytes_per_launch": latest["hbm_bytes_per_launch"], "source": latest["source"]}}
+for kname in ("k_gram", "k_gram3"):
+    if kname in out and "hbm_bytes_per_launch" in out[kname]:
+        latest[kname] = {"hbm_bytes_per_launch": out[kname]["hbm_bytes_per_launch"], "source": f"{tag}_pmc.json"}
+json.dump(latest, open(latest_path, "w"), indent=1)
 print(json.dumps(out, indent=1)[:3000])

@@ -1,7 +1,8 @@
 """Test-only CPU stand-in for ``ocm.engine`` (NumPy / torch-CPU arithmetic).
 
 Used ONLY by the CPU test suite to exercise the host and multi-rank logic of
-the fold engine (ocm/cv.py) under torch.distributed ``gloo`` without a GPU.
+the fold engine (ocm/cv.py) and the row-sharded SIMCA (ocm/dist.py) under
+torch.distributed ``gloo`` without a GPU.
 It implements the same contracts as the libocm entry points it stands in for
 (include/ocm.h) with exact fp64 NumPy arithmetic: it is never imported by the
 package, and the GPU tests call the real HIP kernels.
@@ -129,3 +130,88 @@ def cv_counts(T, Q, inv_evals, positive, m_split, configs, want_accept=False):
 
 def percentile(v, pct):
     return float(np.percentile(v.numpy(), pct))
+
+
+def _okey(v: np.ndarray) -> np.ndarray:
+    """Order-preserving unsigned keys (the IEEE sign trick of ocm_select.hip)."""
+    if v.dtype == np.float64:
+        u = v.view(np.uint64)
+        return np.where(u >> np.uint64(63), ~u, u | np.uint64(1 << 63))
+    u = v.view(np.uint32).astype(np.uint64)
+    return np.where(u >> np.uint64(31), (~u) & np.uint64(0xFFFFFFFF), u | np.uint64(0x80000000))
+
+
+def radix_hist(v, prefix, shift, hist=None):
+    a = v.numpy()
+    nbits = 64 if a.dtype == np.float64 else 32
+    keys = _okey(a)
+    if shift + 8 >= nbits:
+        sel = keys
+    else:
+        hi = np.uint64(((~0) << (shift + 8)) & ((1 << nbits) - 1))
+        sel = keys[((keys ^ np.uint64(prefix)) & hi) == 0]
+    digits = ((sel >> np.uint64(shift)) & np.uint64(255)).astype(np.int64)
+    return torch.from_numpy(np.bincount(digits, minlength=256).astype(np.int64))
+
+
+def make_decision(type_name, t2_scale, q_scale, dlim):
+    from ocm._lib import OcmDecision, TYPE_CODES
+
+    return OcmDecision(TYPE_CODES[type_name], 0, float(t2_scale), float(q_scale), float(dlim))
+
+
+def _dred(code, t, q):
+    return {0: np.maximum(t, q), 1: np.sqrt(t * t + q * q)}.get(code, t + q)
+
+
+_score_plain = score
+
+
+def score(X, rows, m, P64, mean64, A, want_T=False, want_T2=True, want_Q=True, decision=None, accept_out=None,
+          accept_stride=1, want_stats=False):
+    out = _score_plain(X, rows, m, P64, mean64, A, want_T=True, want_T2=True, want_Q=True, want_stats=want_stats)
+    if decision is not None:
+        d = _dred(decision.type, out["T2"].numpy() * decision.t2_scale,
+                  out["Q"].numpy().astype(np.float64) * decision.q_scale)
+        accept_out[::accept_stride][:m].copy_(torch.from_numpy((d < decision.dlim).astype(np.float64)))
+    if not want_T:
+        out["T"] = None
+    return out
+
+
+class _Fit:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+        self.extra = {}
+
+
+def invcov_from_evals(evals, rcond=1e-15):
+    lam = evals.to(torch.float64)
+    cut = rcond * lam.abs().max()
+    return torch.diag(torch.where(lam.abs() > cut, 1.0 / lam, torch.zeros_like(lam)))
+
+
+def fit_class(X, rows, n, k, theta_mode, want_T=True, keep_C=False, shift32=None, allreduce=None):
+    """Same control flow and collectives as ocm.engine.fit_class."""
+    p = X.shape[1]
+    if shift32 is None:
+        shift32 = cast_f32(colmean(X, rows, min(n, SHIFT_SAMPLE)))
+        if allreduce is not None:
+            allreduce([shift32], op="mean")
+    G, cs = gram(X, rows, [0, n], shift32)
+    n_total = n
+    if allreduce is not None:
+        cnt = torch.tensor([float(n)], dtype=torch.float64)
+        allreduce([G, cs, cnt])
+        n_total = int(round(cnt.item()))
+    C, mean64 = cov_from_gram([(1.0, G[0], cs[0])], shift32, n_total)
+    evals, evecs, theta, iters = eig_topk(C, k, theta_mode)
+    invcov = invcov_from_evals(evals)
+    sc = score(X, rows, n, evecs, mean64, invcov, want_T=want_T, want_stats=True)
+    stats = sc["stats"]
+    if allreduce is not None:
+        allreduce([stats])
+    st = stats.numpy()
+    return _Fit(k=k, n=n_total, p=p, mean64=mean64, evals=evals, P64=evecs, invcov=invcov,
+                thetas=tuple(float(v) for v in theta.numpy()), evals_host=evals.numpy(), T=sc["T"], T2=sc["T2"],
+                Q=sc["Q"], T2_stats=(st[0], st[1]), Q_stats=(st[2], st[3]), eig_iters=iters, C=None)

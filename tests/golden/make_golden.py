@@ -194,8 +194,9 @@ def make_vae():
         m = ConvVAE1D(L, d, mean, std, **kw)
         out = {"x": x, "x_cal": x_cal, "x_test": x_test, "mean": mean, "std": std,
                "config_json": np.array(json.dumps({"input_length": L, "latent_dim": d, **kw}))}
-        for k, v in m.state_dict().items():
-            out["sd/" + k] = v.detach().numpy().copy()
+        sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
+        for k, v in sd0.items():
+            out["sd/" + k] = v.numpy().copy()
         xt = torch.from_numpy(x)
         with torch.no_grad():
             m.eval()
@@ -211,6 +212,7 @@ def make_vae():
             l2 = beta_vae_cosine_loss(xt, x_rec_t, mu_t, lv_t, beta=0.5)
             out["bce_loss"] = np.array([float(l1[0]), l1[1], l1[2]])
             out["cos_loss"] = np.array([float(l2[0]), l2[1], l2[2]])
+            m.load_state_dict(sd0)  # the train-mode forward above moved the BN running stats
             m.eval()
             for tag, xs in (("cal", x_cal), ("test", x_test)):
                 xs_t = torch.from_numpy(xs)

@@ -39,3 +39,36 @@ def test_trainer_step_matches_reference_step(loss):
                                    rtol=1e-6)
     for (n1, p1), (n2, p2) in zip(m1.named_parameters(), m2.named_parameters()):
         torch.testing.assert_close(p1, p2, rtol=1e-6, atol=1e-7, msg=n1)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_graph_step_trains_like_eager(dtype):
+    """HIP-graph replays start from the initial weights (the capture warm-up is
+    undone) and train like the eager step: finite, decreasing losses whose
+    tail mean matches the eager run's (ε differs between the two generators,
+    so trajectories agree statistically, not bitwise)."""
+    from ocm.vae_train import GraphedVAETrainer
+
+    dev = torch.device("cuda", 0)
+    L, d, B = 256, 8, 128
+    g = torch.Generator(device="cpu").manual_seed(0)
+    X = (1.0 + 0.3 * torch.randn(B * 8, L, generator=g)).to(dev)
+    mean, std = X.mean(0).cpu().numpy(), X.std(0).cpu().numpy()
+    torch.manual_seed(0)
+    m1 = V.ConvVAE1D(L, d, mean, std, conv_blocks=2, n_filters=3, kernel_size=5, hidden_fc=32).to(dev)
+    m2 = copy.deepcopy(m1)
+    sd0 = {k: v.clone() for k, v in m1.state_dict().items()}
+    tg = GraphedVAETrainer(m1, B, lr=1e-3, dtype=dtype, graph=True)
+    for k, v in m1.state_dict().items():  # capture left the model at its initial state
+        torch.testing.assert_close(v, sd0[k], rtol=0, atol=0, msg=k)
+    te = GraphedVAETrainer(m2, B, lr=1e-3, dtype=dtype, graph=False)
+    lg, le = [], []
+    for i in range(60):
+        xb = X[(i % 8) * B:(i % 8 + 1) * B]
+        lg.append(float(tg.step(xb)[0]))
+        le.append(float(te.step(xb)[0]))
+    assert all(np.isfinite(lg)) and all(np.isfinite(le))
+    assert np.mean(lg[-10:]) < 0.5 * lg[0]
+    np.testing.assert_allclose(np.mean(lg[-10:]), np.mean(le[-10:]), rtol=0.2)
