@@ -33,7 +33,7 @@ sys.path.insert(0, REPO)
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix)
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: Peak BF16 MFMA, dense
-GRAM_MODE_DEFAULT = "f32"
+GRAM_MODE_DEFAULT = "bf16x3"
 METRIC = "spectra/sec SIMCA fit+Q/T² score at 1M×2048"
 
 

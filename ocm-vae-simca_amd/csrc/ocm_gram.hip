@@ -376,6 +376,9 @@ __global__ __launch_bounds__(G3THREADS, 1) void k_gram3(
           t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[c][0], t, 0, 0, 0);
           t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[c][1], t, 0, 0, 0);
           t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[c][0], t, 0, 0, 0);
+          // packed f32 adds: the compiler inserts the MFMA→VALU wait states
+          // (an inline-asm v_add_f32 reading t without them reads stale
+          // accumulators — measured: Gram error 0.8)
           acc[a][c] += t;
         }
       }
@@ -772,9 +775,10 @@ int ocm_gram_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows,
   if (const char* e = std::getenv("OCM_GRAM_TILE")) tile = std::atoi(e) == 128 ? 128 : 256;
   if (const char* e = std::getenv("OCM_GRAM_BK")) bk = std::atoi(e) == 16 ? 16 : 32;
   if (const char* e = std::getenv("OCM_GRAM_CHUNK")) chunk_rows = std::max<int64_t>(64, std::atoll(e));
-  // OCM_GRAM_MODE: "f32" (FP32 MFMA) or "bf16x3" (exact 3-level bf16 split on bf16 MFMA)
-  bool split3 = false;
-  if (const char* e = std::getenv("OCM_GRAM_MODE")) split3 = std::string(e) == "bf16x3";
+  // OCM_GRAM_MODE: "bf16x3" (default: exact 3-level bf16 split on bf16 MFMA, 1.33× the
+  // FP32-MFMA kernel and ~5× lower Gram error, profiles/) or "f32" (FP32 MFMA)
+  bool split3 = true;
+  if (const char* e = std::getenv("OCM_GRAM_MODE")) split3 = std::string(e) != "f32";
   if (split3)
     return gram_impl<256, 32>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows,
                               true);

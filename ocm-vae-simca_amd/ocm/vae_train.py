@@ -32,7 +32,7 @@ class GraphedVAETrainer:
     lr / weight_decay as torch.optim.Adam (vae_bce_nut.py:155-159)."""
 
     def __init__(self, model, batch: int, lr=1e-3, weight_decay=0.0, beta=1.0, loss="bce",
-                 dtype=torch.bfloat16, graph=True, warmup=3):
+                 dtype=torch.bfloat16, graph=True, warmup=3, restore=True):
         self.model = model
         self.module = getattr(model, "module", model)
         dev = next(self.module.parameters()).device
@@ -43,6 +43,7 @@ class GraphedVAETrainer:
                                     foreach=True)
         self.x = torch.zeros((batch, self.module.input_length), dtype=torch.float32, device=dev)
         self.graph = None
+        self.restore = restore
         if graph:
             self._capture(warmup)
 
@@ -76,6 +77,8 @@ class GraphedVAETrainer:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = self._body()
+        if not self.restore:
+            return
         with torch.no_grad():
             for k, v in self.module.state_dict().items():
                 v.copy_(saved[k])

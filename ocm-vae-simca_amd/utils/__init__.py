@@ -8,5 +8,6 @@ from .CVSIMCA import (
     plot_cv,
     ClasswiseKFoldWithExternalVal,
 )
+from .data_utils import object_aware_splits
 
-__all__ = ["SIMCA", "cross_validate_simca_grid", "plot_cv", "ClasswiseKFoldWithExternalVal"]
+__all__ = ["SIMCA", "cross_validate_simca_grid", "plot_cv", "ClasswiseKFoldWithExternalVal", "object_aware_splits"]

@@ -35,7 +35,11 @@ def main():
     flop = args.rows * args.p * (args.p + 1)
     for r in range(args.rounds):
         for mode, name, chunk in variants:
-            os.environ["OCM_GRAM_MODE"] = mode
+            os.environ["OCM_GRAM_MODE"] = "bf16x3" if mode.startswith("bf16x3") else mode
+            if mode == "bf16x3pk":
+                os.environ["OCM_GRAM3_PK"] = "1"
+            else:
+                os.environ.pop("OCM_GRAM3_PK", None)
             os.environ["OCM_GRAM_TILE"], os.environ["OCM_GRAM_BK"] = name.split("x")
             os.environ["OCM_GRAM_CHUNK"] = chunk
             key = f"{mode}:{name}:{chunk}"
@@ -53,7 +57,8 @@ def main():
     ns = min(args.rows, 65536)
     Y = (X[:ns].double() - shift.double())
     Gref = Y.T @ Y
-    for mode in sorted({v[0] for v in variants}):
+    os.environ.pop("OCM_GRAM3_PK", None)
+    for mode in sorted({v[0] for v in variants} - {"bf16x3pk"}):
         os.environ["OCM_GRAM_MODE"] = mode
         Gm, _ = engine.gram(X, None, [0, ns], shift)
         print(f"{mode:8s} sample Gram max rel err vs fp64: {((Gm[0] - Gref).abs().max() / Gref.abs().max()).item():.2e}")

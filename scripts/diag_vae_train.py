@@ -17,15 +17,17 @@ B, L, nb = 512, 2048, 16
 X = synth_device(B * nb, L, 20, seed=99, device=dev)
 mean = X.mean(0).cpu().numpy()
 std = X.std(0).cpu().numpy() + 1e-6
-for dtype in (torch.float32, torch.bfloat16):
-    for graph in (False, True):
+for dtype, graph, restore in ((torch.float32, False, True), (torch.float32, True, True), (torch.float32, True, False),
+                              (torch.bfloat16, False, True), (torch.bfloat16, True, True),
+                              (torch.bfloat16, True, False)):
+    if True:
         torch.manual_seed(0)
         m = V.ConvVAE1D(L, 32, mean, std, conv_blocks=3, n_filters=3, kernel_size=7, hidden_fc=64).to(dev)
-        tr = GraphedVAETrainer(m, B, lr=1e-3, dtype=dtype, graph=graph)
+        tr = GraphedVAETrainer(m, B, lr=1e-3, dtype=dtype, graph=graph, restore=restore)
         traj = []
-        for i in range(300):
+        for i in range(400):
             out = tr.step(X[(i % nb) * B:(i % nb + 1) * B])
-            if i % 25 == 0 or i == 299:
+            if i % 25 == 0 or i == 399:
                 traj.append(round(float(out[0]), 4))
         bad = [n for n, p in m.named_parameters() if not torch.isfinite(p).all()]
-        print(f"{str(dtype):15s} graph={graph!s:5s} loss {traj}  nonfinite params: {bad[:4]}", flush=True)
+        print(f"{str(dtype):15s} graph={graph!s:5s} restore={restore!s:5s} loss {traj}  nonfinite params: {bad[:4]}", flush=True)

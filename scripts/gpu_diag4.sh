@@ -1,0 +1,6 @@
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python scripts/diag_vae_train.py > gpurun_out/diag_vae_train.log 2>&1 || { echo "vae diag failed"; tail -20 gpurun_out/diag_vae_train.log; exit 3; }
+grep -v amdgpu.ids gpurun_out/diag_vae_train.log
+echo done

@@ -15,6 +15,7 @@ outputs.  They are data (inputs and expected outputs), not reference source.
   set, predictions and transform() outputs on X_test.
 * cv_<name>.npz      — cross_validate_simca_grid records (spec/sens/eff per LV).
 * qhf.npz            — vae_model.compute_q_h_f on a fixed batch.
+* splits.npz         — utils.data_utils.object_aware_splits on synthetic objects.
 * vae_<name>.npz     — vae_model.ConvVAE1D (seeded init → state_dict), eval /
   train forward on a fixed batch with seeded ε, both losses, and the latent
   inputs of VAESIMCA (encoder μ, round trip ẑ) on a calibration / test set.
@@ -224,6 +225,38 @@ def make_vae():
         print("vae", name, sum(v.numel() for v in m.parameters()), "params")
 
 
+def make_splits():
+    """utils.data_utils.object_aware_splits on a synthetic 3-type object set
+    (with NaN rows and shifted outlier pixels)."""
+    from utils.data_utils import object_aware_splits
+
+    rng = np.random.default_rng(31)
+    p = 40
+    wl = np.linspace(0, 1, p)
+    data, inputs = {}, {}
+    for t, nut in enumerate(["almond", "hazelnut", "peanut"]):
+        objs = []
+        for o in range(7 + t):
+            n_o = int(rng.integers(30, 90))
+            base = 1.0 + 0.3 * np.sin((3 + t) * wl) + 0.05 * o
+            X = (base + 0.02 * rng.standard_normal((n_o, p))).astype(np.float32)
+            X[rng.random(n_o) < 0.05] += 0.3 * np.exp(-0.5 * ((wl - 0.6) / 0.05) ** 2).astype(np.float32)
+            if o == 1:
+                X[3, 5] = np.nan
+            objs.append({"spectral_data": X})
+            inputs[f"in/{nut}/{o}"] = X
+        data[nut] = objs
+    with contextlib.redirect_stdout(io.StringIO()):
+        splits, Xts, yts, Xc, Xv, Xti, Xto = object_aware_splits(data, list(data), "peanut", p)
+    out = dict(inputs)
+    out.update({"Xts": Xts, "yts": yts, "Xc": Xc, "Xv": Xv, "Xti": Xti, "Xto": Xto})
+    for nut, d in splits.items():
+        for k, v in d.items():
+            out[f"split/{nut}/{k}"] = v
+    np.savez_compressed(os.path.join(HERE, "splits.npz"), **out)
+    print("splits", Xc.shape, Xv.shape, Xti.shape, Xto.shape)
+
+
 def main():
     # A: one class, spectral gap at k (SURVEY.md §8d), wavelength-correlated bands.
     # The last 100 rows carry the out-of-class band; fit on the first 1200.
@@ -259,6 +292,7 @@ def main():
 
     make_qhf()
     make_vae()
+    make_splits()
 
 
 if __name__ == "__main__":
