@@ -27,6 +27,9 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
+# before HIP initialises: the VAE's HIP-graph step needs the runtime's graph
+# packet capture off (ocm/__init__.py explains the race)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 sys.path.insert(0, os.path.join(REPO, "ocm-vae-simca_amd"))
 sys.path.insert(0, REPO)
 

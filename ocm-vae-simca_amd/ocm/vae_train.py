@@ -18,6 +18,9 @@ trainer; the gradient all-reduce (RCCL over xGMI) is captured with the step.
 """
 from __future__ import annotations
 
+import os
+import warnings
+
 import torch
 
 import vae_model as V
@@ -44,6 +47,13 @@ class GraphedVAETrainer:
         self.x = torch.zeros((batch, self.module.input_length), dtype=torch.float32, device=dev)
         self.graph = None
         self.restore = restore
+        if graph and os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") != "0":
+            # the runtime's packet-capture replay races (ocm/__init__.py); the
+            # flag only takes effect if set before HIP initialises
+            warnings.warn("DEBUG_CLR_GRAPH_PACKET_CAPTURE is not 0 (import ocm before torch initialises the GPU): "
+                          "HIP-graph VAE steps are unsafe on this runtime, running the step eagerly")
+            graph = False
+        self.graphed = graph
         if graph:
             self._capture(warmup)
 

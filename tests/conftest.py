@@ -3,6 +3,9 @@ import sys
 
 import pytest
 
+# before any HIP initialisation: see ocm/__init__.py (graph packet-capture race)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "ocm-vae-simca_amd")
 for p in (REPO, PKG):

@@ -72,3 +72,32 @@ def test_graph_step_trains_like_eager(dtype):
     assert all(np.isfinite(lg)) and all(np.isfinite(le))
     assert np.mean(lg[-10:]) < 0.5 * lg[0]
     np.testing.assert_allclose(np.mean(lg[-10:]), np.mean(le[-10:]), rtol=0.2)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+def test_graph_replays_queued_after_sync_stay_finite():
+    """Regression: bench-shaped replays queued back to back after a host sync
+    (the ROCm graph packet-capture race turned the loss NaN two replays after
+    the sync, every run).  The flag is set in conftest / ocm before HIP init."""
+    import os
+
+    from ocm.vae_train import GraphedVAETrainer
+
+    assert os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") == "0"
+    dev = torch.device("cuda", 0)
+    L, d, B = 1024, 16, 256
+    g = torch.Generator(device="cpu").manual_seed(1)
+    X = (1.0 + 0.3 * torch.randn(B * 8, L, generator=g)).to(dev)
+    mean, std = X.mean(0).cpu().numpy(), X.std(0).cpu().numpy()
+    torch.manual_seed(0)
+    m = V.ConvVAE1D(L, d, mean, std, conv_blocks=3, n_filters=3, kernel_size=7, hidden_fc=64).to(dev)
+    tr = GraphedVAETrainer(m, B, lr=1e-3, dtype=torch.bfloat16, graph=True)
+    assert tr.graphed
+    losses = torch.zeros(80, device=dev)
+    for i in range(80):
+        losses[i].copy_(tr.step(X[(i % 8) * B:(i % 8 + 1) * B])[0])
+        if i in (9, 39):
+            torch.cuda.synchronize()
+    assert bool(torch.isfinite(losses).all()), losses.cpu()
+    assert all(bool(torch.isfinite(p).all()) for p in m.parameters())
