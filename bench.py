@@ -36,7 +36,8 @@ sys.path.insert(0, REPO)
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix)
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: Peak BF16 MFMA, dense
-GRAM_MODE_DEFAULT = "bf16x3"
+I8_MFMA_PEAK_TOPS = 5000.0      # MI355X_MICROARCH.md: I8 MFMA = 2x BF16 per clock (dense)
+GRAM_MODE_DEFAULT = "i8x3"
 METRIC = "spectra/sec SIMCA fit+Q/T² score at 1M×2048"
 
 
@@ -53,7 +54,8 @@ def parse():
     ap.add_argument("--no-vae", action="store_true", help="skip the secondary VAE train-steps/s measurement")
     ap.add_argument("--vae-steps", type=int, default=200)
     ap.add_argument("--gram-mode", default=os.environ.get("OCM_GRAM_MODE", GRAM_MODE_DEFAULT),
-                    choices=["f32", "bf16x3"], help="Gram kernel: FP32 MFMA or the exact bf16x3 split")
+                    choices=["f32", "bf16x3", "i8x3"],
+                    help="Gram kernel: int8 digit split (default), bf16x3 split or FP32 MFMA")
     return ap.parse_args()
 
 
@@ -172,8 +174,8 @@ def main():
     for _ in range(args.warmup):
         step()
     ctx = _lib.Context.get(device.index)
-    ctx.read_timing(0)
-    ctx.read_timing(1)
+    for kid in range(3):
+        ctx.read_timing(kid)
     ctx.set_timing(True)
     if world > 1:
         dist.barrier()
@@ -188,6 +190,7 @@ def main():
     ctx.set_timing(False)
     gram_ms, gram_n = ctx.read_timing(0)
     score_ms, score_n = ctx.read_timing(1)
+    quant_ms, quant_n = ctx.read_timing(2)
     dt = t1 - t0
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=device)
@@ -202,8 +205,13 @@ def main():
     score_avg_s = score_ms / max(score_n, 1) / 1e3
     score_gbs = n * p * 4 / score_avg_s / 1e9 if score_avg_s > 0 else 0.0
 
-    gram_kernel = "k_gram3" if args.gram_mode == "bf16x3" else "k_gram"
-    if args.gram_mode == "bf16x3":
+    gram_kernel = {"bf16x3": "k_gram3", "i8x3": "k_gram8"}.get(args.gram_mode, "k_gram")
+    if args.gram_mode == "i8x3":
+        # fp32-grade product from 6 int8 MFMA digit products (exact int32 sums)
+        gram_desc = "k_gram8 (shifted Gram, 3 int8 digits per value, 6 i8 MFMA products per fp32 product)"
+        gram_peak = round(I8_MFMA_PEAK_TOPS / 6, 1)
+        peak_basis = "int8 MFMA dense peak / 6 (fp32-equivalent); achieved counts algorithmic fp32 flops n*p*(p+1)"
+    elif args.gram_mode == "bf16x3":
         # fp32-exact product from 6 bf16 MFMA products: the attainable fp32-equivalent peak is the bf16 peak / 6
         gram_desc = "k_gram3 (shifted Gram, exact 3-level bf16 split, 6 bf16 MFMA products per fp32 product)"
         gram_peak = round(BF16_MFMA_PEAK_TFLOPS / 6, 1)
@@ -251,6 +259,7 @@ def main():
             "peak_basis": peak_basis,
             "traffic": traffic,
             "flop_per_launch": gram_flop,
+            "quantise_ms": round(quant_ms / max(quant_n, 1), 4) if quant_n else None,
             "avg_launch_ms": round(gram_avg_s * 1e3, 4),
             "launches": gram_n,
         },

@@ -71,9 +71,10 @@ int ocm_ctx_reserve(ocm_ctx* ctx, size_t bytes);
  * kernel is bracketed by a hipEvent pair on its stream (no synchronisation).
  * ocm_ctx_read_timing waits for the recorded events, returns the summed
  * duration (ms) and launch count of kernel `kernel_id`, and clears them. */
-#define OCM_TIMED_KERNELS 2
-#define OCM_KERNEL_GRAM 0  /* k_gram: the FP32-MFMA Gram main kernel */
+#define OCM_TIMED_KERNELS 3
+#define OCM_KERNEL_GRAM 0  /* the Gram main kernel (k_gram8 / k_gram3 / k_gram) */
 #define OCM_KERNEL_SCORE 1 /* k_score: fused projection / Q / T² kernel */
+#define OCM_KERNEL_QUANT 2 /* k_q8_quant: int8 digit split feeding k_gram8 */
 int ocm_ctx_set_timing(ocm_ctx* ctx, int enable);
 int ocm_ctx_read_timing(ocm_ctx* ctx, int kernel_id, double* total_ms, int64_t* count);
 

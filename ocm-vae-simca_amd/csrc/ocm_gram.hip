@@ -413,7 +413,7 @@ template <int GT>
 __global__ __launch_bounds__(256) void k_gram_reduce(const float* __restrict__ part,
                                                      const double* __restrict__ colpart, int nt, int ntiles, int p,
                                                      int c0, int c1, double* __restrict__ G,
-                                                     double* __restrict__ colsum) {
+                                                     double* __restrict__ colsum, int cmul = 1) {
   const int tile = blockIdx.y;
   const int e4 = blockIdx.x * blockDim.x + threadIdx.x;  // float4 index in tile
   int ti, tj;
@@ -453,10 +453,11 @@ __global__ __launch_bounds__(256) void k_gram_reduce(const float* __restrict__ p
     }
   }
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ti == tj && e < GT) {
+  if (ti == tj && e < GT && cmul > 0) {
     const int gi = ti * GT + e;
     double v = 0.0;
-    for (int c = c0; c < c1; ++c) v += colpart[((size_t)c * nt + ti) * GT + e];
+    // colpart rows: cmul per chunk (the i8 quantiser writes one per scale block)
+    for (int c = c0 * cmul; c < c1 * cmul; ++c) v += colpart[((size_t)c * nt + ti) * GT + e];
     if (gi < p) colsum[gi] = v;
   }
 }
@@ -608,6 +609,381 @@ __global__ __launch_bounds__(256) void k_gram_small_reduce(const double* __restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// i8×3 Gram (default): the Gram on integer MFMA (v_mfma_i32_32x32x32_i8, 2×
+// the bf16 rate, exact int32 accumulation).
+//
+// k_q8_quant (one HBM read of X) writes y = x − shift as three signed int8
+// digit planes per 256-row scale block b and column j:
+//     y = s_bj · (a1 + a2/254 + a3/254²),   |a·| ≤ 127,   s_bj = 2^e ≥ max|y|/127
+// (s a power of two, so y/s is exact; a1 = rint(y/s), a2 = rint(254·r1), a3 =
+// rint(254·r2) with |r·| ≤ ½; the residual is ≤ ½·254⁻²·s ≈ 2⁻²⁴·max|y|).
+// k_gram8 accumulates, per 128×128 tile, the six digit products of weight
+// ≥ 254⁻² in three int32 sets (A1 = Σa1a1', A2 = Σa1a2'+a2a1', A3 = Σa1a3'+
+// a3a1'+a2a2' — exact: |A| < 2²⁴ per block) and folds each scale block into
+// f64 running sums: G += s_i s_j (A1 + A2/254 + A3/254²).  The dropped
+// products are ≤ 2⁻²⁴·max|y_i|·max|y_j| per row, the size of an f32 rounding
+// of the largest product (numpy emulation at 20k×256: Frobenius error 3.8e-8
+// vs 4.5e-8 for f32 accumulation).  No rounding happens inside the MFMA, so
+// there is no truncation bias and no VALU add per K-step (cf. k_gram3).
+//
+// Digit planes: [digit][32-row group][column P8][32 B] (the 32 B of a column
+// are its 32 rows of one group — one MFMA K-step).  A workgroup (4 waves, one
+// per SIMD, 2×2 waves of 64×64) owns one upper-triangle 128×128 tile over one
+// chunk; stages of 32 rows are register-prefetched two ahead and stored to a
+// double-buffered LDS image with the k_gram3 half swizzle (conflict-free
+// ds_read_b128 fragments).  The digit planes are in processed-row order, so
+// class subsets / CV folds (gather lists) are gathered once, by the quantiser.
+// ---------------------------------------------------------------------------
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+constexpr int Q8T = 128, Q8K = 32, Q8BLK = 256, Q8SPB = Q8BLK / Q8K;
+constexpr float Q8BASE = 254.f;
+
+struct Q8Plan {
+  char* digits;   // 3 planes
+  size_t plane;   // bytes per plane
+  float* scale;   // [chunk][nblk][P8]
+  int P8;         // padded columns (multiple of Q8T)
+  int nblk;       // scale blocks per chunk
+};
+
+__device__ __forceinline__ uint32_t q8_byte(float a, int u) { return ((uint32_t)(int)a & 0xffu) << (8 * u); }
+
+__device__ __forceinline__ uint32_t q8_pack4(float a0, float a1, float a2, float a3) {
+  // low bytes of the four digits (two's complement int8) into one dword
+  const uint32_t lo = __builtin_amdgcn_perm((uint32_t)(int)a1, (uint32_t)(int)a0, 0x0c0c0400u);
+  const uint32_t hi = __builtin_amdgcn_perm((uint32_t)(int)a3, (uint32_t)(int)a2, 0x04000c0cu);
+  return lo | hi;
+}
+
+// grid (chunk · nblk + block, P8 / 128), 512 threads: one 256-row scale
+// block × 128 columns.  Wave w, lane half h own rows 32w + 16h .. +15 (= half
+// h of 32-row group w) and lane l&31 owns columns 4(l&31) .. +3: float4 loads,
+// 2 × 512 B per wave instruction, and each (column, digit) of a thread is one
+// 16-B piece of the digit image.  The pieces are staged through LDS (one
+// digit plane at a time) so that the stores leave as contiguous 1-KiB runs.
+template <bool GATHER>
+__global__ __launch_bounds__(512, 2) void k_q8_quant(const float* __restrict__ X, int64_t ldx,
+                                                     const int64_t* __restrict__ rows, int p,
+                                                     const float* __restrict__ shift, SegTable st, Q8Plan q,
+                                                     double* __restrict__ colblk) {
+  constexpr int QC = 128;                            // columns per workgroup
+  __shared__ __attribute__((aligned(16))) char stage[Q8SPB * QC * 32];  // one digit plane: 32 KiB
+  __shared__ __attribute__((aligned(16))) float wmax[16][QC];
+  __shared__ __attribute__((aligned(16))) double wsum[16][QC];
+  __shared__ __attribute__((aligned(16))) float fmax_[QC];
+  const int chunk = blockIdx.x / q.nblk, b = blockIdx.x - chunk * q.nblk;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, cl = lane & 31;
+  const int cg0 = blockIdx.y * QC;      // first column of the workgroup
+  const int c0 = cg0 + 4 * cl;          // first of this thread's 4 columns
+  int s = 0;
+  while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
+  const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
+  const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
+  if (r0 + (int64_t)b * Q8BLK >= r1) return;  // block past the chunk's rows (whole workgroup)
+  const int64_t rb = r0 + (int64_t)b * Q8BLK + 32 * wave + 16 * h;
+  const bool vec = (ldx % 4 == 0) && (c0 + 3 < p) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+  f32x4 sh;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sh[e] = c0 + e < p ? shift[c0 + e] : 0.f;
+  f32x4 v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int64_t g = rb + j;
+    const int64_t gc = g < r1 ? g : r1 - 1;  // clamped: always a valid row
+    const float* xr = X + (GATHER ? rows[gc] : gc) * ldx;
+    f32x4 x;
+    if (vec) {
+      x = *reinterpret_cast<const f32x4*>(xr + c0);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = xr[min(c0 + e, p - 1)];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[j][e] = (g < r1 && c0 + e < p) ? x[e] - sh[e] : 0.f;
+  }
+  f32x4 m = {0.f, 0.f, 0.f, 0.f};
+  double cs[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      m[e] = fmaxf(m[e], fabsf(v[j][e]));
+      cs[e] += (double)v[j][e];
+    }
+  const int wr = 2 * wave + h;  // 16 row slices
+  *reinterpret_cast<f32x4*>(&wmax[wr][4 * cl]) = m;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) wsum[wr][4 * cl + e] = cs[e];
+  __syncthreads();
+  if (tid < QC) {
+    float mm = 0.f;
+    double ss = 0.0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      mm = fmaxf(mm, wmax[w][tid]);
+      ss += wsum[w][tid];
+    }
+    fmax_[tid] = mm;
+    int ex = 0;
+    (void)frexpf(mm * (1.f / 127.f), &ex);
+    const size_t o = ((size_t)chunk * q.nblk + b) * q.P8 + cg0 + tid;
+    q.scale[o] = mm > 0.f ? ldexpf(1.f, ex) : 1.f;
+    colblk[o] = ss;
+  }
+  __syncthreads();
+  const f32x4 mx = *reinterpret_cast<const f32x4*>(&fmax_[4 * cl]);
+  i32x4 w[3][4];  // [digit][column e]
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    int ex = 0;
+    (void)frexpf(mx[e] * (1.f / 127.f), &ex);
+    const float inv = mx[e] > 0.f ? ldexpf(1.f, -ex) : 1.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float d1[4], d2[4], d3[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float t = v[4 * k + u][e] * inv;  // exact (power of two), |t| ≤ 127
+        const float a1 = rintf(t);
+        const float t2 = (t - a1) * Q8BASE;
+        const float a2 = rintf(t2);
+        d1[u] = a1;
+        d2[u] = a2;
+        d3[u] = rintf((t2 - a2) * Q8BASE);
+      }
+      w[0][e][k] = (int)q8_pack4(d1[0], d1[1], d1[2], d1[3]);
+      w[1][e][k] = (int)q8_pack4(d2[0], d2[1], d2[2], d2[3]);
+      w[2][e][k] = (int)q8_pack4(d3[0], d3[1], d3[2], d3[3]);
+    }
+  }
+  // stage image: [group w][column 0..127][32 B]; copy-out: 16 B per thread and
+  // pass, 1 KiB contiguous per wave instruction
+  char* gdst = q.digits + ((size_t)chunk * (st.chunk_rows / Q8K) + (size_t)b * Q8SPB) * q.P8 * 32 + (size_t)cg0 * 32;
+#pragma unroll
+  for (int dg = 0; dg < 3; ++dg) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      *reinterpret_cast<i32x4*>(&stage[(wave * QC + 4 * cl + e) * 32 + 16 * h]) = w[dg][e];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int o = 16 * (tid + 512 * k);  // byte offset in the stage image
+      const int g = o / (QC * 32), within = o - g * (QC * 32);
+      *reinterpret_cast<i32x4*>(gdst + (size_t)dg * q.plane + (size_t)g * q.P8 * 32 + within) =
+          *reinterpret_cast<const i32x4*>(&stage[o]);
+    }
+    __syncthreads();
+  }
+}
+
+// Column sums of the quantiser's per-block partials: rows [c0, c1) of colblk
+// (P8 wide) → colsum (p).  16 fixed row slices per column, combined in order.
+__global__ __launch_bounds__(256) void k_colblk_sum(const double* __restrict__ colblk, int64_t c0, int64_t c1,
+                                                    int P8, int p, double* __restrict__ colsum) {
+  __shared__ double red[16][16];
+  const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + cl;
+  double v0 = 0.0, v1 = 0.0;
+  int64_t r = c0 + sl;
+  for (; r + 16 < c1; r += 32) {
+    v0 += colblk[(size_t)r * P8 + col];
+    v1 += colblk[(size_t)(r + 16) * P8 + col];
+  }
+  if (r < c1) v0 += colblk[(size_t)r * P8 + col];
+  red[sl][cl] = v0 + v1;
+  __syncthreads();
+  if (sl == 0 && col < p) {
+    double t = 0.0;
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    colsum[col] = t;
+  }
+}
+
+__device__ __forceinline__ int q8_off(int panel, int dg, int col, int half) {
+  return (((panel * 3 + dg) * Q8T + col) << 5) + ((half ^ ((col >> 3) & 1)) << 4);
+}
+
+__global__ __launch_bounds__(256, 1) void k_gram8(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
+                                                  float* __restrict__ part) {
+  constexpr int STAGE = 2 * 3 * Q8T * 32;  // 24 KiB: both panels, three digits
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+  __shared__ float sc[2][2 * Q8T];  // scale-block parity × [panel][column]
+  // f32 running sums of the flushed scale blocks, wave-private: [wave][a·2+c][r/4][lane][4]
+  __shared__ __attribute__((aligned(16))) float runl[4][4][4][64][4];
+
+  const int b = blockIdx.x;
+  const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
+  const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int chunk = wg / ntiles;
+  const int tile = wg - chunk * ntiles;
+  int ti, tj;
+  tile_coords(tile, nt, ti, tj);
+  const bool diag = (ti == tj);
+  const int I = ti * Q8T, J = tj * Q8T;
+  int s = 0;
+  while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
+  const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
+  const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
+  // whole scale blocks: the quantiser zero-fills a block's rows past r1, so
+  // every loop trip is identical (branch-free loads → exact vmcnt waits)
+  const int nb = (int)((r1 - r0 + Q8BLK - 1) / Q8BLK);
+  const int nstage = nb * Q8SPB;
+  const size_t gbase = (size_t)chunk * (st.chunk_rows / Q8K);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int l31 = lane & 31, h = lane >> 5;
+  const bool idle = diag && wm > wn;  // strictly-lower 64×64 block of a diagonal tile
+  // loader: thread → one 16-B piece (column lcol, half lhalf) of each of the six images
+  const int lcol = tid >> 1, lhalf = tid & 1;
+  const size_t gstride = (size_t)q.P8 * 32;
+  const char* srcA = q.digits + (size_t)(I + lcol) * 32 + lhalf * 16 + gbase * gstride;
+  const char* srcB = q.digits + (size_t)(J + lcol) * 32 + lhalf * 16 + gbase * gstride;
+  const float* sblk = q.scale + (size_t)chunk * q.nblk * q.P8 + (tid < Q8T ? I + tid : J + tid - Q8T);
+  const int wo0 = q8_off(0, 0, lcol, lhalf), wo1 = q8_off(1, 0, lcol, lhalf);
+
+#define Q8_GLOAD(R, STG)                                                                     \
+  do {                                                                                     \
+    const size_t go_ = (size_t)(STG) * gstride;                                            \
+    R##0 = *reinterpret_cast<const i32x4*>(srcA + go_);                                    \
+    R##1 = *reinterpret_cast<const i32x4*>(srcA + q.plane + go_);                          \
+    R##2 = *reinterpret_cast<const i32x4*>(srcA + 2 * q.plane + go_);                      \
+    R##3 = *reinterpret_cast<const i32x4*>(srcB + go_);                                    \
+    R##4 = *reinterpret_cast<const i32x4*>(srcB + q.plane + go_);                          \
+    R##5 = *reinterpret_cast<const i32x4*>(srcB + 2 * q.plane + go_);                      \
+  } while (0)
+#define Q8_SSTORE(R, BI)                                                                     \
+  do {                                                                                     \
+    char* buf_ = lds + (BI) * STAGE;                                                       \
+    *reinterpret_cast<i32x4*>(buf_ + wo0) = R##0;                                          \
+    *reinterpret_cast<i32x4*>(buf_ + wo0 + Q8T * 32) = R##1;                               \
+    *reinterpret_cast<i32x4*>(buf_ + wo0 + 2 * Q8T * 32) = R##2;                           \
+    *reinterpret_cast<i32x4*>(buf_ + wo1) = R##3;                                          \
+    *reinterpret_cast<i32x4*>(buf_ + wo1 + Q8T * 32) = R##4;                               \
+    *reinterpret_cast<i32x4*>(buf_ + wo1 + 2 * Q8T * 32) = R##5;                           \
+  } while (0)
+
+  i32x16 acc1[2][2], acc2[2][2], acc3[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      acc1[a][c] = i32x16{};
+      acc2[a][c] = i32x16{};
+      acc3[a][c] = i32x16{};
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(&runl[wave][a * 2 + c][g][lane][0]) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  auto compute = [&](int bi) __attribute__((always_inline)) {
+    if (idle) return;
+    const char* buf = lds + bi * STAGE;
+    i32x4 bv[2][3];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int dg = 0; dg < 3; ++dg)
+        bv[c][dg] = *reinterpret_cast<const i32x4*>(buf + q8_off(1, dg, wn * 64 + c * 32 + l31, h));
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      i32x4 av[3];
+#pragma unroll
+      for (int dg = 0; dg < 3; ++dg)
+        av[dg] = *reinterpret_cast<const i32x4*>(buf + q8_off(0, dg, wm * 64 + a * 32 + l31, h));
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        acc1[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[0], bv[c][0], acc1[a][c], 0, 0, 0);
+        acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[0], bv[c][1], acc2[a][c], 0, 0, 0);
+        acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[1], bv[c][0], acc2[a][c], 0, 0, 0);
+        acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[0], bv[c][2], acc3[a][c], 0, 0, 0);
+        acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[2], bv[c][0], acc3[a][c], 0, 0, 0);
+        acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[1], bv[c][1], acc3[a][c], 0, 0, 0);
+      }
+    }
+  };
+  auto flush = [&](int par) __attribute__((always_inline)) {
+    if (idle) return;
+    constexpr float w2 = 1.f / 254.f, w3 = 1.f / (254.f * 254.f);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const float sj = sc[par][Q8T + wn * 64 + c * 32 + l31];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4* rp = reinterpret_cast<f32x4*>(&runl[wave][a * 2 + c][g][lane][0]);
+          f32x4 rv = *rp;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g + e;
+            // |A·| < 2²⁴ per block: the int → f32 conversions are exact; si·sj is a power of two
+            const float si = sc[par][wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h];
+            const float v = fmaf((float)acc3[a][c][r], w3, fmaf((float)acc2[a][c][r], w2, (float)acc1[a][c][r]));
+            rv[e] = fmaf(v, si * sj, rv[e]);
+          }
+          *rp = rv;
+        }
+        acc1[a][c] = i32x16{};
+        acc2[a][c] = i32x16{};
+        acc3[a][c] = i32x16{};
+      }
+    }
+  };
+  // one pipeline step: stage STG (LDS buffer BI) is computed; stage STG+1
+  // (registers RN) is stored to the other buffer; RN then loads stage STG+3.
+  // The scale of stage STG+2's block was loaded one step earlier (SCN) and is
+  // staged to LDS here; the scale of stage STG+3's block is loaded before
+  // the stage loads, so every wait is on the oldest loads only.
+#define Q8_STEP(STG, BI, RN)                                                                          \
+  do {                                                                                              \
+    sc[(((STG) + 2) / Q8SPB) & 1][tid] = scn;                                                       \
+    compute(BI);                                                                                    \
+    Q8_SSTORE(RN, (BI) ^ 1);                                                                        \
+    __syncthreads();                                                                                \
+    const int nx_ = min((STG) + 3, nstage - 1);                                                     \
+    scn = sblk[(size_t)(nx_ / Q8SPB) * q.P8];                                                       \
+    Q8_GLOAD(RN, nx_);                                                                              \
+  } while (0)
+
+  i32x4 RA0, RA1, RA2, RA3, RA4, RA5, RB0, RB1, RB2, RB3, RB4, RB5;
+  sc[0][tid] = sblk[0];
+  float scn = sblk[(size_t)(min(2, nstage - 1) / Q8SPB) * q.P8];
+  Q8_GLOAD(RA, 0);
+  Q8_GLOAD(RB, 1);
+  Q8_SSTORE(RA, 0);
+  __syncthreads();
+  Q8_GLOAD(RA, 2);
+  for (int blk = 0; blk < nb; ++blk) {
+#pragma unroll
+    for (int u = 0; u < Q8SPB; u += 2) {
+      const int stg = blk * Q8SPB + u;
+      Q8_STEP(stg, 0, RB);
+      Q8_STEP(stg + 1, 1, RA);
+    }
+    flush(blk & 1);
+  }
+#undef Q8_STEP
+#undef Q8_SSTORE
+#undef Q8_GLOAD
+
+  if (idle) return;
+  float* out = part + ((size_t)chunk * ntiles + tile) * (Q8T * Q8T);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int col = wn * 64 + c * 32 + l31;
+        out[row * Q8T + col] = runl[wave][a * 2 + c][r >> 2][lane][r & 3];
+      }
+}
+
 int gram_small(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int32_t p, const float* shift,
                const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out, hipStream_t st) {
   // chunks never straddle a segment: span = (lo, hi) row range per chunk
@@ -730,6 +1106,94 @@ int gram_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, in
   return OCM_OK;
 }
 
+// i8×3 path: quantise (one read of X) → integer-MFMA Gram → f64 reduce.
+int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+               const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
+               hipStream_t st, int64_t chunk_rows) {
+  const int P8 = (int)ocm::align_up((size_t)p, Q8T);
+  const int nt = P8 / Q8T;
+  const int ntiles = nt * (nt + 1) / 2;
+  if (chunk_rows <= 0) {
+    // enough workgroups to fill the chip (≥ 4 per CU), ≤ 4096 rows per chunk
+    const int64_t want = std::max<int64_t>(1, (4LL * ctx->num_cus + ntiles - 1) / ntiles);
+    chunk_rows = std::min<int64_t>(4096, (n + want - 1) / want);
+  }
+  chunk_rows = std::max<int64_t>(Q8BLK, (int64_t)ocm::align_up((size_t)chunk_rows, Q8BLK));
+  std::vector<int32_t> cprefix(nseg + 1, 0);
+  for (int s = 0; s < nseg; ++s) {
+    const int64_t len = seg_offsets[s + 1] - seg_offsets[s];
+    cprefix[s + 1] = cprefix[s] + (int32_t)((len + chunk_rows - 1) / chunk_rows);
+  }
+  const int64_t nchunks = cprefix[nseg];
+  const int nblk = (int)(chunk_rows / Q8BLK);
+  const size_t plane = (size_t)nchunks * chunk_rows * P8;  // 1 B per digit
+  const size_t scale_elems = (size_t)nchunks * nblk * P8;
+  const size_t col_elems = (size_t)nchunks * nblk * P8;  // per scale block
+  const size_t part_elems = (size_t)nchunks * ntiles * Q8T * Q8T;
+  void* wsp = ocm::workspace(ctx, 3 * plane + scale_elems * 4 + col_elems * 8 + part_elems * 4 + 4 * 4096, st);
+  if (!wsp) return OCM_ERR_NOMEM;
+  ocm::Carve cv{static_cast<char*>(wsp)};
+  char* digits = cv.take<char>(3 * plane);
+  float* scale = cv.take<float>(scale_elems);
+  double* colpart = cv.take<double>(col_elems);
+  float* part = cv.take<float>(part_elems);
+
+  for (int s0 = 0; s0 < nseg; s0 += MAXSEG) {
+    const int s1 = std::min(nseg, s0 + MAXSEG);
+    SegTable tab{};
+    tab.nseg = s1 - s0;
+    tab.chunk_rows = (int32_t)chunk_rows;
+    for (int s = s0; s <= s1; ++s) {
+      tab.begin[s - s0] = seg_offsets[s];
+      tab.cprefix[s - s0] = cprefix[s] - cprefix[s0];
+    }
+    const int64_t gchunks = cprefix[s1] - cprefix[s0];
+    if (gchunks == 0) continue;
+    const int64_t total = gchunks * ntiles;
+    OCM_REQUIRE(total < (1LL << 31) && gchunks < 65536 * 1024LL, "ocm_gram_f32: too many workgroups");
+    Q8Plan q{};
+    q.digits = digits + (size_t)cprefix[s0] * chunk_rows * P8;
+    q.plane = plane;
+    q.scale = scale + (size_t)cprefix[s0] * nblk * P8;
+    q.P8 = P8;
+    q.nblk = nblk;
+    double* col_g = colpart + (size_t)cprefix[s0] * nblk * P8;
+    float* pg = part + (size_t)cprefix[s0] * ntiles * Q8T * Q8T;
+    {
+      ocm::TimedRegion tq(ctx, OCM_KERNEL_QUANT, st);
+      dim3 gq((unsigned)(gchunks * nblk), (unsigned)(P8 / 128));
+      if (rows)
+        hipLaunchKernelGGL(k_q8_quant<true>, gq, dim3(512), 0, st, X, ldx, rows, p, shift, tab, q, col_g);
+      else
+        hipLaunchKernelGGL(k_q8_quant<false>, gq, dim3(512), 0, st, X, ldx, rows, p, shift, tab, q, col_g);
+      OCM_CHECK_LAUNCH("k_q8_quant");
+    }
+    {
+      ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
+      hipLaunchKernelGGL(k_gram8, dim3((unsigned)total), dim3(256), 0, st, q, tab, nt, ntiles, (int)total, pg);
+      OCM_CHECK_LAUNCH("k_gram8");
+    }
+  }
+  for (int s = 0; s < nseg; ++s) {
+    double* Gs = G_out + (size_t)s * p * p;
+    double* cs = colsum_out + (size_t)s * p;
+    if (cprefix[s + 1] == cprefix[s]) {
+      OCM_HIP(hipMemsetAsync(Gs, 0, (size_t)p * p * sizeof(double), st));
+      OCM_HIP(hipMemsetAsync(cs, 0, (size_t)p * sizeof(double), st));
+      continue;
+    }
+    dim3 g((Q8T * Q8T / 4 + 255) / 256, ntiles);
+    // colsum comes from k_colblk_sum (cmul = 0: the reduce skips it)
+    hipLaunchKernelGGL(k_gram_reduce<Q8T>, g, dim3(256), 0, st, part, colpart, nt, ntiles, p, cprefix[s],
+                       cprefix[s + 1], Gs, cs, 0);
+    hipLaunchKernelGGL(k_colblk_sum, dim3(P8 / 16), dim3(256), 0, st, colpart, (int64_t)cprefix[s] * nblk,
+                       (int64_t)cprefix[s + 1] * nblk, P8, p, cs);
+    OCM_CHECK_LAUNCH("k_colblk_sum");
+    OCM_CHECK_LAUNCH("k_gram_reduce");
+  }
+  return OCM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -775,10 +1239,16 @@ int ocm_gram_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows,
   if (const char* e = std::getenv("OCM_GRAM_TILE")) tile = std::atoi(e) == 128 ? 128 : 256;
   if (const char* e = std::getenv("OCM_GRAM_BK")) bk = std::atoi(e) == 16 ? 16 : 32;
   if (const char* e = std::getenv("OCM_GRAM_CHUNK")) chunk_rows = std::max<int64_t>(64, std::atoll(e));
-  // OCM_GRAM_MODE: "bf16x3" (default: exact 3-level bf16 split on bf16 MFMA, 1.33× the
-  // FP32-MFMA kernel and ~5× lower Gram error, profiles/) or "f32" (FP32 MFMA)
-  bool split3 = true;
-  if (const char* e = std::getenv("OCM_GRAM_MODE")) split3 = std::string(e) != "f32";
+  // OCM_GRAM_MODE: "i8x3" (default: int8 digit split on integer MFMA, exact
+  // accumulation), "bf16x3" (3-level bf16 split on bf16 MFMA) or "f32" (FP32 MFMA)
+  std::string mode = "i8x3";
+  if (const char* e = std::getenv("OCM_GRAM_MODE")) mode = e;
+  if (mode == "i8x3") {
+    const char* e = std::getenv("OCM_GRAM_CHUNK");
+    return gram_impl8(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st,
+                      e ? std::atoll(e) : 0);
+  }
+  const bool split3 = mode != "f32";
   if (split3)
     return gram_impl<256, 32>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows,
                               true);

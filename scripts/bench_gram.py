@@ -17,7 +17,7 @@ def main():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--p", type=int, default=2048)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="f32:256x32:2048,bf16x3:256x32:2048,bf16x3:256x32:4096,bf16x3:256x32:1024")
+    ap.add_argument("--variants", default="bf16x3:256x32:2048,i8x3:128x32:4096,i8x3:128x32:2048,i8x3:128x32:1024")
     args = ap.parse_args()
     import torch
 
@@ -35,7 +35,7 @@ def main():
     flop = args.rows * args.p * (args.p + 1)
     for r in range(args.rounds):
         for mode, name, chunk in variants:
-            os.environ["OCM_GRAM_MODE"] = "bf16x3" if mode.startswith("bf16x3") else mode
+            os.environ["OCM_GRAM_MODE"] = "bf16x3" if mode.startswith("bf16x3") else mode  # f32 | i8x3 pass through
             if mode == "bf16x3pk":
                 os.environ["OCM_GRAM3_PK"] = "1"
             else:

@@ -15,9 +15,10 @@ def eng():
     return engine
 
 
-@pytest.fixture(params=["f32", "bf16x3"])
+@pytest.fixture(params=["f32", "bf16x3", "i8x3"])
 def gram_mode(request, monkeypatch):
-    """Both Gram kernels: FP32 MFMA and the exact bf16×3 split on bf16 MFMA."""
+    """All Gram kernels: FP32 MFMA, the bf16×3 split on bf16 MFMA and the int8
+    digit split on integer MFMA (the default)."""
     monkeypatch.setenv("OCM_GRAM_MODE", request.param)
     return request.param
 
@@ -205,3 +206,29 @@ def test_rowsq_residual_broadcast_and_strided(eng):
     view = big[:, 10:42]
     q = eng.rowsq_residual(view, _dev(mu)).cpu().numpy()
     np.testing.assert_allclose(q, ((view.cpu().numpy().astype(np.float64) - mu) ** 2).sum(1), rtol=1e-6)
+
+
+@pytest.mark.parametrize("n,p", [(9000, 257), (300, 2048)])
+def test_gram_i8_digit_split_edge_cases(eng, monkeypatch, n, p):
+    """i8x3 fixed-point split: per-(256-row block, column) power-of-two scales
+    must cope with zero / constant columns, a far-off shift, a single huge
+    outlier row (it sets its block's scale), ragged chunk/block tails and
+    p not a multiple of the 128 tile."""
+    monkeypatch.setenv("OCM_GRAM_MODE", "i8x3")
+    monkeypatch.setenv("OCM_GRAM_CHUNK", "512")
+    rng = np.random.default_rng(p)
+    X = rng.standard_normal((n, p)).astype(np.float32) * np.float32(0.5)
+    X[:, 3] = 0.0
+    X[:, 5] = 7.25
+    X[:, 7] += np.float32(1e4)
+    X[n // 3, 11] = np.float32(3e5)
+    X[:, -1] = np.float32(1e-20) * rng.standard_normal(n).astype(np.float32)
+    Xd = _dev(X)
+    shift = _dev(X[:5].mean(0).astype(np.float32))
+    G, cs = eng.gram(Xd, None, [0, n], shift)
+    Y = X.astype(np.float64) - shift.cpu().numpy().astype(np.float64)
+    Gref = Y.T @ Y
+    d = np.sqrt(np.maximum(np.diag(Gref), 1e-300))
+    err = np.abs(G[0].cpu().numpy() - Gref) / np.outer(d, d)
+    assert err.max() < 2e-6, err.max()
+    np.testing.assert_allclose(cs[0].cpu().numpy(), Y.sum(0), rtol=1e-6, atol=1e-6 * np.abs(Y).sum(0).max())
