@@ -646,6 +646,7 @@ struct Q8Plan {
   float* scale;   // [chunk][nblk][P8]
   int P8;         // padded columns (multiple of Q8T)
   int nblk;       // scale blocks per chunk
+  int noload;     // timing-only experiments: digit loads dropped by the range check
 };
 
 __device__ __forceinline__ uint32_t q8_byte(float a, int u) { return ((uint32_t)(int)a & 0xffu) << (8 * u); }
@@ -806,13 +807,23 @@ __device__ __forceinline__ int q8_off(int panel, int dg, int col, int half) {
   return (((panel * 3 + dg) * Q8T + col) << 5) + ((half ^ ((col >> 3) & 1)) << 4);
 }
 
-__global__ __launch_bounds__(256, 1) void k_gram8(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
+// 8 waves (two per SIMD), waves 2 (M, 64 rows) × 4 (N, 32 columns): 3 × 2
+// int32 32×32 accumulator tiles per wave; f32 running sums of the flushed
+// scale blocks in LDS.  Stages of 32 rows go through a ring of three LDS
+// buffers, so the barrier at the top of an iteration only drains LDS
+// traffic issued a full iteration earlier:
+//   iteration s:  barrier · store stage s+2 (registers → ring) · read the
+//                 fragments of stage s+1 · issue the loads of stage s+4 ·
+//                 12 MFMAs on the fragments of stage s (read one iteration ago)
+// Stage t is loaded at iteration t-4, stored at t-2, read at t-1, used at t.
+__global__ __launch_bounds__(512, 1) void k_gram8(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
                                                   float* __restrict__ part) {
   constexpr int STAGE = 2 * 3 * Q8T * 32;  // 24 KiB: both panels, three digits
-  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
-  __shared__ float sc[2][2 * Q8T];  // scale-block parity × [panel][column]
-  // f32 running sums of the flushed scale blocks, wave-private: [wave][a·2+c][r/4][lane][4]
-  __shared__ __attribute__((aligned(16))) float runl[4][4][4][64][4];
+  constexpr int IMG = Q8T * 32;            // one (panel, digit) image: 4 KiB
+  __shared__ __attribute__((aligned(16))) char lds[3 * STAGE];
+  __shared__ __attribute__((aligned(16))) float sc[2][2 * Q8T];  // scale-block parity × [panel][column]
+  // f32 running sums of the flushed scale blocks, wave-private: [wave][a][r/4][lane][4]
+  __shared__ __attribute__((aligned(16))) float runl[8][2][4][64][4];
 
   const int b = blockIdx.x;
   const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
@@ -835,138 +846,151 @@ __global__ __launch_bounds__(256, 1) void k_gram8(Q8Plan q, SegTable st, int nt,
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave >> 2, wn = wave & 3;
   const int l31 = lane & 31, h = lane >> 5;
-  const bool idle = diag && wm > wn;  // strictly-lower 64×64 block of a diagonal tile
-  // loader: thread → one 16-B piece (column lcol, half lhalf) of each of the six images
-  const int lcol = tid >> 1, lhalf = tid & 1;
+  const bool idle = diag && (64 * wm >= 32 * wn + 32);  // strictly below the diagonal
+  const int xflags = __builtin_amdgcn_readfirstlane(q.noload);  // timing ablations (OCM_GRAM8_NOLOAD bits)
   const size_t gstride = (size_t)q.P8 * 32;
-  const char* srcA = q.digits + (size_t)(I + lcol) * 32 + lhalf * 16 + gbase * gstride;
-  const char* srcB = q.digits + (size_t)(J + lcol) * 32 + lhalf * 16 + gbase * gstride;
-  const float* sblk = q.scale + (size_t)chunk * q.nblk * q.P8 + (tid < Q8T ? I + tid : J + tid - Q8T);
-  const int wo0 = q8_off(0, 0, lcol, lhalf), wo1 = q8_off(1, 0, lcol, lhalf);
+  const int st8 = tid & 255;  // scale staging: threads t and t+256 write the same (identical) entry
+  const float* sblk = q.scale + (size_t)chunk * q.nblk * q.P8 + (st8 < Q8T ? I + st8 : J + st8 - Q8T);
+  // loader: thread → pieces (column lp>>1, half lp&1) of images hf, hf+2, hf+4
+  // (image = panel·3 + digit)
+  const int hf = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int lp = tid & 255, lcol = lp >> 1, lhalf = lp & 1;
+  const uint32_t span = (xflags & 1) ? 0u : (uint32_t)((size_t)nstage * gstride);
+  const char* cbase = q.digits + gbase * gstride;
+  __amdgpu_buffer_rsrc_t rs[3];
+  int wo[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int img = hf + 2 * k, panel = img / 3, dg = img - 3 * panel;
+    rs[k] = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(cbase + dg * q.plane + (size_t)(panel ? J : I) * 32), 0, span, 0x00020000);
+    wo[k] = q8_off(panel, dg, lcol, lhalf);
+  }
+  const int voff = lcol * 32 + lhalf * 16;
+  const int fa0 = q8_off(0, 0, wm * 64 + l31, h), fa1 = q8_off(0, 0, wm * 64 + 32 + l31, h);
+  const int fb0 = q8_off(1, 0, wn * 32 + l31, h);
 
 #define Q8_GLOAD(R, STG)                                                                     \
   do {                                                                                     \
-    const size_t go_ = (size_t)(STG) * gstride;                                            \
-    R##0 = *reinterpret_cast<const i32x4*>(srcA + go_);                                    \
-    R##1 = *reinterpret_cast<const i32x4*>(srcA + q.plane + go_);                          \
-    R##2 = *reinterpret_cast<const i32x4*>(srcA + 2 * q.plane + go_);                      \
-    R##3 = *reinterpret_cast<const i32x4*>(srcB + go_);                                    \
-    R##4 = *reinterpret_cast<const i32x4*>(srcB + q.plane + go_);                          \
-    R##5 = *reinterpret_cast<const i32x4*>(srcB + 2 * q.plane + go_);                      \
+    const int so_ = (STG) * (int)gstride;                                                  \
+    _Pragma("unroll") for (int k_ = 0; k_ < 3; ++k_)                                       \
+      R[k_] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(rs[k_], voff, so_, 0);          \
   } while (0)
-#define Q8_SSTORE(R, BI)                                                                     \
+#define Q8_SSTORE(R, SLOT)                                                                   \
   do {                                                                                     \
-    char* buf_ = lds + (BI) * STAGE;                                                       \
-    *reinterpret_cast<i32x4*>(buf_ + wo0) = R##0;                                          \
-    *reinterpret_cast<i32x4*>(buf_ + wo0 + Q8T * 32) = R##1;                               \
-    *reinterpret_cast<i32x4*>(buf_ + wo0 + 2 * Q8T * 32) = R##2;                           \
-    *reinterpret_cast<i32x4*>(buf_ + wo1) = R##3;                                          \
-    *reinterpret_cast<i32x4*>(buf_ + wo1 + Q8T * 32) = R##4;                               \
-    *reinterpret_cast<i32x4*>(buf_ + wo1 + 2 * Q8T * 32) = R##5;                           \
+    char* buf_ = lds + (SLOT) * STAGE;                                                     \
+    _Pragma("unroll") for (int k_ = 0; k_ < 3; ++k_)                                       \
+      *reinterpret_cast<i32x4*>(buf_ + wo[k_]) = R[k_];                                    \
+  } while (0)
+#define Q8_FRAGS(FA, FB, SLOT)                                                                        \
+  do {                                                                                              \
+    const char* buf_ = lds + (SLOT) * STAGE;                                                        \
+    _Pragma("unroll") for (int dg_ = 0; dg_ < 3; ++dg_) {                                           \
+      FB[dg_] = *reinterpret_cast<const i32x4*>(buf_ + fb0 + dg_ * IMG);                            \
+      FA[0][dg_] = *reinterpret_cast<const i32x4*>(buf_ + fa0 + dg_ * IMG);                         \
+      FA[1][dg_] = *reinterpret_cast<const i32x4*>(buf_ + fa1 + dg_ * IMG);                         \
+    }                                                                                               \
+  } while (0)
+#define Q8_MFMA(FA, FB)                                                                               \
+  do {                                                                                              \
+    if (!idle) {                                                                                    \
+      _Pragma("unroll") for (int a_ = 0; a_ < 2; ++a_) {                                            \
+        acc1[a_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[0], acc1[a_], 0, 0, 0);      \
+        acc2[a_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[1], acc2[a_], 0, 0, 0);      \
+        acc2[a_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][1], FB[0], acc2[a_], 0, 0, 0);      \
+        acc3[a_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[2], acc3[a_], 0, 0, 0);      \
+        acc3[a_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][2], FB[0], acc3[a_], 0, 0, 0);      \
+        acc3[a_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][1], FB[1], acc3[a_], 0, 0, 0);      \
+      }                                                                                             \
+    }                                                                                               \
   } while (0)
 
-  i32x16 acc1[2][2], acc2[2][2], acc3[2][2];
+  i32x16 acc1[2], acc2[2], acc3[2];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < 2; ++a) {
+    acc1[a] = i32x16{};
+    acc2[a] = i32x16{};
+    acc3[a] = i32x16{};
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      acc1[a][c] = i32x16{};
-      acc2[a][c] = i32x16{};
-      acc3[a][c] = i32x16{};
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<f32x4*>(&runl[wave][a * 2 + c][g][lane][0]) = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  auto compute = [&](int bi) __attribute__((always_inline)) {
-    if (idle) return;
-    const char* buf = lds + bi * STAGE;
-    i32x4 bv[2][3];
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int dg = 0; dg < 3; ++dg)
-        bv[c][dg] = *reinterpret_cast<const i32x4*>(buf + q8_off(1, dg, wn * 64 + c * 32 + l31, h));
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      i32x4 av[3];
-#pragma unroll
-      for (int dg = 0; dg < 3; ++dg)
-        av[dg] = *reinterpret_cast<const i32x4*>(buf + q8_off(0, dg, wm * 64 + a * 32 + l31, h));
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        acc1[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[0], bv[c][0], acc1[a][c], 0, 0, 0);
-        acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[0], bv[c][1], acc2[a][c], 0, 0, 0);
-        acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[1], bv[c][0], acc2[a][c], 0, 0, 0);
-        acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[0], bv[c][2], acc3[a][c], 0, 0, 0);
-        acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[2], bv[c][0], acc3[a][c], 0, 0, 0);
-        acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[1], bv[c][1], acc3[a][c], 0, 0, 0);
-      }
-    }
-  };
+    for (int g = 0; g < 4; ++g) *reinterpret_cast<f32x4*>(&runl[wave][a][g][lane][0]) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   auto flush = [&](int par) __attribute__((always_inline)) {
     if (idle) return;
     constexpr float w2 = 1.f / 254.f, w3 = 1.f / (254.f * 254.f);
+    const float sj = sc[par][Q8T + wn * 32 + l31];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const float sj = sc[par][Q8T + wn * 64 + c * 32 + l31];
+    for (int a = 0; a < 2; ++a) {
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
+      for (int g = 0; g < 4; ++g) {
+        // row scales of registers 4g..4g+3: rows 8g + 4h + 0..3
+        const f32x4 si = *reinterpret_cast<const f32x4*>(&sc[par][wm * 64 + a * 32 + 8 * g + 4 * h]);
+        f32x4* rp = reinterpret_cast<f32x4*>(&runl[wave][a][g][lane][0]);
+        f32x4 rv = *rp;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          f32x4* rp = reinterpret_cast<f32x4*>(&runl[wave][a * 2 + c][g][lane][0]);
-          f32x4 rv = *rp;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * g + e;
-            // |A·| < 2²⁴ per block: the int → f32 conversions are exact; si·sj is a power of two
-            const float si = sc[par][wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h];
-            const float v = fmaf((float)acc3[a][c][r], w3, fmaf((float)acc2[a][c][r], w2, (float)acc1[a][c][r]));
-            rv[e] = fmaf(v, si * sj, rv[e]);
-          }
-          *rp = rv;
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e;
+          // |A·| < 2²⁴ per block: the int → f32 conversions are exact; si·sj is a power of two
+          const float v = fmaf((float)acc3[a][r], w3, fmaf((float)acc2[a][r], w2, (float)acc1[a][r]));
+          rv[e] = fmaf(v, si[e] * sj, rv[e]);
         }
-        acc1[a][c] = i32x16{};
-        acc2[a][c] = i32x16{};
-        acc3[a][c] = i32x16{};
+        *rp = rv;
       }
+      acc1[a] = i32x16{};
+      acc2[a] = i32x16{};
+      acc3[a] = i32x16{};
+      __builtin_amdgcn_sched_barrier(0);  // one 32×32 block at a time: bounded temporaries
     }
   };
-  // one pipeline step: stage STG (LDS buffer BI) is computed; stage STG+1
-  // (registers RN) is stored to the other buffer; RN then loads stage STG+3.
-  // The scale of stage STG+2's block was loaded one step earlier (SCN) and is
-  // staged to LDS here; the scale of stage STG+3's block is loaded before
-  // the stage loads, so every wait is on the oldest loads only.
-#define Q8_STEP(STG, BI, RN)                                                                          \
+#define Q8_MEM(STG, FAN, FBN, RS, SCS)                                                                \
   do {                                                                                              \
-    sc[(((STG) + 2) / Q8SPB) & 1][tid] = scn;                                                       \
-    compute(BI);                                                                                    \
-    Q8_SSTORE(RN, (BI) ^ 1);                                                                        \
+    Q8_SSTORE(RS, ((STG) + 2) % 3);                                                                 \
+    sc[(((STG) + 2) / Q8SPB) & 1][st8] = SCS;                                                       \
+    if (!(xflags & 2)) Q8_FRAGS(FAN, FBN, ((STG) + 1) % 3);                                         \
+    const int nx_ = min((STG) + 4, nstage - 1);                                                     \
+    SCS = sblk[(size_t)(nx_ / Q8SPB) * q.P8];                                                       \
+    Q8_GLOAD(RS, nx_);                                                                              \
+  } while (0)
+#define Q8_STEP(STG, FAC, FBC, FAN, FBN, RS, SCS)                                                     \
+  do {                                                                                              \
     __syncthreads();                                                                                \
-    const int nx_ = min((STG) + 3, nstage - 1);                                                     \
-    scn = sblk[(size_t)(nx_ / Q8SPB) * q.P8];                                                       \
-    Q8_GLOAD(RN, nx_);                                                                              \
+    Q8_MEM(STG, FAN, FBN, RS, SCS);                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                              \
+    if (!(xflags & 4)) Q8_MFMA(FAC, FBC);                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                              \
   } while (0)
 
-  i32x4 RA0, RA1, RA2, RA3, RA4, RA5, RB0, RB1, RB2, RB3, RB4, RB5;
-  sc[0][tid] = sblk[0];
-  float scn = sblk[(size_t)(min(2, nstage - 1) / Q8SPB) * q.P8];
+  i32x4 RA[3], RB[3];  // stage parity 0 / 1
+  float SA, SB;
+  i32x4 FA0[2][3], FB0[3], FA1[2][3], FB1[3];
+  // prologue: stages 0, 1 stored; stage 0 fragments read; stages 2, 3 in flight
+  SA = sblk[0];
   Q8_GLOAD(RA, 0);
-  Q8_GLOAD(RB, 1);
+  SB = sblk[(size_t)(min(1, nstage - 1) / Q8SPB) * q.P8];
+  Q8_GLOAD(RB, min(1, nstage - 1));
   Q8_SSTORE(RA, 0);
+  sc[0][st8] = SA;
+  SA = sblk[(size_t)(min(2, nstage - 1) / Q8SPB) * q.P8];
+  Q8_GLOAD(RA, min(2, nstage - 1));
+  Q8_SSTORE(RB, 1);
+  SB = sblk[(size_t)(min(3, nstage - 1) / Q8SPB) * q.P8];
+  Q8_GLOAD(RB, min(3, nstage - 1));
   __syncthreads();
-  Q8_GLOAD(RA, 2);
+  Q8_FRAGS(FA0, FB0, 0);
   for (int blk = 0; blk < nb; ++blk) {
+    const int s0 = blk * Q8SPB;
 #pragma unroll
     for (int u = 0; u < Q8SPB; u += 2) {
-      const int stg = blk * Q8SPB + u;
-      Q8_STEP(stg, 0, RB);
-      Q8_STEP(stg + 1, 1, RA);
+      Q8_STEP(s0 + u, FA0, FB0, FA1, FB1, RA, SA);
+      Q8_STEP(s0 + u + 1, FA1, FB1, FA0, FB0, RB, SB);
     }
-    flush(blk & 1);
+    if (!(xflags & 8)) flush(blk & 1);
   }
 #undef Q8_STEP
+#undef Q8_MEM
+#undef Q8_MFMA
+#undef Q8_FRAGS
 #undef Q8_SSTORE
 #undef Q8_GLOAD
 
@@ -975,13 +999,11 @@ __global__ __launch_bounds__(256, 1) void k_gram8(Q8Plan q, SegTable st, int nt,
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int col = wn * 64 + c * 32 + l31;
-        out[row * Q8T + col] = runl[wave][a * 2 + c][r >> 2][lane][r & 3];
-      }
+    for (int r = 0; r < 16; ++r) {
+      const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int col = wn * 32 + l31;
+      out[row * Q8T + col] = runl[wave][a][r >> 2][lane][r & 3];
+    }
 }
 
 int gram_small(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int32_t p, const float* shift,
@@ -1157,6 +1179,8 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     q.scale = scale + (size_t)cprefix[s0] * nblk * P8;
     q.P8 = P8;
     q.nblk = nblk;
+    // timing ablations only (wrong G): bit 0 no digit loads, 1 no fragment reads, 2 no MFMA, 3 no flush
+    q.noload = std::getenv("OCM_GRAM8_NOLOAD") ? std::atoi(std::getenv("OCM_GRAM8_NOLOAD")) : 0;
     double* col_g = colpart + (size_t)cprefix[s0] * nblk * P8;
     float* pg = part + (size_t)cprefix[s0] * ntiles * Q8T * Q8T;
     {
@@ -1170,7 +1194,7 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     }
     {
       ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
-      hipLaunchKernelGGL(k_gram8, dim3((unsigned)total), dim3(256), 0, st, q, tab, nt, ntiles, (int)total, pg);
+      hipLaunchKernelGGL(k_gram8, dim3((unsigned)total), dim3(512), 0, st, q, tab, nt, ntiles, (int)total, pg);
       OCM_CHECK_LAUNCH("k_gram8");
     }
   }
