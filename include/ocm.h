@@ -225,6 +225,24 @@ int ocm_cv_counts(ocm_ctx* ctx, const float* T, int64_t m, int32_t k, const floa
 int ocm_snv_savgol_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, int32_t p, int32_t snv,
                        int32_t window, const double* taps, float* out, int64_t ldo, void* stream);
 
+/* ---- VAE network support (vae_model.py:37-81, BatchNorm1d in train mode) ----
+ * Training-mode batch norm over (N, C, L) contiguous activations, bf16 or f32,
+ * statistics per channel over N·L (torch.nn.functional.batch_norm semantics:
+ * biased variance normalises, unbiased variance feeds running_var with
+ * `momentum`).  Replaces the MIOpen spatial BN the reference's nn.BatchNorm1d
+ * lowers to (vae_model.py:45-47, 75-77).  running_mean / running_var may both
+ * be NULL (no update); gamma / beta may be NULL (affine=False).  Workspace is
+ * the context arena; all work is stream-ordered (graph-capturable). */
+#define OCM_DTYPE_F32 0
+#define OCM_DTYPE_BF16 1
+int ocm_bn_fwd_train(ocm_ctx* ctx, int32_t dtype, const void* x, int32_t N, int32_t C, int32_t L,
+                     const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
+                     float* running_var, void* y, float* save_mean, float* save_invstd, void* stream);
+/* dx = γ·invstd·(dy − mean(dy) − x̂·mean(dy·x̂)); dgamma = Σ dy·x̂, dbeta = Σ dy (either may be NULL). */
+int ocm_bn_bwd(ocm_ctx* ctx, int32_t dtype, const void* x, const void* dy, int32_t N, int32_t C, int32_t L,
+               const float* gamma, const float* save_mean, const float* save_invstd, void* dx, float* dgamma,
+               float* dbeta, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,225 @@
+// Training-mode BatchNorm1d for the VAE's narrow convolution stacks
+// (vae_model.py:37-81: Conv1d/ConvTranspose1d → BatchNorm1d → ELU, 3-12
+// channels × 512-2048 positions × B = 512).  MIOpen's spatial BN runs such
+// shapes at a few GB/s (one workgroup per channel: 0.41 ms fwd + 0.19 ms bwd
+// per layer at B=512, C=3, L=2048 — 63 % of the whole HIP-graph training step,
+// profiles/r01_bench_i8x3_kernel_stats.md).  Here each channel's N·L
+// reduction is split over many workgroups (f64 partials, fixed-order
+// combine: deterministic), and the normalisation is one coalesced pass.
+//
+// x, y, dy, dx: (N, C, L) contiguous, bf16 (under autocast) or f32.
+// Statistics f32 out (save_mean, save_invstd), math in f32/f64.
+// Semantics = torch.nn.functional.batch_norm(training=True): biased variance
+// for the normalisation, unbiased for running_var, momentum update.
+#include "ocm_internal.h"
+
+namespace {
+
+constexpr int BN_SPLIT = 64;   // workgroups per channel for the reductions
+constexpr int BN_T = 256;
+
+struct bf16_t {  // raw bfloat16 storage (torch.bfloat16 bit layout)
+  uint16_t bits;
+};
+__device__ __forceinline__ float bn_ld(const float* p, int64_t i) { return p[i]; }
+__device__ __forceinline__ float bn_ld(const bf16_t* p, int64_t i) { return __uint_as_float((uint32_t)p[i].bits << 16); }
+__device__ __forceinline__ void bn_st(float* p, int64_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void bn_st(bf16_t* p, int64_t i, float v) {
+  // round to nearest even (NaN kept quiet), as torch's float → bfloat16 cast
+  const uint32_t u = __float_as_uint(v);
+  const uint32_t r = (u & 0x7fffffffu) > 0x7f800000u ? (u | 0x00400000u) : u + 0x7fffu + ((u >> 16) & 1u);
+  p[i].bits = (uint16_t)(r >> 16);
+}
+
+__device__ __forceinline__ double block_sum_f64(double v, double* red) {
+  v = wave_sum_f64(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < BN_T / 64; ++i) t += red[i];
+  return t;
+}
+
+// grid (BN_SPLIT, C): partial Σx, Σx² of channel c over its share of the N·L elements
+template <typename T>
+__global__ __launch_bounds__(BN_T) void k_bn_stats(const T* __restrict__ x, int N, int C, int L,
+                                                   double* __restrict__ part) {
+  __shared__ double red[BN_T / 64];
+  const int c = blockIdx.y, sp = blockIdx.x;
+  const int64_t M = (int64_t)N * L;
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t e = (int64_t)sp * BN_T + threadIdx.x; e < M; e += (int64_t)BN_SPLIT * BN_T) {
+    const int64_t n = e / L, l = e - n * L;
+    const float v = bn_ld(x, (n * C + c) * L + l);
+    s1 += v;
+    s2 += (double)v * v;
+  }
+  s1 = block_sum_f64(s1, red);
+  s2 = block_sum_f64(s2, red);
+  if (threadIdx.x == 0) {
+    part[((size_t)c * BN_SPLIT + sp) * 2 + 0] = s1;
+    part[((size_t)c * BN_SPLIT + sp) * 2 + 1] = s2;
+  }
+}
+
+// one thread per channel: mean / invstd and the running-stat update
+__global__ void k_bn_finalize(const double* __restrict__ part, int C, int64_t M, float eps, float momentum,
+                              float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                              float* __restrict__ running_mean, float* __restrict__ running_var) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = 0; i < BN_SPLIT; ++i) {
+    s1 += part[((size_t)c * BN_SPLIT + i) * 2 + 0];
+    s2 += part[((size_t)c * BN_SPLIT + i) * 2 + 1];
+  }
+  const double mean = s1 / (double)M;
+  const double var = fmax(s2 / (double)M - mean * mean, 0.0);
+  save_mean[c] = (float)mean;
+  save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (running_mean) {
+    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+  }
+}
+
+// grid (ceil(L / BN_T), N·C): y = (x − μ)·invstd·γ + β
+template <typename T>
+__global__ __launch_bounds__(BN_T) void k_bn_apply(const T* __restrict__ x, int C, int L,
+                                                   const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   T* __restrict__ y) {
+  const int row = blockIdx.y, c = row % C;
+  const int l = blockIdx.x * BN_T + threadIdx.x;
+  if (l >= L) return;
+  const float a = invstd[c] * (gamma ? gamma[c] : 1.f);
+  const float b = (beta ? beta[c] : 0.f) - mean[c] * a;
+  const int64_t i = (int64_t)row * L + l;
+  bn_st(y, i, fmaf(bn_ld(x, i), a, b));
+}
+
+// grid (BN_SPLIT, C): partial Σdy, Σdy·x̂
+template <typename T>
+__global__ __launch_bounds__(BN_T) void k_bn_bwd_stats(const T* __restrict__ x, const T* __restrict__ dy, int N,
+                                                       int C, int L, const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd, double* __restrict__ part) {
+  __shared__ double red[BN_T / 64];
+  const int c = blockIdx.y, sp = blockIdx.x;
+  const int64_t M = (int64_t)N * L;
+  const float mu = mean[c], is = invstd[c];
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t e = (int64_t)sp * BN_T + threadIdx.x; e < M; e += (int64_t)BN_SPLIT * BN_T) {
+    const int64_t n = e / L, l = e - n * L;
+    const int64_t i = (n * C + c) * L + l;
+    const float g = bn_ld(dy, i);
+    s1 += g;
+    s2 += (double)g * ((bn_ld(x, i) - mu) * is);
+  }
+  s1 = block_sum_f64(s1, red);
+  s2 = block_sum_f64(s2, red);
+  if (threadIdx.x == 0) {
+    part[((size_t)c * BN_SPLIT + sp) * 2 + 0] = s1;
+    part[((size_t)c * BN_SPLIT + sp) * 2 + 1] = s2;
+  }
+}
+
+__global__ void k_bn_bwd_finalize(const double* __restrict__ part, int C, double* __restrict__ sums,
+                                  float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = 0; i < BN_SPLIT; ++i) {
+    s1 += part[((size_t)c * BN_SPLIT + i) * 2 + 0];
+    s2 += part[((size_t)c * BN_SPLIT + i) * 2 + 1];
+  }
+  sums[2 * c] = s1;
+  sums[2 * c + 1] = s2;
+  if (dbeta) dbeta[c] = (float)s1;
+  if (dgamma) dgamma[c] = (float)s2;
+}
+
+// dx = γ·invstd·(dy − Σdy/M − x̂·Σ(dy·x̂)/M)
+template <typename T>
+__global__ __launch_bounds__(BN_T) void k_bn_bwd_apply(const T* __restrict__ x, const T* __restrict__ dy, int C,
+                                                       int L, int64_t M, const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd,
+                                                       const float* __restrict__ gamma,
+                                                       const double* __restrict__ sums, T* __restrict__ dx) {
+  const int row = blockIdx.y, c = row % C;
+  const int l = blockIdx.x * BN_T + threadIdx.x;
+  if (l >= L) return;
+  const float is = invstd[c], mu = mean[c];
+  const float k = is * (gamma ? gamma[c] : 1.f);
+  const float m1 = (float)(sums[2 * c] / (double)M), m2 = (float)(sums[2 * c + 1] / (double)M);
+  const int64_t i = (int64_t)row * L + l;
+  const float xh = (bn_ld(x, i) - mu) * is;
+  bn_st(dx, i, k * (bn_ld(dy, i) - m1 - xh * m2));
+}
+
+template <typename T>
+int bn_fwd(ocm_ctx* ctx, const void* x, int N, int C, int L, const float* gamma, const float* beta, float eps,
+           float momentum, float* rmean, float* rvar, void* y, float* smean, float* sinv, hipStream_t st) {
+  auto* part = static_cast<double*>(ocm::workspace(ctx, (size_t)C * BN_SPLIT * 2 * sizeof(double), st));
+  if (!part) return OCM_ERR_NOMEM;
+  hipLaunchKernelGGL(k_bn_stats<T>, dim3(BN_SPLIT, C), dim3(BN_T), 0, st, static_cast<const T*>(x), N, C, L, part);
+  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 63) / 64), dim3(64), 0, st, part, C, (int64_t)N * L, eps, momentum,
+                     smean, sinv, rmean, rvar);
+  hipLaunchKernelGGL(k_bn_apply<T>, dim3((L + BN_T - 1) / BN_T, N * C), dim3(BN_T), 0, st,
+                     static_cast<const T*>(x), C, L, smean, sinv, gamma, beta, static_cast<T*>(y));
+  OCM_CHECK_LAUNCH("k_bn_fwd");
+  return OCM_OK;
+}
+
+template <typename T>
+int bn_bwd(ocm_ctx* ctx, const void* x, const void* dy, int N, int C, int L, const float* gamma, const float* smean,
+           const float* sinv, void* dx, float* dgamma, float* dbeta, hipStream_t st) {
+  auto* part = static_cast<double*>(ocm::workspace(ctx, ((size_t)C * BN_SPLIT * 2 + 2 * (size_t)C) * sizeof(double), st));
+  if (!part) return OCM_ERR_NOMEM;
+  double* sums = part + (size_t)C * BN_SPLIT * 2;
+  hipLaunchKernelGGL(k_bn_bwd_stats<T>, dim3(BN_SPLIT, C), dim3(BN_T), 0, st, static_cast<const T*>(x),
+                     static_cast<const T*>(dy), N, C, L, smean, sinv, part);
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64), 0, st, part, C, sums, dgamma, dbeta);
+  hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3((L + BN_T - 1) / BN_T, N * C), dim3(BN_T), 0, st,
+                     static_cast<const T*>(x), static_cast<const T*>(dy), C, L, (int64_t)N * L, smean, sinv, gamma,
+                     sums, static_cast<T*>(dx));
+  OCM_CHECK_LAUNCH("k_bn_bwd");
+  return OCM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ocm_bn_fwd_train(ocm_ctx* ctx, int32_t dtype, const void* x, int32_t N, int32_t C, int32_t L,
+                     const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
+                     float* running_var, void* y, float* save_mean, float* save_invstd, void* stream) {
+  OCM_REQUIRE(ctx && x && y && save_mean && save_invstd, "ocm_bn_fwd_train: NULL argument");
+  OCM_REQUIRE(N > 0 && C > 0 && L > 0, "ocm_bn_fwd_train: bad shape");
+  OCM_REQUIRE(!running_mean == !running_var, "ocm_bn_fwd_train: running_mean and running_var go together");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == OCM_DTYPE_F32)
+    return bn_fwd<float>(ctx, x, N, C, L, gamma, beta, eps, momentum, running_mean, running_var, y, save_mean,
+                         save_invstd, st);
+  if (dtype == OCM_DTYPE_BF16)
+    return bn_fwd<bf16_t>(ctx, x, N, C, L, gamma, beta, eps, momentum, running_mean, running_var, y,
+                                  save_mean, save_invstd, st);
+  return ocm::fail(OCM_ERR_ARG, "ocm_bn_fwd_train: dtype must be OCM_DTYPE_F32 or OCM_DTYPE_BF16");
+}
+
+int ocm_bn_bwd(ocm_ctx* ctx, int32_t dtype, const void* x, const void* dy, int32_t N, int32_t C, int32_t L,
+               const float* gamma, const float* save_mean, const float* save_invstd, void* dx, float* dgamma,
+               float* dbeta, void* stream) {
+  OCM_REQUIRE(ctx && x && dy && dx && save_mean && save_invstd, "ocm_bn_bwd: NULL argument");
+  OCM_REQUIRE(N > 0 && C > 0 && L > 0, "ocm_bn_bwd: bad shape");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == OCM_DTYPE_F32)
+    return bn_bwd<float>(ctx, x, dy, N, C, L, gamma, save_mean, save_invstd, dx, dgamma, dbeta, st);
+  if (dtype == OCM_DTYPE_BF16)
+    return bn_bwd<bf16_t>(ctx, x, dy, N, C, L, gamma, save_mean, save_invstd, dx, dgamma, dbeta, st);
+  return ocm::fail(OCM_ERR_ARG, "ocm_bn_bwd: dtype must be OCM_DTYPE_F32 or OCM_DTYPE_BF16");
+}
+
+}  // extern "C"

@@ -86,6 +86,10 @@ SIGNATURES = {
                                    ctypes.POINTER(c_f64), c_void_p, c_i64, c_void_p]),
     "ocm_cv_counts": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_void_p, c_i64,
                               ctypes.POINTER(OcmCvConfig), c_i32, c_void_p, c_void_p, c_void_p]),
+    "ocm_bn_fwd_train": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, ctypes.c_float,
+                                 ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ocm_bn_bwd": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 _lib = None

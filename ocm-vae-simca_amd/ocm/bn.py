@@ -1,0 +1,69 @@
+"""Training-mode BatchNorm1d on libocm (ocm_bn_fwd_train / ocm_bn_bwd).
+
+``FastBatchNorm1d`` is an ``nn.BatchNorm1d`` (same parameters, buffers and
+state_dict keys — vae_model.py:45-47, 75-77 build plain ``nn.BatchNorm1d``)
+whose training-mode forward on a HIP device runs the split-reduction kernels
+of csrc/ocm_bn.hip instead of MIOpen's spatial BN, which handles the VAE's
+3-12-channel × 512-2048-position activations at a few GB/s.  Evaluation mode
+(running statistics) and host tensors use the stock module.  The kernels
+launch on the current stream, so the module is HIP-graph capturable
+(ocm/vae_train.py).
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import _lib
+from ._lib import Context, check, ptr, stream_handle
+
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+class _BNTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum):
+        x = x.contiguous()
+        N, C, L = x.shape
+        dev = x.device
+        y = torch.empty_like(x)
+        smean = torch.empty(C, dtype=torch.float32, device=dev)
+        sinv = torch.empty(C, dtype=torch.float32, device=dev)
+        w = weight.detach().float().contiguous() if weight is not None else None
+        b = bias.detach().float().contiguous() if bias is not None else None
+        h = Context.get(dev.index).handle
+        check(_lib.load().ocm_bn_fwd_train(h, _DT[x.dtype], ptr(x), N, C, L, ptr(w), ptr(b), float(eps),
+                                           float(momentum), ptr(running_mean), ptr(running_var), ptr(y),
+                                           ptr(smean), ptr(sinv), stream_handle(dev)), "ocm_bn_fwd_train")
+        ctx.save_for_backward(x, w, smean, sinv)
+        ctx.has_w, ctx.has_b = weight is not None, bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, smean, sinv = ctx.saved_tensors
+        dy = dy.contiguous().to(x.dtype)
+        N, C, L = x.shape
+        dev = x.device
+        dx = torch.empty_like(x)
+        dw = torch.empty(C, dtype=torch.float32, device=dev) if ctx.has_w else None
+        db = torch.empty(C, dtype=torch.float32, device=dev) if ctx.has_b else None
+        h = Context.get(dev.index).handle
+        check(_lib.load().ocm_bn_bwd(h, _DT[x.dtype], ptr(x), ptr(dy), N, C, L, ptr(w), ptr(smean), ptr(sinv),
+                                     ptr(dx), ptr(dw), ptr(db), stream_handle(dev)), "ocm_bn_bwd")
+        return dx, dw, db, None, None, None, None
+
+
+class FastBatchNorm1d(nn.BatchNorm1d):
+    """nn.BatchNorm1d with the libocm training-mode kernels on HIP tensors."""
+
+    def forward(self, x):
+        if not (self.training and x.is_cuda and x.dim() == 3 and x.dtype in _DT) or self.momentum is None:
+            # eval (running statistics), host tensors, cumulative-average momentum: the stock module
+            return super().forward(x)
+        if self.track_running_stats and self.num_batches_tracked is not None:
+            self.num_batches_tracked.add_(1)
+        momentum = self.momentum
+        track = self.track_running_stats and self.running_mean is not None
+        return _BNTrain.apply(x, self.weight, self.bias, self.running_mean if track else None,
+                              self.running_var if track else None, self.eps, momentum)

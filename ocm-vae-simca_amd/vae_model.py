@@ -18,6 +18,8 @@ import torch.nn.functional as F
 from scipy.stats import chi2
 from torch import nn
 
+from ocm.bn import FastBatchNorm1d
+
 __all__ = ["ConvVAE1D", "beta_vae_cosine_loss", "beta_vae_bce_loss", "compute_q_h_f"]
 
 
@@ -96,7 +98,8 @@ class ConvVAE1D(nn.Module):
     def _block(self, conv: nn.Module, chans: int, act_cls) -> list:
         mods = [conv]
         if self.use_batchnorm:
-            mods.append(nn.BatchNorm1d(chans))
+            # nn.BatchNorm1d with libocm's training kernels on HIP tensors (same state_dict)
+            mods.append(FastBatchNorm1d(chans))
         mods.append(act_cls())
         if self.dropout > 0:
             mods.append(nn.Dropout(self.dropout))

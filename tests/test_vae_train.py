@@ -101,3 +101,38 @@ def test_graph_replays_queued_after_sync_stay_finite():
             torch.cuda.synchronize()
     assert bool(torch.isfinite(losses).all()), losses.cpu()
     assert all(bool(torch.isfinite(p).all()) for p in m.parameters())
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(512, 3, 2048), (64, 12, 512), (7, 5, 33)])
+def test_fast_batchnorm_matches_torch(dtype, shape):
+    """libocm training-mode BN == torch.nn.BatchNorm1d: output, running
+    statistics, num_batches_tracked and the input / weight / bias gradients."""
+    from ocm.bn import FastBatchNorm1d
+
+    dev = torch.device("cuda", 0)
+    N, C, L = shape
+    g = torch.Generator(device="cpu").manual_seed(C * L)
+    x0 = (3.0 + 2.0 * torch.randn(N, C, L, generator=g)).to(dev)
+    ref = torch.nn.BatchNorm1d(C).to(dev)
+    fast = FastBatchNorm1d(C).to(dev)
+    with torch.no_grad():
+        ref.weight.copy_(torch.linspace(0.5, 1.5, C))
+        ref.bias.copy_(torch.linspace(-0.2, 0.3, C))
+    fast.load_state_dict(ref.state_dict())
+    xr = x0.to(dtype).requires_grad_(True)
+    xf = x0.to(dtype).requires_grad_(True)
+    yr, yf = ref(xr), fast(xf)
+    gy = torch.randn(N, C, L, generator=g).to(dev).to(dtype)
+    (yr.float() * gy.float()).sum().backward()
+    (yf.float() * gy.float()).sum().backward()
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(yf.float(), yr.float(), **tol)
+    torch.testing.assert_close(xf.grad.float(), xr.grad.float(), **tol)
+    torch.testing.assert_close(fast.weight.grad, ref.weight.grad, rtol=1e-3, atol=1e-2 * N * L / 1000)
+    torch.testing.assert_close(fast.bias.grad, ref.bias.grad, rtol=1e-3, atol=1e-2 * N * L / 1000)
+    torch.testing.assert_close(fast.running_mean, ref.running_mean, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(fast.running_var, ref.running_var, rtol=1e-3, atol=1e-4)
+    assert int(fast.num_batches_tracked) == int(ref.num_batches_tracked) == 1
