@@ -945,7 +945,7 @@ __global__ __launch_bounds__(512, 1) void k_gram8(Q8Plan q, SegTable st, int nt,
   };
 #define Q8_MEM(STG, FAN, FBN, RS, SCS)                                                                \
   do {                                                                                              \
-    Q8_SSTORE(RS, ((STG) + 2) % 3);                                                                 \
+    if (!(xflags & 16)) Q8_SSTORE(RS, ((STG) + 2) % 3);                                             \
     sc[(((STG) + 2) / Q8SPB) & 1][st8] = SCS;                                                       \
     if (!(xflags & 2)) Q8_FRAGS(FAN, FBN, ((STG) + 1) % 3);                                         \
     const int nx_ = min((STG) + 4, nstage - 1);                                                     \
@@ -1179,7 +1179,8 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     q.scale = scale + (size_t)cprefix[s0] * nblk * P8;
     q.P8 = P8;
     q.nblk = nblk;
-    // timing ablations only (wrong G): bit 0 no digit loads, 1 no fragment reads, 2 no MFMA, 3 no flush
+    // timing ablations only (wrong G): bit 0 no digit loads, 1 no fragment reads, 2 no MFMA, 3 no flush,
+    // 4 no LDS stores of the stage
     q.noload = std::getenv("OCM_GRAM8_NOLOAD") ? std::atoi(std::getenv("OCM_GRAM8_NOLOAD")) : 0;
     double* col_g = colpart + (size_t)cprefix[s0] * nblk * P8;
     float* pg = part + (size_t)cprefix[s0] * ntiles * Q8T * Q8T;
