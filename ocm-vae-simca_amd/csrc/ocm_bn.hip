@@ -48,13 +48,19 @@ __global__ __launch_bounds__(BN_T) void k_bn_stats(const T* __restrict__ x, int 
                                                    double* __restrict__ part) {
   __shared__ double red[BN_T / 64];
   const int c = blockIdx.y, sp = blockIdx.x;
-  const int64_t M = (int64_t)N * L;
   double s1 = 0.0, s2 = 0.0;
-  for (int64_t e = (int64_t)sp * BN_T + threadIdx.x; e < M; e += (int64_t)BN_SPLIT * BN_T) {
-    const int64_t n = e / L, l = e - n * L;
-    const float v = bn_ld(x, (n * C + c) * L + l);
-    s1 += v;
-    s2 += (double)v * v;
+  // rows n ≡ sp (mod BN_SPLIT) of channel c, each L contiguous elements:
+  // f32 per-row partials (≤ L/BN_T terms per thread), f64 across rows
+  for (int n = sp; n < N; n += BN_SPLIT) {
+    const T* xr = x + ((int64_t)n * C + c) * L;
+    float a1 = 0.f, a2 = 0.f;
+    for (int l = threadIdx.x; l < L; l += BN_T) {
+      const float v = bn_ld(xr, l);
+      a1 += v;
+      a2 = fmaf(v, v, a2);
+    }
+    s1 += a1;
+    s2 += a2;
   }
   s1 = block_sum_f64(s1, red);
   s2 = block_sum_f64(s2, red);
@@ -108,15 +114,18 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_stats(const T* __restrict__ x, 
                                                        const float* __restrict__ invstd, double* __restrict__ part) {
   __shared__ double red[BN_T / 64];
   const int c = blockIdx.y, sp = blockIdx.x;
-  const int64_t M = (int64_t)N * L;
   const float mu = mean[c], is = invstd[c];
   double s1 = 0.0, s2 = 0.0;
-  for (int64_t e = (int64_t)sp * BN_T + threadIdx.x; e < M; e += (int64_t)BN_SPLIT * BN_T) {
-    const int64_t n = e / L, l = e - n * L;
-    const int64_t i = (n * C + c) * L + l;
-    const float g = bn_ld(dy, i);
-    s1 += g;
-    s2 += (double)g * ((bn_ld(x, i) - mu) * is);
+  for (int n = sp; n < N; n += BN_SPLIT) {
+    const int64_t r = ((int64_t)n * C + c) * L;
+    float a1 = 0.f, a2 = 0.f;
+    for (int l = threadIdx.x; l < L; l += BN_T) {
+      const float g = bn_ld(dy, r + l);
+      a1 += g;
+      a2 = fmaf(g, (bn_ld(x, r + l) - mu) * is, a2);
+    }
+    s1 += a1;
+    s2 += a2;
   }
   s1 = block_sum_f64(s1, red);
   s2 = block_sum_f64(s2, red);

@@ -658,6 +658,12 @@ __device__ __forceinline__ uint32_t q8_pack4(float a0, float a1, float a2, float
   return lo | hi;
 }
 
+// 16-B slot of piece P = 2·column + half in a group's staging image: the low
+// four bits are XORed with bits 4-7 (an involution).  The writes (16 lanes:
+// columns 4cl+e, one half) and the linear copy-out reads then both hit 16
+// distinct 16-B bank groups per pass (no LDS bank conflicts).
+__device__ __forceinline__ int q8_qslot(int P) { return P ^ ((P >> 4) & 15); }
+
 // grid (chunk · nblk + block, P8 / 128), 512 threads: one 256-row scale
 // block × 128 columns.  Wave w, lane half h own rows 32w + 16h .. +15 (= half
 // h of 32-row group w) and lane l&31 owns columns 4(l&31) .. +3: float4 loads,
@@ -683,7 +689,8 @@ __global__ __launch_bounds__(512, 2) void k_q8_quant(const float* __restrict__ X
   while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
   const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
   const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
-  if (r0 + (int64_t)b * Q8BLK >= r1) return;  // block past the chunk's rows (whole workgroup)
+  // blocks past the chunk's rows are written too (zero digits, scale 1): the
+  // Gram kernels read whole blocks (k_gram8d: whole triples of blocks)
   const int64_t rb = r0 + (int64_t)b * Q8BLK + 32 * wave + 16 * h;
   const bool vec = (ldx % 4 == 0) && (c0 + 3 < p) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
   f32x4 sh;
@@ -767,14 +774,14 @@ __global__ __launch_bounds__(512, 2) void k_q8_quant(const float* __restrict__ X
   for (int dg = 0; dg < 3; ++dg) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-      *reinterpret_cast<i32x4*>(&stage[(wave * QC + 4 * cl + e) * 32 + 16 * h]) = w[dg][e];
+      *reinterpret_cast<i32x4*>(&stage[wave * (QC * 32) + q8_qslot(2 * (4 * cl + e) + h) * 16]) = w[dg][e];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int o = 16 * (tid + 512 * k);  // byte offset in the stage image
       const int g = o / (QC * 32), within = o - g * (QC * 32);
       *reinterpret_cast<i32x4*>(gdst + (size_t)dg * q.plane + (size_t)g * q.P8 * 32 + within) =
-          *reinterpret_cast<const i32x4*>(&stage[o]);
+          *reinterpret_cast<const i32x4*>(&stage[g * (QC * 32) + q8_qslot(within >> 4) * 16]);
     }
     __syncthreads();
   }
@@ -1006,6 +1013,184 @@ __global__ __launch_bounds__(512, 1) void k_gram8(Q8Plan q, SegTable st, int nt,
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_gram8d — the i8×3 Gram without an LDS stage or workgroup barrier.  The
+// digit-plane layout makes one MFMA operand fragment (32 columns × 32 rows:
+// lane (r, h) ← column r, bytes 16h..16h+15 of the group) one contiguous
+// 1-KiB run, so every wave loads its own A and B fragments straight into
+// registers with buffer loads, two stages ahead (2 × 48 VGPRs).  The two
+// waves sharing a panel read the same bytes (the CU's L1 serves the second).
+// One wave per SIMD, 64×64 per wave; the scale-block flush goes through
+// wave-private LDS.  The default i8×3 Gram kernel (OCM_GRAM8_VARIANT=lds: k_gram8).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
+                                                   float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float scl[4][2 * 64];        // wave-private: row, column scales
+  __shared__ __attribute__((aligned(16))) float runl[4][4][4][64][4];  // wave-private f32 running sums
+
+  const int b = blockIdx.x;
+  const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
+  const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int chunk = wg / ntiles;
+  const int tile = wg - chunk * ntiles;
+  int ti, tj;
+  tile_coords(tile, nt, ti, tj);
+  const int I = ti * Q8T, J = tj * Q8T;
+  int s = 0;
+  while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
+  const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
+  const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
+  const int nb = (int)((r1 - r0 + Q8BLK - 1) / Q8BLK);
+  // whole triples of scale blocks (the loop body is three blocks); the
+  // quantiser zero-fills every block of a chunk, chunk_rows is a multiple of 768
+  const int nb3 = (nb + 2) / 3 * 3;
+  const int nstage3 = nb3 * Q8SPB;
+  const size_t gbase = (size_t)chunk * (st.chunk_rows / Q8K);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int l31 = lane & 31, h = lane >> 5;
+  if (ti == tj && wm > wn) return;  // strictly-lower block of a diagonal tile; no barrier to keep
+  const size_t gstride = (size_t)q.P8 * 32;
+  const int xflags = __builtin_amdgcn_readfirstlane(q.noload);  // timing ablations (OCM_GRAM8_NOLOAD bits)
+  const uint32_t span = (xflags & 1) ? 0u : (uint32_t)((size_t)nstage3 * gstride);
+  const char* cbase = q.digits + gbase * gstride;
+  __amdgpu_buffer_rsrc_t ra[3], rb[3];
+#pragma unroll
+  for (int dg = 0; dg < 3; ++dg) {
+    ra[dg] = __builtin_amdgcn_make_buffer_rsrc((void*)(cbase + dg * q.plane + (size_t)(I + wm * 64) * 32), 0, span,
+                                               0x00020000);
+    rb[dg] = __builtin_amdgcn_make_buffer_rsrc((void*)(cbase + dg * q.plane + (size_t)(J + wn * 64) * 32), 0, span,
+                                               0x00020000);
+  }
+  const int voff = l31 * 32 + h * 16;
+  const float* srow = q.scale + (size_t)chunk * q.nblk * q.P8 + I + wm * 64 + lane;
+  const float* scol = q.scale + (size_t)chunk * q.nblk * q.P8 + J + wn * 64 + lane;
+
+#define Q8D_LOAD(FA, FB, STG)                                                                         \
+  do {                                                                                              \
+    const int so_ = (STG) * (int)gstride;                                                           \
+    _Pragma("unroll") for (int x_ = 0; x_ < 2; ++x_)                                                \
+    _Pragma("unroll") for (int dg_ = 0; dg_ < 3; ++dg_) {                                           \
+      FA[x_][dg_] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(ra[dg_], voff + x_ * 1024, so_, 0); \
+      FB[x_][dg_] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(rb[dg_], voff + x_ * 1024, so_, 0); \
+    }                                                                                               \
+  } while (0)
+#define Q8D_MFMA(FA, FB)                                                                              \
+  do {                                                                                              \
+    _Pragma("unroll") for (int a_ = 0; a_ < 2; ++a_)                                                \
+    _Pragma("unroll") for (int c_ = 0; c_ < 2; ++c_) {                                              \
+      acc1[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[c_][0], acc1[a_][c_], 0, 0, 0); \
+      acc2[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[c_][1], acc2[a_][c_], 0, 0, 0); \
+      acc2[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][1], FB[c_][0], acc2[a_][c_], 0, 0, 0); \
+      acc3[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[c_][2], acc3[a_][c_], 0, 0, 0); \
+      acc3[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][2], FB[c_][0], acc3[a_][c_], 0, 0, 0); \
+      acc3[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][1], FB[c_][1], acc3[a_][c_], 0, 0, 0); \
+    }                                                                                               \
+  } while (0)
+
+  i32x16 acc1[2][2], acc2[2][2], acc3[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      acc1[a][c] = i32x16{};
+      acc2[a][c] = i32x16{};
+      acc3[a][c] = i32x16{};
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(&runl[wave][a * 2 + c][g][lane][0]) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  float SR = 0.f, SC = 0.f;  // this lane's row / column scale of the current block
+  auto flush = [&]() __attribute__((always_inline)) {
+    constexpr float w2 = 1.f / 254.f, w3 = 1.f / (254.f * 254.f);
+    scl[wave][lane] = SR;  // wave-private: LDS is in order within the wave
+    scl[wave][64 + lane] = SC;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float sj = scl[wave][64 + c * 32 + l31];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          // row scales of registers 4g..4g+3: rows 8g + 4h + 0..3
+          const f32x4 si = *reinterpret_cast<const f32x4*>(&scl[wave][a * 32 + 8 * g + 4 * h]);
+          f32x4* rp = reinterpret_cast<f32x4*>(&runl[wave][a * 2 + c][g][lane][0]);
+          f32x4 rv = *rp;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g + e;
+            const float v = fmaf((float)acc3[a][c][r], w3, fmaf((float)acc2[a][c][r], w2, (float)acc1[a][c][r]));
+            rv[e] = fmaf(v, si[e] * sj, rv[e]);
+          }
+          *rp = rv;
+        }
+        acc1[a][c] = i32x16{};
+        acc2[a][c] = i32x16{};
+        acc3[a][c] = i32x16{};
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+// stage STG computes on set CUR; the loads of stage STG+2 fill set NXT first
+#define Q8D_S0 F0A, F0B, F2A, F2B
+#define Q8D_S1 F1A, F1B, F0A, F0B
+#define Q8D_S2 F2A, F2B, F1A, F1B
+#define Q8D_STEP_(STG, CA, CB, NA, NB)                                                                \
+  do {                                                                                              \
+    Q8D_LOAD(NA, NB, min((STG) + 2, nstage3 - 1));                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                              \
+    if (!(xflags & 4)) Q8D_MFMA(CA, CB);                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                              \
+  } while (0)
+#define Q8D_STEP(STG, ...) Q8D_STEP_(STG, __VA_ARGS__)
+
+  i32x4 F0A[2][3], F0B[2][3], F1A[2][3], F1B[2][3], F2A[2][3], F2B[2][3];
+  Q8D_LOAD(F0A, F0B, 0);
+  Q8D_LOAD(F1A, F1B, min(1, nstage3 - 1));
+  for (int blk = 0; blk < nb3; blk += 3) {
+    const int s0 = blk * Q8SPB;
+#define Q8D_BLOCK(B0, SA, SB, SC_, SD, SE, SF, SG, SH)                                                \
+    Q8D_STEP(B0 + 0, SA);                                                                           \
+    Q8D_STEP(B0 + 1, SB);                                                                           \
+    SR = srow[(size_t)((B0) / Q8SPB) * q.P8];                                                       \
+    SC = scol[(size_t)((B0) / Q8SPB) * q.P8];                                                       \
+    Q8D_STEP(B0 + 2, SC_);                                                                          \
+    Q8D_STEP(B0 + 3, SD);                                                                           \
+    Q8D_STEP(B0 + 4, SE);                                                                           \
+    Q8D_STEP(B0 + 5, SF);                                                                           \
+    Q8D_STEP(B0 + 6, SG);                                                                           \
+    Q8D_STEP(B0 + 7, SH);                                                                           \
+    if (!(xflags & 8)) flush();
+    // stage s0+u uses set (s0+u) % 3 = u % 3 (s0 is a multiple of 24); the
+    // loads of stage s0+u+2 go to set (u+2) % 3
+    Q8D_BLOCK(s0, Q8D_S0, Q8D_S1, Q8D_S2, Q8D_S0, Q8D_S1, Q8D_S2, Q8D_S0, Q8D_S1)
+    Q8D_BLOCK(s0 + 8, Q8D_S2, Q8D_S0, Q8D_S1, Q8D_S2, Q8D_S0, Q8D_S1, Q8D_S2, Q8D_S0)
+    Q8D_BLOCK(s0 + 16, Q8D_S1, Q8D_S2, Q8D_S0, Q8D_S1, Q8D_S2, Q8D_S0, Q8D_S1, Q8D_S2)
+#undef Q8D_BLOCK
+  }
+#undef Q8D_STEP
+#undef Q8D_STEP_
+#undef Q8D_S0
+#undef Q8D_S1
+#undef Q8D_S2
+#undef Q8D_MFMA
+#undef Q8D_LOAD
+
+  float* out = part + ((size_t)chunk * ntiles + tile) * (Q8T * Q8T);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int col = wn * 64 + c * 32 + l31;
+        out[row * Q8T + col] = runl[wave][a * 2 + c][r >> 2][lane][r & 3];
+      }
+}
+
 int gram_small(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int32_t p, const float* shift,
                const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out, hipStream_t st) {
   // chunks never straddle a segment: span = (lo, hi) row range per chunk
@@ -1140,7 +1325,8 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     const int64_t want = std::max<int64_t>(1, (4LL * ctx->num_cus + ntiles - 1) / ntiles);
     chunk_rows = std::min<int64_t>(4096, (n + want - 1) / want);
   }
-  chunk_rows = std::max<int64_t>(Q8BLK, (int64_t)ocm::align_up((size_t)chunk_rows, Q8BLK));
+  // multiple of three scale blocks (k_gram8d's loop body)
+  chunk_rows = std::max<int64_t>(3 * Q8BLK, (int64_t)ocm::align_up((size_t)chunk_rows, 3 * Q8BLK));
   std::vector<int32_t> cprefix(nseg + 1, 0);
   for (int s = 0; s < nseg; ++s) {
     const int64_t len = seg_offsets[s + 1] - seg_offsets[s];
@@ -1195,7 +1381,12 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     }
     {
       ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
-      hipLaunchKernelGGL(k_gram8, dim3((unsigned)total), dim3(512), 0, st, q, tab, nt, ntiles, (int)total, pg);
+      // "direct" (default: k_gram8d, register fragments, no LDS stage) or "lds" (k_gram8)
+      const char* v = std::getenv("OCM_GRAM8_VARIANT");
+      if (!v || std::string(v) != "lds")
+        hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tab, nt, ntiles, (int)total, pg);
+      else
+        hipLaunchKernelGGL(k_gram8, dim3((unsigned)total), dim3(512), 0, st, q, tab, nt, ntiles, (int)total, pg);
       OCM_CHECK_LAUNCH("k_gram8");
     }
   }
