@@ -205,10 +205,13 @@ def main():
     score_avg_s = score_ms / max(score_n, 1) / 1e3
     score_gbs = n * p * 4 / score_avg_s / 1e9 if score_avg_s > 0 else 0.0
 
-    gram_kernel = {"bf16x3": "k_gram3", "i8x3": "k_gram8"}.get(args.gram_mode, "k_gram")
+    variant8 = os.environ.get("OCM_GRAM8_VARIANT", "direct")
+    gram_kernel = {"bf16x3": "k_gram3", "i8x3": "k_gram8d" if variant8 != "lds" else "k_gram8"}.get(
+        args.gram_mode, "k_gram")
     if args.gram_mode == "i8x3":
         # fp32-grade product from 6 int8 MFMA digit products (exact int32 sums)
-        gram_desc = "k_gram8 (shifted Gram, 3 int8 digits per value, 6 i8 MFMA products per fp32 product)"
+        gram_desc = (f"{gram_kernel} (shifted Gram, 3 int8 digits per value, 6 i8 MFMA products per fp32 "
+                     "product, exact int32 sums)")
         gram_peak = round(I8_MFMA_PEAK_TOPS / 6, 1)
         peak_basis = "int8 MFMA dense peak / 6 (fp32-equivalent); achieved counts algorithmic fp32 flops n*p*(p+1)"
     elif args.gram_mode == "bf16x3":
@@ -263,7 +266,7 @@ def main():
             "avg_launch_ms": round(gram_avg_s * 1e3, 4),
             "launches": gram_n,
         },
-        "score_kernel": {"kernel": "k_score (fused projection/Q/T2)", "bound": "hbm",
+        "score_kernel": {"kernel": "k_score_direct (fused projection/Q/T2, two sweeps)", "bound": "hbm",
                          "achieved_GBs": round(score_gbs, 1), "peak_GBs": HBM_PEAK_GBS,
                          "frac": round(score_gbs / HBM_PEAK_GBS, 4), "avg_launch_ms": round(score_avg_s * 1e3, 4),
                          "launches": score_n, "bytes_per_launch": n * p * 4},

@@ -6,7 +6,7 @@ OUT=gpurun_out/prof
 mkdir -p $OUT
 A="bench.py --steps 2 --warmup 1 --no-cpu --no-vae"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-vae > $OUT/bench_trace.log 2>&1 || exit 1
-K="--kernel-include-regex k_gram8|k_score_direct|k_q8_quant"
+K="--kernel-include-regex k_gram8d|k_score_direct|k_q8_quant"
 timeout -s KILL 200 rocprofv3 $K --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d $OUT/pmc1 -o p --output-format csv -- python3 $A > $OUT/pmc1.log 2>&1 || exit 2
 timeout -s KILL 200 rocprofv3 $K --pmc FETCH_SIZE -d $OUT/pmc2 -o p --output-format csv -- python3 $A > $OUT/pmc2.log 2>&1 || exit 3
 timeout -s KILL 200 rocprofv3 $K --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum -d $OUT/pmc3 -o p --output-format csv -- python3 $A > $OUT/pmc3.log 2>&1 || exit 4

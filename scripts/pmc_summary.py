@@ -16,7 +16,7 @@ os.makedirs(prof, exist_ok=True)
 
 
 def short(name):
-    for key in ("k_gram_reduce", "k_gram8", "k_gram3", "k_gram", "k_q8_quant", "k_score_direct", "k_score"):
+    for key in ("k_gram_reduce", "k_gram8d", "k_gram8", "k_gram3", "k_gram", "k_q8_quant", "k_score_direct", "k_score"):
         if key + "<" in name or key + "(" in name:
             return key
     return name[:60]
@@ -65,7 +65,7 @@ latest_path = os.path.join(prof, "pmc_gram_latest.json")
 latest = json.load(open(latest_path)) if os.path.exists(latest_path) else {}
 if "kernel" in latest:  # older single-kernel format
     latest = {latest["kernel"]: {"hbm_bytes_per_launch": latest["hbm_bytes_per_launch"], "source": latest["source"]}}
-for kname in ("k_gram", "k_gram3", "k_gram8", "k_q8_quant", "k_score_direct"):
+for kname in ("k_gram", "k_gram3", "k_gram8", "k_gram8d", "k_q8_quant", "k_score_direct"):
     if kname in out and "hbm_bytes_per_launch" in out[kname]:
         latest[kname] = {"hbm_bytes_per_launch": out[kname]["hbm_bytes_per_launch"], "source": f"{tag}_pmc.json"}
 json.dump(latest, open(latest_path, "w"), indent=1)
