@@ -637,7 +637,7 @@ __global__ __launch_bounds__(256) void k_gram_small_reduce(const double* __restr
 // ---------------------------------------------------------------------------
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
-constexpr int Q8T = 128, Q8K = 32, Q8BLK = 256, Q8SPB = Q8BLK / Q8K;
+constexpr int Q8T = 128, Q8K = 32, Q8BLK = 768, Q8SPB = Q8BLK / Q8K;
 constexpr float Q8BASE = 254.f;
 
 struct Q8Plan {
@@ -658,40 +658,47 @@ __device__ __forceinline__ uint32_t q8_pack4(float a0, float a1, float a2, float
   return lo | hi;
 }
 
-// 16-B slot of piece P = 2·column + half in a group's staging image: the low
-// four bits are XORed with bits 4-7 (an involution).  The writes (16 lanes:
-// columns 4cl+e, one half) and the linear copy-out reads then both hit 16
-// distinct 16-B bank groups per pass (no LDS bank conflicts).
-__device__ __forceinline__ int q8_qslot(int P) { return P ^ ((P >> 4) & 15); }
+// 16-B slot of piece P = 2·column + half in a group's staging image (32
+// columns = 64 pieces): bits 0-2 are XORed with bits 3-5 (an involution).
+// The writes (8 consecutive lanes: column quads 0..7 of one row slice, i.e.
+// pieces 8cq + const) and the linear copy-out reads then hit 8 distinct 16-B
+// bank groups per ds_write_b128 / ds_read_b128 lane group.
+__device__ __forceinline__ int q8_qslot(int P) { return P ^ ((P >> 3) & 7); }
 
-// grid (chunk · nblk + block, P8 / 128), 512 threads: one 256-row scale
-// block × 128 columns.  Wave w, lane half h own rows 32w + 16h .. +15 (= half
-// h of 32-row group w) and lane l&31 owns columns 4(l&31) .. +3: float4 loads,
-// 2 × 512 B per wave instruction, and each (column, digit) of a thread is one
-// 16-B piece of the digit image.  The pieces are staged through LDS (one
-// digit plane at a time) so that the stores leave as contiguous 1-KiB runs.
+// grid (chunk · nblk + block, P8 / 32), 384 threads (6 waves): one 768-row
+// scale block × 32 columns.  Thread t owns column quad cq = t & 7 (columns
+// 4cq .. 4cq+3: a wave instruction reads 8 rows × 128 B) and row slice
+// rs = t >> 3 (rows 16rs .. 16rs+15 = half rs&1 of 32-row group rs>>1), so
+// each (column, digit) of a thread is one 16-B piece of the digit image.  The
+// pieces are staged through LDS (one digit plane, 24 KiB, at a time) so that
+// the stores leave as contiguous 1-KiB runs (one 32-row group × 32 columns).
+constexpr int Q8QC = 32;                   // columns per quantiser workgroup
+constexpr int Q8QS = Q8BLK / 16;           // 16-row slices per block (48)
+constexpr int Q8QT = Q8QS * (Q8QC / 4);    // threads (384)
 template <bool GATHER>
-__global__ __launch_bounds__(512, 2) void k_q8_quant(const float* __restrict__ X, int64_t ldx,
-                                                     const int64_t* __restrict__ rows, int p,
-                                                     const float* __restrict__ shift, SegTable st, Q8Plan q,
-                                                     double* __restrict__ colblk) {
-  constexpr int QC = 128;                            // columns per workgroup
-  __shared__ __attribute__((aligned(16))) char stage[Q8SPB * QC * 32];  // one digit plane: 32 KiB
-  __shared__ __attribute__((aligned(16))) float wmax[16][QC];
-  __shared__ __attribute__((aligned(16))) double wsum[16][QC];
+__global__ __launch_bounds__(Q8QT, 2) void k_q8_quant(const float* __restrict__ X, int64_t ldx,
+                                                      const int64_t* __restrict__ rows, int p,
+                                                      const float* __restrict__ shift, SegTable st, Q8Plan q,
+                                                      double* __restrict__ colblk) {
+  constexpr int QC = Q8QC;
+  __shared__ __attribute__((aligned(16))) char stage[Q8SPB * QC * 32];  // one digit plane: 24 KiB
+  __shared__ __attribute__((aligned(16))) float wmax[Q8QS][QC];
+  __shared__ __attribute__((aligned(16))) double wsum[Q8QS][QC];
+  __shared__ float pmax[8][QC];
+  __shared__ double psum[8][QC];
   __shared__ __attribute__((aligned(16))) float fmax_[QC];
   const int chunk = blockIdx.x / q.nblk, b = blockIdx.x - chunk * q.nblk;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, cl = lane & 31;
+  const int tid = threadIdx.x;
+  const int cq = tid & 7, rs = tid >> 3;
   const int cg0 = blockIdx.y * QC;      // first column of the workgroup
-  const int c0 = cg0 + 4 * cl;          // first of this thread's 4 columns
+  const int c0 = cg0 + 4 * cq;          // first of this thread's 4 columns
   int s = 0;
   while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
   const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
   const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
   // blocks past the chunk's rows are written too (zero digits, scale 1): the
-  // Gram kernels read whole blocks (k_gram8d: whole triples of blocks)
-  const int64_t rb = r0 + (int64_t)b * Q8BLK + 32 * wave + 16 * h;
+  // Gram kernels read whole blocks
+  const int64_t rb = r0 + (int64_t)b * Q8BLK + 16 * rs;
   const bool vec = (ldx % 4 == 0) && (c0 + 3 < p) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
   f32x4 sh;
 #pragma unroll
@@ -721,18 +728,30 @@ __global__ __launch_bounds__(512, 2) void k_q8_quant(const float* __restrict__ X
       m[e] = fmaxf(m[e], fabsf(v[j][e]));
       cs[e] += (double)v[j][e];
     }
-  const int wr = 2 * wave + h;  // 16 row slices
-  *reinterpret_cast<f32x4*>(&wmax[wr][4 * cl]) = m;
+  *reinterpret_cast<f32x4*>(&wmax[rs][4 * cq]) = m;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) wsum[wr][4 * cl + e] = cs[e];
+  for (int e = 0; e < 4; ++e) wsum[rs][4 * cq + e] = cs[e];
+  __syncthreads();
+  // two-level column reduction over the 48 slices (fixed order)
+  if (tid < 8 * QC) {
+    const int col = tid & (QC - 1), part = tid / QC;
+    float mm = 0.f;
+    double ss = 0.0;
+    for (int w = part * (Q8QS / 8); w < (part + 1) * (Q8QS / 8); ++w) {
+      mm = fmaxf(mm, wmax[w][col]);
+      ss += wsum[w][col];
+    }
+    pmax[part][col] = mm;
+    psum[part][col] = ss;
+  }
   __syncthreads();
   if (tid < QC) {
     float mm = 0.f;
     double ss = 0.0;
 #pragma unroll
-    for (int w = 0; w < 16; ++w) {
-      mm = fmaxf(mm, wmax[w][tid]);
-      ss += wsum[w][tid];
+    for (int w = 0; w < 8; ++w) {
+      mm = fmaxf(mm, pmax[w][tid]);
+      ss += psum[w][tid];
     }
     fmax_[tid] = mm;
     int ex = 0;
@@ -742,7 +761,7 @@ __global__ __launch_bounds__(512, 2) void k_q8_quant(const float* __restrict__ X
     colblk[o] = ss;
   }
   __syncthreads();
-  const f32x4 mx = *reinterpret_cast<const f32x4*>(&fmax_[4 * cl]);
+  const f32x4 mx = *reinterpret_cast<const f32x4*>(&fmax_[4 * cq]);
   i32x4 w[3][4];  // [digit][column e]
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -767,21 +786,23 @@ __global__ __launch_bounds__(512, 2) void k_q8_quant(const float* __restrict__ X
       w[2][e][k] = (int)q8_pack4(d3[0], d3[1], d3[2], d3[3]);
     }
   }
-  // stage image: [group w][column 0..127][32 B]; copy-out: 16 B per thread and
-  // pass, 1 KiB contiguous per wave instruction
+  // stage image: [group][column 0..31][32 B]; copy-out: 16 B per thread and
+  // pass, 1 KiB contiguous per wave instruction (= one group)
+  constexpr int GIMG = QC * 32;  // bytes per group image
   char* gdst = q.digits + ((size_t)chunk * (st.chunk_rows / Q8K) + (size_t)b * Q8SPB) * q.P8 * 32 + (size_t)cg0 * 32;
+  const int grp = rs >> 1, half = rs & 1;
 #pragma unroll
   for (int dg = 0; dg < 3; ++dg) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-      *reinterpret_cast<i32x4*>(&stage[wave * (QC * 32) + q8_qslot(2 * (4 * cl + e) + h) * 16]) = w[dg][e];
+      *reinterpret_cast<i32x4*>(&stage[grp * GIMG + q8_qslot(2 * (4 * cq + e) + half) * 16]) = w[dg][e];
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int o = 16 * (tid + 512 * k);  // byte offset in the stage image
-      const int g = o / (QC * 32), within = o - g * (QC * 32);
+    for (int k = 0; k < Q8SPB * GIMG / (16 * Q8QT); ++k) {
+      const int o = 16 * (tid + Q8QT * k);  // byte offset in the stage image
+      const int g = o / GIMG, within = o - g * GIMG;
       *reinterpret_cast<i32x4*>(gdst + (size_t)dg * q.plane + (size_t)g * q.P8 * 32 + within) =
-          *reinterpret_cast<const i32x4*>(&stage[g * (QC * 32) + q8_qslot(within >> 4) * 16]);
+          *reinterpret_cast<const i32x4*>(&stage[g * GIMG + q8_qslot(within >> 4) * 16]);
     }
     __syncthreads();
   }
@@ -808,209 +829,6 @@ __global__ __launch_bounds__(256) void k_colblk_sum(const double* __restrict__ c
     for (int k = 0; k < 16; ++k) t += red[k][cl];
     colsum[col] = t;
   }
-}
-
-__device__ __forceinline__ int q8_off(int panel, int dg, int col, int half) {
-  return (((panel * 3 + dg) * Q8T + col) << 5) + ((half ^ ((col >> 3) & 1)) << 4);
-}
-
-// 8 waves (two per SIMD), waves 2 (M, 64 rows) × 4 (N, 32 columns): 3 × 2
-// int32 32×32 accumulator tiles per wave; f32 running sums of the flushed
-// scale blocks in LDS.  Stages of 32 rows go through a ring of three LDS
-// buffers, so the barrier at the top of an iteration only drains LDS
-// traffic issued a full iteration earlier:
-//   iteration s:  barrier · store stage s+2 (registers → ring) · read the
-//                 fragments of stage s+1 · issue the loads of stage s+4 ·
-//                 12 MFMAs on the fragments of stage s (read one iteration ago)
-// Stage t is loaded at iteration t-4, stored at t-2, read at t-1, used at t.
-__global__ __launch_bounds__(512, 1) void k_gram8(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
-                                                  float* __restrict__ part) {
-  constexpr int STAGE = 2 * 3 * Q8T * 32;  // 24 KiB: both panels, three digits
-  constexpr int IMG = Q8T * 32;            // one (panel, digit) image: 4 KiB
-  __shared__ __attribute__((aligned(16))) char lds[3 * STAGE];
-  __shared__ __attribute__((aligned(16))) float sc[2][2 * Q8T];  // scale-block parity × [panel][column]
-  // f32 running sums of the flushed scale blocks, wave-private: [wave][a][r/4][lane][4]
-  __shared__ __attribute__((aligned(16))) float runl[8][2][4][64][4];
-
-  const int b = blockIdx.x;
-  const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
-  const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
-  const int chunk = wg / ntiles;
-  const int tile = wg - chunk * ntiles;
-  int ti, tj;
-  tile_coords(tile, nt, ti, tj);
-  const bool diag = (ti == tj);
-  const int I = ti * Q8T, J = tj * Q8T;
-  int s = 0;
-  while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
-  const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
-  const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
-  // whole scale blocks: the quantiser zero-fills a block's rows past r1, so
-  // every loop trip is identical (branch-free loads → exact vmcnt waits)
-  const int nb = (int)((r1 - r0 + Q8BLK - 1) / Q8BLK);
-  const int nstage = nb * Q8SPB;
-  const size_t gbase = (size_t)chunk * (st.chunk_rows / Q8K);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int l31 = lane & 31, h = lane >> 5;
-  const bool idle = diag && (64 * wm >= 32 * wn + 32);  // strictly below the diagonal
-  const int xflags = __builtin_amdgcn_readfirstlane(q.noload);  // timing ablations (OCM_GRAM8_NOLOAD bits)
-  const size_t gstride = (size_t)q.P8 * 32;
-  const int st8 = tid & 255;  // scale staging: threads t and t+256 write the same (identical) entry
-  const float* sblk = q.scale + (size_t)chunk * q.nblk * q.P8 + (st8 < Q8T ? I + st8 : J + st8 - Q8T);
-  // loader: thread → pieces (column lp>>1, half lp&1) of images hf, hf+2, hf+4
-  // (image = panel·3 + digit)
-  const int hf = __builtin_amdgcn_readfirstlane(tid >> 8);
-  const int lp = tid & 255, lcol = lp >> 1, lhalf = lp & 1;
-  const uint32_t span = (xflags & 1) ? 0u : (uint32_t)((size_t)nstage * gstride);
-  const char* cbase = q.digits + gbase * gstride;
-  __amdgpu_buffer_rsrc_t rs[3];
-  int wo[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int img = hf + 2 * k, panel = img / 3, dg = img - 3 * panel;
-    rs[k] = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(cbase + dg * q.plane + (size_t)(panel ? J : I) * 32), 0, span, 0x00020000);
-    wo[k] = q8_off(panel, dg, lcol, lhalf);
-  }
-  const int voff = lcol * 32 + lhalf * 16;
-  const int fa0 = q8_off(0, 0, wm * 64 + l31, h), fa1 = q8_off(0, 0, wm * 64 + 32 + l31, h);
-  const int fb0 = q8_off(1, 0, wn * 32 + l31, h);
-
-#define Q8_GLOAD(R, STG)                                                                     \
-  do {                                                                                     \
-    const int so_ = (STG) * (int)gstride;                                                  \
-    _Pragma("unroll") for (int k_ = 0; k_ < 3; ++k_)                                       \
-      R[k_] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(rs[k_], voff, so_, 0);          \
-  } while (0)
-#define Q8_SSTORE(R, SLOT)                                                                   \
-  do {                                                                                     \
-    char* buf_ = lds + (SLOT) * STAGE;                                                     \
-    _Pragma("unroll") for (int k_ = 0; k_ < 3; ++k_)                                       \
-      *reinterpret_cast<i32x4*>(buf_ + wo[k_]) = R[k_];                                    \
-  } while (0)
-#define Q8_FRAGS(FA, FB, SLOT)                                                                        \
-  do {                                                                                              \
-    const char* buf_ = lds + (SLOT) * STAGE;                                                        \
-    _Pragma("unroll") for (int dg_ = 0; dg_ < 3; ++dg_) {                                           \
-      FB[dg_] = *reinterpret_cast<const i32x4*>(buf_ + fb0 + dg_ * IMG);                            \
-      FA[0][dg_] = *reinterpret_cast<const i32x4*>(buf_ + fa0 + dg_ * IMG);                         \
-      FA[1][dg_] = *reinterpret_cast<const i32x4*>(buf_ + fa1 + dg_ * IMG);                         \
-    }                                                                                               \
-  } while (0)
-#define Q8_MFMA(FA, FB)                                                                               \
-  do {                                                                                              \
-    if (!idle) {                                                                                    \
-      _Pragma("unroll") for (int a_ = 0; a_ < 2; ++a_) {                                            \
-        acc1[a_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[0], acc1[a_], 0, 0, 0);      \
-        acc2[a_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[1], acc2[a_], 0, 0, 0);      \
-        acc2[a_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][1], FB[0], acc2[a_], 0, 0, 0);      \
-        acc3[a_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[2], acc3[a_], 0, 0, 0);      \
-        acc3[a_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][2], FB[0], acc3[a_], 0, 0, 0);      \
-        acc3[a_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][1], FB[1], acc3[a_], 0, 0, 0);      \
-      }                                                                                             \
-    }                                                                                               \
-  } while (0)
-
-  i32x16 acc1[2], acc2[2], acc3[2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    acc1[a] = i32x16{};
-    acc2[a] = i32x16{};
-    acc3[a] = i32x16{};
-#pragma unroll
-    for (int g = 0; g < 4; ++g) *reinterpret_cast<f32x4*>(&runl[wave][a][g][lane][0]) = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  auto flush = [&](int par) __attribute__((always_inline)) {
-    if (idle) return;
-    constexpr float w2 = 1.f / 254.f, w3 = 1.f / (254.f * 254.f);
-    const float sj = sc[par][Q8T + wn * 32 + l31];
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        // row scales of registers 4g..4g+3: rows 8g + 4h + 0..3
-        const f32x4 si = *reinterpret_cast<const f32x4*>(&sc[par][wm * 64 + a * 32 + 8 * g + 4 * h]);
-        f32x4* rp = reinterpret_cast<f32x4*>(&runl[wave][a][g][lane][0]);
-        f32x4 rv = *rp;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = 4 * g + e;
-          // |A·| < 2²⁴ per block: the int → f32 conversions are exact; si·sj is a power of two
-          const float v = fmaf((float)acc3[a][r], w3, fmaf((float)acc2[a][r], w2, (float)acc1[a][r]));
-          rv[e] = fmaf(v, si[e] * sj, rv[e]);
-        }
-        *rp = rv;
-      }
-      acc1[a] = i32x16{};
-      acc2[a] = i32x16{};
-      acc3[a] = i32x16{};
-      __builtin_amdgcn_sched_barrier(0);  // one 32×32 block at a time: bounded temporaries
-    }
-  };
-#define Q8_MEM(STG, FAN, FBN, RS, SCS)                                                                \
-  do {                                                                                              \
-    if (!(xflags & 16)) Q8_SSTORE(RS, ((STG) + 2) % 3);                                             \
-    sc[(((STG) + 2) / Q8SPB) & 1][st8] = SCS;                                                       \
-    if (!(xflags & 2)) Q8_FRAGS(FAN, FBN, ((STG) + 1) % 3);                                         \
-    const int nx_ = min((STG) + 4, nstage - 1);                                                     \
-    SCS = sblk[(size_t)(nx_ / Q8SPB) * q.P8];                                                       \
-    Q8_GLOAD(RS, nx_);                                                                              \
-  } while (0)
-#define Q8_STEP(STG, FAC, FBC, FAN, FBN, RS, SCS)                                                     \
-  do {                                                                                              \
-    __syncthreads();                                                                                \
-    Q8_MEM(STG, FAN, FBN, RS, SCS);                                                                 \
-    __builtin_amdgcn_sched_barrier(0);                                                              \
-    if (!(xflags & 4)) Q8_MFMA(FAC, FBC);                                                           \
-    __builtin_amdgcn_sched_barrier(0);                                                              \
-  } while (0)
-
-  i32x4 RA[3], RB[3];  // stage parity 0 / 1
-  float SA, SB;
-  i32x4 FA0[2][3], FB0[3], FA1[2][3], FB1[3];
-  // prologue: stages 0, 1 stored; stage 0 fragments read; stages 2, 3 in flight
-  SA = sblk[0];
-  Q8_GLOAD(RA, 0);
-  SB = sblk[(size_t)(min(1, nstage - 1) / Q8SPB) * q.P8];
-  Q8_GLOAD(RB, min(1, nstage - 1));
-  Q8_SSTORE(RA, 0);
-  sc[0][st8] = SA;
-  SA = sblk[(size_t)(min(2, nstage - 1) / Q8SPB) * q.P8];
-  Q8_GLOAD(RA, min(2, nstage - 1));
-  Q8_SSTORE(RB, 1);
-  SB = sblk[(size_t)(min(3, nstage - 1) / Q8SPB) * q.P8];
-  Q8_GLOAD(RB, min(3, nstage - 1));
-  __syncthreads();
-  Q8_FRAGS(FA0, FB0, 0);
-  for (int blk = 0; blk < nb; ++blk) {
-    const int s0 = blk * Q8SPB;
-#pragma unroll
-    for (int u = 0; u < Q8SPB; u += 2) {
-      Q8_STEP(s0 + u, FA0, FB0, FA1, FB1, RA, SA);
-      Q8_STEP(s0 + u + 1, FA1, FB1, FA0, FB0, RB, SB);
-    }
-    if (!(xflags & 8)) flush(blk & 1);
-  }
-#undef Q8_STEP
-#undef Q8_MEM
-#undef Q8_MFMA
-#undef Q8_FRAGS
-#undef Q8_SSTORE
-#undef Q8_GLOAD
-
-  if (idle) return;
-  float* out = part + ((size_t)chunk * ntiles + tile) * (Q8T * Q8T);
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int col = wn * 32 + l31;
-      out[row * Q8T + col] = runl[wave][a][r >> 2][lane][r & 3];
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1041,10 +859,9 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
   const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
   const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
   const int nb = (int)((r1 - r0 + Q8BLK - 1) / Q8BLK);
-  // whole triples of scale blocks (the loop body is three blocks); the
-  // quantiser zero-fills every block of a chunk, chunk_rows is a multiple of 768
-  const int nb3 = (nb + 2) / 3 * 3;
-  const int nstage3 = nb3 * Q8SPB;
+  // whole scale blocks (the loop body is one block of 24 stages); the
+  // quantiser zero-fills every block of a chunk
+  const int nstage3 = nb * Q8SPB;
   const size_t gbase = (size_t)chunk * (st.chunk_rows / Q8K);
 
   const int lane = threadIdx.x & 63;
@@ -1149,26 +966,22 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
   i32x4 F0A[2][3], F0B[2][3], F1A[2][3], F1B[2][3], F2A[2][3], F2B[2][3];
   Q8D_LOAD(F0A, F0B, 0);
   Q8D_LOAD(F1A, F1B, min(1, nstage3 - 1));
-  for (int blk = 0; blk < nb3; blk += 3) {
+  for (int blk = 0; blk < nb; ++blk) {
+    // stage s0+u uses set u % 3 (s0 is a multiple of 24); the loads of stage
+    // s0+u+2 go to set (u+2) % 3.  The block's scales are fetched early (they
+    // are used by the flush after the last stage).
     const int s0 = blk * Q8SPB;
-#define Q8D_BLOCK(B0, SA, SB, SC_, SD, SE, SF, SG, SH)                                                \
-    Q8D_STEP(B0 + 0, SA);                                                                           \
-    Q8D_STEP(B0 + 1, SB);                                                                           \
-    SR = srow[(size_t)((B0) / Q8SPB) * q.P8];                                                       \
-    SC = scol[(size_t)((B0) / Q8SPB) * q.P8];                                                       \
-    Q8D_STEP(B0 + 2, SC_);                                                                          \
-    Q8D_STEP(B0 + 3, SD);                                                                           \
-    Q8D_STEP(B0 + 4, SE);                                                                           \
-    Q8D_STEP(B0 + 5, SF);                                                                           \
-    Q8D_STEP(B0 + 6, SG);                                                                           \
-    Q8D_STEP(B0 + 7, SH);                                                                           \
+#pragma unroll
+    for (int u = 0; u < Q8SPB; u += 3) {
+      Q8D_STEP(s0 + u, Q8D_S0);
+      Q8D_STEP(s0 + u + 1, Q8D_S1);
+      if (u == 0) {
+        SR = srow[(size_t)blk * q.P8];
+        SC = scol[(size_t)blk * q.P8];
+      }
+      Q8D_STEP(s0 + u + 2, Q8D_S2);
+    }
     if (!(xflags & 8)) flush();
-    // stage s0+u uses set (s0+u) % 3 = u % 3 (s0 is a multiple of 24); the
-    // loads of stage s0+u+2 go to set (u+2) % 3
-    Q8D_BLOCK(s0, Q8D_S0, Q8D_S1, Q8D_S2, Q8D_S0, Q8D_S1, Q8D_S2, Q8D_S0, Q8D_S1)
-    Q8D_BLOCK(s0 + 8, Q8D_S2, Q8D_S0, Q8D_S1, Q8D_S2, Q8D_S0, Q8D_S1, Q8D_S2, Q8D_S0)
-    Q8D_BLOCK(s0 + 16, Q8D_S1, Q8D_S2, Q8D_S0, Q8D_S1, Q8D_S2, Q8D_S0, Q8D_S1, Q8D_S2)
-#undef Q8D_BLOCK
   }
 #undef Q8D_STEP
 #undef Q8D_STEP_
@@ -1188,6 +1001,206 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
         const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int col = wn * 64 + c * 32 + l31;
         out[row * Q8T + col] = runl[wave][a * 2 + c][r >> 2][lane][r & 3];
+      }
+}
+
+// ---------------------------------------------------------------------------
+// k_gram8s — the i8×3 Gram with the operand panels shared through LDS.
+// k_gram8d feeds each wave's 64×64 tile from its own register loads: 12 KiB
+// per 32-row stage for 24 MFMAs, which saturates the CU's vector-memory path
+// (64 B/clk) exactly when the MFMA pipe is busy, so loads and MFMAs take
+// turns.  Here the workgroup's two 128-column panels (24 KiB per stage) are
+// copied ONCE into LDS by LDS-DMA (global_load_lds_dwordx4: 1 KiB = one
+// fragment per wave-instruction, no VGPR staging) and each wave reads its
+// fragments with ds_read_b128 — half the vector-memory bytes per MFMA, and
+// LDS reads at 64 B/clk of the array's 256.
+//   * phase = 2 stages (64 rows); a 3-slot ring, 50 KiB per slot: loads run
+//     two phases ahead; one counted vmcnt wait + one barrier per phase (the
+//     DMA of the next phase stays in flight across it);
+//   * the LDS image is lane-linear per fragment; the bank swizzle (the two
+//     16-B halves of column r swapped when bit 3 of r is set) is applied on
+//     the DMA's per-lane SOURCE address and on the ds_read address, so the
+//     fragment reads are conflict-free;
+//   * the scale-block scales ride along as two 256-B DMAs per wave and phase;
+//   * f32 running sums stay in registers (64 per lane; no LDS round trip).
+// Selected by OCM_GRAM8_VARIANT=shared.
+// ---------------------------------------------------------------------------
+constexpr int G8S_FRAG = 1024;                       // one 32-col × 32-row digit fragment
+constexpr int G8S_OPS = 2 * 2 * 3 * 4 * G8S_FRAG;    // [stage][A|B][digit][32-col block] = 48 KiB
+constexpr int G8S_SLOT = G8S_OPS + 4 * 512;          // + per-wave row / column scales
+constexpr int G8S_NSLOT = 3;
+
+__device__ __forceinline__ void g8s_dma16(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
+}
+__device__ __forceinline__ void g8s_dma4(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
+}
+
+__global__ __launch_bounds__(256, 1) void k_gram8s(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
+                                                   float* __restrict__ part) {
+  __shared__ __attribute__((aligned(1024))) char ring[G8S_NSLOT * G8S_SLOT];
+
+  const int b = blockIdx.x;
+  const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
+  const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int chunk = wg / ntiles;
+  const int tile = wg - chunk * ntiles;
+  int ti, tj;
+  tile_coords(tile, nt, ti, tj);
+  const int I = ti * Q8T, J = tj * Q8T;
+  int s = 0;
+  while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
+  const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
+  const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
+  const int nb = (int)((r1 - r0 + Q8BLK - 1) / Q8BLK);  // whole (zero-filled) scale blocks
+  constexpr int PPB = Q8SPB / 2;                        // phases per scale block
+  const int nph = nb * PPB;
+  const size_t gbase = (size_t)chunk * (st.chunk_rows / Q8K);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int l31 = lane & 31, h = lane >> 5;
+  // strictly-lower quadrant of a diagonal tile: loads and barriers, no MFMA
+  const bool skip = (ti == tj && wm > wn);
+  const size_t gstride = (size_t)q.P8 * 32;  // bytes per 32-row group and plane
+
+  // DMA role of this wave: stage (wave >> 1) of a phase, operand (wave & 1) —
+  // 12 fragments (3 digits × 4 column blocks); the swizzle on the source:
+  // LDS slot 2r + h' holds column r, half h' ^ bit3(r)
+  const int sg_dma = wave >> 1, op_dma = wave & 1;
+  const size_t srcoff = (size_t)(lane >> 1) * 32 + 16 * ((lane & 1) ^ ((lane >> 4) & 1));
+  const char* dma_base = q.digits + (gbase + sg_dma) * gstride + (size_t)(op_dma ? J : I) * 32 + srcoff;
+  const uint32_t ring0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ring);
+  const float* scl_src = q.scale + (size_t)chunk * q.nblk * q.P8 + lane;
+  const int srow0 = I + wm * 64, scol0 = J + wn * 64;
+
+  auto issue = [&](int ph, int slot) __attribute__((always_inline)) {
+    const uint32_t sb = ring0 + slot * G8S_SLOT;
+    const size_t poff = (size_t)ph * 2 * gstride;
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg)
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+        g8s_dma16(dma_base + dg * q.plane + poff + x * G8S_FRAG,
+                  sb + (((sg_dma * 2 + op_dma) * 3 + dg) * 4 + x) * G8S_FRAG);
+    const size_t so = (size_t)(ph / PPB) * q.P8;
+    g8s_dma4(scl_src + so + srow0, sb + G8S_OPS + wave * 512);
+    g8s_dma4(scl_src + so + scol0, sb + G8S_OPS + wave * 512 + 256);
+  };
+  // fragment read: lane (r, h) ← 16 B at swizzled slot 2r + (h ^ bit3(r))
+  const int rdoff = 16 * (2 * l31 + (h ^ ((l31 >> 3) & 1)));
+  auto frag = [&](int slot, int sg, int op, int dg, int xb) __attribute__((always_inline)) -> i32x4 {
+    return *reinterpret_cast<const i32x4*>(ring + slot * G8S_SLOT + (((sg * 2 + op) * 3 + dg) * 4 + xb) * G8S_FRAG +
+                                           rdoff);
+  };
+
+  i32x16 acc1[2][2], acc2[2][2], acc3[2][2];
+  float run[2][2][16];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      acc1[a][c] = i32x16{};
+      acc2[a][c] = i32x16{};
+      acc3[a][c] = i32x16{};
+#pragma unroll
+      for (int r = 0; r < 16; ++r) run[a][c][r] = 0.f;
+    }
+
+  // timing ablations (OCM_GRAM8_NOLOAD bits): 1 no DMA, 2 no fragment reads, 4 no MFMA, 8 no flush
+  const int xflags = __builtin_amdgcn_readfirstlane(q.noload);
+  i32x4 F0 = frag(0, 0, 0, 0, 0);
+  if (!(xflags & 1)) {
+    issue(0, 0);
+    issue(min(1, nph - 1), 1);
+  }
+  for (int ph = 0; ph < nph; ++ph) {
+    const int slot = ph % G8S_NSLOT;
+    // this wave's DMAs of phase ph are done (those of ph+1, 14, may still fly);
+    // after the barrier every wave's are, and slot (ph+2)%3 is free
+    asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (!(xflags & 1)) issue(min(ph + 2, nph - 1), (ph + 2) % G8S_NSLOT);
+    if (!skip) {
+#pragma unroll
+      for (int sg = 0; sg < 2; ++sg) {
+        i32x4 FA[2][3], FB[2][3];
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+          for (int dg = 0; dg < 3; ++dg) {
+            FA[x][dg] = (xflags & 2) ? F0 + dg : frag(slot, sg, 0, dg, 2 * wm + x);
+            FB[x][dg] = (xflags & 2) ? F0 - x : frag(slot, sg, 1, dg, 2 * wn + x);
+          }
+        if (xflags & 4) {
+#pragma unroll
+          for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int dg = 0; dg < 3; ++dg) acc1[x][dg & 1][dg] += FA[x][dg][0] ^ FB[x][dg][1];
+        } else
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            acc1[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a][0], FB[c][0], acc1[a][c], 0, 0, 0);
+            acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a][0], FB[c][1], acc2[a][c], 0, 0, 0);
+            acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a][1], FB[c][0], acc2[a][c], 0, 0, 0);
+            acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a][0], FB[c][2], acc3[a][c], 0, 0, 0);
+            acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a][2], FB[c][0], acc3[a][c], 0, 0, 0);
+            acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a][1], FB[c][1], acc3[a][c], 0, 0, 0);
+          }
+      }
+      if (ph % PPB == PPB - 1 && !(xflags & 8)) {
+        // scale-block flush: run += s_i s_j (A1 + A2/254 + A3/254²)
+        constexpr float w2 = 1.f / 254.f, w3 = 1.f / (254.f * 254.f);
+        const float* scl = reinterpret_cast<const float*>(ring + slot * G8S_SLOT + G8S_OPS + wave * 512);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const float sj = scl[64 + c * 32 + l31];
+#pragma unroll
+          for (int a = 0; a < 2; ++a) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              // rows of registers 4g..4g+3: a·32 + 8g + 4h + 0..3
+              const f32x4 si = *reinterpret_cast<const f32x4*>(&scl[a * 32 + 8 * g + 4 * h]);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int r = 4 * g + e;
+                const float v =
+                    fmaf((float)acc3[a][c][r], w3, fmaf((float)acc2[a][c][r], w2, (float)acc1[a][c][r]));
+                run[a][c][r] = fmaf(v, si[e] * sj, run[a][c][r]);
+              }
+            }
+            acc1[a][c] = i32x16{};
+            acc2[a][c] = i32x16{};
+            acc3[a][c] = i32x16{};
+          }
+        }
+      }
+    }
+  }
+  // no LDS-DMA may still be landing when the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (skip) return;
+  float* out = part + ((size_t)chunk * ntiles + tile) * (Q8T * Q8T);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int col = wn * 64 + c * 32 + l31;
+        out[row * Q8T + col] = run[a][c][r];
       }
 }
 
@@ -1325,8 +1338,8 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     const int64_t want = std::max<int64_t>(1, (4LL * ctx->num_cus + ntiles - 1) / ntiles);
     chunk_rows = std::min<int64_t>(4096, (n + want - 1) / want);
   }
-  // multiple of three scale blocks (k_gram8d's loop body)
-  chunk_rows = std::max<int64_t>(3 * Q8BLK, (int64_t)ocm::align_up((size_t)chunk_rows, 3 * Q8BLK));
+  // whole scale blocks (the Gram kernels' loop body)
+  chunk_rows = std::max<int64_t>(Q8BLK, (int64_t)ocm::align_up((size_t)chunk_rows, Q8BLK));
   std::vector<int32_t> cprefix(nseg + 1, 0);
   for (int s = 0; s < nseg; ++s) {
     const int64_t len = seg_offsets[s + 1] - seg_offsets[s];
@@ -1372,21 +1385,22 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     float* pg = part + (size_t)cprefix[s0] * ntiles * Q8T * Q8T;
     {
       ocm::TimedRegion tq(ctx, OCM_KERNEL_QUANT, st);
-      dim3 gq((unsigned)(gchunks * nblk), (unsigned)(P8 / 128));
+      dim3 gq((unsigned)(gchunks * nblk), (unsigned)(P8 / Q8QC));
       if (rows)
-        hipLaunchKernelGGL(k_q8_quant<true>, gq, dim3(512), 0, st, X, ldx, rows, p, shift, tab, q, col_g);
+        hipLaunchKernelGGL(k_q8_quant<true>, gq, dim3(Q8QT), 0, st, X, ldx, rows, p, shift, tab, q, col_g);
       else
-        hipLaunchKernelGGL(k_q8_quant<false>, gq, dim3(512), 0, st, X, ldx, rows, p, shift, tab, q, col_g);
+        hipLaunchKernelGGL(k_q8_quant<false>, gq, dim3(Q8QT), 0, st, X, ldx, rows, p, shift, tab, q, col_g);
       OCM_CHECK_LAUNCH("k_q8_quant");
     }
     {
       ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
-      // "direct" (default: k_gram8d, register fragments, no LDS stage) or "lds" (k_gram8)
+      // "direct" (default: k_gram8d, register fragments, no LDS stage) or "shared" (k_gram8s, LDS panels)
       const char* v = std::getenv("OCM_GRAM8_VARIANT");
-      if (!v || std::string(v) != "lds")
-        hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tab, nt, ntiles, (int)total, pg);
+      const std::string var = v ? v : "";
+      if (var == "shared")
+        hipLaunchKernelGGL(k_gram8s, dim3((unsigned)total), dim3(256), 0, st, q, tab, nt, ntiles, (int)total, pg);
       else
-        hipLaunchKernelGGL(k_gram8, dim3((unsigned)total), dim3(512), 0, st, q, tab, nt, ntiles, (int)total, pg);
+        hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tab, nt, ntiles, (int)total, pg);
       OCM_CHECK_LAUNCH("k_gram8");
     }
   }

@@ -35,7 +35,13 @@ def main():
     flop = args.rows * args.p * (args.p + 1)
     for r in range(args.rounds):
         for mode, name, chunk in variants:
-            os.environ["OCM_GRAM_MODE"] = "bf16x3" if mode.startswith("bf16x3") else mode  # f32 | i8x3 pass through
+            os.environ["OCM_GRAM_MODE"] = "bf16x3" if mode.startswith("bf16x3") else mode[:4] if mode.startswith("i8x3") else mode
+            # i8x3 kernel variants: i8x3 (default) | i8x3d (direct) | i8x3s (shared LDS) | i8x3l (LDS ring)
+            var = {"i8x3d": "direct", "i8x3s": "shared", "i8x3l": "lds"}.get(mode)
+            if var:
+                os.environ["OCM_GRAM8_VARIANT"] = var
+            else:
+                os.environ.pop("OCM_GRAM8_VARIANT", None)
             if mode == "bf16x3pk":
                 os.environ["OCM_GRAM3_PK"] = "1"
             else:
@@ -58,7 +64,8 @@ def main():
     Y = (X[:ns].double() - shift.double())
     Gref = Y.T @ Y
     os.environ.pop("OCM_GRAM3_PK", None)
-    for mode in sorted({v[0] for v in variants} - {"bf16x3pk"}):
+    os.environ.pop("OCM_GRAM8_VARIANT", None)
+    for mode in sorted({v[0][:4] if v[0].startswith("i8x3") else v[0] for v in variants} - {"bf16x3pk"}):
         os.environ["OCM_GRAM_MODE"] = mode
         Gm, _ = engine.gram(X, None, [0, ns], shift)
         print(f"{mode:8s} sample Gram max rel err vs fp64: {((Gm[0] - Gref).abs().max() / Gref.abs().max()).item():.2e}")
