@@ -1007,47 +1007,59 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
 // ---------------------------------------------------------------------------
 // k_gram8s — the i8×3 Gram with the operand panels shared through LDS.
 // k_gram8d feeds each wave's 64×64 tile from its own register loads: 12 KiB
-// per 32-row stage for 24 MFMAs, which saturates the CU's vector-memory path
-// (64 B/clk) exactly when the MFMA pipe is busy, so loads and MFMAs take
-// turns.  Here the workgroup's two 128-column panels (24 KiB per stage) are
-// copied ONCE into LDS by LDS-DMA (global_load_lds_dwordx4: 1 KiB = one
-// fragment per wave-instruction, no VGPR staging) and each wave reads its
-// fragments with ds_read_b128 — half the vector-memory bytes per MFMA, and
-// LDS reads at 64 B/clk of the array's 256.
-//   * phase = 2 stages (64 rows); a 3-slot ring, 50 KiB per slot: loads run
-//     two phases ahead; one counted vmcnt wait + one barrier per phase (the
-//     DMA of the next phase stays in flight across it);
+// per 32-row stage for 24 MFMAs, which keeps the CU's vector-memory path
+// (64 B/clk) as busy as the MFMA pipe, so the two take turns.  Here the
+// workgroup's two 128-column panels (24 KiB per stage) are copied ONCE into
+// LDS by LDS-DMA (global_load_lds_dwordx4: 1 KiB = one fragment per wave
+// instruction, no VGPR staging) and every wave reads its fragments with
+// ds_read_b128: half the vector-memory instructions per MFMA.
+//   * a 3-slot ring of stages (24 KiB each).  Iteration s (one barrier):
+//        wait (own DMA of stage s+1) · barrier
+//        24 MFMAs on the fragments of stage s (registers), interleaved one by
+//        one with the DMA of stage s+3 into slot s%3 (freed by the barrier)
+//        and the ds_reads of stage s+1's fragments (other register set);
+//     each DMA has two iterations to land;
 //   * the LDS image is lane-linear per fragment; the bank swizzle (the two
 //     16-B halves of column r swapped when bit 3 of r is set) is applied on
 //     the DMA's per-lane SOURCE address and on the ds_read address, so the
 //     fragment reads are conflict-free;
-//   * the scale-block scales ride along as two 256-B DMAs per wave and phase;
-//   * f32 running sums stay in registers (64 per lane; no LDS round trip).
+//   * the scale-block scales ride along (two 256-B DMAs per wave and stage,
+//     into a per-block double buffer: every stage of a block rewrites the same
+//     wave-private values);
+//   * f32 running sums in wave-private LDS (as k_gram8d).
 // Selected by OCM_GRAM8_VARIANT=shared.
 // ---------------------------------------------------------------------------
 constexpr int G8S_FRAG = 1024;                       // one 32-col × 32-row digit fragment
-constexpr int G8S_OPS = 2 * 2 * 3 * 4 * G8S_FRAG;    // [stage][A|B][digit][32-col block] = 48 KiB
-constexpr int G8S_SLOT = G8S_OPS + 4 * 512;          // + per-wave row / column scales
-constexpr int G8S_NSLOT = 3;
+constexpr int G8S_OPS = 2 * 3 * 4 * G8S_FRAG;        // [A|B][digit][32-col block] = 24 KiB
+constexpr int G8S_SCL = 2 * 4 * 512;                 // [block & 1][wave][row | column scales]
+constexpr int G8S_DMA = 8;                           // DMAs per wave and stage
 
-__device__ __forceinline__ void g8s_dma16(const void* src, uint32_t lds) {
+// LDS-DMA with a scalar (wave-uniform) 64-bit base and a per-lane 32-bit
+// offset; M0 = the wave-uniform LDS destination (written in the same asm
+// statement: the compiler owns M0 otherwise).  Invisible to the compiler's
+// vmcnt bookkeeping: the kernel counts these itself.
+__device__ __forceinline__ void g8s_dma16(uint64_t sbase, uint32_t voff, uint32_t lds) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(lds)
-               : "memory");
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds)
+      : "memory");
 }
-__device__ __forceinline__ void g8s_dma4(const void* src, uint32_t lds) {
+__device__ __forceinline__ void g8s_dma4(uint64_t sbase, uint32_t voff, uint32_t lds) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(lds)
-               : "memory");
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds)
+      : "memory");
 }
 
+// ABL: timing ablations (results wrong): 1 no DMA in the loop, 2 no fragment reads, 8 no flush
+template <int NS, int ABL = 0>
 __global__ __launch_bounds__(256, 1) void k_gram8s(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
                                                    float* __restrict__ part) {
-  __shared__ __attribute__((aligned(1024))) char ring[G8S_NSLOT * G8S_SLOT];
+  __shared__ __attribute__((aligned(1024))) char lds[NS * G8S_OPS + G8S_SCL];
 
   const int b = blockIdx.x;
   const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
@@ -1062,45 +1074,46 @@ __global__ __launch_bounds__(256, 1) void k_gram8s(Q8Plan q, SegTable st, int nt
   const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
   const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
   const int nb = (int)((r1 - r0 + Q8BLK - 1) / Q8BLK);  // whole (zero-filled) scale blocks
-  constexpr int PPB = Q8SPB / 2;                        // phases per scale block
-  const int nph = nb * PPB;
+  const int nstg = nb * Q8SPB;                          // even (Q8SPB = 24)
   const size_t gbase = (size_t)chunk * (st.chunk_rows / Q8K);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int l31 = lane & 31, h = lane >> 5;
-  // strictly-lower quadrant of a diagonal tile: loads and barriers, no MFMA
-  const bool skip = (ti == tj && wm > wn);
   const size_t gstride = (size_t)q.P8 * 32;  // bytes per 32-row group and plane
 
-  // DMA role of this wave: stage (wave >> 1) of a phase, operand (wave & 1) —
-  // 12 fragments (3 digits × 4 column blocks); the swizzle on the source:
-  // LDS slot 2r + h' holds column r, half h' ^ bit3(r)
-  const int sg_dma = wave >> 1, op_dma = wave & 1;
-  const size_t srcoff = (size_t)(lane >> 1) * 32 + 16 * ((lane & 1) ^ ((lane >> 4) & 1));
-  const char* dma_base = q.digits + (gbase + sg_dma) * gstride + (size_t)(op_dma ? J : I) * 32 + srcoff;
-  const uint32_t ring0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ring);
-  const float* scl_src = q.scale + (size_t)chunk * q.nblk * q.P8 + lane;
+  // DMA role: wave w copies operand (w >> 1), digit/column-block pairs
+  // 6(w & 1) .. +5 of the 12; the swizzle on the source: LDS slot 2r + h'
+  // holds column r, half h' ^ bit3(r)
+  const int op_dma = wave >> 1, part_dma = wave & 1;
+  const uint32_t srcoff = (uint32_t)(lane >> 1) * 32 + 16 * ((lane & 1) ^ ((lane >> 4) & 1));
+  const uint64_t dma_base = (uint64_t)(uintptr_t)q.digits + gbase * gstride + (uint64_t)(op_dma ? J : I) * 32;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds);
+  const uint64_t scl_base = (uint64_t)(uintptr_t)(q.scale + (size_t)chunk * q.nblk * q.P8);
   const int srow0 = I + wm * 64, scol0 = J + wn * 64;
+  char* const sclw = lds + NS * G8S_OPS + wave * 512;  // + (blk & 1) * 2048
 
-  auto issue = [&](int ph, int slot) __attribute__((always_inline)) {
-    const uint32_t sb = ring0 + slot * G8S_SLOT;
-    const size_t poff = (size_t)ph * 2 * gstride;
-#pragma unroll
-    for (int dg = 0; dg < 3; ++dg)
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-        g8s_dma16(dma_base + dg * q.plane + poff + x * G8S_FRAG,
-                  sb + (((sg_dma * 2 + op_dma) * 3 + dg) * 4 + x) * G8S_FRAG);
-    const size_t so = (size_t)(ph / PPB) * q.P8;
-    g8s_dma4(scl_src + so + srow0, sb + G8S_OPS + wave * 512);
-    g8s_dma4(scl_src + so + scol0, sb + G8S_OPS + wave * 512 + 256);
+  // DMA number i (< 8) of stage stg into its slot
+  auto dma = [&](int i, int stg) __attribute__((always_inline)) {
+    const int slot = stg % NS;
+    if (i < 6) {
+      const int f = 6 * part_dma + i, dg = f >> 2, x = f & 3;
+      g8s_dma16(dma_base + (uint64_t)stg * gstride + dg * q.plane + x * G8S_FRAG, srcoff,
+                lds0 + slot * G8S_OPS + ((op_dma * 3 + dg) * 4 + x) * G8S_FRAG);
+    } else {
+      const int blk = stg / Q8SPB;
+      const uint32_t sc = lds0 + NS * G8S_OPS + ((blk & 1) * 4 + wave) * 512 + (i - 6) * 256;
+      g8s_dma4(scl_base + ((uint64_t)blk * q.P8 + (i == 6 ? srow0 : scol0)) * 4, lane * 4, sc);
+    }
   };
   // fragment read: lane (r, h) ← 16 B at swizzled slot 2r + (h ^ bit3(r))
   const int rdoff = 16 * (2 * l31 + (h ^ ((l31 >> 3) & 1)));
-  auto frag = [&](int slot, int sg, int op, int dg, int xb) __attribute__((always_inline)) -> i32x4 {
-    return *reinterpret_cast<const i32x4*>(ring + slot * G8S_SLOT + (((sg * 2 + op) * 3 + dg) * 4 + xb) * G8S_FRAG +
+  // fragment j (< 12) of stage stg: A (x, dg) for j < 6, B for j ≥ 6
+  auto frag = [&](int j, int stg) __attribute__((always_inline)) -> i32x4 {
+    const int op = j / 6, x = (j % 6) / 3, dg = j % 3;
+    const int xb = 2 * (op ? wn : wm) + x;
+    return *reinterpret_cast<const i32x4*>(lds + (stg % NS) * G8S_OPS + ((op * 3 + dg) * 4 + xb) * G8S_FRAG +
                                            rdoff);
   };
 
@@ -1116,81 +1129,83 @@ __global__ __launch_bounds__(256, 1) void k_gram8s(Q8Plan q, SegTable st, int nt
 #pragma unroll
       for (int r = 0; r < 16; ++r) run[a][c][r] = 0.f;
     }
-
-  // timing ablations (OCM_GRAM8_NOLOAD bits): 1 no DMA, 2 no fragment reads, 4 no MFMA, 8 no flush
-  const int xflags = __builtin_amdgcn_readfirstlane(q.noload);
-  i32x4 F0 = frag(0, 0, 0, 0, 0);
-  if (!(xflags & 1)) {
-    issue(0, 0);
-    issue(min(1, nph - 1), 1);
-  }
-  for (int ph = 0; ph < nph; ++ph) {
-    const int slot = ph % G8S_NSLOT;
-    // this wave's DMAs of phase ph are done (those of ph+1, 14, may still fly);
-    // after the barrier every wave's are, and slot (ph+2)%3 is free
-    asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (!(xflags & 1)) issue(min(ph + 2, nph - 1), (ph + 2) % G8S_NSLOT);
-    if (!skip) {
+  // MFMA number i (< 24): sub-block (a, c) = i / 6, product i % 6
+  auto mfma = [&](int i, const i32x4 (&F)[12]) __attribute__((always_inline)) {
+    const int a = (i / 6) >> 1, c = (i / 6) & 1, k = i % 6;
+    const i32x4 A0 = F[a * 3 + 0], A1 = F[a * 3 + 1], A2 = F[a * 3 + 2];
+    const i32x4 B0 = F[6 + c * 3 + 0], B1 = F[6 + c * 3 + 1], B2 = F[6 + c * 3 + 2];
+    if (k == 0) acc1[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A0, B0, acc1[a][c], 0, 0, 0);
+    if (k == 1) acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A0, B1, acc2[a][c], 0, 0, 0);
+    if (k == 2) acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A1, B0, acc2[a][c], 0, 0, 0);
+    if (k == 3) acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A0, B2, acc3[a][c], 0, 0, 0);
+    if (k == 4) acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A2, B0, acc3[a][c], 0, 0, 0);
+    if (k == 5) acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A1, B1, acc3[a][c], 0, 0, 0);
+  };
+  auto flush = [&](int blk) __attribute__((always_inline)) {
+    constexpr float w2 = 1.f / 254.f, w3 = 1.f / (254.f * 254.f);
+    const float* scl = reinterpret_cast<const float*>(sclw + (blk & 1) * 2048);
 #pragma unroll
-      for (int sg = 0; sg < 2; ++sg) {
-        i32x4 FA[2][3], FB[2][3];
+    for (int c = 0; c < 2; ++c) {
+      const float sj = scl[64 + c * 32 + l31];
 #pragma unroll
-        for (int x = 0; x < 2; ++x)
+      for (int a = 0; a < 2; ++a) {
 #pragma unroll
-          for (int dg = 0; dg < 3; ++dg) {
-            FA[x][dg] = (xflags & 2) ? F0 + dg : frag(slot, sg, 0, dg, 2 * wm + x);
-            FB[x][dg] = (xflags & 2) ? F0 - x : frag(slot, sg, 1, dg, 2 * wn + x);
-          }
-        if (xflags & 4) {
+        for (int g = 0; g < 4; ++g) {
+          // rows of registers 4g..4g+3: a·32 + 8g + 4h + 0..3
+          const f32x4 si = *reinterpret_cast<const f32x4*>(&scl[a * 32 + 8 * g + 4 * h]);
 #pragma unroll
-          for (int x = 0; x < 2; ++x)
-#pragma unroll
-            for (int dg = 0; dg < 3; ++dg) acc1[x][dg & 1][dg] += FA[x][dg][0] ^ FB[x][dg][1];
-        } else
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            acc1[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a][0], FB[c][0], acc1[a][c], 0, 0, 0);
-            acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a][0], FB[c][1], acc2[a][c], 0, 0, 0);
-            acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a][1], FB[c][0], acc2[a][c], 0, 0, 0);
-            acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a][0], FB[c][2], acc3[a][c], 0, 0, 0);
-            acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a][2], FB[c][0], acc3[a][c], 0, 0, 0);
-            acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a][1], FB[c][1], acc3[a][c], 0, 0, 0);
-          }
-      }
-      if (ph % PPB == PPB - 1 && !(xflags & 8)) {
-        // scale-block flush: run += s_i s_j (A1 + A2/254 + A3/254²)
-        constexpr float w2 = 1.f / 254.f, w3 = 1.f / (254.f * 254.f);
-        const float* scl = reinterpret_cast<const float*>(ring + slot * G8S_SLOT + G8S_OPS + wave * 512);
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const float sj = scl[64 + c * 32 + l31];
-#pragma unroll
-          for (int a = 0; a < 2; ++a) {
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              // rows of registers 4g..4g+3: a·32 + 8g + 4h + 0..3
-              const f32x4 si = *reinterpret_cast<const f32x4*>(&scl[a * 32 + 8 * g + 4 * h]);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const int r = 4 * g + e;
-                const float v =
-                    fmaf((float)acc3[a][c][r], w3, fmaf((float)acc2[a][c][r], w2, (float)acc1[a][c][r]));
-                run[a][c][r] = fmaf(v, si[e] * sj, run[a][c][r]);
-              }
-            }
-            acc1[a][c] = i32x16{};
-            acc2[a][c] = i32x16{};
-            acc3[a][c] = i32x16{};
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g + e;
+            const float v = fmaf((float)acc3[a][c][r], w3, fmaf((float)acc2[a][c][r], w2, (float)acc1[a][c][r]));
+            run[a][c][r] = fmaf(v, si[e] * sj, run[a][c][r]);
           }
         }
+        acc1[a][c] = i32x16{};
+        acc2[a][c] = i32x16{};
+        acc3[a][c] = i32x16{};
       }
     }
+  };
+
+  // one iteration: barrier, then MFMAs of stage stg (fragments FC) with the
+  // DMA of stage stg+3 and the reads of stage stg+1 (into FN) between them
+  auto iter = [&](int stg, const i32x4 (&FC)[12], i32x4 (&FN)[12]) __attribute__((always_inline)) {
+    // own DMAs of stg+1 landed (those of stg+2, 8, may fly) and this wave's
+    // reads of slot stg%3 are done; after the barrier both hold for all waves
+    if constexpr ((ABL & 1) != 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (NS == 3) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (NS == 4) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (NS == 5) asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (NS == 6) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int sd = min(stg + NS, nstg - 1);  // clamped: a duplicate into a dead slot
+    const int sr = min(stg + 1, nstg - 1);
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      mfma(i, FC);
+      if (i < 8 && !(ABL & 1)) dma(i, sd);
+      if (i >= 8 && i < 20 && !(ABL & 2)) FN[i - 8] = frag(i - 8, sr);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (!(ABL & 8) && stg % Q8SPB == Q8SPB - 1) flush(stg / Q8SPB);
+  };
+
+  i32x4 FX[12], FY[12];
+#pragma unroll
+  for (int t = 0; t < NS; ++t)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma(i, min(t, nstg - 1));
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // prologue: everything landed
+#pragma unroll
+  for (int j = 0; j < 12; ++j) FX[j] = frag(j, 0);
+  for (int stg = 0; stg < nstg; stg += 2) {
+    iter(stg, FX, FY);
+    iter(stg + 1, FY, FX);
   }
   // no LDS-DMA may still be landing when the workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (skip) return;
+  // strictly-lower quadrant of a diagonal tile: computed (branch-free: a
+  // uniform skip duplicates live ranges) but not written
+  if (ti == tj && wm > wn) return;
   float* out = part + ((size_t)chunk * ntiles + tile) * (Q8T * Q8T);
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -1397,9 +1412,21 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
       // "direct" (default: k_gram8d, register fragments, no LDS stage) or "shared" (k_gram8s, LDS panels)
       const char* v = std::getenv("OCM_GRAM8_VARIANT");
       const std::string var = v ? v : "";
-      if (var == "shared")
-        hipLaunchKernelGGL(k_gram8s, dim3((unsigned)total), dim3(256), 0, st, q, tab, nt, ntiles, (int)total, pg);
-      else
+      if (var.rfind("shared", 0) == 0) {
+        // shared[N]: N-slot LDS ring (default 4); OCM_GRAM8_NOLOAD = timing ablations (wrong G)
+        const int ns = var.size() > 6 ? std::atoi(var.c_str() + 6) : 4;
+        const dim3 g8((unsigned)total), b8(256);
+#define OCM_G8S(N_, A_) hipLaunchKernelGGL((k_gram8s<N_, A_>), g8, b8, 0, st, q, tab, nt, ntiles, (int)total, pg)
+        if (q.noload == 1) OCM_G8S(4, 1);
+        else if (q.noload == 2) OCM_G8S(4, 2);
+        else if (q.noload == 8) OCM_G8S(4, 8);
+        else if (q.noload == 9) OCM_G8S(4, 9);
+        else if (ns == 3) OCM_G8S(3, 0);
+        else if (ns == 5) OCM_G8S(5, 0);
+        else if (ns == 6) OCM_G8S(6, 0);
+        else OCM_G8S(4, 0);
+#undef OCM_G8S
+      } else
         hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tab, nt, ntiles, (int)total, pg);
       OCM_CHECK_LAUNCH("k_gram8");
     }

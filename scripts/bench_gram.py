@@ -36,8 +36,8 @@ def main():
     for r in range(args.rounds):
         for mode, name, chunk in variants:
             os.environ["OCM_GRAM_MODE"] = "bf16x3" if mode.startswith("bf16x3") else mode[:4] if mode.startswith("i8x3") else mode
-            # i8x3 kernel variants: i8x3 (default) | i8x3d (direct) | i8x3s (shared LDS) | i8x3l (LDS ring)
-            var = {"i8x3d": "direct", "i8x3s": "shared", "i8x3l": "lds"}.get(mode)
+            # i8x3 kernel variants: i8x3 (default) | i8x3d (direct) | i8x3s[N] (shared LDS, N-slot ring)
+            var = {"i8x3d": "direct"}.get(mode) or ("shared" + mode[5:] if mode.startswith("i8x3s") else None)
             if var:
                 os.environ["OCM_GRAM8_VARIANT"] = var
             else:

@@ -4,6 +4,6 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 OCM_GRAM8_VARIANT=shared timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "gram" > gpurun_out/g8s_tests.log 2>&1
 rc=$?; tail -5 gpurun_out/g8s_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python scripts/bench_gram.py --rounds 3 --variants i8x3d:128x32:4096,i8x3s:128x32:4096,i8x3s:128x32:2048 > gpurun_out/g8s_bench.log 2>&1 || { echo "bench_gram failed"; tail -20 gpurun_out/g8s_bench.log; exit 3; }
+timeout -k 10 300 python scripts/bench_gram.py --rounds 3 --variants ${VARIANTS:-i8x3d:128x32:4096,i8x3s:128x32:4096,i8x3s:128x32:9216} > gpurun_out/g8s_bench.log 2>&1 || { echo "bench_gram failed"; tail -20 gpurun_out/g8s_bench.log; exit 3; }
 grep -v amdgpu.ids gpurun_out/g8s_bench.log
 echo done
