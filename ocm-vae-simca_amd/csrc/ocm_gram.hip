@@ -637,7 +637,7 @@ __global__ __launch_bounds__(256) void k_gram_small_reduce(const double* __restr
 // ---------------------------------------------------------------------------
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
-constexpr int Q8T = 128, Q8K = 32, Q8BLK = 768, Q8SPB = Q8BLK / Q8K;
+constexpr int Q8T = 128, Q8K = 32, Q8BLK = 1536, Q8SPB = Q8BLK / Q8K;
 constexpr float Q8BASE = 254.f;
 
 struct Q8Plan {
@@ -673,10 +673,10 @@ __device__ __forceinline__ int q8_qslot(int P) { return P ^ ((P >> 3) & 7); }
 // pieces are staged through LDS (one digit plane, 24 KiB, at a time) so that
 // the stores leave as contiguous 1-KiB runs (one 32-row group × 32 columns).
 constexpr int Q8QC = 32;                   // columns per quantiser workgroup
-constexpr int Q8QS = Q8BLK / 16;           // 16-row slices per block (48)
-constexpr int Q8QT = Q8QS * (Q8QC / 4);    // threads (384)
+constexpr int Q8QS = Q8BLK / 16;           // 16-row slices per block (96)
+constexpr int Q8QT = Q8QS * (Q8QC / 4);    // threads (768)
 template <bool GATHER>
-__global__ __launch_bounds__(Q8QT, 2) void k_q8_quant(const float* __restrict__ X, int64_t ldx,
+__global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ X, int64_t ldx,
                                                       const int64_t* __restrict__ rows, int p,
                                                       const float* __restrict__ shift, SegTable st, Q8Plan q,
                                                       double* __restrict__ colblk) {
@@ -894,14 +894,16 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
       FB[x_][dg_] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(rb[dg_], voff + x_ * 1024, so_, 0); \
     }                                                                                               \
   } while (0)
-#define Q8D_MFMA(FA, FB)                                                                              \
+// Z: first stage of a scale block — each accumulator's first product starts
+// from an inline zero (no separate reset after the flush)
+#define Q8D_MFMA(FA, FB, Z)                                                                           \
   do {                                                                                              \
     _Pragma("unroll") for (int a_ = 0; a_ < 2; ++a_)                                                \
     _Pragma("unroll") for (int c_ = 0; c_ < 2; ++c_) {                                              \
-      acc1[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[c_][0], acc1[a_][c_], 0, 0, 0); \
-      acc2[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[c_][1], acc2[a_][c_], 0, 0, 0); \
+      acc1[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[c_][0], (Z) ? i32x16{} : acc1[a_][c_], 0, 0, 0); \
+      acc2[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[c_][1], (Z) ? i32x16{} : acc2[a_][c_], 0, 0, 0); \
       acc2[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][1], FB[c_][0], acc2[a_][c_], 0, 0, 0); \
-      acc3[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[c_][2], acc3[a_][c_], 0, 0, 0); \
+      acc3[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][0], FB[c_][2], (Z) ? i32x16{} : acc3[a_][c_], 0, 0, 0); \
       acc3[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][2], FB[c_][0], acc3[a_][c_], 0, 0, 0); \
       acc3[a_][c_] = __builtin_amdgcn_mfma_i32_32x32x32_i8(FA[a_][1], FB[c_][1], acc3[a_][c_], 0, 0, 0); \
     }                                                                                               \
@@ -943,9 +945,6 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
           }
           *rp = rv;
         }
-        acc1[a][c] = i32x16{};
-        acc2[a][c] = i32x16{};
-        acc3[a][c] = i32x16{};
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -954,14 +953,14 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
 #define Q8D_S0 F0A, F0B, F2A, F2B
 #define Q8D_S1 F1A, F1B, F0A, F0B
 #define Q8D_S2 F2A, F2B, F1A, F1B
-#define Q8D_STEP_(STG, CA, CB, NA, NB)                                                                \
+#define Q8D_STEP_(STG, Z, CA, CB, NA, NB)                                                             \
   do {                                                                                              \
     Q8D_LOAD(NA, NB, min((STG) + 2, nstage3 - 1));                                                  \
     __builtin_amdgcn_sched_barrier(0);                                                              \
-    if (!(xflags & 4)) Q8D_MFMA(CA, CB);                                                            \
+    if (!(xflags & 4)) Q8D_MFMA(CA, CB, Z);                                                         \
     __builtin_amdgcn_sched_barrier(0);                                                              \
   } while (0)
-#define Q8D_STEP(STG, ...) Q8D_STEP_(STG, __VA_ARGS__)
+#define Q8D_STEP(STG, Z, ...) Q8D_STEP_(STG, Z, __VA_ARGS__)
 
   i32x4 F0A[2][3], F0B[2][3], F1A[2][3], F1B[2][3], F2A[2][3], F2B[2][3];
   Q8D_LOAD(F0A, F0B, 0);
@@ -973,13 +972,13 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
     const int s0 = blk * Q8SPB;
 #pragma unroll
     for (int u = 0; u < Q8SPB; u += 3) {
-      Q8D_STEP(s0 + u, Q8D_S0);
-      Q8D_STEP(s0 + u + 1, Q8D_S1);
+      Q8D_STEP(s0 + u, u == 0, Q8D_S0);
+      Q8D_STEP(s0 + u + 1, false, Q8D_S1);
       if (u == 0) {
         SR = srow[(size_t)blk * q.P8];
         SC = scol[(size_t)blk * q.P8];
       }
-      Q8D_STEP(s0 + u + 2, Q8D_S2);
+      Q8D_STEP(s0 + u + 2, false, Q8D_S2);
     }
     if (!(xflags & 8)) flush();
   }

@@ -210,7 +210,7 @@ def test_rowsq_residual_broadcast_and_strided(eng):
 
 @pytest.mark.parametrize("n,p", [(9000, 257), (300, 2048)])
 def test_gram_i8_digit_split_edge_cases(eng, monkeypatch, n, p):
-    """i8x3 fixed-point split: per-(768-row block, column) power-of-two scales
+    """i8x3 fixed-point split: per-(1536-row block, column) power-of-two scales
     must cope with zero / constant columns, a far-off shift, a single huge
     outlier row (it sets its block's scale), ragged chunk/block tails and
     p not a multiple of the 128 tile."""
