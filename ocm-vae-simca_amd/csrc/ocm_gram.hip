@@ -665,7 +665,7 @@ __device__ __forceinline__ uint32_t q8_pack4(float a0, float a1, float a2, float
 // bank groups per ds_write_b128 / ds_read_b128 lane group.
 __device__ __forceinline__ int q8_qslot(int P) { return P ^ ((P >> 3) & 7); }
 
-// grid (chunk · nblk + block, P8 / 32), 384 threads (6 waves): one 768-row
+// grid (chunk · nblk + block, P8 / 32), 768 threads (12 waves): one 1536-row
 // scale block × 32 columns.  Thread t owns column quad cq = t & 7 (columns
 // 4cq .. 4cq+3: a wave instruction reads 8 rows × 128 B) and row slice
 // rs = t >> 3 (rows 16rs .. 16rs+15 = half rs&1 of 32-row group rs>>1), so
@@ -1459,7 +1459,8 @@ int ocm_colmean_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* ro
   OCM_REQUIRE(ctx && X && mean_out, "ocm_colmean_f32: NULL argument");
   OCM_REQUIRE(n > 0 && p > 0 && ldx >= p, "ocm_colmean_f32: bad shape");
   hipStream_t st = (hipStream_t)stream;
-  const int64_t per = 256;
+  // short row splits: the shift sample (4096 rows) spreads over ≥ 1024 workgroups
+  const int64_t per = 32;
   const int nsplit = (int)std::min<int64_t>((n + per - 1) / per, 4096);
   const int64_t rps = (n + nsplit - 1) / nsplit;
   auto* part = static_cast<double*>(ocm::workspace(ctx, (size_t)nsplit * p * sizeof(double), st));

@@ -106,8 +106,8 @@ class ShardedSIMCA:
         self.fit_ = fit = engine.fit_class(X_local, rows, n_local, k, limits.theta_mode_for(self), want_T=False,
                                            allreduce=ar)
         n = fit.n
-        T2m = limits.Moments(n, *fit.T2_stats, lambda pct: percentile_sharded(fit.T2, pct, n, self.group))
-        Qm = limits.Moments(n, *fit.Q_stats, lambda pct: percentile_sharded(fit.Q, pct, n, self.group))
+        T2m = limits.Moments(n, lambda: fit.T2_stats, None, lambda pct: percentile_sharded(fit.T2, pct, n, self.group))
+        Qm = limits.Moments(n, lambda: fit.Q_stats, None, lambda pct: percentile_sharded(fit.Q, pct, n, self.group))
         self.T2_limit = limits.t2_limit(self, T2m, k)
         self.Q_limit = limits.q_limit(self, Qm, fit.thetas)
         self.D_limit = limits.critic_distance(self, self.T2_limit, self.Q_limit, fit.thetas, k)

@@ -69,11 +69,28 @@ class ClassFit:
     T: torch.Tensor | None = None
     T2: torch.Tensor | None = None
     Q: torch.Tensor | None = None
-    T2_stats: tuple = (0.0, 0.0)
-    Q_stats: tuple = (0.0, 0.0)
+    stats_dev: torch.Tensor | None = None  # (4,) f64 on the device: ΣT², Σ(T²)², ΣQ, ΣQ² (all ranks)
     eig_iters: int = 0
     C: torch.Tensor | None = None
     extra: dict = field(default_factory=dict)
+
+    def _stats(self) -> np.ndarray:
+        # read on first use only: nothing on the Fdist / jm path waits for the
+        # fit-set scoring kernel (its launch returns at once)
+        if "stats_host" not in self.extra:
+            self.extra["stats_host"] = (self.stats_dev.cpu().numpy() if self.stats_dev is not None
+                                        else np.zeros(4))
+        return self.extra["stats_host"]
+
+    @property
+    def T2_stats(self) -> tuple:
+        s = self._stats()
+        return (float(s[0]), float(s[1]))
+
+    @property
+    def Q_stats(self) -> tuple:
+        s = self._stats()
+        return (float(s[2]), float(s[3]))
 
 
 def _stream(dev):
@@ -314,18 +331,18 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
     C, mean64 = cov_from_gram([(1.0, G[0], cs[0])], shift32, n_total)
     del G
     evals, evecs, theta, iters = eig_topk(C, k, theta_mode)
-    invcov = invcov_from_evals(evals)
-    sc = score(X, rows, n, evecs, mean64, invcov, want_T=want_T, want_stats=True)
-    host = torch.cat([evals, theta, sc["stats"]]).cpu().numpy()
+    # the host scalars of the eigensolve are read BEFORE the fit-set scoring is
+    # launched, so the limits (host SciPy) overlap that kernel
+    host = torch.cat([evals, theta]).cpu().numpy()
     ev_h = host[:k]
     th = tuple(float(v) for v in host[k:k + 3])
-    stats = host[k + 3:]
+    invcov = invcov_from_evals(evals)
+    sc = score(X, rows, n, evecs, mean64, invcov, want_T=want_T, want_stats=True)
+    stats = sc["stats"]
     if allreduce is not None:
-        stt = torch.tensor(stats, dtype=torch.float64, device=X.device)
-        allreduce([stt])
-        stats = stt.cpu().numpy()
-    fit = ClassFit(k=k, n=n_total, p=p, mean64=mean64, evals=evals, P64=evecs, invcov=invcov, thetas=th, evals_host=ev_h, T=sc["T"], T2=sc["T2"], Q=sc["Q"],
-                   T2_stats=(stats[0], stats[1]), Q_stats=(stats[2], stats[3]), eig_iters=iters,
+        allreduce([stats])  # stream-ordered: no host wait
+    fit = ClassFit(k=k, n=n_total, p=p, mean64=mean64, evals=evals, P64=evecs, invcov=invcov, thetas=th,
+                   evals_host=ev_h, T=sc["T"], T2=sc["T2"], Q=sc["Q"], stats_dev=stats, eig_iters=iters,
                    C=C if keep_C else None)
     fit.extra["shift32"] = shift32
     return fit

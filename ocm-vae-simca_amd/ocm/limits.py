@@ -16,13 +16,32 @@ from scipy.special import erfinv
 
 class Moments:
     """n, Σx, Σx² of a device vector (from the scoring kernel's fused stats)
-    plus a lazy percentile callback (device radix select)."""
+    plus a lazy percentile callback (device radix select).  ``s1`` may be a
+    callable returning (Σx, Σx²): the sums are then read from the device only
+    if a limit needs them (chi2pom / moments), so the Fdist / jm path never
+    waits for the fit-set scoring kernel."""
 
-    def __init__(self, n, s1, s2, percentile):
+    def __init__(self, n, s1, s2=None, percentile=None):
         self.n = int(n)
-        self.s1 = float(s1)
-        self.s2 = float(s2)
+        if callable(s1):
+            self._sums, self._s = s1, None
+        else:
+            self._sums, self._s = None, (float(s1), float(s2))
         self._pct = percentile
+
+    def _get(self):
+        if self._s is None:
+            a, b = self._sums()
+            self._s = (float(a), float(b))
+        return self._s
+
+    @property
+    def s1(self) -> float:
+        return self._get()[0]
+
+    @property
+    def s2(self) -> float:
+        return self._get()[1]
 
     @property
     def mean(self) -> float:

@@ -161,8 +161,8 @@ class SIMCA(BaseEstimator, ClassifierMixin):
     def _fit_one_class(self, Xd, rows, n, k):
         """utils/SIMCA.py:62-99 on the device."""
         fit = engine.fit_class(Xd, rows, n, k, limits.theta_mode_for(self), want_T=True, keep_C=True)
-        T2m = limits.Moments(n, *fit.T2_stats, lambda pct: engine.percentile(fit.T2, pct))
-        Qm = limits.Moments(n, *fit.Q_stats, lambda pct: engine.percentile(fit.Q, pct))
+        T2m = limits.Moments(n, lambda: fit.T2_stats, None, lambda pct: engine.percentile(fit.T2, pct))
+        Qm = limits.Moments(n, lambda: fit.Q_stats, None, lambda pct: engine.percentile(fit.Q, pct))
         T2_limit = limits.t2_limit(self, T2m, k)
         Q_limit = limits.q_limit(self, Qm, fit.thetas)
         D_limit = limits.critic_distance(self, T2_limit, Q_limit, fit.thetas, k)
