@@ -807,13 +807,27 @@ __global__ __launch_bounds__(256, 2) void k_score_f64(const float* __restrict__ 
   }
 }
 
-__global__ void k_stats_reduce(const double* __restrict__ part, int64_t nblk, double* __restrict__ out) {
-  // 4 waves, wave w sums column w in a fixed order (deterministic)
+__global__ __launch_bounds__(1024) void k_stats_reduce(const double* __restrict__ part, int64_t nblk,
+                                                       double* __restrict__ out) {
+  // 16 waves: wave w sums column w & 3 over row slice w >> 2 (4 slices), four
+  // independent accumulators per lane; slices combined in a fixed order
+  // (deterministic)
+  __shared__ double red[16];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  double v = 0.0;
-  for (int64_t i = lane; i < nblk; i += 64) v += part[i * 4 + w];
-  v = wave_sum_f64(v);
-  if (lane == 0) out[w] = v;
+  const int col = w & 3, sl = w >> 2;
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+  int64_t i = (int64_t)sl * 64 + lane;
+  for (; i + 3 * 256 < nblk; i += 4 * 256) {
+    v0 += part[i * 4 + col];
+    v1 += part[(i + 256) * 4 + col];
+    v2 += part[(i + 512) * 4 + col];
+    v3 += part[(i + 768) * 4 + col];
+  }
+  for (; i < nblk; i += 256) v0 += part[i * 4 + col];
+  double v = wave_sum_f64((v0 + v1) + (v2 + v3));
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  if (threadIdx.x < 4) out[threadIdx.x] = (red[threadIdx.x] + red[4 + threadIdx.x]) + (red[8 + threadIdx.x] + red[12 + threadIdx.x]);
 }
 
 __global__ void k_decide(const double* __restrict__ T2, const float* __restrict__ Q, int64_t m, DecArgs dec,
@@ -940,7 +954,7 @@ int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
   }
   OCM_CHECK_LAUNCH("k_score");
   if (stats_out) {
-    hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(256), 0, st, part, nblk, stats_out);
+    hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, st, part, nblk, stats_out);
     OCM_CHECK_LAUNCH("k_stats_reduce");
   }
   return OCM_OK;
