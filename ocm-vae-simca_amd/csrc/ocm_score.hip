@@ -9,8 +9,6 @@
 //   k_score_direct (default)  f32 MFMA, each wave streams its 32 rows from
 //       HBM straight into operand registers; loadings/mean in LDS blocks.
 //   k_score                   f32 MFMA, row tiles staged through LDS.
-//   k_score_coop              f32 MFMA, 4 waves split one 32-row tile by
-//       columns (OCM_SCORE_VARIANT=coop; measured slower: 4.4 vs 3.5 ms).
 //   k_score_f64               one pass, f64 MFMA, Q = ‖d‖² − ‖t‖².
 // The f32 kernels run two sweeps over the row's columns:
 //   sweep 1  Tᵀ (comps × rows) += P_chunk · D_chunkᵀ        v_mfma_f32_32x32x2_f32
@@ -442,210 +440,6 @@ __global__ __launch_bounds__(256, 2) void k_score_direct(const float* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// k_score_coop — the four waves of a workgroup share ONE 32-row tile and
-// split its wavelengths (wave w: columns [w·pq, (w+1)·pq), pq = p/4 rounded
-// up to 32).  Same math and MFMA layouts as k_score_direct (sweep 1
-// Tᵀ = P·Dᵀ, sweep 2 Rᵀ = Pᵀ·Tᵀ with the explicit residual), but:
-//   * the per-wave partial T (f32 over the wave's quarter) is summed in f64
-//     across the four waves through LDS — every wave then holds the full t;
-//   * the sweep-2 re-read of a row quarter follows its sweep-1 read by a
-//     quarter of a row's MFMA time and the workgroup's whole tile is 256 KiB,
-//     so the re-read is served on-die (Infinity Cache) instead of HBM;
-//   * loadings and mean are read from global memory (L2-resident: 160 KiB
-//     at k = 20, p = 2048), comps ≥ k as zero operands, no LDS staging and no
-//     barrier inside the sweeps.
-// k ≤ 32 (one 32-component MFMA tile).
-// ---------------------------------------------------------------------------
-template <int KT_UNUSED, bool VEC>
-__global__ __launch_bounds__(256, 2) void k_score_coop(const float* __restrict__ X, int64_t ldx,
-                                                       const int64_t* __restrict__ rows, int64_t m, int p,
-                                                       const float* __restrict__ P, const float* __restrict__ mu,
-                                                       const double* __restrict__ A, int k, int a_diag,
-                                                       float* __restrict__ T_out, double* __restrict__ T2_out,
-                                                       float* __restrict__ Q_out, DecArgs dec,
-                                                       double* __restrict__ acc_out, int64_t acc_stride,
-                                                       double* __restrict__ stat_part) {
-  __shared__ float tpart[4][16][64];   // per-wave partial T (MFMA accumulator layout)
-  __shared__ double tfull[32][33];     // full t per row (f64), for the epilogue
-  __shared__ double qpart[4][32];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l31 = lane & 31, h = lane >> 5;
-  const int64_t row0 = (int64_t)blockIdx.x * 32;
-  const int64_t grow = row0 + l31;
-  const float rowmask = grow < m ? 1.f : 0.f;
-  const int64_t gcl = grow < m ? grow : m - 1;
-  const float* xrow = X + (rows ? rows[gcl] : gcl) * ldx;
-  const int pq = ((p + 127) / 128) * 32;
-  const int cbeg = wave * pq, cend = min(cbeg + pq, p);
-  // this lane's loadings row in sweep 1 (A operand: component = l31)
-  const float pmask = l31 < k ? 1.f : 0.f;
-  const float* prow = P + (int64_t)min(l31, k - 1) * p;
-
-  auto ld4 = [&](const float* base, int col) -> f32x4 {
-    if (VEC) return *reinterpret_cast<const f32x4*>(base + (col < p ? col : 0));
-    f32x4 v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = base[min(col + e, p - 1)];
-    return v;
-  };
-  auto cmask = [&](int col, int e) -> float { return col + e < p ? 1.f : 0.f; };
-
-  // ---- sweep 1: partial Tᵀ over this wave's columns -------------------------
-  struct S1 {
-    f32x4 d[4], u[4], w[4];
-  };
-  auto load1 = [&](S1& S, int c0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int col = c0 + 8 * i + 4 * h;
-      S.d[i] = ld4(xrow, col);
-      S.u[i] = ld4(mu, col);
-      S.w[i] = ld4(prow, col);
-    }
-  };
-  f32x16 accT;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) accT[r] = 0.f;
-  auto comp1 = [&](const S1& S, int c0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int col = c0 + 8 * i + 4 * h;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float m_ = rowmask * cmask(col, e);
-        const float b = (S.d[i][e] - S.u[i][e]) * m_;
-        accT = __builtin_amdgcn_mfma_f32_32x32x2f32(S.w[i][e] * pmask, b, accT, 0, 0, 0);
-      }
-    }
-  };
-  if (cbeg < cend) {
-    S1 SA, SB;
-    load1(SA, cbeg);
-    for (int c0 = cbeg; c0 < cend; c0 += 64) {
-      if (c0 + 32 < cend) load1(SB, c0 + 32);
-      comp1(SA, c0);
-      if (c0 + 64 < cend) load1(SA, c0 + 64);
-      if (c0 + 32 < cend) comp1(SB, c0 + 32);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) tpart[wave][r][lane] = accT[r];
-  __syncthreads();
-  double t64[16];
-  f32x16 tf;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    t64[r] = ((double)tpart[0][r][lane] + (double)tpart[1][r][lane]) +
-             ((double)tpart[2][r][lane] + (double)tpart[3][r][lane]);
-    tf[r] = (float)t64[r];
-  }
-
-  // ---- sweep 2: Rᵀ = Pᵀ·Tᵀ per 32-column chunk, Q = Σ (d − R)² --------------
-  // step r consumes comps κ_r + 4h (κ_r = (r&3) + 8(r>>2)); trailing steps that
-  // hold only zero loadings are skipped
-  const int nsteps = k > 24 ? 16 : (k > 16 ? 12 : (k > 8 ? 8 : 4));
-  struct S2 {
-    f32x4 d[4], u[4];
-    float w[16];
-  };
-  auto load2 = [&](S2& S, int c0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int col = c0 + 8 * i + 4 * h;
-      S.d[i] = ld4(xrow, col);
-      S.u[i] = ld4(mu, col);
-    }
-    const int lc = min(c0 + l31, p - 1);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      if (r >= nsteps) break;
-      const int comp = (r & 3) + 8 * (r >> 2) + 4 * h;
-      S.w[r] = comp < k ? P[(int64_t)comp * p + lc] : 0.f;
-    }
-  };
-  double q64 = 0.0;
-  auto comp2 = [&](const S2& S, int c0) {
-    f32x16 accR;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) accR[r] = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      if (r >= nsteps) break;
-      accR = __builtin_amdgcn_mfma_f32_32x32x2f32(S.w[r], tf[r], accR, 0, 0, 0);
-    }
-    float qc = 0.f;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      // accR register 4g+e holds column 8g + 4h + e of the chunk (row lane&31)
-      const int col = c0 + 8 * g + 4 * h;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float r_ = ((S.d[g][e] - S.u[g][e]) - accR[4 * g + e]) * cmask(col, e);
-        qc += r_ * r_;
-      }
-    }
-    q64 += (double)(qc * rowmask);
-  };
-  if (cbeg < cend) {
-    S2 SA, SB;
-    load2(SA, cbeg);
-    for (int c0 = cbeg; c0 < cend; c0 += 64) {
-      if (c0 + 32 < cend) load2(SB, c0 + 32);
-      comp2(SA, c0);
-      if (c0 + 64 < cend) load2(SA, c0 + 64);
-      if (c0 + 32 < cend) comp2(SB, c0 + 32);
-    }
-  }
-  q64 += __shfl_xor(q64, 32, 64);
-  if (h == 0) qpart[wave][l31] = q64;
-  if (wave == 0) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tfull[l31][(r & 3) + 8 * (r >> 2) + 4 * h] = t64[r];
-  }
-  __syncthreads();
-
-  // ---- epilogue (wave 0, lanes 0..31: one row each) --------------------------
-  if (wave != 0) return;
-  const bool own = (h == 0) && (grow < m);
-  double T2 = 0.0;
-  const double Q = (qpart[0][l31] + qpart[1][l31]) + (qpart[2][l31] + qpart[3][l31]);
-  if (own) {
-    const double* trow = tfull[l31];
-    if (a_diag) {
-      for (int a = 0; a < k; ++a) T2 += trow[a] * trow[a] * A[a * k + a];
-    } else {
-      for (int a = 0; a < k; ++a) {
-        double s_ = 0.0;
-        for (int b = 0; b < k; ++b) s_ += A[a * k + b] * trow[b];
-        T2 += trow[a] * s_;
-      }
-    }
-    if (T_out)
-      for (int a = 0; a < k; ++a) T_out[grow * k + a] = (float)trow[a];
-    if (T2_out) T2_out[grow] = T2;
-    if (Q_out) Q_out[grow] = (float)Q;
-    if (dec.enabled) {
-      const double dr = dred_of(dec.type, T2 * dec.t2_scale, (double)(float)Q * dec.q_scale);
-      acc_out[grow * acc_stride] = dr < dec.dlim ? 1.0 : 0.0;
-    }
-  }
-  if (stat_part) {
-    const double qf = (double)(float)Q;
-    double s0 = own ? T2 : 0.0, s1 = own ? T2 * T2 : 0.0, s2 = own ? qf : 0.0, s3 = own ? qf * qf : 0.0;
-    s0 = wave_sum_f64(s0);
-    s1 = wave_sum_f64(s1);
-    s2 = wave_sum_f64(s2);
-    s3 = wave_sum_f64(s3);
-    if (lane == 0) {
-      stat_part[(int64_t)blockIdx.x * 4 + 0] = s0;
-      stat_part[(int64_t)blockIdx.x * 4 + 1] = s1;
-      stat_part[(int64_t)blockIdx.x * 4 + 2] = s2;
-      stat_part[(int64_t)blockIdx.x * 4 + 3] = s3;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // k_score_f64 — single-pass scoring on FP64 MFMA (v_mfma_f64_16x16x4_f64).
 // d = (double)x − μ is exact; t = P·d accumulates in f64 (≈1e-15 relative),
 // so the orthogonal distance can use the norm identity Q = ‖d‖² − ‖t‖²
@@ -888,10 +682,9 @@ int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
   int variant = 1;
   if (const char* e = std::getenv("OCM_SCORE_VARIANT")) {
     const std::string v(e);
-    variant = v == "f64" ? 0 : (v == "lds" ? 2 : (v == "coop" ? 3 : 1));
+    variant = v == "f64" ? 0 : (v == "lds" ? 2 : 1);
   }
-  if (variant == 3 && k > 32) variant = 1;  // k_score_coop: one 32-component tile
-  const int64_t rows_per_blk = variant == 0 ? (int64_t)SW * FR : (variant == 3 ? 32 : (int64_t)SROWS);
+  const int64_t rows_per_blk = variant == 0 ? (int64_t)SW * FR : (int64_t)SROWS;
   const int64_t nblk = (m + rows_per_blk - 1) / rows_per_blk;
   OCM_REQUIRE(nblk < (1LL << 31), "ocm_score_f32: too many rows");
   const size_t part_bytes = stats_out ? (size_t)nblk * 4 * sizeof(double) : 0;
@@ -942,8 +735,7 @@ int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
       } else {
         OCM_SCORE_KT(k_score_f64, 3, 4, k <= 48, P, mu)
       }
-    } else if (variant == 3) {
-      OCM_SCORE_KT(k_score_coop, 1, 1, true, P32, mu32)
+
     } else if (variant == 1) {
       OCM_SCORE_KT(k_score_direct, 1, 2, k <= 32, P32, mu32)
     } else {
