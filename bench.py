@@ -3,7 +3,8 @@
 
 One step = the full SIMCA hot path on the synthetic 1M×2048 fp32 batch each
 rank holds in HBM, k = 20, type 'alt', t2lim 'Fdist', qlim 'jm' (the driver
-defaults, simca_nuts.py:186): shifted Gram (FP32 MFMA) → [RCCL all-reduce of
+defaults, simca_nuts.py:186): int8-digit quantiser + shifted Gram on integer
+MFMA (i8×3) → [RCCL all-reduce of
 Gram/colsum/n when N > 1] → covariance → top-20 eigenpairs + θ1..θ3 →
 fit-set scoring (T², Q, moments) → limits → predict (fused decision) on the
 same rows.  value = rows of all ranks / max-over-ranks step time
@@ -12,7 +13,7 @@ same rows.  value = rows of all ranks / max-over-ranks step time
     python bench.py [--gpus N --steps K --warmup W --rows R --no-cpu]
 
 Prints ONE JSON line (rank 0).  The `roofline` object is for the dominant
-kernel, k_gram: algorithmic FLOP per launch = rows × p(p+1) (symmetric Gram)
+kernel, k_gram8d: algorithmic FLOP per launch = rows × p(p+1) (symmetric Gram)
 ÷ its mean duration, timed live with HIP events around every launch in the
 timed region.  `cpu_baseline` times the oracle's reference-precision path
 (float32 full SVD + randomized PCA(k) + NumPy scoring) on a bounded row

@@ -72,9 +72,9 @@ int ocm_ctx_reserve(ocm_ctx* ctx, size_t bytes);
  * ocm_ctx_read_timing waits for the recorded events, returns the summed
  * duration (ms) and launch count of kernel `kernel_id`, and clears them. */
 #define OCM_TIMED_KERNELS 3
-#define OCM_KERNEL_GRAM 0  /* the Gram main kernel (k_gram8 / k_gram3 / k_gram) */
+#define OCM_KERNEL_GRAM 0  /* the Gram main kernel (k_gram8d / k_gram8s / k_gram3 / k_gram) */
 #define OCM_KERNEL_SCORE 1 /* k_score: fused projection / Q / T² kernel */
-#define OCM_KERNEL_QUANT 2 /* k_q8_quant: int8 digit split feeding k_gram8 */
+#define OCM_KERNEL_QUANT 2 /* k_q8_quant: int8 digit split feeding k_gram8d */
 int ocm_ctx_set_timing(ocm_ctx* ctx, int enable);
 int ocm_ctx_read_timing(ocm_ctx* ctx, int kernel_id, double* total_ms, int64_t* count);
 
@@ -86,10 +86,10 @@ int ocm_colmean_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* ro
                     double* mean_out, void* stream);
 
 /* Per-segment shifted Gram.  Default (OCM_GRAM_MODE=i8x3): y = x − shift is
- * split into three int8 digits per value (power-of-two scale per 256-row
+ * split into three int8 digits per value (power-of-two scale per 1536-row
  * block and column) and the six digit products of weight ≥ 254⁻² are summed
  * exactly in int32 on integer MFMA (fp32-grade Gram: max relative error
- * ≈ 2.4e-8 on the bench data); OCM_GRAM_MODE=bf16x3 / f32 select the bf16
+ * ≈ 5e-8 on the bench data); OCM_GRAM_MODE=bf16x3 / f32 select the bf16
  * split / FP32-MFMA kernels.  Workspace: ≈ 3 B per value for the digit planes
  * plus the chunk partials (≈ 8.4 GB at 1M × 2048).
  * Replaces the SVD of the centred class matrix (utils/SIMCA.py:64-66 ->
