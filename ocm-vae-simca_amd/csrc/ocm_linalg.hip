@@ -441,45 +441,45 @@ __global__ __launch_bounds__(256) void k_jacobi_blk(const double* __restrict__ A
 // One-workgroup Cholesky S = L Lᵀ (b ≤ 64).  A pivot below 1e-14·max diag is
 // clamped (the CholQR2 second pass restores orthogonality).
 // ---------------------------------------------------------------------------
+// Right-looking Cholesky, one barrier per column: column j is read unscaled
+// by every thread (its L column goes to a separate array), so the trailing
+// update and the scaling need no barrier between them; threads form a 16×16
+// grid over the trailing block (no integer division in the loop).
 __global__ __launch_bounds__(256) void k_chol(const double* __restrict__ S, int b, double* __restrict__ L) {
   __shared__ double a[JMAX][JMAX + 1];
-  __shared__ double dmax;
-  const int tid = threadIdx.x;
-  for (int e = tid; e < b * b; e += 256) a[e / b][e % b] = S[e];
-  __syncthreads();
-  if (tid == 0) {
-    double m = 0.0;
-    for (int i = 0; i < b; ++i) m = fmax(m, a[i][i]);
-    dmax = m > 0.0 ? m : 1.0;
-  }
-  __syncthreads();
-  for (int j = 0; j < b; ++j) {
-    if (tid == 0) a[j][j] = sqrt(fmax(a[j][j], 1e-14 * dmax));
-    __syncthreads();
-    const double djj = a[j][j];
-    for (int i = j + 1 + tid; i < b; i += 256) a[i][j] /= djj;
-    __syncthreads();
-    const int m = b - j - 1;
-    for (int e = tid; e < m * m; e += 256) {
-      const int i = j + 1 + e / m, l = j + 1 + e % m;
-      if (l <= i) a[i][l] -= a[i][j] * a[l][j];
-    }
-    __syncthreads();
-  }
+  __shared__ double lc[JMAX][JMAX + 1];
+  const int tid = threadIdx.x, ti = tid >> 4, tl = tid & 15;
   for (int e = tid; e < b * b; e += 256) {
-    const int i = e / b, j = e % b;
-    L[e] = (j <= i) ? a[i][j] : 0.0;
+    a[e / b][e % b] = S[e];
+    lc[e / b][e % b] = 0.0;
   }
+  __syncthreads();
+  double dmax = 0.0;
+  for (int i = 0; i < b; ++i) dmax = fmax(dmax, a[i][i]);
+  if (!(dmax > 0.0)) dmax = 1.0;
+  for (int j = 0; j < b; ++j) {
+    const double djj = sqrt(fmax(a[j][j], 1e-14 * dmax));
+    const double inv = 1.0 / djj;
+    for (int i = j + 1 + ti; i < b; i += 16) {
+      const double aij = a[i][j] * inv;
+      for (int l = j + 1 + tl; l <= i; l += 16) a[i][l] -= aij * (a[l][j] * inv);
+    }
+    if (tid < b - j) lc[j + tid][j] = tid == 0 ? djj : a[j + tid][j] * inv;
+    __syncthreads();
+  }
+  for (int e = tid; e < b * b; e += 256) L[e] = lc[e / b][e % b];
 }
 
 // V = W · L⁻ᵀ row by row (forward substitution), b = compile-time block.
 template <int BB>
-__global__ __launch_bounds__(256) void k_trsm_rows(const double* __restrict__ W, const double* __restrict__ L, int p,
+__global__ __launch_bounds__(64) void k_trsm_rows(const double* __restrict__ W, const double* __restrict__ L, int p,
                                                    double* __restrict__ V) {
   __shared__ double sl[BB][BB + 1];
-  for (int e = threadIdx.x; e < BB * BB; e += 256) sl[e / BB][e % BB] = L[e];
+  __shared__ double rd[BB];  // reciprocal diagonal: no division on the dependency chain
+  for (int e = threadIdx.x; e < BB * BB; e += blockDim.x) sl[e / BB][e % BB] = L[e];
+  for (int j = threadIdx.x; j < BB; j += blockDim.x) rd[j] = 1.0 / L[j * BB + j];
   __syncthreads();
-  const int r = blockIdx.x * 256 + threadIdx.x;
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= p) return;
   double v[BB];
 #pragma unroll
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(256) void k_trsm_rows(const double* __restrict__ W,
     double s = W[(int64_t)r * BB + j];
 #pragma unroll
     for (int l = 0; l < j; ++l) s -= v[l] * sl[j][l];
-    v[j] = s / sl[j][j];
+    v[j] = s * rd[j];
   }
 #pragma unroll
   for (int j = 0; j < BB; ++j) V[(int64_t)r * BB + j] = v[j];
@@ -733,12 +733,13 @@ int atb(const double* A, const double* B, int p, int b, double* out, double* par
 }
 
 int trsm_rows(const double* W, const double* L, int p, int b, double* V, hipStream_t st) {
-  dim3 g((p + 255) / 256);
+  // 64-thread workgroups: the p rows spread over p/64 CUs (the per-row chain is serial)
+  dim3 g((p + 63) / 64);
   switch (b) {
-    case 16: hipLaunchKernelGGL(k_trsm_rows<16>, g, dim3(256), 0, st, W, L, p, V); break;
-    case 32: hipLaunchKernelGGL(k_trsm_rows<32>, g, dim3(256), 0, st, W, L, p, V); break;
-    case 48: hipLaunchKernelGGL(k_trsm_rows<48>, g, dim3(256), 0, st, W, L, p, V); break;
-    case 64: hipLaunchKernelGGL(k_trsm_rows<64>, g, dim3(256), 0, st, W, L, p, V); break;
+    case 16: hipLaunchKernelGGL(k_trsm_rows<16>, g, dim3(64), 0, st, W, L, p, V); break;
+    case 32: hipLaunchKernelGGL(k_trsm_rows<32>, g, dim3(64), 0, st, W, L, p, V); break;
+    case 48: hipLaunchKernelGGL(k_trsm_rows<48>, g, dim3(64), 0, st, W, L, p, V); break;
+    case 64: hipLaunchKernelGGL(k_trsm_rows<64>, g, dim3(64), 0, st, W, L, p, V); break;
     default: return ocm::fail(OCM_ERR_UNSUPPORTED, "trsm block must be 16/32/48/64");
   }
   OCM_CHECK_LAUNCH("k_trsm_rows");
