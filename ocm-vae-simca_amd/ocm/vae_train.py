@@ -42,9 +42,11 @@ class GraphedVAETrainer:
         self.beta = float(beta)
         self.loss = loss
         self.dtype = dtype
-        # torch's fused Adam (one multi-tensor kernel per step): 480 vs 437 steps/s
-        # for the foreach form on MI355X (C4 net, B = 512); OCM_VAE_ADAM=foreach for A/B
-        fused = os.environ.get("OCM_VAE_ADAM", "fused") == "fused"
+        # torch's fused Adam on the GPU (one multi-tensor kernel per step): 480 vs 437
+        # steps/s for the foreach form on MI355X (C4 net, B = 512), losses equal to
+        # 1e-4; OCM_VAE_ADAM=foreach for A/B.  Eager CPU steps keep the reference's
+        # Adam arithmetic exactly (tests/test_vae_train.py)
+        fused = dev.type == "cuda" and os.environ.get("OCM_VAE_ADAM", "fused") == "fused"
         self.opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay, capturable=graph,
                                     **({"fused": True} if fused else {"foreach": True}))
         self.x = torch.zeros((batch, self.module.input_length), dtype=torch.float32, device=dev)
