@@ -108,7 +108,7 @@ def cpu_baseline(rows, p, k):
                       f"NumPy scores, fit+predict on the same rows ({dt:.2f} s)"}
 
 
-def vae_bench(device, steps, warmup, batch=512, length=2048):
+def vae_bench(device, steps, warmup, batch=512, length=2048, dtype=None):
     """Secondary metric (BASELINE.json): VAE-SIMCA train steps/s, C4 network
     (cb=3, nf=3, ks=7, hid=64, d=32) at B=512 × L=2048 in bf16,
     one HIP-graph replay per optimizer step (ocm/vae_train.py)."""
@@ -123,7 +123,9 @@ def vae_bench(device, steps, warmup, batch=512, length=2048):
     std = X.std(0).cpu().numpy() + 1e-6
     torch.manual_seed(0)
     m = V.ConvVAE1D(length, 32, mean, std, conv_blocks=3, n_filters=3, kernel_size=7, hidden_fc=64).to(device)
-    tr = GraphedVAETrainer(m, batch, lr=1e-3, dtype=torch.bfloat16)
+    if dtype is None:
+        dtype = torch.float32 if os.environ.get("OCM_VAE_DTYPE") == "f32" else torch.bfloat16
+    tr = GraphedVAETrainer(m, batch, lr=1e-3, dtype=dtype)
     for i in range(warmup):
         tr.step(X[(i % nb) * batch:(i % nb + 1) * batch])
     first = float(tr.out[0].item())
@@ -136,7 +138,8 @@ def vae_bench(device, steps, warmup, batch=512, length=2048):
     loss = float(tr.out[0].item())
     finite = all(bool(torch.isfinite(p).all()) for p in m.parameters())
     return {"metric": "VAE-SIMCA train steps/sec", "value": round(steps / dt, 2), "unit": "steps/s",
-            "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "dtype": "bf16",
+            "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps,
+            "dtype": "f32" if dtype == torch.float32 else "bf16",
             "config": {"workload": f"ConvVAE1D cb=3 nf=3 ks=7 hid=64 d=32, B={batch}, L={length}, "
                                    "BCE-with-logits + KL, Adam, HIP-graph step",
                        "params": sum(p.numel() for p in m.parameters())},

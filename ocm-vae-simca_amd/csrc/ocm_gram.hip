@@ -1031,7 +1031,6 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
 constexpr int G8S_FRAG = 1024;                       // one 32-col × 32-row digit fragment
 constexpr int G8S_OPS = 2 * 3 * 4 * G8S_FRAG;        // [A|B][digit][32-col block] = 24 KiB
 constexpr int G8S_SCL = 2 * 4 * 512;                 // [block & 1][wave][row | column scales]
-constexpr int G8S_DMA = 8;                           // DMAs per wave and stage
 
 // LDS-DMA with a scalar (wave-uniform) 64-bit base and a per-lane 32-bit
 // offset; M0 = the wave-uniform LDS destination (written in the same asm
