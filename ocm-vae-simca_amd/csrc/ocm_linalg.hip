@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int
     __syncthreads();
     if (tid == 0) {
       if (MODE == 1) {
-        part[blockIdx.x] = wtile * ((red[0] + red[1]) + (red[2] + red[3]));
+        part[blockIdx.z * gridDim.x + blockIdx.x] = wtile * ((red[0] + red[1]) + (red[2] + red[3]));
       } else {
         const int wg = blockIdx.y * gridDim.x + blockIdx.x;
         part[2 * wg] = (red[0] + red[1]) + (red[2] + red[3]);
@@ -787,7 +787,8 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
   const size_t pb = (size_t)p * b, bb = (size_t)b * b;
   const int nblk = (p + 63) / 64;
   const size_t def_blocks = (size_t)((p + DT - 1) / DT) * ((p + DT - 1) / DT);  // deflate GEMM tiles
-  const size_t trace_wgs = (size_t)((p + DT - 1) / DT) * ((p + DT - 1) / DT);
+  constexpr int TRACE_KSPLIT = 4;  // the trace GEMM's K split (the trace is linear in the K segments)
+  const size_t trace_wgs = (size_t)TRACE_KSPLIT * ((p + DT - 1) / DT) * ((p + DT - 1) / DT);
   size_t need = (6 * pb + 6 * bb + (size_t)ksplit * pb + (size_t)nblk * bb + 4 * b + 64) * sizeof(double);
   if (theta_mode) need += ((size_t)p * p + 4 * (size_t)k * p + 2 * def_blocks + trace_wgs + 8) * sizeof(double);
   void* w = ocm::workspace(ctx, need + 16 * 256, st);
@@ -906,11 +907,16 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
     OCM_HIP(hipMemcpyAsync(theta_out, tr2, 2 * sizeof(double), hipMemcpyDeviceToDevice, st));
     if (theta_mode >= 2) {
       const int nt = (p + DT - 1) / DT;
-      dim3 g((unsigned)(nt * (nt + 1) / 2), 1, 1);
-      hipLaunchKernelGGL(k_dgemm<1>, g, dim3(256), 0, st, Ct, (int64_t)p, Ct, (int64_t)p, nullptr, 0, p, p, p, p, Ct,
+      // split-K: 4× the workgroups of the upper-triangle tile grid (528 tiles at p = 2048 fill the
+      // chip only once), partial traces summed in a fixed order
+      int kper = (p + TRACE_KSPLIT - 1) / TRACE_KSPLIT;
+      kper = (kper + DBK - 1) / DBK * DBK;
+      const int nz = (p + kper - 1) / kper;
+      dim3 g((unsigned)(nt * (nt + 1) / 2), 1, (unsigned)nz);
+      hipLaunchKernelGGL(k_dgemm<1>, g, dim3(256), 0, st, Ct, (int64_t)p, Ct, (int64_t)p, nullptr, 0, p, p, p, kper, Ct,
                          (int64_t)p, tpart);
       OCM_CHECK_LAUNCH("k_dgemm trace");
-      hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, tpart, (int)g.x, theta_out + 2);
+      hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, tpart, (int)(g.x * g.z), theta_out + 2);
       OCM_CHECK_LAUNCH("k_sum_partials");
     } else {
       OCM_HIP(hipMemsetAsync(theta_out + 2, 0, sizeof(double), st));
