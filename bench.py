@@ -3,12 +3,14 @@
 
 One step = the full SIMCA hot path on the synthetic 1M×2048 fp32 batch each
 rank holds in HBM, k = 20, type 'alt', t2lim 'Fdist', qlim 'jm' (the driver
-defaults, simca_nuts.py:186): int8-digit quantiser + shifted Gram on integer
-MFMA (i8×3) → [RCCL all-reduce of
-Gram/colsum/n when N > 1] → covariance → top-20 eigenpairs + θ1..θ3 →
-fit-set scoring (T², Q, moments) → limits → predict (fused decision) on the
-same rows.  value = rows of all ranks / max-over-ranks step time
-(weak scaling: rows per GPU fixed).
+defaults, simca_nuts.py:186).  At N = 1 the step is the drop-in itself,
+``utils.SIMCA(...).fit(X, y)`` then ``.predict(X)`` on the device tensors; at
+N > 1 it is ``ocm.dist.ShardedSIMCA`` on each rank's rows.  Both run:
+outlier-screened int8-digit quantiser + shifted Gram on integer MFMA (i8×3)
+→ [RCCL all-reduce of Gram/colsum/n when N > 1] → covariance → top-20
+eigenpairs + θ1..θ3 → fit-set scoring (T, T², Q, moments) → limits → predict
+(fused decision) on the same rows.  value = rows of all ranks / max-over-ranks
+step time (weak scaling: rows per GPU fixed).
 
     python bench.py [--gpus N --steps K --warmup W --rows R --no-cpu]
 
@@ -50,12 +52,11 @@ def parse():
     ap.add_argument("--rows", type=int, default=1_000_000, help="spectra per GPU")
     ap.add_argument("--p", type=int, default=2048)
     ap.add_argument("--k", type=int, default=20)
-    ap.add_argument("--cpu-sample", type=int, default=65536, help="rows for the CPU baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=131072, help="rows for the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-vae", action="store_true", help="skip the secondary VAE train-steps/s measurement")
     ap.add_argument("--vae-steps", type=int, default=200)
-    ap.add_argument("--gram-mode", default=os.environ.get("OCM_GRAM_MODE", GRAM_MODE_DEFAULT),
-                    choices=["f32", "bf16x3", "i8x3"],
+    ap.add_argument("--gram-mode", default=GRAM_MODE_DEFAULT, choices=["f32", "bf16x3", "i8x3"],
                     help="Gram kernel: int8 digit split (default), bf16x3 split or FP32 MFMA")
     return ap.parse_args()
 
@@ -84,8 +85,21 @@ def synth_device(n, p, k, seed, device, rank_count=40, noise=0.05):
     return X
 
 
-def cpu_baseline(rows, p, k):
-    """Oracle at reference precision on a bounded sample (fit + predict)."""
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(rows, p, k, repeats=3):
+    """Oracle at reference precision (float32 full SVD + randomized PCA(k) +
+    NumPy scoring, the reference's solver sequence) on a bounded sample:
+    one warm-up on a small sample, then the median of ``repeats`` timed
+    fit + predict runs (SURVEY.md §8d protocol)."""
     import numpy as np
 
     from oracle import simca_oracle as O
@@ -96,16 +110,24 @@ def cpu_baseline(rows, p, k):
         threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
     except Exception:
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    X = O.synth_spectra(rows, p, k, rank=40, seed=1234)
-    y = np.zeros(rows, dtype=np.int64)
-    est = O.OracleSIMCA(n_components=k, model_class=0, precision="reference", predict_loadings="randomized")
-    t0 = time.perf_counter()
-    est.fit(X, y, rng=np.random.RandomState(0))
-    est.predict(X)
-    dt = time.perf_counter() - t0
-    return {"value": rows / dt, "unit": "spectra/s", "cores": int(threads), "kind": "port",
+
+    def run(m):
+        X = O.synth_spectra(m, p, k, rank=40, seed=1234)
+        y = np.zeros(m, dtype=np.int64)
+        est = O.OracleSIMCA(n_components=k, model_class=0, precision="reference", predict_loadings="randomized")
+        t0 = time.perf_counter()
+        est.fit(X, y, rng=np.random.RandomState(0))
+        est.predict(X)
+        return time.perf_counter() - t0
+
+    run(min(rows, 16384))  # warm-up (BLAS threads, page faults)
+    times = sorted(run(rows) for _ in range(repeats))
+    dt = times[len(times) // 2]
+    return {"value": round(rows / dt, 1), "unit": "spectra/s", "cores": int(threads), "kind": "port",
+            "cpu_model": _cpu_model(), "protocol": f"1 warm-up + median of {repeats}",
+            "runs_s": [round(t, 3) for t in times],
             "sample": f"{rows}x{p} fp32, k={k}, alt/Fdist/jm: float32 full SVD + randomized PCA(k) + "
-                      f"NumPy scores, fit+predict on the same rows ({dt:.2f} s)"}
+                      f"NumPy scores, fit+predict on the same rows (median {dt:.2f} s)"}
 
 
 def vae_bench(device, steps, warmup, batch=512, length=2048, dtype=None):
@@ -149,7 +171,6 @@ def vae_bench(device, steps, warmup, batch=512, length=2048, dtype=None):
 
 def main():
     args = parse()
-    os.environ["OCM_GRAM_MODE"] = args.gram_mode
     import torch
     import torch.distributed as dist
 
@@ -162,17 +183,29 @@ def main():
     device = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(device)
 
-    from ocm import _lib
+    from ocm import _lib, engine
     from ocm.dist import ShardedSIMCA
+    from utils import SIMCA
 
+    engine.set_gram_mode(args.gram_mode)
     n, p, k = args.rows, args.p, args.k
     X = synth_device(n, p, k, seed=4321 + rank, device=device)
+    y = torch.zeros(n, dtype=torch.int64, device=device)
     pred = torch.empty(n, dtype=torch.float64, device=device)
     torch.cuda.synchronize()
+    result = {}
 
     def step():
-        model = ShardedSIMCA(n_components=k, type="alt", t2lim="Fdist", qlim="jm").fit(X)
-        model.predict(X, out=pred)
+        if world == 1:  # the drop-in estimator on device tensors
+            model = SIMCA(n_components=k, model_class=0, type="alt", t2lim="Fdist", qlim="jm", verbose=False)
+            model.fit(X, y)
+            result["pred"] = model.predict(X)
+            info = model._model[0]
+            result.update(fit=model._fits[0], T2_limit=info["T2_limit"], Q_limit=info["Q_limit"])
+        else:
+            model = ShardedSIMCA(n_components=k, type="alt", t2lim="Fdist", qlim="jm").fit(X)
+            result["pred"] = model.predict(X, out=pred)
+            result.update(fit=model.fit_, T2_limit=model.T2_limit, Q_limit=model.Q_limit)
         return model
 
     for _ in range(args.warmup):
@@ -209,9 +242,7 @@ def main():
     score_avg_s = score_ms / max(score_n, 1) / 1e3
     score_gbs = n * p * 4 / score_avg_s / 1e9 if score_avg_s > 0 else 0.0
 
-    variant8 = os.environ.get("OCM_GRAM8_VARIANT", "direct")
-    gram_kernel = {"bf16x3": "k_gram3", "i8x3": "k_gram8d" if variant8 != "lds" else "k_gram8"}.get(
-        args.gram_mode, "k_gram")
+    gram_kernel = {"bf16x3": "k_gram3", "i8x3": "k_gram8d"}.get(args.gram_mode, "k_gram")
     if args.gram_mode == "i8x3":
         # fp32-grade product from 6 int8 MFMA digit products (exact int32 sums)
         gram_desc = (f"{gram_kernel} (shifted Gram, 3 int8 digits per value, 6 i8 MFMA products per fp32 "
@@ -237,7 +268,7 @@ def main():
         except Exception:
             traffic = None
 
-    accepted = float(pred.sum().item()) / n
+    accepted = float(result["pred"].sum().item()) / n
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -253,6 +284,8 @@ def main():
         "data": "synthetic (rank-40 band spectra + noise, generated in HBM)",
         "config": {
             "workload": f"SIMCA fit+score, synthetic {n}x{p} fp32 per GPU, k={k}, type=alt t2lim=Fdist qlim=jm",
+            "step": ("utils.SIMCA(...).fit(X, y) + .predict(X), device tensors (drop-in)" if world == 1 else
+                     "ocm.dist.ShardedSIMCA fit (T kept) + predict per rank"),
             "rows_per_gpu": n, "p": p, "k": k,
             "parallelism": f"row shards x{world} (RCCL all-reduce of Gram/colsum/n)",
         },
@@ -274,8 +307,9 @@ def main():
                          "achieved_GBs": round(score_gbs, 1), "peak_GBs": HBM_PEAK_GBS,
                          "frac": round(score_gbs / HBM_PEAK_GBS, 4), "avg_launch_ms": round(score_avg_s * 1e3, 4),
                          "launches": score_n, "bytes_per_launch": n * p * 4},
-        "checks": {"accept_rate": round(accepted, 4), "eig_iters": model.fit_.eig_iters,
-                   "T2_limit": model.T2_limit, "Q_limit": model.Q_limit},
+        "checks": {"accept_rate": round(accepted, 4), "eig_iters": result["fit"].eig_iters,
+                   "T2_limit": result["T2_limit"], "Q_limit": result["Q_limit"],
+                   "gram_guard_marks": engine.last_gram_marks(device.index)},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         try:

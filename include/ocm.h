@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCM_ABI_VERSION 1
+#define OCM_ABI_VERSION 2
 
 #define OCM_OK 0
 #define OCM_ERR_ARG (-1)         /* invalid argument (maps to ValueError) */
@@ -72,7 +72,7 @@ int ocm_ctx_reserve(ocm_ctx* ctx, size_t bytes);
  * ocm_ctx_read_timing waits for the recorded events, returns the summed
  * duration (ms) and launch count of kernel `kernel_id`, and clears them. */
 #define OCM_TIMED_KERNELS 3
-#define OCM_KERNEL_GRAM 0  /* the Gram main kernel (k_gram8d / k_gram8s / k_gram3 / k_gram) */
+#define OCM_KERNEL_GRAM 0  /* the Gram main kernel (k_gram8d / k_gram3 / k_gram) */
 #define OCM_KERNEL_SCORE 1 /* k_score: fused projection / Q / T² kernel */
 #define OCM_KERNEL_QUANT 2 /* k_q8_quant: int8 digit split feeding k_gram8d */
 int ocm_ctx_set_timing(ocm_ctx* ctx, int enable);
@@ -85,23 +85,42 @@ int ocm_ctx_read_timing(ocm_ctx* ctx, int kernel_id, double* total_ms, int64_t* 
 int ocm_colmean_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
                     double* mean_out, void* stream);
 
-/* Per-segment shifted Gram.  Default (OCM_GRAM_MODE=i8x3): y = x − shift is
+/* Per-segment shifted Gram (default mode OCM_GRAM_I8X3): y = x − shift is
  * split into three int8 digits per value (power-of-two scale per 1536-row
  * block and column) and the six digit products of weight ≥ 254⁻² are summed
  * exactly in int32 on integer MFMA (fp32-grade Gram: max relative error
- * ≈ 5e-8 on the bench data); OCM_GRAM_MODE=bf16x3 / f32 select the bf16
- * split / FP32-MFMA kernels.  Workspace: ≈ 3 B per value for the digit planes
- * plus the chunk partials (≈ 8.4 GB at 1M × 2048).
+ * ≈ 5e-8 on the bench data).  Outlier guard: values above 32× their column's
+ * robust sample scale (2^e ≥ median|y| over the first ≤ 4096 rows) are
+ * screened out of the digits of their 32-column group and
+ * added back exactly (fp64 fix-up), so one extreme row does not coarsen the
+ * other rows of its block; when more than n/8 values are screened the call
+ * recomputes the Gram on FP32 MFMA.  Workspace: ≈ 3 B per value for the digit
+ * planes plus the chunk partials (≈ 8.4 GB at 1M × 2048).
  * Replaces the SVD of the centred class matrix (utils/SIMCA.py:64-66 ->
  * sklearn _pca.py:569-584 scipy.linalg.svd gesdd): the covariance
  * eigen-decomposition needs only Σ yᵀy and Σ y with y = x - shift.
  * Segment s covers processed rows [seg_offsets[s], seg_offsets[s+1]).
  * G_out [dev] nseg·p·p doubles (full symmetric), colsum_out [dev] nseg·p.
  * seg_offsets [host] nseg+1 ascending, seg_offsets[0] = 0, last = n.
- * shift [dev] p floats. */
+ * shift [dev] p floats.  p ≤ 64 always takes an fp64-accumulated VALU Gram. */
 int ocm_gram_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
                  const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
                  void* stream);
+
+/* Same with an explicit arithmetic mode and row-chunk length (0 = automatic):
+ *   OCM_GRAM_I8X3   the default above;
+ *   OCM_GRAM_F32    FP32 MFMA (v_mfma_f32_32x32x2_f32), f32 chunk partials summed in f64;
+ *   OCM_GRAM_BF16X3 exact three-level bf16 split on bf16 MFMA. */
+#define OCM_GRAM_I8X3 0
+#define OCM_GRAM_F32 1
+#define OCM_GRAM_BF16X3 2
+int ocm_gram_f32_ex(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                    const float* shift, const int64_t* seg_offsets, int32_t nseg, int32_t mode, int64_t chunk_rows,
+                    double* G_out, double* colsum_out, void* stream);
+
+/* Outlier-guard marks ((row, 32-column group) pairs screened out) of the
+ * context's last i8×3 Gram that synchronised (diagnostics / tests). */
+int ocm_gram_last_marks(ocm_ctx* ctx, int64_t* marks_out);
 
 /* Covariance from a signed combination of segment Grams (CV downdating):
  *   Gc = Σ_t coef[t]·G[t], sc = Σ_t coef[t]·colsum[t], d = sc/n,
@@ -133,9 +152,8 @@ int ocm_sym_pinv_f64(ocm_ctx* ctx, const double* A, int32_t d, double rcond, dou
 
 /* Fused scoring of float32 spectra (utils/SIMCA.py:65-71 fit, 104-107
  * transform, 127-130 predict):  y = x - mu; t = P·y (k); Q = ‖y − Pᵀt‖²;
- * T2 = tᵀ·A·t.  Default kernel: FP32 MFMA projection + explicit residual
- * (two register-streamed sweeps); alternative FP64-MFMA single pass with
- * Q = ‖y‖² − ‖t‖².  P [dev] k×p float64 row-major with orthonormal rows
+ * T2 = tᵀ·A·t.  FP32 MFMA projection + explicit residual (first-order
+ * insensitive to rounding in t).  P [dev] k×p float64 row-major with orthonormal rows
  * (ldp = p), mu [dev] p doubles, A [dev] k×k doubles.
  * Outputs (all nullable, [dev]): T_out m×k float32,
  * T2_out m doubles, Q_out m floats.  If dec != NULL [host] the decision is
@@ -237,17 +255,22 @@ int ocm_snv_savgol_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, int
  * biased variance normalises, unbiased variance feeds running_var with
  * `momentum`).  Replaces the MIOpen spatial BN the reference's nn.BatchNorm1d
  * lowers to (vae_model.py:45-47, 75-77).  running_mean / running_var may both
- * be NULL (no update); gamma / beta may be NULL (affine=False).  Workspace is
- * the context arena; all work is stream-ordered (graph-capturable). */
+ * be NULL (no update); gamma / beta may be NULL (affine=False).  scratch [dev,
+ * nullable] ocm_bn_scratch_bytes(C) bytes: caller-owned memory that stays
+ * put while a captured hipGraph replays the launches (NULL = the context
+ * arena, which a later, larger libocm call may re-allocate — do not capture
+ * with NULL).  All work is stream-ordered (graph-capturable). */
 #define OCM_DTYPE_F32 0
 #define OCM_DTYPE_BF16 1
+size_t ocm_bn_scratch_bytes(int32_t C);
 int ocm_bn_fwd_train(ocm_ctx* ctx, int32_t dtype, const void* x, int32_t N, int32_t C, int32_t L,
                      const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
-                     float* running_var, void* y, float* save_mean, float* save_invstd, void* stream);
+                     float* running_var, void* y, float* save_mean, float* save_invstd, void* scratch,
+                     void* stream);
 /* dx = γ·invstd·(dy − mean(dy) − x̂·mean(dy·x̂)); dgamma = Σ dy·x̂, dbeta = Σ dy (either may be NULL). */
 int ocm_bn_bwd(ocm_ctx* ctx, int32_t dtype, const void* x, const void* dy, int32_t N, int32_t C, int32_t L,
                const float* gamma, const float* save_mean, const float* save_invstd, void* dx, float* dgamma,
-               float* dbeta, void* stream);
+               float* dbeta, void* scratch, void* stream);
 
 #ifdef __cplusplus
 }

@@ -168,10 +168,15 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_apply(const T* __restrict__ x, 
   bn_st(dx, i, k * (bn_ld(dy, i) - m1 - xh * m2));
 }
 
+// scratch of one forward / backward call: per-(channel, split) partials + the
+// backward's channel sums
+size_t bn_scratch(int C) { return ((size_t)C * BN_SPLIT * 2 + 2 * (size_t)C) * sizeof(double); }
+
 template <typename T>
 int bn_fwd(ocm_ctx* ctx, const void* x, int N, int C, int L, const float* gamma, const float* beta, float eps,
-           float momentum, float* rmean, float* rvar, void* y, float* smean, float* sinv, hipStream_t st) {
-  auto* part = static_cast<double*>(ocm::workspace(ctx, (size_t)C * BN_SPLIT * 2 * sizeof(double), st));
+           float momentum, float* rmean, float* rvar, void* y, float* smean, float* sinv, void* scratch,
+           hipStream_t st) {
+  auto* part = static_cast<double*>(scratch ? scratch : ocm::workspace(ctx, bn_scratch(C), st));
   if (!part) return OCM_ERR_NOMEM;
   hipLaunchKernelGGL(k_bn_stats<T>, dim3(BN_SPLIT, C), dim3(BN_T), 0, st, static_cast<const T*>(x), N, C, L, part);
   hipLaunchKernelGGL(k_bn_finalize, dim3((C + 63) / 64), dim3(64), 0, st, part, C, (int64_t)N * L, eps, momentum,
@@ -184,8 +189,8 @@ int bn_fwd(ocm_ctx* ctx, const void* x, int N, int C, int L, const float* gamma,
 
 template <typename T>
 int bn_bwd(ocm_ctx* ctx, const void* x, const void* dy, int N, int C, int L, const float* gamma, const float* smean,
-           const float* sinv, void* dx, float* dgamma, float* dbeta, hipStream_t st) {
-  auto* part = static_cast<double*>(ocm::workspace(ctx, ((size_t)C * BN_SPLIT * 2 + 2 * (size_t)C) * sizeof(double), st));
+           const float* sinv, void* dx, float* dgamma, float* dbeta, void* scratch, hipStream_t st) {
+  auto* part = static_cast<double*>(scratch ? scratch : ocm::workspace(ctx, bn_scratch(C), st));
   if (!part) return OCM_ERR_NOMEM;
   double* sums = part + (size_t)C * BN_SPLIT * 2;
   hipLaunchKernelGGL(k_bn_bwd_stats<T>, dim3(BN_SPLIT, C), dim3(BN_T), 0, st, static_cast<const T*>(x),
@@ -202,32 +207,35 @@ int bn_bwd(ocm_ctx* ctx, const void* x, const void* dy, int N, int C, int L, con
 
 extern "C" {
 
+size_t ocm_bn_scratch_bytes(int32_t C) { return C > 0 ? bn_scratch(C) : 0; }
+
 int ocm_bn_fwd_train(ocm_ctx* ctx, int32_t dtype, const void* x, int32_t N, int32_t C, int32_t L,
                      const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
-                     float* running_var, void* y, float* save_mean, float* save_invstd, void* stream) {
+                     float* running_var, void* y, float* save_mean, float* save_invstd, void* scratch,
+                     void* stream) {
   OCM_REQUIRE(ctx && x && y && save_mean && save_invstd, "ocm_bn_fwd_train: NULL argument");
   OCM_REQUIRE(N > 0 && C > 0 && L > 0, "ocm_bn_fwd_train: bad shape");
   OCM_REQUIRE(!running_mean == !running_var, "ocm_bn_fwd_train: running_mean and running_var go together");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == OCM_DTYPE_F32)
     return bn_fwd<float>(ctx, x, N, C, L, gamma, beta, eps, momentum, running_mean, running_var, y, save_mean,
-                         save_invstd, st);
+                         save_invstd, scratch, st);
   if (dtype == OCM_DTYPE_BF16)
     return bn_fwd<bf16_t>(ctx, x, N, C, L, gamma, beta, eps, momentum, running_mean, running_var, y,
-                                  save_mean, save_invstd, st);
+                                  save_mean, save_invstd, scratch, st);
   return ocm::fail(OCM_ERR_ARG, "ocm_bn_fwd_train: dtype must be OCM_DTYPE_F32 or OCM_DTYPE_BF16");
 }
 
 int ocm_bn_bwd(ocm_ctx* ctx, int32_t dtype, const void* x, const void* dy, int32_t N, int32_t C, int32_t L,
                const float* gamma, const float* save_mean, const float* save_invstd, void* dx, float* dgamma,
-               float* dbeta, void* stream) {
+               float* dbeta, void* scratch, void* stream) {
   OCM_REQUIRE(ctx && x && dy && dx && save_mean && save_invstd, "ocm_bn_bwd: NULL argument");
   OCM_REQUIRE(N > 0 && C > 0 && L > 0, "ocm_bn_bwd: bad shape");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == OCM_DTYPE_F32)
-    return bn_bwd<float>(ctx, x, dy, N, C, L, gamma, save_mean, save_invstd, dx, dgamma, dbeta, st);
+    return bn_bwd<float>(ctx, x, dy, N, C, L, gamma, save_mean, save_invstd, dx, dgamma, dbeta, scratch, st);
   if (dtype == OCM_DTYPE_BF16)
-    return bn_bwd<bf16_t>(ctx, x, dy, N, C, L, gamma, save_mean, save_invstd, dx, dgamma, dbeta, st);
+    return bn_bwd<bf16_t>(ctx, x, dy, N, C, L, gamma, save_mean, save_invstd, dx, dgamma, dbeta, scratch, st);
   return ocm::fail(OCM_ERR_ARG, "ocm_bn_bwd: dtype must be OCM_DTYPE_F32 or OCM_DTYPE_BF16");
 }
 

@@ -16,7 +16,6 @@
 // consecutive tiles of one row chunk land on one XCD and share its L2.
 //   GT = 256 (default): 8 waves, BK = 16, 64 KiB LDS, 128 accumulators/lane.
 //   GT = 128:           4 waves, BK = 32, 64 KiB LDS,  64 accumulators/lane.
-#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -614,26 +613,35 @@ __global__ __launch_bounds__(256) void k_gram_small_reduce(const double* __restr
 // the bf16 rate, exact int32 accumulation).
 //
 // k_q8_quant (one HBM read of X) writes y = x − shift as three signed int8
-// digit planes per 256-row scale block b and column j:
+// digit planes per 1536-row scale block b and column j:
 //     y = s_bj · (a1 + a2/254 + a3/254²),   |a·| ≤ 127,   s_bj = 2^e ≥ max|y|/127
 // (s a power of two, so y/s is exact; a1 = rint(y/s), a2 = rint(254·r1), a3 =
 // rint(254·r2) with |r·| ≤ ½; the residual is ≤ ½·254⁻²·s ≈ 2⁻²⁴·max|y|).
-// k_gram8 accumulates, per 128×128 tile, the six digit products of weight
+// k_gram8d accumulates, per 128×128 tile, the six digit products of weight
 // ≥ 254⁻² in three int32 sets (A1 = Σa1a1', A2 = Σa1a2'+a2a1', A3 = Σa1a3'+
-// a3a1'+a2a2' — exact: |A| < 2²⁴ per block) and folds each scale block into
-// f64 running sums: G += s_i s_j (A1 + A2/254 + A3/254²).  The dropped
-// products are ≤ 2⁻²⁴·max|y_i|·max|y_j| per row, the size of an f32 rounding
-// of the largest product (numpy emulation at 20k×256: Frobenius error 3.8e-8
-// vs 4.5e-8 for f32 accumulation).  No rounding happens inside the MFMA, so
-// there is no truncation bias and no VALU add per K-step (cf. k_gram3).
+// a3a1'+a2a2'; per block |A1| ≤ 1536·127² ≈ 2.5e7, |A3| ≤ 3·1536·127² ≈ 7.4e7
+// < 2³¹, so the int32 sums are exact) and converts each block's sets to f32
+// (a rounded int32 → f32 conversion: ≤ 2⁻²⁴ relative) folded into f32 running
+// sums per 4096-row chunk: G += s_i s_j (A1 + A2/254 + A3/254²); chunks are
+// summed in f64.  The dropped products are ≤ 2⁻²⁴·max|y_i|·max|y_j| per row,
+// the size of an f32 rounding of the largest product.
+//
+// Outlier guard.  The representation error is relative to the block's
+// column maximum, so one extreme row would cost the other 1535 rows of its
+// block their precision.  k_q8_quant therefore screens every value against a
+// per-column threshold τ·2^e_j (2^e_j ≥ median|y_j| over the first ≤ 4096
+// rows, a robust scale; τ = 32; k_colexp_hist / k_q8_thresholds): a row with any value above it inside the workgroup's 32
+// columns is left out of those columns' scale and digits (its digits there
+// are 0) and marked in a per-row column-group bitmask.  k_gram_fixup adds the
+// marked rows' missing products exactly (fp64: y_i y_j for every pair with
+// at least one column in a marked group).  Clean data marks nothing and pays
+// one scalar read-back; heavily marked data (> n/8 marks) falls back to the
+// FP32-MFMA Gram.
 //
 // Digit planes: [digit][32-row group][column P8][32 B] (the 32 B of a column
-// are its 32 rows of one group — one MFMA K-step).  A workgroup (4 waves, one
-// per SIMD, 2×2 waves of 64×64) owns one upper-triangle 128×128 tile over one
-// chunk; stages of 32 rows are register-prefetched two ahead and stored to a
-// double-buffered LDS image with the k_gram3 half swizzle (conflict-free
-// ds_read_b128 fragments).  The digit planes are in processed-row order, so
-// class subsets / CV folds (gather lists) are gathered once, by the quantiser.
+// are its 32 rows of one group — one MFMA K-step).  The digit planes are in
+// processed-row order, so class subsets / CV folds (gather lists) are
+// gathered once, by the quantiser.
 // ---------------------------------------------------------------------------
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
@@ -646,8 +654,14 @@ struct Q8Plan {
   float* scale;   // [chunk][nblk][P8]
   int P8;         // padded columns (multiple of Q8T)
   int nblk;       // scale blocks per chunk
-  int noload;     // timing-only experiments: digit loads dropped by the range check
+  const float* thr;  // [P8] outlier thresholds (τ × robust column scale)
+  uint32_t* flags;   // [processed row][fw] column-group bitmask of screened-out values
+  int fw;            // bitmask words per row
+  uint32_t* nmark;   // number of (row, column group) marks
 };
+
+constexpr float Q8TAU = 32.f;     // outlier threshold in robust column scales (2^e ≥ median|y|)
+constexpr int Q8GROUP = 32;       // columns per guard group (= quantiser workgroup width)
 
 __device__ __forceinline__ uint32_t q8_byte(float a, int u) { return ((uint32_t)(int)a & 0xffu) << (8 * u); }
 
@@ -719,15 +733,42 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ 
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[j][e] = (g < r1 && c0 + e < p) ? x[e] - sh[e] : 0.f;
   }
-  f32x4 m = {0.f, 0.f, 0.f, 0.f};
+  // column sums over every row (the fix-up does not touch them)
   double cs[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int j = 0; j < 16; ++j)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      m[e] = fmaxf(m[e], fabsf(v[j][e]));
-      cs[e] += (double)v[j][e];
+    for (int e = 0; e < 4; ++e) cs[e] += (double)v[j][e];
+  // outlier screen: rows with a value above the threshold in this column group are
+  // taken out of its scale and digits (k_gram_fixup adds them exactly)
+  {
+    const f32x4 th = *reinterpret_cast<const f32x4*>(q.thr + c0);
+    uint32_t ext = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ext |= (fabsf(v[j][e]) > th[e]) ? (1u << j) : 0u;
+    // OR over the 8 threads (consecutive lanes) that share this row slice
+    ext |= __shfl_xor(ext, 1, 64);
+    ext |= __shfl_xor(ext, 2, 64);
+    ext |= __shfl_xor(ext, 4, 64);
+    if (ext) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if ((ext >> j) & 1u) v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (cq == 0) {
+        const int grp = cg0 / Q8GROUP;
+        for (int j = 0; j < 16; ++j)
+          if ((ext >> j) & 1u) atomicOr(q.flags + (size_t)(rb + j) * q.fw + (grp >> 5), 1u << (grp & 31));
+        atomicAdd(q.nmark, (uint32_t)__popc(ext));
+      }
     }
+  }
+  f32x4 m = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], fabsf(v[j][e]));
   *reinterpret_cast<f32x4*>(&wmax[rs][4 * cq]) = m;
 #pragma unroll
   for (int e = 0; e < 4; ++e) wsum[rs][4 * cq + e] = cs[e];
@@ -832,6 +873,213 @@ __global__ __launch_bounds__(256) void k_colblk_sum(const double* __restrict__ c
 }
 
 // ---------------------------------------------------------------------------
+// Outlier guard kernels (see the i8×3 header above).
+// ---------------------------------------------------------------------------
+// Robust column scale of the sample: a histogram of the binary exponent of
+// |y| (y = x − shift) per column over the first ≤ 4096 processed rows; the
+// median bin gives 2^e ≥ median|y| (≈ 0.67σ for Gaussian data, and a few
+// extreme rows in the sample do not move it).  grid (⌈p/64⌉, row splits),
+// 256 threads: lane = column, the 4 waves stride over the split's rows.
+constexpr int QX_BINS = 128, QX_EMIN = -62;  // bin = clamp(e, −62, 65) + 62; zeros → bin 0
+__global__ __launch_bounds__(256) void k_colexp_hist(const float* __restrict__ X, int64_t ldx,
+                                                     const int64_t* __restrict__ rows, int64_t n, int p,
+                                                     const float* __restrict__ shift, int64_t rows_per_split,
+                                                     uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[64][QX_BINS];
+  for (int e = threadIdx.x; e < 64 * QX_BINS; e += 256) (&h[0][0])[e] = 0u;
+  __syncthreads();
+  const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + c;
+  const int64_t a = (int64_t)blockIdx.y * rows_per_split;
+  const int64_t e = min(n, a + rows_per_split);
+  if (col < p) {
+    const float sh = shift[col];
+    for (int64_t r = a + w; r < e; r += 4) {
+      const float y = fabsf(X[(rows ? rows[r] : r) * ldx + col] - sh);
+      int ex = 0;
+      (void)frexpf(y, &ex);
+      const int bin = y > 0.f ? min(max(ex, QX_EMIN), QX_EMIN + QX_BINS - 1) - QX_EMIN : 0;
+      atomicAdd(&h[c][bin], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * QX_BINS; i += 256) {
+    const int cc = i / QX_BINS, bin = i % QX_BINS;
+    const uint32_t v = h[cc][bin];
+    if (v && blockIdx.x * 64 + cc < p) atomicAdd(hist + (size_t)(blockIdx.x * 64 + cc) * QX_BINS + bin, v);
+  }
+}
+
+// thr_j = τ·max(2^e_j, 2⁻⁸·max_k 2^e_k), e_j the median exponent bin of
+// column j (padded columns: +inf).  The floor keeps near-constant sample
+// columns from marking every later row.  One workgroup of 1024 threads.
+__global__ __launch_bounds__(1024) void k_q8_thresholds(const uint32_t* __restrict__ hist, int64_t nsamp, int p,
+                                                        int P8, float* __restrict__ thr) {
+  __shared__ float red[16];
+  float mx = 0.f;
+  const uint32_t half = (uint32_t)((nsamp + 1) / 2);
+  for (int c = threadIdx.x; c < p; c += 1024) {
+    uint32_t acc = 0;
+    int bin = 0;
+    for (; bin < QX_BINS - 1; ++bin) {
+      acc += hist[(size_t)c * QX_BINS + bin];
+      if (acc >= half) break;
+    }
+    const float sc = bin == 0 ? 0.f : ldexpf(1.f, bin + QX_EMIN);
+    thr[c] = sc;  // provisional
+    mx = fmaxf(mx, sc);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  float gmax = 0.f;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) gmax = fmaxf(gmax, red[w]);
+  const float floor_ = gmax * (1.f / 256.f);
+  __syncthreads();
+  for (int c = threadIdx.x; c < P8; c += 1024)
+    thr[c] = c < p ? Q8TAU * fmaxf(thr[c], floor_) : __builtin_inff();
+}
+
+// Marked-row compaction, in processed-row order: per 4096-row block the
+// number of marked rows, then each block writes its rows at the prefix of the
+// counts before it (ordered lists → a deterministic fix-up sum).
+constexpr int FLAG_BLK = 4096;
+__device__ __forceinline__ bool row_marked(const uint32_t* __restrict__ flags, int fw, int64_t r) {
+  uint32_t o = 0;
+  for (int w = 0; w < fw; ++w) o |= flags[(size_t)r * fw + w];
+  return o != 0;
+}
+
+__global__ __launch_bounds__(256) void k_flag_count(const uint32_t* __restrict__ flags, int fw, int64_t n,
+                                                    uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t red[4];
+  const int64_t base = (int64_t)blockIdx.x * FLAG_BLK + 16 * threadIdx.x;
+  uint32_t c = 0;
+  for (int j = 0; j < 16; ++j)
+    if (base + j < n && row_marked(flags, fw, base + j)) ++c;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void k_flag_emit(const uint32_t* __restrict__ flags, int fw, int64_t n,
+                                                   const uint32_t* __restrict__ cnt, int nblk,
+                                                   int64_t* __restrict__ list, uint32_t* __restrict__ nlist) {
+  __shared__ uint32_t pre[256];
+  uint32_t off = 0;
+  for (int b = 0; b < (int)blockIdx.x; ++b) off += cnt[b];
+  const int64_t base = (int64_t)blockIdx.x * FLAG_BLK + 16 * threadIdx.x;
+  uint32_t mine = 0;
+  for (int j = 0; j < 16; ++j)
+    if (base + j < n && row_marked(flags, fw, base + j)) mine |= 1u << j;
+  pre[threadIdx.x] = (uint32_t)__popc(mine);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // 256-entry exclusive scan
+    uint32_t acc = 0;
+    for (int t = 0; t < 256; ++t) {
+      const uint32_t v = pre[t];
+      pre[t] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  uint32_t w = off + pre[threadIdx.x];
+  for (int j = 0; j < 16; ++j)
+    if ((mine >> j) & 1u) list[w++] = base + j;
+  if (blockIdx.x == (unsigned)(nblk - 1) && threadIdx.x == 255) *nlist = w;
+}
+
+// G_s += Σ_{marked rows f of segment s} [group(i) or group(j) marked for f] · y_fi y_fj
+// (fp64).  grid (upper-triangle 64×64 tiles, segments), 256 threads, each
+// thread a 4×4 block of the tile; 16 marked rows per LDS stage.
+struct FixSeg {
+  int64_t begin[MAXSEG + 1];
+  int32_t nseg;
+};
+constexpr int FX_T = 64, FX_R = 16;
+__global__ __launch_bounds__(256) void k_gram_fixup(const float* __restrict__ X, int64_t ldx,
+                                                    const int64_t* __restrict__ rows, int p,
+                                                    const float* __restrict__ shift, FixSeg fs,
+                                                    const int64_t* __restrict__ list,
+                                                    const uint32_t* __restrict__ nlist,
+                                                    const uint32_t* __restrict__ flags, int fw, int nt,
+                                                    double* __restrict__ G) {
+  __shared__ double yi[FX_R][FX_T], yj[FX_R][FX_T];
+  __shared__ uint32_t mk[FX_R];  // bit 0/1: groups of the I columns, bit 2/3: of the J columns
+  const int seg = blockIdx.y;
+  int ti, tj;
+  tile_coords(blockIdx.x, nt, ti, tj);
+  const int I = ti * FX_T, J = tj * FX_T;
+  const int64_t lo = fs.begin[seg], hi = fs.begin[seg + 1];
+  const int64_t total = (int64_t)*nlist;
+  auto lower = [&](int64_t key) {
+    int64_t a = 0, b = total;
+    while (a < b) {
+      const int64_t m = (a + b) >> 1;
+      if (list[m] < key) a = m + 1; else b = m;
+    }
+    return a;
+  };
+  const int64_t fa = lower(lo), fb = lower(hi);
+  if (fa >= fb) return;
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int gI = I / Q8GROUP, gJ = J / Q8GROUP;
+  double acc[4][4] = {};
+  for (int64_t f0 = fa; f0 < fb; f0 += FX_R) {
+    const int nr = (int)min<int64_t>(FX_R, fb - f0);
+    __syncthreads();
+    for (int e = tid; e < FX_R * FX_T; e += 256) {
+      const int r = e / FX_T, c = e % FX_T;
+      double a = 0.0, b = 0.0;
+      if (r < nr) {
+        const int64_t pos = list[f0 + r];
+        const float* xr = X + (rows ? rows[pos] : pos) * ldx;
+        if (I + c < p) a = (double)xr[I + c] - (double)shift[I + c];
+        if (J + c < p) b = (double)xr[J + c] - (double)shift[J + c];
+      }
+      yi[r][c] = a;
+      yj[r][c] = b;
+    }
+    if (tid < FX_R) {
+      uint32_t m = 0;
+      if (tid < nr) {
+        const int64_t pos = list[f0 + tid];
+        auto bit = [&](int g) { return (flags[(size_t)pos * fw + (g >> 5)] >> (g & 31)) & 1u; };
+        m = bit(gI) | (bit(gI + 1) << 1) | (bit(gJ) << 2) | (bit(gJ + 1) << 3);
+      }
+      mk[tid] = m;
+    }
+    __syncthreads();
+    for (int r = 0; r < nr; ++r) {
+      const uint32_t m = mk[r];
+      const bool mi = (m >> (ty >> 3)) & 1u;        // rows 4ty..4ty+3 lie in group gI + (ty >= 8)
+      const bool mj = (m >> (2 + (tx >> 3))) & 1u;
+      if (!(mi || mj)) continue;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const double u = yi[r][4 * ty + a];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = fma(u, yj[r][4 * tx + b], acc[a][b]);
+      }
+    }
+  }
+  double* Gs = G + (size_t)seg * p * p;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int gi = I + 4 * ty + a, gj = J + 4 * tx + b;
+      if (gi >= p || gj >= p) continue;
+      Gs[(size_t)gi * p + gj] += acc[a][b];
+      if (ti != tj) Gs[(size_t)gj * p + gi] += acc[a][b];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_gram8d — the i8×3 Gram without an LDS stage or workgroup barrier.  The
 // digit-plane layout makes one MFMA operand fragment (32 columns × 32 rows:
 // lane (r, h) ← column r, bytes 16h..16h+15 of the group) one contiguous
@@ -839,7 +1087,7 @@ __global__ __launch_bounds__(256) void k_colblk_sum(const double* __restrict__ c
 // registers with buffer loads, two stages ahead (2 × 48 VGPRs).  The two
 // waves sharing a panel read the same bytes (the CU's L1 serves the second).
 // One wave per SIMD, 64×64 per wave; the scale-block flush goes through
-// wave-private LDS.  The default i8×3 Gram kernel (OCM_GRAM8_VARIANT=lds: k_gram8).
+// wave-private LDS.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
                                                    float* __restrict__ part) {
@@ -870,8 +1118,7 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
   const int l31 = lane & 31, h = lane >> 5;
   if (ti == tj && wm > wn) return;  // strictly-lower block of a diagonal tile; no barrier to keep
   const size_t gstride = (size_t)q.P8 * 32;
-  const int xflags = __builtin_amdgcn_readfirstlane(q.noload);  // timing ablations (OCM_GRAM8_NOLOAD bits)
-  const uint32_t span = (xflags & 1) ? 0u : (uint32_t)((size_t)nstage3 * gstride);
+  const uint32_t span = (uint32_t)((size_t)nstage3 * gstride);
   const char* cbase = q.digits + gbase * gstride;
   __amdgpu_buffer_rsrc_t ra[3], rb[3];
 #pragma unroll
@@ -957,7 +1204,7 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
   do {                                                                                              \
     Q8D_LOAD(NA, NB, min((STG) + 2, nstage3 - 1));                                                  \
     __builtin_amdgcn_sched_barrier(0);                                                              \
-    if (!(xflags & 4)) Q8D_MFMA(CA, CB, Z);                                                         \
+    Q8D_MFMA(CA, CB, Z);                                                         \
     __builtin_amdgcn_sched_barrier(0);                                                              \
   } while (0)
 #define Q8D_STEP(STG, Z, ...) Q8D_STEP_(STG, Z, __VA_ARGS__)
@@ -980,7 +1227,7 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
       }
       Q8D_STEP(s0 + u + 2, false, Q8D_S2);
     }
-    if (!(xflags & 8)) flush();
+    flush();
   }
 #undef Q8D_STEP
 #undef Q8D_STEP_
@@ -1000,220 +1247,6 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
         const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int col = wn * 64 + c * 32 + l31;
         out[row * Q8T + col] = runl[wave][a * 2 + c][r >> 2][lane][r & 3];
-      }
-}
-
-// ---------------------------------------------------------------------------
-// k_gram8s — the i8×3 Gram with the operand panels shared through LDS.
-// k_gram8d feeds each wave's 64×64 tile from its own register loads: 12 KiB
-// per 32-row stage for 24 MFMAs, which keeps the CU's vector-memory path
-// (64 B/clk) as busy as the MFMA pipe, so the two take turns.  Here the
-// workgroup's two 128-column panels (24 KiB per stage) are copied ONCE into
-// LDS by LDS-DMA (global_load_lds_dwordx4: 1 KiB = one fragment per wave
-// instruction, no VGPR staging) and every wave reads its fragments with
-// ds_read_b128: half the vector-memory instructions per MFMA.
-//   * a 3-slot ring of stages (24 KiB each).  Iteration s (one barrier):
-//        wait (own DMA of stage s+1) · barrier
-//        24 MFMAs on the fragments of stage s (registers), interleaved one by
-//        one with the DMA of stage s+3 into slot s%3 (freed by the barrier)
-//        and the ds_reads of stage s+1's fragments (other register set);
-//     each DMA has two iterations to land;
-//   * the LDS image is lane-linear per fragment; the bank swizzle (the two
-//     16-B halves of column r swapped when bit 3 of r is set) is applied on
-//     the DMA's per-lane SOURCE address and on the ds_read address, so the
-//     fragment reads are conflict-free;
-//   * the scale-block scales ride along (two 256-B DMAs per wave and stage,
-//     into a per-block double buffer: every stage of a block rewrites the same
-//     wave-private values);
-//   * f32 running sums in wave-private LDS (as k_gram8d).
-// Selected by OCM_GRAM8_VARIANT=shared.
-// ---------------------------------------------------------------------------
-constexpr int G8S_FRAG = 1024;                       // one 32-col × 32-row digit fragment
-constexpr int G8S_OPS = 2 * 3 * 4 * G8S_FRAG;        // [A|B][digit][32-col block] = 24 KiB
-constexpr int G8S_SCL = 2 * 4 * 512;                 // [block & 1][wave][row | column scales]
-
-// LDS-DMA with a scalar (wave-uniform) 64-bit base and a per-lane 32-bit
-// offset; M0 = the wave-uniform LDS destination (written in the same asm
-// statement: the compiler owns M0 otherwise).  Invisible to the compiler's
-// vmcnt bookkeeping: the kernel counts these itself.
-__device__ __forceinline__ void g8s_dma16(uint64_t sbase, uint32_t voff, uint32_t lds) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(lds)
-      : "memory");
-}
-__device__ __forceinline__ void g8s_dma4(uint64_t sbase, uint32_t voff, uint32_t lds) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(lds)
-      : "memory");
-}
-
-// ABL: timing ablations (results wrong): 1 no DMA in the loop, 2 no fragment reads, 8 no flush
-template <int NS, int ABL = 0>
-__global__ __launch_bounds__(256, 1) void k_gram8s(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
-                                                   float* __restrict__ part) {
-  __shared__ __attribute__((aligned(1024))) char lds[NS * G8S_OPS + G8S_SCL];
-
-  const int b = blockIdx.x;
-  const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
-  const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
-  const int chunk = wg / ntiles;
-  const int tile = wg - chunk * ntiles;
-  int ti, tj;
-  tile_coords(tile, nt, ti, tj);
-  const int I = ti * Q8T, J = tj * Q8T;
-  int s = 0;
-  while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
-  const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
-  const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
-  const int nb = (int)((r1 - r0 + Q8BLK - 1) / Q8BLK);  // whole (zero-filled) scale blocks
-  const int nstg = nb * Q8SPB;                          // even (Q8SPB = 24)
-  const size_t gbase = (size_t)chunk * (st.chunk_rows / Q8K);
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int l31 = lane & 31, h = lane >> 5;
-  const size_t gstride = (size_t)q.P8 * 32;  // bytes per 32-row group and plane
-
-  // DMA role: wave w copies operand (w >> 1), digit/column-block pairs
-  // 6(w & 1) .. +5 of the 12; the swizzle on the source: LDS slot 2r + h'
-  // holds column r, half h' ^ bit3(r)
-  const int op_dma = wave >> 1, part_dma = wave & 1;
-  const uint32_t srcoff = (uint32_t)(lane >> 1) * 32 + 16 * ((lane & 1) ^ ((lane >> 4) & 1));
-  const uint64_t dma_base = (uint64_t)(uintptr_t)q.digits + gbase * gstride + (uint64_t)(op_dma ? J : I) * 32;
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds);
-  const uint64_t scl_base = (uint64_t)(uintptr_t)(q.scale + (size_t)chunk * q.nblk * q.P8);
-  const int srow0 = I + wm * 64, scol0 = J + wn * 64;
-  char* const sclw = lds + NS * G8S_OPS + wave * 512;  // + (blk & 1) * 2048
-
-  // DMA number i (< 8) of stage stg into its slot
-  auto dma = [&](int i, int stg) __attribute__((always_inline)) {
-    const int slot = stg % NS;
-    if (i < 6) {
-      const int f = 6 * part_dma + i, dg = f >> 2, x = f & 3;
-      g8s_dma16(dma_base + (uint64_t)stg * gstride + dg * q.plane + x * G8S_FRAG, srcoff,
-                lds0 + slot * G8S_OPS + ((op_dma * 3 + dg) * 4 + x) * G8S_FRAG);
-    } else {
-      const int blk = stg / Q8SPB;
-      const uint32_t sc = lds0 + NS * G8S_OPS + ((blk & 1) * 4 + wave) * 512 + (i - 6) * 256;
-      g8s_dma4(scl_base + ((uint64_t)blk * q.P8 + (i == 6 ? srow0 : scol0)) * 4, lane * 4, sc);
-    }
-  };
-  // fragment read: lane (r, h) ← 16 B at swizzled slot 2r + (h ^ bit3(r))
-  const int rdoff = 16 * (2 * l31 + (h ^ ((l31 >> 3) & 1)));
-  // fragment j (< 12) of stage stg: A (x, dg) for j < 6, B for j ≥ 6
-  auto frag = [&](int j, int stg) __attribute__((always_inline)) -> i32x4 {
-    const int op = j / 6, x = (j % 6) / 3, dg = j % 3;
-    const int xb = 2 * (op ? wn : wm) + x;
-    return *reinterpret_cast<const i32x4*>(lds + (stg % NS) * G8S_OPS + ((op * 3 + dg) * 4 + xb) * G8S_FRAG +
-                                           rdoff);
-  };
-
-  i32x16 acc1[2][2], acc2[2][2], acc3[2][2];
-  float run[2][2][16];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      acc1[a][c] = i32x16{};
-      acc2[a][c] = i32x16{};
-      acc3[a][c] = i32x16{};
-#pragma unroll
-      for (int r = 0; r < 16; ++r) run[a][c][r] = 0.f;
-    }
-  // MFMA number i (< 24): sub-block (a, c) = i / 6, product i % 6
-  auto mfma = [&](int i, const i32x4 (&F)[12]) __attribute__((always_inline)) {
-    const int a = (i / 6) >> 1, c = (i / 6) & 1, k = i % 6;
-    const i32x4 A0 = F[a * 3 + 0], A1 = F[a * 3 + 1], A2 = F[a * 3 + 2];
-    const i32x4 B0 = F[6 + c * 3 + 0], B1 = F[6 + c * 3 + 1], B2 = F[6 + c * 3 + 2];
-    if (k == 0) acc1[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A0, B0, acc1[a][c], 0, 0, 0);
-    if (k == 1) acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A0, B1, acc2[a][c], 0, 0, 0);
-    if (k == 2) acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A1, B0, acc2[a][c], 0, 0, 0);
-    if (k == 3) acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A0, B2, acc3[a][c], 0, 0, 0);
-    if (k == 4) acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A2, B0, acc3[a][c], 0, 0, 0);
-    if (k == 5) acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A1, B1, acc3[a][c], 0, 0, 0);
-  };
-  auto flush = [&](int blk) __attribute__((always_inline)) {
-    constexpr float w2 = 1.f / 254.f, w3 = 1.f / (254.f * 254.f);
-    const float* scl = reinterpret_cast<const float*>(sclw + (blk & 1) * 2048);
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const float sj = scl[64 + c * 32 + l31];
-#pragma unroll
-      for (int a = 0; a < 2; ++a) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          // rows of registers 4g..4g+3: a·32 + 8g + 4h + 0..3
-          const f32x4 si = *reinterpret_cast<const f32x4*>(&scl[a * 32 + 8 * g + 4 * h]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * g + e;
-            const float v = fmaf((float)acc3[a][c][r], w3, fmaf((float)acc2[a][c][r], w2, (float)acc1[a][c][r]));
-            run[a][c][r] = fmaf(v, si[e] * sj, run[a][c][r]);
-          }
-        }
-        acc1[a][c] = i32x16{};
-        acc2[a][c] = i32x16{};
-        acc3[a][c] = i32x16{};
-      }
-    }
-  };
-
-  // one iteration: barrier, then MFMAs of stage stg (fragments FC) with the
-  // DMA of stage stg+3 and the reads of stage stg+1 (into FN) between them
-  auto iter = [&](int stg, const i32x4 (&FC)[12], i32x4 (&FN)[12]) __attribute__((always_inline)) {
-    // own DMAs of stg+1 landed (those of stg+2, 8, may fly) and this wave's
-    // reads of slot stg%3 are done; after the barrier both hold for all waves
-    if constexpr ((ABL & 1) != 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if constexpr (NS == 3) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if constexpr (NS == 4) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if constexpr (NS == 5) asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if constexpr (NS == 6) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const int sd = min(stg + NS, nstg - 1);  // clamped: a duplicate into a dead slot
-    const int sr = min(stg + 1, nstg - 1);
-#pragma unroll
-    for (int i = 0; i < 24; ++i) {
-      mfma(i, FC);
-      if (i < 8 && !(ABL & 1)) dma(i, sd);
-      if (i >= 8 && i < 20 && !(ABL & 2)) FN[i - 8] = frag(i - 8, sr);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (!(ABL & 8) && stg % Q8SPB == Q8SPB - 1) flush(stg / Q8SPB);
-  };
-
-  i32x4 FX[12], FY[12];
-#pragma unroll
-  for (int t = 0; t < NS; ++t)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) dma(i, min(t, nstg - 1));
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // prologue: everything landed
-#pragma unroll
-  for (int j = 0; j < 12; ++j) FX[j] = frag(j, 0);
-  for (int stg = 0; stg < nstg; stg += 2) {
-    iter(stg, FX, FY);
-    iter(stg + 1, FY, FX);
-  }
-  // no LDS-DMA may still be landing when the workgroup's LDS is released
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // strictly-lower quadrant of a diagonal tile: computed (branch-free: a
-  // uniform skip duplicates live ranges) but not written
-  if (ti == tj && wm > wn) return;
-  float* out = part + ((size_t)chunk * ntiles + tile) * (Q8T * Q8T);
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int col = wn * 64 + c * 32 + l31;
-        out[row * Q8T + col] = run[a][c][r];
       }
 }
 
@@ -1339,7 +1372,10 @@ int gram_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, in
   return OCM_OK;
 }
 
-// i8×3 path: quantise (one read of X) → integer-MFMA Gram → f64 reduce.
+// i8×3 path: thresholds → quantise (one read of X, outlier screen) →
+// integer-MFMA Gram → f64 reduce → (marked rows only) exact fix-up.
+// Returns OCM_OK, or 1 when more than n/8 values were screened out: the
+// caller then recomputes the Gram on the FP32-MFMA path.
 int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
                const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
                hipStream_t st, int64_t chunk_rows) {
@@ -1364,14 +1400,43 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   const size_t scale_elems = (size_t)nchunks * nblk * P8;
   const size_t col_elems = (size_t)nchunks * nblk * P8;  // per scale block
   const size_t part_elems = (size_t)nchunks * ntiles * Q8T * Q8T;
-  void* wsp = ocm::workspace(ctx, 3 * plane + scale_elems * 4 + col_elems * 8 + part_elems * 4 + 4 * 4096, st);
+  // guard buffers
+  const int ngrp = P8 / Q8GROUP, fw = (ngrp + 31) / 32;
+  const int64_t nsamp = std::min<int64_t>(n, 4096);
+  const int nsplit = (int)std::min<int64_t>((nsamp + 255) / 256, 16);
+  const int64_t rps = (nsamp + nsplit - 1) / nsplit;
+  const int nfblk = (int)((n + FLAG_BLK - 1) / FLAG_BLK);
+  const size_t guard_bytes = (size_t)P8 * 4 + (size_t)n * fw * 4 + (size_t)p * QX_BINS * 4 + (size_t)nfblk * 4 +
+                             (size_t)n * 8 + 16 * 256;
+  void* wsp = ocm::workspace(ctx, 3 * plane + scale_elems * 4 + col_elems * 8 + part_elems * 4 + guard_bytes +
+                                      4 * 4096, st);
   if (!wsp) return OCM_ERR_NOMEM;
   ocm::Carve cv{static_cast<char*>(wsp)};
   char* digits = cv.take<char>(3 * plane);
   float* scale = cv.take<float>(scale_elems);
   double* colpart = cv.take<double>(col_elems);
   float* part = cv.take<float>(part_elems);
+  float* thr = cv.take<float>(P8);
+  uint32_t* flags = cv.take<uint32_t>((size_t)n * fw);
+  uint32_t* xhist = cv.take<uint32_t>((size_t)p * QX_BINS);
+  uint32_t* fcnt = cv.take<uint32_t>(nfblk);
+  int64_t* flist = cv.take<int64_t>(n);
+  uint32_t* counters = cv.take<uint32_t>(4);  // [0] marks, [1] listed rows
+  auto* host = static_cast<uint32_t*>(ocm::host_staging(ctx, 64));
+  if (!host) return OCM_ERR_NOMEM;
 
+  OCM_HIP(hipMemsetAsync(flags, 0, (size_t)n * fw * 4, st));
+  OCM_HIP(hipMemsetAsync(counters, 0, 16, st));
+  OCM_HIP(hipMemsetAsync(xhist, 0, (size_t)p * QX_BINS * 4, st));
+  hipLaunchKernelGGL(k_colexp_hist, dim3((p + 63) / 64, nsplit), dim3(256), 0, st, X, ldx, rows, nsamp, p, shift, rps,
+                     xhist);
+  hipLaunchKernelGGL(k_q8_thresholds, dim3(1), dim3(1024), 0, st, xhist, nsamp, p, P8, thr);
+  OCM_CHECK_LAUNCH("k_q8_thresholds");
+
+  // all quantiser launches first, then the mark count is read back while the
+  // Gram runs
+  std::vector<SegTable> tabs;
+  std::vector<int> tab_s0;
   for (int s0 = 0; s0 < nseg; s0 += MAXSEG) {
     const int s1 = std::min(nseg, s0 + MAXSEG);
     SegTable tab{};
@@ -1383,51 +1448,55 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     }
     const int64_t gchunks = cprefix[s1] - cprefix[s0];
     if (gchunks == 0) continue;
-    const int64_t total = gchunks * ntiles;
-    OCM_REQUIRE(total < (1LL << 31) && gchunks < 65536 * 1024LL, "ocm_gram_f32: too many workgroups");
+    OCM_REQUIRE(gchunks * ntiles < (1LL << 31) && gchunks < 65536 * 1024LL, "ocm_gram_f32: too many workgroups");
+    tabs.push_back(tab);
+    tab_s0.push_back(s0);
+  }
+  auto plan_for = [&](int s0) {
     Q8Plan q{};
     q.digits = digits + (size_t)cprefix[s0] * chunk_rows * P8;
     q.plane = plane;
     q.scale = scale + (size_t)cprefix[s0] * nblk * P8;
     q.P8 = P8;
     q.nblk = nblk;
-    // timing ablations only (wrong G): bit 0 no digit loads, 1 no fragment reads, 2 no MFMA, 3 no flush,
-    // 4 no LDS stores of the stage
-    q.noload = std::getenv("OCM_GRAM8_NOLOAD") ? std::atoi(std::getenv("OCM_GRAM8_NOLOAD")) : 0;
-    double* col_g = colpart + (size_t)cprefix[s0] * nblk * P8;
-    float* pg = part + (size_t)cprefix[s0] * ntiles * Q8T * Q8T;
-    {
-      ocm::TimedRegion tq(ctx, OCM_KERNEL_QUANT, st);
+    q.thr = thr;
+    q.flags = flags;
+    q.fw = fw;
+    q.nmark = counters;
+    return q;
+  };
+  {
+    ocm::TimedRegion tq(ctx, OCM_KERNEL_QUANT, st);
+    for (size_t t = 0; t < tabs.size(); ++t) {
+      const int s0 = tab_s0[t];
+      const int64_t gchunks = cprefix[s0 + tabs[t].nseg] - cprefix[s0];
+      const Q8Plan q = plan_for(s0);
+      double* col_g = colpart + (size_t)cprefix[s0] * nblk * P8;
       dim3 gq((unsigned)(gchunks * nblk), (unsigned)(P8 / Q8QC));
       if (rows)
-        hipLaunchKernelGGL(k_q8_quant<true>, gq, dim3(Q8QT), 0, st, X, ldx, rows, p, shift, tab, q, col_g);
+        hipLaunchKernelGGL(k_q8_quant<true>, gq, dim3(Q8QT), 0, st, X, ldx, rows, p, shift, tabs[t], q, col_g);
       else
-        hipLaunchKernelGGL(k_q8_quant<false>, gq, dim3(Q8QT), 0, st, X, ldx, rows, p, shift, tab, q, col_g);
-      OCM_CHECK_LAUNCH("k_q8_quant");
+        hipLaunchKernelGGL(k_q8_quant<false>, gq, dim3(Q8QT), 0, st, X, ldx, rows, p, shift, tabs[t], q, col_g);
     }
-    {
-      ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
-      // "direct" (default: k_gram8d, register fragments, no LDS stage) or "shared" (k_gram8s, LDS panels)
-      const char* v = std::getenv("OCM_GRAM8_VARIANT");
-      const std::string var = v ? v : "";
-      if (var.rfind("shared", 0) == 0) {
-        // shared[N]: N-slot LDS ring (default 4); OCM_GRAM8_NOLOAD = timing ablations (wrong G)
-        const int ns = var.size() > 6 ? std::atoi(var.c_str() + 6) : 4;
-        const dim3 g8((unsigned)total), b8(256);
-#define OCM_G8S(N_, A_) hipLaunchKernelGGL((k_gram8s<N_, A_>), g8, b8, 0, st, q, tab, nt, ntiles, (int)total, pg)
-        if (q.noload == 1) OCM_G8S(4, 1);
-        else if (q.noload == 2) OCM_G8S(4, 2);
-        else if (q.noload == 8) OCM_G8S(4, 8);
-        else if (q.noload == 9) OCM_G8S(4, 9);
-        else if (ns == 3) OCM_G8S(3, 0);
-        else if (ns == 5) OCM_G8S(5, 0);
-        else if (ns == 6) OCM_G8S(6, 0);
-        else OCM_G8S(4, 0);
-#undef OCM_G8S
-      } else
-        hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tab, nt, ntiles, (int)total, pg);
-      OCM_CHECK_LAUNCH("k_gram8");
-    }
+    OCM_CHECK_LAUNCH("k_q8_quant");
+  }
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  OCM_HIP(hipStreamIsCapturing(st, &cap));
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  if (!capturing) OCM_HIP(hipMemcpyAsync(host, counters, 4, hipMemcpyDeviceToHost, st));
+  hipEvent_t ev = nullptr;
+  if (!capturing) {
+    OCM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    OCM_HIP(hipEventRecord(ev, st));
+  }
+  for (size_t t = 0; t < tabs.size(); ++t) {
+    const int s0 = tab_s0[t];
+    const int64_t total = (cprefix[s0 + tabs[t].nseg] - cprefix[s0]) * ntiles;
+    const Q8Plan q = plan_for(s0);
+    float* pg = part + (size_t)cprefix[s0] * ntiles * Q8T * Q8T;
+    ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
+    hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, pg);
+    OCM_CHECK_LAUNCH("k_gram8d");
   }
   for (int s = 0; s < nseg; ++s) {
     double* Gs = G_out + (size_t)s * p * p;
@@ -1446,7 +1515,50 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     OCM_CHECK_LAUNCH("k_colblk_sum");
     OCM_CHECK_LAUNCH("k_gram_reduce");
   }
+  uint32_t marks = 1;  // capturing: the fix-up runs on device-side counts
+  if (!capturing) {
+    const hipError_t e = hipEventSynchronize(ev);
+    (void)hipEventDestroy(ev);
+    if (e != hipSuccess) return ocm::fail(OCM_ERR_HIP, std::string("gram mark read-back: ") + hipGetErrorString(e));
+    marks = host[0];
+    ctx->last_gram_marks = marks;
+    if (marks == 0) return OCM_OK;
+    if ((int64_t)marks > n / 8) return 1;
+  }
+  hipLaunchKernelGGL(k_flag_count, dim3(nfblk), dim3(256), 0, st, flags, fw, n, fcnt);
+  hipLaunchKernelGGL(k_flag_emit, dim3(nfblk), dim3(256), 0, st, flags, fw, n, fcnt, nfblk, flist, counters + 1);
+  OCM_CHECK_LAUNCH("k_flag_emit");
+  const int nt64 = (p + FX_T - 1) / FX_T;
+  for (int s0 = 0; s0 < nseg; s0 += MAXSEG) {
+    const int s1 = std::min(nseg, s0 + MAXSEG);
+    FixSeg fs{};
+    fs.nseg = s1 - s0;
+    for (int s = s0; s <= s1; ++s) fs.begin[s - s0] = seg_offsets[s];
+    hipLaunchKernelGGL(k_gram_fixup, dim3(nt64 * (nt64 + 1) / 2, s1 - s0), dim3(256), 0, st, X, ldx, rows, p, shift,
+                       fs, flist, counters + 1, flags, fw, nt64, G_out + (size_t)s0 * p * p);
+  }
+  OCM_CHECK_LAUNCH("k_gram_fixup");
   return OCM_OK;
+}
+
+int gram_dispatch(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                  const float* shift, const int64_t* seg_offsets, int32_t nseg, int32_t mode, int64_t chunk_rows,
+                  double* G_out, double* colsum_out, hipStream_t st) {
+  if (p <= SMALL_P) return gram_small(ctx, X, ldx, rows, p, shift, seg_offsets, nseg, G_out, colsum_out, st);
+  if (mode == OCM_GRAM_I8X3) {
+    const int rc = gram_impl8(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows);
+    if (rc != 1) return rc;
+    mode = OCM_GRAM_F32;  // too many screened values: recompute on FP32 MFMA
+  }
+  // f32 accumulation length per partial: short chunks keep the tiles of one
+  // chunk co-resident on an XCD (L2 reuse) and the tail short; the partial
+  // buffer is capped at 512 chunks (≈4.7 GB for p = 2048).
+  const int64_t cr = chunk_rows > 0 ? std::max<int64_t>(64, chunk_rows) : std::max<int64_t>(2048, (n + 511) / 512);
+  if (mode == OCM_GRAM_BF16X3)
+    return gram_impl<256, 32>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, cr, true);
+  if (p > 128)
+    return gram_impl<256, 32>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, cr);
+  return gram_impl<128, 32>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, cr);
 }
 
 }  // namespace
@@ -1473,46 +1585,30 @@ int ocm_colmean_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* ro
   return OCM_OK;
 }
 
-int ocm_gram_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
-                 const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
-                 void* stream) {
+int ocm_gram_f32_ex(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                    const float* shift, const int64_t* seg_offsets, int32_t nseg, int32_t mode, int64_t chunk_rows,
+                    double* G_out, double* colsum_out, void* stream) {
   OCM_REQUIRE(ctx && X && shift && seg_offsets && G_out && colsum_out, "ocm_gram_f32: NULL argument");
   OCM_REQUIRE(n > 0 && p > 0 && ldx >= p && nseg > 0, "ocm_gram_f32: bad shape");
   OCM_REQUIRE(seg_offsets[0] == 0 && seg_offsets[nseg] == n, "ocm_gram_f32: seg_offsets must span [0, n]");
+  OCM_REQUIRE(mode == OCM_GRAM_I8X3 || mode == OCM_GRAM_F32 || mode == OCM_GRAM_BF16X3, "ocm_gram_f32: bad mode");
   for (int s = 0; s < nseg; ++s)
     OCM_REQUIRE(seg_offsets[s + 1] >= seg_offsets[s], "ocm_gram_f32: seg_offsets not ascending");
-  hipStream_t st = (hipStream_t)stream;
-  if (p <= SMALL_P && !std::getenv("OCM_GRAM_FORCE_MFMA"))
-    return gram_small(ctx, X, ldx, rows, p, shift, seg_offsets, nseg, G_out, colsum_out, st);
-  // Tile: 256 when p fills at least one 256 block, else 128 (less padding).
-  // OCM_GRAM_TILE / OCM_GRAM_CHUNK override for A/B runs.
-  int tile = p > 128 ? 256 : 128;
-  int bk = 32;
-  // f32 accumulation length per partial: short chunks keep the tiles of one
-  // chunk co-resident on an XCD (L2 reuse) and the tail short; the partial
-  // buffer is capped at 512 chunks (≈4.7 GB for p = 2048).
-  int64_t chunk_rows = std::max<int64_t>(2048, (n + 511) / 512);
-  if (const char* e = std::getenv("OCM_GRAM_TILE")) tile = std::atoi(e) == 128 ? 128 : 256;
-  if (const char* e = std::getenv("OCM_GRAM_BK")) bk = std::atoi(e) == 16 ? 16 : 32;
-  if (const char* e = std::getenv("OCM_GRAM_CHUNK")) chunk_rows = std::max<int64_t>(64, std::atoll(e));
-  // OCM_GRAM_MODE: "i8x3" (default: int8 digit split on integer MFMA, exact
-  // accumulation), "bf16x3" (3-level bf16 split on bf16 MFMA) or "f32" (FP32 MFMA)
-  std::string mode = "i8x3";
-  if (const char* e = std::getenv("OCM_GRAM_MODE")) mode = e;
-  if (mode == "i8x3") {
-    const char* e = std::getenv("OCM_GRAM_CHUNK");
-    return gram_impl8(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st,
-                      e ? std::atoll(e) : 0);
-  }
-  const bool split3 = mode != "f32";
-  if (split3)
-    return gram_impl<256, 32>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows,
-                              true);
-  if (tile == 256 && bk == 32)
-    return gram_impl<256, 32>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows);
-  if (tile == 256)
-    return gram_impl<256, 16>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows);
-  return gram_impl<128, 32>(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows);
+  return gram_dispatch(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, mode, chunk_rows, G_out, colsum_out,
+                       (hipStream_t)stream);
+}
+
+int ocm_gram_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                 const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
+                 void* stream) {
+  return ocm_gram_f32_ex(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, OCM_GRAM_I8X3, 0, G_out, colsum_out,
+                         stream);
+}
+
+int ocm_gram_last_marks(ocm_ctx* ctx, int64_t* marks_out) {
+  OCM_REQUIRE(ctx && marks_out, "ocm_gram_last_marks: NULL argument");
+  *marks_out = (int64_t)ctx->last_gram_marks;
+  return OCM_OK;
 }
 
 int ocm_cov_from_gram(ocm_ctx* ctx, const double* const* G_list, const double* const* colsum_list,

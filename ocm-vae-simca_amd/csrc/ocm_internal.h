@@ -18,6 +18,7 @@ struct ocm_ctx {
   void* host_pinned = nullptr;  // small pinned staging area for D2H scalars
   size_t host_bytes = 0;
   int num_cus = 256;
+  uint32_t last_gram_marks = 0;  // outlier-guard marks of the last i8×3 Gram (ocm_gram_last_marks)
   // live kernel timing (ocm_ctx_set_timing): event pairs per timed kernel
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[OCM_TIMED_KERNELS];

@@ -5,12 +5,9 @@
 // (predict + decision), sklearn/decomposition/_base.py:147-153,197
 // (transform / inverse_transform), vae_model.py:164.
 //
-// Three kernels share one epilogue (T², Q, fused decision, moments):
-//   k_score_direct (default)  f32 MFMA, each wave streams its 32 rows from
-//       HBM straight into operand registers; loadings/mean in LDS blocks.
-//   k_score                   f32 MFMA, row tiles staged through LDS.
-//   k_score_f64               one pass, f64 MFMA, Q = ‖d‖² − ‖t‖².
-// The f32 kernels run two sweeps over the row's columns:
+// k_score_direct: f32 MFMA, each wave streams its 32 rows from HBM straight
+// into operand registers; loadings / mean in LDS blocks.  Two sweeps over the
+// row's columns:
 //   sweep 1  Tᵀ (comps × rows) += P_chunk · D_chunkᵀ        v_mfma_f32_32x32x2_f32
 //   sweep 2  Rᵀ (cols × rows)   = P_chunkᵀ · Tᵀ → r = d − R, q += r²
 // Sweep 2 feeds the sweep-1 accumulator registers straight back as the B
@@ -18,16 +15,12 @@
 // Q is the explicit residual (first-order insensitive to error in t, unlike
 // the ‖d‖² − ‖t‖² identity, which f32 accumulation cannot afford).  T is
 // flushed to f64 every chunk.
-#include <cstdlib>
-#include <string>
-
 #include "ocm_internal.h"
 
 namespace {
 
 constexpr int SW = 4;   // waves per workgroup
 constexpr int SR = 32;  // spectra per wave
-constexpr int SC = 64;  // wavelengths per chunk
 constexpr int SROWS = SW * SR;
 
 struct DecArgs {
@@ -104,164 +97,6 @@ __device__ __forceinline__ void score_epilogue(double* tls, double* sred, const 
       stat_part[(int64_t)blockIdx.x * 4 + tid] = v;
     }
   }
-}
-
-template <int KT, bool VEC>
-__global__ __launch_bounds__(256) void k_score(const float* __restrict__ X, int64_t ldx,
-                                               const int64_t* __restrict__ rows, int64_t m, int p,
-                                               const float* __restrict__ P, const float* __restrict__ mu,
-                                               const double* __restrict__ A, int k, int a_diag,
-                                               float* __restrict__ T_out, double* __restrict__ T2_out,
-                                               float* __restrict__ Q_out, DecArgs dec, double* __restrict__ acc_out,
-                                               int64_t acc_stride, double* __restrict__ stat_part) {
-  constexpr int KP = KT * 32;
-  constexpr int D_FLOATS = SW * SR * (SC + 1);
-  constexpr int P_FLOATS = KP * (SC + 1);
-  constexpr int MAIN_BYTES = (D_FLOATS + P_FLOATS) * 4;
-  constexpr int EPI_BYTES = SW * SR * (KP + 1) * 8;
-  constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-  __shared__ double sred[SW][4];
-  float* Ds = reinterpret_cast<float*>(smem);
-  float* Ps = Ds + D_FLOATS;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l31 = lane & 31, h = lane >> 5;
-  const int64_t row0 = (int64_t)blockIdx.x * SROWS + wave * SR;
-  float* Dw = Ds + wave * SR * (SC + 1);
-
-  // loaders: D chunk — lane → (row = 4j + lane/16, col4 = (lane%16)*4), j < 8
-  const int dcol = (lane & 15) * 4, drow = lane >> 4;
-  int64_t srow[8];
-  unsigned rmask = 0;  // bit j: row j of this lane's loader set is real
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int64_t g = row0 + 4 * j + drow;
-    const bool ok = g < m;
-    rmask |= ok ? (1u << j) : 0u;
-    const int64_t gc = ok ? g : m - 1;  // clamp: always a valid address
-    srow[j] = rows ? rows[gc] : gc;
-  }
-  // P chunk — thread → (comp = e/16, col4 = (e%16)*4), e = tid + 256·i
-  constexpr int PV = KP * SC / 4 / 256;  // float4 per thread (2 or 4)
-
-  // Branch-free prefetch (clamped addresses, loads left in flight); the mean
-  // subtraction and the row / column / component masks are applied in
-  // sstore, after the MFMAs that hide the loads.
-  f32x4 rd[8], rp[PV], rmu;
-  auto ld4 = [&](const float* base, int col) -> f32x4 {
-    if (VEC) return *reinterpret_cast<const f32x4*>(base + (col < p ? col : 0));
-    f32x4 v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = base[min(col + e, p - 1)];
-    return v;
-  };
-  auto gload = [&](int c0) {
-    rmu = ld4(mu, c0 + dcol);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) rd[j] = ld4(X + srow[j] * ldx, c0 + dcol);
-#pragma unroll
-    for (int i = 0; i < PV; ++i) {
-      const int e = tid + 256 * i;
-      const int comp = e >> 4, col = (e & 15) * 4;
-      rp[i] = ld4(P + (int64_t)min(comp, k - 1) * p, c0 + col);
-    }
-  };
-  auto sstore = [&](int c0) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float* d = Dw + (4 * j + drow) * (SC + 1) + dcol;
-      const bool rv = (rmask >> j) & 1u;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) d[e] = (rv && c0 + dcol + e < p) ? rd[j][e] - rmu[e] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < PV; ++i) {
-      const int e = tid + 256 * i;
-      const int comp = e >> 4, col = (e & 15) * 4;
-      float* d = Ps + comp * (SC + 1) + col;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) d[q] = (comp < k && c0 + col + q < p) ? rp[i][q] : 0.f;
-    }
-  };
-
-  const int nchunk = (p + SC - 1) / SC;
-  f32x16 accT[KT];
-  double accT64[KT][16];
-#pragma unroll
-  for (int t = 0; t < KT; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      accT[t][r] = 0.f;
-      accT64[t][r] = 0.0;
-    }
-
-  // ---- sweep 1: projection ------------------------------------------------
-  gload(0);
-  for (int c = 0; c < nchunk; ++c) {
-    __syncthreads();  // previous chunk's LDS reads are done
-    sstore(c * SC);
-    __syncthreads();
-    if (c + 1 < nchunk) gload((c + 1) * SC);
-#pragma unroll
-    for (int s = 0; s < SC / 2; ++s) {
-      const float b = Dw[l31 * (SC + 1) + 2 * s + h];
-#pragma unroll
-      for (int t = 0; t < KT; ++t) {
-        const float a = Ps[(t * 32 + l31) * (SC + 1) + 2 * s + h];
-        accT[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, accT[t], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < KT; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        accT64[t][r] += (double)accT[t][r];
-        accT[t][r] = 0.f;
-      }
-  }
-
-  // T back to f32 as the sweep-2 B operand
-#pragma unroll
-  for (int t = 0; t < KT; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) accT[t][r] = (float)accT64[t][r];
-
-  // ---- sweep 2: reconstruction residual ------------------------------------
-  double q64 = 0.0;
-  gload(0);
-  for (int c = 0; c < nchunk; ++c) {
-    __syncthreads();
-    sstore(c * SC);
-    __syncthreads();
-    if (c + 1 < nchunk) gload((c + 1) * SC);
-    float qc = 0.f;
-#pragma unroll
-    for (int cb = 0; cb < SC / 32; ++cb) {
-      f32x16 accR;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) accR[r] = 0.f;
-#pragma unroll
-      for (int t = 0; t < KT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int comp = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float a = Ps[comp * (SC + 1) + cb * 32 + l31];
-          accR = __builtin_amdgcn_mfma_f32_32x32x2f32(a, accT[t][r], accR, 0, 0, 0);
-        }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int col = cb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float d = Dw[l31 * (SC + 1) + col] - accR[r];
-        qc += d * d;
-      }
-    }
-    q64 += (double)qc;
-  }
-  q64 += __shfl_xor(q64, 32, 64);
-
-  score_epilogue<KT, SW>(reinterpret_cast<double*>(smem), &sred[0][0], accT64, q64, row0, m, k, a_diag, A, T_out,
-                         T2_out, Q_out, dec, acc_out, acc_stride, stat_part);
 }
 
 // ---------------------------------------------------------------------------
@@ -439,168 +274,6 @@ __global__ __launch_bounds__(256, 2) void k_score_direct(const float* __restrict
                          Q_out, dec, acc_out, acc_stride, stat_part);
 }
 
-// ---------------------------------------------------------------------------
-// k_score_f64 — single-pass scoring on FP64 MFMA (v_mfma_f64_16x16x4_f64).
-// d = (double)x − μ is exact; t = P·d accumulates in f64 (≈1e-15 relative),
-// so the orthogonal distance can use the norm identity Q = ‖d‖² − ‖t‖²
-// (P has orthonormal rows) with no catastrophic loss — X is read ONCE (the
-// f32 kernels need a second, explicit-residual sweep).  A wave owns 16 rows;
-// lane (row = lane&15, q = lane>>4) streams columns 16q … 16q+15 of every
-// 64-column chunk of its row (K order permuted identically for P and d).
-// Loadings (f64) and mean (f64) are staged per workgroup in 256-column LDS
-// blocks.  KT16 = number of 16-component MFMA tiles (k ≤ 16·KT16).
-// ---------------------------------------------------------------------------
-typedef double f64x4_t __attribute__((ext_vector_type(4)));
-constexpr int FR = 16;  // rows per wave
-constexpr int FPB = 256;
-
-template <int KT16, bool VEC>
-__global__ __launch_bounds__(256, 2) void k_score_f64(const float* __restrict__ X, int64_t ldx,
-                                                      const int64_t* __restrict__ rows, int64_t m, int p,
-                                                      const double* __restrict__ P, const double* __restrict__ mu,
-                                                      const double* __restrict__ A, int k, int a_diag,
-                                                      float* __restrict__ T_out, double* __restrict__ T2_out,
-                                                      float* __restrict__ Q_out, DecArgs dec,
-                                                      double* __restrict__ acc_out, int64_t acc_stride,
-                                                      double* __restrict__ stat_part) {
-  constexpr int KP = 16 * KT16;
-  constexpr int PS = FPB + 1;  // odd stride (doubles): conflict-free ds_read_b64 across comps and q
-  constexpr int MAIN_D = KP * PS + FPB;
-  constexpr int EPI_D = SW * FR * (KP + 1);
-  __shared__ double smem[MAIN_D > EPI_D ? MAIN_D : EPI_D];
-  __shared__ double sred[SW * 4];
-  double* Pl = smem;
-  double* Ml = smem + KP * PS;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int j16 = lane & 15, q = lane >> 4;
-  const int64_t row0 = (int64_t)blockIdx.x * (SW * FR) + wave * FR;
-  const int64_t grow = row0 + j16;
-  const double rowmask = grow < m ? 1.0 : 0.0;
-  const int64_t gcl = grow < m ? grow : m - 1;
-  const float* xrow = X + (rows ? rows[gcl] : gcl) * ldx;
-
-  auto ld4 = [&](int col) -> f32x4 {
-    if (VEC) return *reinterpret_cast<const f32x4*>(xrow + (col < p ? col : 0));
-    f32x4 v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = xrow[min(col + e, p - 1)];
-    return v;
-  };
-  auto stage = [&](int b0) {
-    __syncthreads();
-    for (int e = tid; e < KP * FPB; e += 256) {
-      const int comp = e / FPB, c = e % FPB;
-      Pl[comp * PS + c] = (comp < k && b0 + c < p) ? P[(int64_t)comp * p + b0 + c] : 0.0;
-    }
-    for (int c = tid; c < FPB; c += 256) Ml[c] = b0 + c < p ? mu[b0 + c] : 0.0;
-    __syncthreads();
-  };
-
-  f64x4_t acc[KT16];
-#pragma unroll
-  for (int t = 0; t < KT16; ++t) acc[t] = (f64x4_t){0.0, 0.0, 0.0, 0.0};
-  double dsq = 0.0;
-
-  struct SD {
-    f32x4 d[4];
-  };
-  auto load = [&](SD& S, int c0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) S.d[i] = ld4(c0 + 16 * q + 4 * i);
-  };
-  auto comp = [&](const SD& S, int c0, int b0) {
-    const int lc = c0 - b0 + 16 * q;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int s = 4 * i + e;
-        // padded columns: μ = 0 and P = 0 there; the mask keeps ‖d‖² clean
-        const double cm = (c0 + 16 * q + s < p) ? rowmask : 0.0;
-        const double dv = ((double)S.d[i][e] - Ml[lc + s]) * cm;
-        dsq = fma(dv, dv, dsq);
-#pragma unroll
-        for (int t = 0; t < KT16; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(Pl[(t * 16 + j16) * PS + lc + s], dv, acc[t], 0, 0, 0);
-      }
-  };
-  for (int b0 = 0; b0 < p; b0 += FPB) {
-    stage(b0);
-    const int bend = min(b0 + FPB, p);
-    SD SA, SB;
-    load(SA, b0);
-    for (int c0 = b0; c0 < bend; c0 += 128) {
-      load(SB, c0 + 64);
-      comp(SA, c0, b0);
-      if (c0 + 128 < bend) load(SA, c0 + 128);
-      if (c0 + 64 < bend) comp(SB, c0 + 64, b0);
-    }
-  }
-
-  // acc[t][r] = t_{16t + q + 4r} of row (lane & 15); rows shared by lanes j, j+16, j+32, j+48
-  double tsq = 0.0;
-#pragma unroll
-  for (int t = 0; t < KT16; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) tsq += acc[t][r] * acc[t][r];
-  tsq += __shfl_xor(tsq, 16, 64);
-  tsq += __shfl_xor(tsq, 32, 64);
-  dsq += __shfl_xor(dsq, 16, 64);
-  dsq += __shfl_xor(dsq, 32, 64);
-  const double Qv = fmax(dsq - tsq, 0.0);
-
-  // gather t rows through LDS (f64) for T², T_out
-  __syncthreads();
-  double* Tt = smem + wave * FR * (KP + 1);
-#pragma unroll
-  for (int t = 0; t < KT16; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) Tt[j16 * (KP + 1) + 16 * t + q + 4 * r] = acc[t][r];
-  __syncthreads();
-  const bool own = (q == 0) && (grow < m);
-  double T2 = 0.0;
-  if (own) {
-    const double* trow = Tt + j16 * (KP + 1);
-    if (a_diag) {
-      for (int a = 0; a < k; ++a) T2 += trow[a] * trow[a] * A[a * k + a];
-    } else {
-      for (int a = 0; a < k; ++a) {
-        double sacc = 0.0;
-        for (int b = 0; b < k; ++b) sacc += A[a * k + b] * trow[b];
-        T2 += trow[a] * sacc;
-      }
-    }
-    if (T_out)
-      for (int a = 0; a < k; ++a) T_out[grow * k + a] = (float)trow[a];
-    if (T2_out) T2_out[grow] = T2;
-    if (Q_out) Q_out[grow] = (float)Qv;
-    if (dec.enabled) {
-      const double dr = dred_of(dec.type, T2 * dec.t2_scale, (double)(float)Qv * dec.q_scale);
-      acc_out[grow * acc_stride] = dr < dec.dlim ? 1.0 : 0.0;
-    }
-  }
-  if (stat_part) {
-    const double qf = (double)(float)Qv;
-    double s0 = own ? T2 : 0.0, s1 = own ? T2 * T2 : 0.0, s2 = own ? qf : 0.0, s3 = own ? qf * qf : 0.0;
-    s0 = wave_sum_f64(s0);
-    s1 = wave_sum_f64(s1);
-    s2 = wave_sum_f64(s2);
-    s3 = wave_sum_f64(s3);
-    if (lane == 0) {
-      sred[wave * 4 + 0] = s0;
-      sred[wave * 4 + 1] = s1;
-      sred[wave * 4 + 2] = s2;
-      sred[wave * 4 + 3] = s3;
-    }
-    __syncthreads();
-    if (tid < 4) {
-      double v = 0.0;
-      for (int w = 0; w < SW; ++w) v += sred[w * 4 + tid];
-      stat_part[(int64_t)blockIdx.x * 4 + tid] = v;
-    }
-  }
-}
-
 __global__ __launch_bounds__(1024) void k_stats_reduce(const double* __restrict__ part, int64_t nblk,
                                                        double* __restrict__ out) {
   // 16 waves: wave w sums column w & 3 over row slice w >> 2 (4 slices), four
@@ -675,36 +348,22 @@ int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
     if (stats_out) OCM_HIP(hipMemsetAsync(stats_out, 0, 4 * sizeof(double), st));
     return OCM_OK;
   }
-  // variant: "direct" (f32 MFMA, two register-streamed sweeps; default),
-  // "f64" (single pass, FP64 MFMA, norm identity) or "lds" (f32, LDS tiles);
-  // OCM_SCORE_VARIANT overrides for A/B runs.  Measured on MI355X at
-  // 1M×2048, k=20: direct 3.61 ms, lds 4.08 ms, f64 4.25 ms (profiles/).
-  int variant = 1;
-  if (const char* e = std::getenv("OCM_SCORE_VARIANT")) {
-    const std::string v(e);
-    variant = v == "f64" ? 0 : (v == "lds" ? 2 : 1);
-  }
-  const int64_t rows_per_blk = variant == 0 ? (int64_t)SW * FR : (int64_t)SROWS;
+  const int64_t rows_per_blk = SROWS;
   const int64_t nblk = (m + rows_per_blk - 1) / rows_per_blk;
   OCM_REQUIRE(nblk < (1LL << 31), "ocm_score_f32: too many rows");
   const size_t part_bytes = stats_out ? (size_t)nblk * 4 * sizeof(double) : 0;
-  const size_t cast_bytes = variant ? ((size_t)k * p + p) * sizeof(float) + 512 : 0;
+  const size_t cast_bytes = ((size_t)k * p + p) * sizeof(float) + 512;
   void* w = ocm::workspace(ctx, part_bytes + cast_bytes + 1024, st);
   if (!w) return OCM_ERR_NOMEM;
   ocm::Carve cv{static_cast<char*>(w)};
   double* part = stats_out ? cv.take<double>((size_t)nblk * 4) : nullptr;
-  const float* P32 = nullptr;
-  const float* mu32 = nullptr;
-  if (variant) {  // f32 kernels take f32 loadings / mean
-    float* pc = cv.take<float>((size_t)k * p);
-    float* mc = cv.take<float>(p);
-    hipLaunchKernelGGL(k_cast_f64_f32, dim3((unsigned)(((int64_t)k * p + 255) / 256)), dim3(256), 0, st, P,
-                       (int64_t)k * p, pc);
-    hipLaunchKernelGGL(k_cast_f64_f32, dim3((p + 255) / 256), dim3(256), 0, st, mu, (int64_t)p, mc);
-    OCM_CHECK_LAUNCH("k_cast_f64_f32");
-    P32 = pc;
-    mu32 = mc;
-  }
+  // the f32 kernel takes f32 loadings / mean
+  float* P32 = cv.take<float>((size_t)k * p);
+  float* mu32 = cv.take<float>(p);
+  hipLaunchKernelGGL(k_cast_f64_f32, dim3((unsigned)(((int64_t)k * p + 255) / 256)), dim3(256), 0, st, P,
+                     (int64_t)k * p, P32);
+  hipLaunchKernelGGL(k_cast_f64_f32, dim3((p + 255) / 256), dim3(256), 0, st, mu, (int64_t)p, mu32);
+  OCM_CHECK_LAUNCH("k_cast_f64_f32");
   const int a_diag = 0;  // general k×k quadratic form (k² FMAs per row are negligible)
   DecArgs d{};
   if (dec) {
@@ -718,30 +377,14 @@ int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
   dim3 g((unsigned)nblk);
   {
     ocm::TimedRegion tr(ctx, OCM_KERNEL_SCORE, st);
-#define OCM_SCORE_LAUNCH(K_, KT_, V_, PP_, MU_)                                                             \
-  hipLaunchKernelGGL((K_<KT_, V_>), g, dim3(256), 0, st, X, ldx, rows, m, p, PP_, MU_, A, k, a_diag, T_out, \
-                     T2_out, Q_out, d, accept_out, accept_stride, part)
-#define OCM_SCORE_KT(K_, KTA_, KTB_, COND_, PP_, MU_)                                         \
-  if (COND_) {                                                                               \
-    if (vec) OCM_SCORE_LAUNCH(K_, KTA_, true, PP_, MU_); else OCM_SCORE_LAUNCH(K_, KTA_, false, PP_, MU_); \
-  } else {                                                                                   \
-    if (vec) OCM_SCORE_LAUNCH(K_, KTB_, true, PP_, MU_); else OCM_SCORE_LAUNCH(K_, KTB_, false, PP_, MU_); \
-  }
-    if (variant == 0) {
-      if (k <= 16) {
-        OCM_SCORE_KT(k_score_f64, 1, 2, true, P, mu)
-      } else if (k <= 32) {
-        OCM_SCORE_KT(k_score_f64, 2, 2, true, P, mu)
-      } else {
-        OCM_SCORE_KT(k_score_f64, 3, 4, k <= 48, P, mu)
-      }
-
-    } else if (variant == 1) {
-      OCM_SCORE_KT(k_score_direct, 1, 2, k <= 32, P32, mu32)
+#define OCM_SCORE_LAUNCH(KT_, V_)                                                                          \
+  hipLaunchKernelGGL((k_score_direct<KT_, V_>), g, dim3(256), 0, st, X, ldx, rows, m, p, P32, mu32, A, k, a_diag, \
+                     T_out, T2_out, Q_out, d, accept_out, accept_stride, part)
+    if (k <= 32) {
+      if (vec) OCM_SCORE_LAUNCH(1, true); else OCM_SCORE_LAUNCH(1, false);
     } else {
-      OCM_SCORE_KT(k_score, 1, 2, k <= 32, P32, mu32)
+      if (vec) OCM_SCORE_LAUNCH(2, true); else OCM_SCORE_LAUNCH(2, false);
     }
-#undef OCM_SCORE_KT
 #undef OCM_SCORE_LAUNCH
   }
   OCM_CHECK_LAUNCH("k_score");

@@ -62,6 +62,9 @@ SIGNATURES = {
     "ocm_colmean_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p]),
     "ocm_gram_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p,
                              ctypes.POINTER(c_i64), c_i32, c_void_p, c_void_p, c_void_p]),
+    "ocm_gram_f32_ex": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p,
+                                ctypes.POINTER(c_i64), c_i32, c_i32, c_i64, c_void_p, c_void_p, c_void_p]),
+    "ocm_gram_last_marks": (c_i32, [c_void_p, ctypes.POINTER(c_i64)]),
     "ocm_cov_from_gram": (c_i32, [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p),
                                   ctypes.POINTER(c_f64), c_i32, c_void_p, c_i64, c_i32, c_void_p, c_void_p,
                                   c_void_p]),
@@ -86,11 +89,15 @@ SIGNATURES = {
                                    ctypes.POINTER(c_f64), c_void_p, c_i64, c_void_p]),
     "ocm_cv_counts": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_void_p, c_i64,
                               ctypes.POINTER(OcmCvConfig), c_i32, c_void_p, c_void_p, c_void_p]),
+    "ocm_bn_scratch_bytes": (ctypes.c_size_t, [c_i32]),
     "ocm_bn_fwd_train": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, ctypes.c_float,
-                                 ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                 ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p]),
     "ocm_bn_bwd": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p,
-                           c_void_p, c_void_p, c_void_p, c_void_p]),
+                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
+
+ABI_VERSION = 2  # include/ocm.h OCM_ABI_VERSION
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -110,7 +117,7 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.ocm_abi_version() != 1:
+        if lib.ocm_abi_version() != ABI_VERSION:
             raise OcmError("libocm ABI version mismatch")
         _lib = lib
         return lib

@@ -7,7 +7,7 @@ of csrc/ocm_bn.hip instead of MIOpen's spatial BN, which handles the VAE's
 3-12-channel × 512-2048-position activations at a few GB/s.  Evaluation mode
 (running statistics) and host tensors use the stock module.  The kernels
 launch on the current stream, so the module is HIP-graph capturable
-(ocm/vae_train.py).
+(ocm/vae_train.py); their reduction scratch is caller-owned (``_scratch``).
 """
 from __future__ import annotations
 
@@ -18,6 +18,15 @@ from . import _lib
 from ._lib import Context, check, ptr, stream_handle
 
 _DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+def _scratch(C: int, dev) -> torch.Tensor:
+    """Per-call reduction scratch from torch's caching allocator.  Under
+    HIP-graph capture it comes from the graph's private pool, so a replay
+    never writes through a pointer that a later (larger) libocm call has
+    re-allocated — the context arena does move."""
+    nbytes = int(_lib.load().ocm_bn_scratch_bytes(C))
+    return torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=dev)
 
 
 class _BNTrain(torch.autograd.Function):
@@ -32,9 +41,11 @@ class _BNTrain(torch.autograd.Function):
         w = weight.detach().float().contiguous() if weight is not None else None
         b = bias.detach().float().contiguous() if bias is not None else None
         h = Context.get(dev.index).handle
+        scratch = _scratch(C, dev)
         check(_lib.load().ocm_bn_fwd_train(h, _DT[x.dtype], ptr(x), N, C, L, ptr(w), ptr(b), float(eps),
                                            float(momentum), ptr(running_mean), ptr(running_var), ptr(y),
-                                           ptr(smean), ptr(sinv), stream_handle(dev)), "ocm_bn_fwd_train")
+                                           ptr(smean), ptr(sinv), ptr(scratch), stream_handle(dev)),
+              "ocm_bn_fwd_train")
         ctx.save_for_backward(x, w, smean, sinv)
         ctx.has_w, ctx.has_b = weight is not None, bias is not None
         return y
@@ -49,8 +60,9 @@ class _BNTrain(torch.autograd.Function):
         dw = torch.empty(C, dtype=torch.float32, device=dev) if ctx.has_w else None
         db = torch.empty(C, dtype=torch.float32, device=dev) if ctx.has_b else None
         h = Context.get(dev.index).handle
+        scratch = _scratch(C, dev)
         check(_lib.load().ocm_bn_bwd(h, _DT[x.dtype], ptr(x), ptr(dy), N, C, L, ptr(w), ptr(smean), ptr(sinv),
-                                     ptr(dx), ptr(dw), ptr(db), stream_handle(dev)), "ocm_bn_bwd")
+                                     ptr(dx), ptr(dw), ptr(db), ptr(scratch), stream_handle(dev)), "ocm_bn_bwd")
         return dx, dw, db, None, None, None, None
 
 

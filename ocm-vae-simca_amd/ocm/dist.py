@@ -92,18 +92,19 @@ class ShardedSIMCA:
     Configuration keywords as utils.SIMCA (type, t2lim, t2cl, qlim, qcl, dcl)."""
 
     def __init__(self, n_components=2, type="alt", t2lim="Fdist", t2cl=0.95, qlim="jm", qcl=0.95, dcl=0.95,
-                 group=None):
+                 group=None, want_T=True):
         self.n_components = int(n_components)
         self.type, self.t2lim, self.t2cl, self.qlim, self.qcl, self.dcl = type, t2lim, t2cl, qlim, qcl, dcl
         if type == "dd":
             self.t2lim = self.qlim = "chi2pom"
         self.group = group
+        self.want_T = want_T  # the reference's fit keeps the n×k scores T (utils/SIMCA.py:65, 89)
 
     def fit(self, X_local: torch.Tensor, rows=None, n_local=None):
         ar = make_allreduce(self.group)
         n_local = X_local.shape[0] if n_local is None else n_local
         k = self.n_components
-        self.fit_ = fit = engine.fit_class(X_local, rows, n_local, k, limits.theta_mode_for(self), want_T=False,
+        self.fit_ = fit = engine.fit_class(X_local, rows, n_local, k, limits.theta_mode_for(self), want_T=self.want_T,
                                            allreduce=ar)
         n = fit.n
         T2m = limits.Moments(n, lambda: fit.T2_stats, None, lambda pct: percentile_sharded(fit.T2, pct, n, self.group))

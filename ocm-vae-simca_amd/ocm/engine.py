@@ -113,7 +113,23 @@ def cast_f32(a: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def gram(X: torch.Tensor, rows: torch.Tensor | None, seg_offsets, shift32: torch.Tensor):
+GRAM_MODES = {"i8x3": 0, "f32": 1, "bf16x3": 2}  # include/ocm.h OCM_GRAM_*
+_gram_mode = "i8x3"
+
+
+def set_gram_mode(name: str) -> str:
+    """Process-wide Gram arithmetic for fits ("i8x3" default, "f32", "bf16x3");
+    returns the previous mode.  An explicit API choice (ocm_gram_f32_ex), not
+    an environment switch inside the library."""
+    global _gram_mode
+    if name not in GRAM_MODES:
+        raise ValueError(f"gram mode must be one of {sorted(GRAM_MODES)}")
+    prev, _gram_mode = _gram_mode, name
+    return prev
+
+
+def gram(X: torch.Tensor, rows: torch.Tensor | None, seg_offsets, shift32: torch.Tensor, mode: str | None = None,
+         chunk_rows: int = 0):
     """Per-segment shifted Gram (nseg, p, p) f64 and column sums (nseg, p)."""
     p = X.shape[1]
     seg = [int(s) for s in seg_offsets]
@@ -123,9 +139,18 @@ def gram(X: torch.Tensor, rows: torch.Tensor | None, seg_offsets, shift32: torch
     cs = torch.empty((nseg, p), dtype=torch.float64, device=X.device)
     arr = (ctypes.c_int64 * len(seg))(*seg)
     ctx = Context.get(X.device.index)
-    check(_lib.load().ocm_gram_f32(ctx.handle, ptr(X), X.stride(0), ptr(rows), n, p, ptr(shift32), arr, nseg,
-                                   ptr(G), ptr(cs), _stream(X.device)), "ocm_gram_f32")
+    code = GRAM_MODES[mode or _gram_mode]
+    check(_lib.load().ocm_gram_f32_ex(ctx.handle, ptr(X), X.stride(0), ptr(rows), n, p, ptr(shift32), arr, nseg,
+                                      code, int(chunk_rows), ptr(G), ptr(cs), _stream(X.device)), "ocm_gram_f32_ex")
     return G, cs
+
+
+def last_gram_marks(device_index: int) -> int:
+    """(row, column-group) values the i8×3 outlier guard screened out in the
+    last Gram on this device (0 on clean data)."""
+    out = ctypes.c_int64(0)
+    check(_lib.load().ocm_gram_last_marks(Context.get(device_index).handle, ctypes.byref(out)), "ocm_gram_last_marks")
+    return int(out.value)
 
 
 def cov_from_gram(terms, shift32: torch.Tensor, n: int):

@@ -271,57 +271,74 @@ class SIMCA(BaseEstimator, ClassifierMixin):
         return metrics["specificity"]
 
     # ------------------------------------------------------------ plotting
+    # Host glue (out of the hot path): the T²red/Qred plane of
+    # transform() with the acceptance boundary of the decision rule.  Method
+    # names and return values follow utils/SIMCA.py:280-381; like there, the
+    # points are transform(X) (the LAST class) on every panel.
+
+    def _t2q_panels(self, X):
+        """(class, T2red, Qred, D_limit, boundary x, boundary y) per class."""
+        _, t2red, _, qred = self.transform(X)
+        t2red = t2red.cpu().numpy() if isinstance(t2red, torch.Tensor) else np.asarray(t2red)
+        qred = qred.cpu().numpy() if isinstance(qred, torch.Tensor) else np.asarray(qred)
+        for cls in self._model:
+            dlim = float(self._model[cls]["D_limit"])
+            bx, by = _boundary(self.type, dlim)
+            yield cls, t2red, qred, dlim, bx, by
+
     def toplotT2Q(self, X, y_test):
-        """T²red–Qred scatter with the decision curve (utils/SIMCA.py:280-307); host plotting glue."""
+        """matplotlib scatter of the first class panel; returns the pyplot module (as the reference)."""
         import matplotlib.pyplot as plt
 
-        for cls in self._model:
-            T2, T2red, Q, Qred = self.transform(X)
-            Dlim = self._model[cls]["D_limit"]
-            a = np.arange(0, Dlim + 0.0001, 0.0001)
-            curve = np.sqrt(np.maximum(Dlim ** 2 - a ** 2, 0))
-            plt.figure(figsize=(6, 6))
-            sc = plt.scatter(T2red, Qred, c=y_test, cmap="viridis", s=40, edgecolor="k", linewidth=0.5, alpha=0.7)
-            plt.plot(a, curve, "b-", lw=2, label=f"Confine classe {cls}")
-            plt.xlabel(r"$T^2_{red}$")
-            plt.ylabel(r"$Q_{red}$")
-            plt.legend(*sc.legend_elements(), title="Class")
-            plt.title(rf"$T^2$ vs $Q$  Classe {cls}")
-            plt.grid(True, alpha=0.3)
-            plt.xlim(left=0)
-            plt.ylim(bottom=0)
-            plt.tight_layout()
+        for cls, t2red, qred, _, bx, by in self._t2q_panels(X):
+            fig, ax = plt.subplots(figsize=(6, 6))
+            pts = ax.scatter(t2red, qred, c=np.asarray(y_test), cmap="viridis", s=40, edgecolor="k",
+                             linewidth=0.5, alpha=0.7)
+            ax.plot(bx, by, "b-", lw=2)
+            ax.legend(*pts.legend_elements(), title="Class")
+            ax.set_xlabel(r"$T^2_{red}$")
+            ax.set_ylabel(r"$Q_{red}$")
+            ax.set_title(rf"$T^2$ vs $Q$  class {cls}")
+            ax.grid(True, alpha=0.3)
+            ax.set_xlim(left=0)
+            ax.set_ylim(bottom=0)
+            fig.tight_layout()
             plt.show()
-            return plt
+            return plt  # the reference stops after the first class
 
     def toplotT2Q_iterative(self, X, y_test):
-        """Plotly version (utils/SIMCA.py:310-381); host plotting glue."""
+        """plotly figure per class (one trace per label + the boundary); one figure or a list."""
         import plotly.graph_objects as go
 
+        labels = np.asarray(y_test).astype(str)
         figs = []
-        y_color = np.asarray(y_test).astype(str)
-        for cls in self._model:
-            T2, T2red, Q, Qred = self.transform(X)
-            Dlim = float(self._model[cls]["D_limit"])
-            a = np.linspace(0, Dlim, 1200)
-            curve = np.sqrt(np.maximum(Dlim ** 2 - a ** 2, 0.0))
-            x_max = max(np.max(T2red), Dlim) * 1.05 if len(T2red) else Dlim * 1.05
-            y_max = max(np.max(Qred), Dlim) * 1.05 if len(Qred) else Dlim * 1.05
+        for cls, t2red, qred, dlim, bx, by in self._t2q_panels(X):
             fig = go.Figure()
-            for c in np.unique(y_color):
-                mask = y_color == c
-                if np.any(mask):
-                    fig.add_trace(go.Scatter(x=T2red[mask], y=Qred[mask], mode="markers",
-                                             marker=dict(size=7, line=dict(width=0.7, color="black")),
-                                             name=f"Class {c}", showlegend=True, visible=True))
-            fig.add_trace(go.Scatter(x=a, y=curve, mode="lines", name="Decision Limit",
-                                     line=dict(color="blue", width=3), opacity=1.0))
-            fig.update_layout(width=600, height=600, xaxis_title="T<sup>2</sup><sub>red</sub>",
-                              yaxis_title="Q</sup><sub>red</sub>")
-            fig.update_xaxes(range=[0, x_max], zeroline=True)
-            fig.update_yaxes(range=[0, y_max], zeroline=True)
+            for lab in np.unique(labels):
+                sel = labels == lab
+                fig.add_trace(go.Scatter(x=t2red[sel], y=qred[sel], mode="markers", name=f"Class {lab}",
+                                         marker=dict(size=7, line=dict(width=0.7, color="black"))))
+            fig.add_trace(go.Scatter(x=bx, y=by, mode="lines", name="Decision Limit",
+                                     line=dict(color="blue", width=3)))
+            top_x = 1.05 * max(float(t2red.max()) if t2red.size else 0.0, dlim)
+            top_y = 1.05 * max(float(qred.max()) if qred.size else 0.0, dlim)
+            fig.update_layout(width=600, height=600, title=f"T2 vs Q, class {cls}",
+                              xaxis=dict(title="T<sup>2</sup><sub>red</sub>", range=[0, top_x]),
+                              yaxis=dict(title="Q<sub>red</sub>", range=[0, top_y]))
             figs.append(fig)
         return figs[0] if len(figs) == 1 else figs
+
+
+def _boundary(type_name, dlim, npts=1201):
+    """Acceptance boundary dred(t, q) = D_limit in the (T2red, Qred) plane:
+    a quarter circle for 'alt', a square corner for 'sim', a line for 'ci'
+    (SURVEY.md §8a predict row); 'dd' is a line in dof-scaled units."""
+    t = np.linspace(0.0, dlim, npts)
+    if type_name == "sim":
+        return np.array([0.0, dlim, dlim]), np.array([dlim, dlim, 0.0])
+    if type_name in ("ci", "dd"):
+        return t, dlim - t
+    return t, np.sqrt(np.maximum(dlim * dlim - t * t, 0.0))
 
 
 def _out_dtype(X):

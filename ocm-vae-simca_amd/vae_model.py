@@ -15,7 +15,6 @@ from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
-from scipy.stats import chi2
 from torch import nn
 
 from ocm.bn import FastBatchNorm1d
@@ -184,21 +183,14 @@ def beta_vae_bce_loss(x, x_recon, mu, logvar, beta=1.0, eps=1e-8):
 def compute_q_h_f(x, x_rec, z):
     """q = Σ(x − x̂)², leverage h of the column-standardised latent, f = h/h0·Nh
     + q/q0·Nq and the χ²₀.₉₅ criticals with moment-matched dof (unbiased
-    std).  Per-batch statistics, as the reference.  On a GPU tensor the
-    arithmetic runs on libocm (ocm.vae.qhf_device); there is no CPU fallback
-    for device tensors."""
-    if x.is_cuda:
-        from ocm.vae import qhf_device
+    std).  Per-batch statistics, as the reference.  The arithmetic runs on
+    libocm (ocm.vae.qhf_device); host tensors are copied to the device and
+    the per-row results come back to the host, like the reference's own
+    return device.  There is no CPU path: without a HIP device this raises."""
+    from ocm.vae import qhf_device
 
-        return qhf_device(x, x_rec, z)
-    # host tensors: the reference's own formulation (float32 torch on the CPU)
-    q = torch.sum((x - x_rec) ** 2, dim=1)
-    q0, sq = q.mean().item(), q.std(unbiased=True).item()
-    Nq = 2 * (q0 / sq) ** 2
-    zs = (z - z.mean(dim=0)) / (z.std(dim=0) + 1e-12)
-    U = torch.linalg.svd(zs, full_matrices=False)[0]
-    h = torch.sum(U ** 2, dim=1)
-    h0, sh = h.mean().item(), h.std(unbiased=True).item()
-    Nh = 2 * (h0 / sh) ** 2
-    f = (h / h0) * Nh + (q / q0) * Nq
-    return q, h, f, chi2.ppf(0.95, df=Nq), chi2.ppf(0.95, df=Nh), chi2.ppf(0.95, df=Nh + Nq)
+    host = not x.is_cuda
+    q, h, f, q_crit, h_crit, f_crit = qhf_device(x, x_rec, z)
+    if host:
+        q, h, f = q.cpu(), h.cpu(), f.cpu()
+    return q, h, f, q_crit, h_crit, f_crit

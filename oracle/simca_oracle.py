@@ -54,15 +54,28 @@ def svd_flip_rows(Vt: np.ndarray, U: np.ndarray | None = None):
     return Vt, U
 
 
-def pca_full(X: np.ndarray, precision: str = "exact"):
+def pca_full(X: np.ndarray, precision: str = "exact", ncomp: int | None = None):
     """Full PCA as ``PCA(n_components=None, svd_solver='full').fit_transform``
     (utils/SIMCA.py:64-65 -> sklearn/decomposition/_pca.py:544-702).
 
     Returns mean (p,), explained_variance (min(n,p),), components Vt, scores
     U*S.  ``precision='exact'`` does the SVD in float64; ``'reference'`` in
-    the input dtype like sklearn (float32 gesdd for float32 X).
+    the input dtype like sklearn (float32 gesdd for float32 X); ``'gram'`` is
+    the same float64 result through the covariance (Xcᵀ Xc, ``eigh``) for the
+    large parity cases (100k × 2048), with scores for the leading ``ncomp``
+    components only.
     """
     n = X.shape[0]
+    if precision == "gram":
+        Xc = np.asarray(X, dtype=np.float64)
+        mean = Xc.mean(axis=0)
+        Xc = Xc - mean
+        w, V = np.linalg.eigh(Xc.T @ Xc)
+        order = np.argsort(w)[::-1][: min(n, X.shape[1])]
+        Vt, _ = svd_flip_rows(V[:, order].T)
+        ev = np.maximum(w[order], 0.0) / (n - 1)
+        kk = Vt.shape[0] if ncomp is None else ncomp
+        return mean, ev, Vt, Xc @ Vt[:kk].T
     work = np.float64 if precision == "exact" else X.dtype
     Xw = np.asarray(X, dtype=work)
     mean = Xw.mean(axis=0)
@@ -249,10 +262,10 @@ def fit_one_class(X: np.ndarray, k: int, cfg: SimcaConfig, st: DDState,
     loadings for predict/transform (the subspace the reference's second
     ``PCA(k)`` estimates, SURVEY.md §8c caveat 1); ``'randomized'`` reruns the
     randomized estimate like the reference (CPU-baseline timing)."""
-    mean, ev, Vt, scores = pca_full(X, precision)
+    mean, ev, Vt, scores = pca_full(X, precision, ncomp=k)
     T = scores[:, :k]
     P = Vt[:k]
-    if precision == "exact":
+    if precision in ("exact", "gram"):
         T_, T2, Q = project_scores(X, P, mean, np.eye(k))
         Tf = np.asarray(T, dtype=np.float64)
         invcovT = np.linalg.pinv(np.atleast_2d(np.cov(Tf, rowvar=False)))
@@ -512,7 +525,7 @@ def vaesimca_fit(Z: np.ndarray, Zhat: np.ndarray, type="alt", t2lim="Fdist", t2c
     Z = np.asarray(Z, np.float32)
     nc = Z.shape[1]
     n = Z.shape[0]
-    x_mean = Z.mean(axis=0, dtype=np.float64)
+    x_mean = np.mean(Z, axis=0)  # float32, as the script (:246): the centring happens in float32
     cov = np.cov(Z, rowvar=False) + np.eye(nc) * 1e-12
     invcovT = np.linalg.pinv(cov)
     diff = Z - x_mean[None, :]

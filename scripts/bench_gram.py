@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
-"""A/B the Gram kernel variants in ONE process (interleaved rounds), on the
-bench workload (1M×2048 fp32 in HBM).  Prints TFLOP/s (symmetric count) per
-variant and the max relative difference of G between variants."""
+"""A/B the Gram arithmetic modes (ocm_gram_f32_ex) in ONE process
+(interleaved rounds) on the bench workload (1M×2048 fp32 in HBM).  Prints
+TFLOP/s (symmetric count n·p(p+1)) per mode/chunk and the max relative error
+of each mode against an fp64 Gram of a row sample.
+
+    python scripts/bench_gram.py [--variants i8x3:0,f32:0,bf16x3:0] [--outliers 0.005]
+"""
 import argparse
 import os
 import sys
-import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "ocm-vae-simca_amd"))
@@ -17,7 +20,8 @@ def main():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--p", type=int, default=2048)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="bf16x3:256x32:2048,i8x3:128x32:4096,i8x3:128x32:2048,i8x3:128x32:1024")
+    ap.add_argument("--variants", default="i8x3:0,bf16x3:0,f32:0", help="mode:chunk_rows (0 = automatic)")
+    ap.add_argument("--outliers", type=float, default=0.0, help="fraction of rows scaled x100..x1000")
     args = ap.parse_args()
     import torch
 
@@ -27,53 +31,38 @@ def main():
 
     dev = torch.device("cuda", 0)
     X = synth_device(args.rows, args.p, 20, seed=7, device=dev)
+    if args.outliers > 0:
+        g = torch.Generator(device=dev).manual_seed(3)
+        m = int(args.outliers * args.rows)
+        idx = torch.randperm(args.rows, generator=g, device=dev)[:m]
+        mu = X[:4096].mean(0)
+        X[idx] = mu + (X[idx] - mu) * (100 + 900 * torch.rand(m, 1, generator=g, device=dev))
     shift = engine.cast_f32(engine.colmean(X, None, 4096))
     ctx = Context.get(0)
-    variants = [v.split(":") for v in args.variants.split(",")]
-    res = {":".join(v): [] for v in variants}
-    Gs = {}
+    variants = [(v.split(":")[0], int(v.split(":")[1])) for v in args.variants.split(",")]
+    res = {f"{m}:{c}": [] for m, c in variants}
     flop = args.rows * args.p * (args.p + 1)
-    for r in range(args.rounds):
-        for mode, name, chunk in variants:
-            os.environ["OCM_GRAM_MODE"] = "bf16x3" if mode.startswith("bf16x3") else mode[:4] if mode.startswith("i8x3") else mode
-            # i8x3 kernel variants: i8x3 (default) | i8x3d (direct) | i8x3s[N] (shared LDS, N-slot ring)
-            var = {"i8x3d": "direct"}.get(mode) or ("shared" + mode[5:] if mode.startswith("i8x3s") else None)
-            if var:
-                os.environ["OCM_GRAM8_VARIANT"] = var
-            else:
-                os.environ.pop("OCM_GRAM8_VARIANT", None)
-            if mode == "bf16x3pk":
-                os.environ["OCM_GRAM3_PK"] = "1"
-            else:
-                os.environ.pop("OCM_GRAM3_PK", None)
-            os.environ["OCM_GRAM_TILE"], os.environ["OCM_GRAM_BK"] = name.split("x")
-            os.environ["OCM_GRAM_CHUNK"] = chunk
-            key = f"{mode}:{name}:{chunk}"
-            engine.gram(X, None, [0, args.rows], shift)  # warm (workspace)
+    for _ in range(args.rounds):
+        for mode, chunk in variants:
+            engine.gram(X, None, [0, args.rows], shift, mode=mode, chunk_rows=chunk)  # warm (workspace)
             torch.cuda.synchronize()
             ctx.read_timing(0)
             ctx.set_timing(True)
-            G, cs = engine.gram(X, None, [0, args.rows], shift)
+            engine.gram(X, None, [0, args.rows], shift, mode=mode, chunk_rows=chunk)
             ctx.set_timing(False)
-            ms, cnt = ctx.read_timing(0)
-            res[key].append(flop / (ms / 1e3) / 1e12)
-            if r == 0:
-                Gs[key] = G[0].clone()
-    # exact reference for the error column: fp64 Gram of a row sample (first 65536 rows)
+            ms, _ = ctx.read_timing(0)
+            res[f"{mode}:{chunk}"].append(flop / (ms / 1e3) / 1e12)
+    print("guard marks (last i8x3 call):", engine.last_gram_marks(0))
     ns = min(args.rows, 65536)
-    Y = (X[:ns].double() - shift.double())
+    Y = X[:ns].double() - shift.double()
     Gref = Y.T @ Y
-    os.environ.pop("OCM_GRAM3_PK", None)
-    os.environ.pop("OCM_GRAM8_VARIANT", None)
-    for mode in sorted({v[0][:4] if v[0].startswith("i8x3") else v[0] for v in variants} - {"bf16x3pk"}):
-        os.environ["OCM_GRAM_MODE"] = mode
-        Gm, _ = engine.gram(X, None, [0, ns], shift)
-        print(f"{mode:8s} sample Gram max rel err vs fp64: {((Gm[0] - Gref).abs().max() / Gref.abs().max()).item():.2e}")
-    ref = next(iter(Gs.values()))
+    for mode in sorted({m for m, _ in variants}):
+        Gm, _ = engine.gram(X, None, [0, ns], shift, mode=mode)
+        err = ((Gm[0] - Gref).abs().max() / Gref.abs().max()).item()
+        print(f"{mode:8s} sample Gram max rel err vs fp64: {err:.2e}")
     for key, vals in res.items():
-        d = ((Gs[key] - ref).abs().max() / ref.abs().max()).item()
-        print(f"{key:24s} TFLOP/s median {sorted(vals)[len(vals)//2]:7.2f}  all {[round(v,1) for v in vals]}  "
-              f"maxrel vs first {d:.2e}", flush=True)
+        print(f"{key:16s} TFLOP/s median {sorted(vals)[len(vals) // 2]:7.2f}  all {[round(v, 1) for v in vals]}",
+              flush=True)
 
 
 if __name__ == "__main__":

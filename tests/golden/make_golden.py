@@ -20,8 +20,26 @@ outputs.  They are data (inputs and expected outputs), not reference source.
   train forward on a fixed batch with seeded ε, both losses, and the latent
   inputs of VAESIMCA (encoder μ, round trip ẑ) on a calibration / test set.
 
+* simca_ns.npz       — north-star shape: p = 2048, k = 20 on 8000 fit rows and
+  2000 test rows (the synth_spectra seed and sizes are stored, not X), five
+  type × t2lim × qlim combinations: xmean, eigs_all, θ1..θ3 of the tail,
+  fit / test T2 and Q, limits, predictions.
+* simca_f64.npz      — SIMCA on float64 input (the reference then runs its PCA
+  in float64): limits, T2/Q, predictions for three combinations.
+* score.npz          — SIMCA.score(X_test, y_test) of the simca_a / simca_multi
+  configurations (utils/SIMCA.py:268-278, 2-D y_pred and list class quirk).
+* vaesimca.npz       — VAESIMCA (VAE_SIMCA.py:215-382) run on the vae_a network:
+  the class is taken from the script's syntax tree (ast) and executed alone —
+  the script itself loads private data at import.  Limits, dofs, T2 / Q and
+  decisions for every type × t2lim × qlim combination (or the error it raises).
+* final_vaesimca.npz — the inline latent-statistics (utils/final_vaesimca.py:
+  428-436) and full-distance decision (:511-533) statements, extracted the same
+  way and executed on the vae_a latents.
+
 np.random.seed is set before every fit: the reference's second PCA(k) draws
 from NumPy's global RNG (SURVEY.md §8c caveat 1).
+
+    python tests/golden/make_golden.py [ns f64 score vaesimca final]   # a subset
 """
 from __future__ import annotations
 
@@ -257,7 +275,234 @@ def make_splits():
     print("splits", Xc.shape, Xv.shape, Xti.shape, Xto.shape)
 
 
-def main():
+NS = dict(n_fit=8000, n_test=2000, p=2048, k=20, rank=40, seed=2026, outlier_frac=0.1)
+NS_COMBOS = [("alt", "Fdist", "jm"), ("sim", "perc", "perc"), ("ci", "chi2", "chi2box"),
+             ("dd", "chi2pom", "chi2pom"), ("alt", "Fdistrig", "chi2pom")]
+
+
+def _tails(eigs, k):
+    tail = np.asarray(eigs, dtype=np.float64)[k:]
+    return np.array([tail.sum(), (tail ** 2).sum(), (tail ** 3).sum()])
+
+
+def _simca_combo_run(X_fit, y_fit, X_test, k, combos, seed=7):
+    """Per combo: fit + predict + transform with the reference; per-fit arrays once."""
+    from utils import SIMCA
+
+    out, per = {}, {"T2_limit": [], "Q_limit": [], "D_limit": []}
+    preds, first = [], True
+    for ty, t2, ql in combos:
+        np.random.seed(seed)
+        est = SIMCA(n_components=k, model_class=0, type=ty, t2lim=t2, qlim=ql, verbose=False)
+        with contextlib.redirect_stdout(io.StringIO()):
+            est.fit(X_fit, y_fit)
+            pr = est.predict(X_test)
+            tr = est.transform(X_test)
+        m = est._model[0]
+        if first:
+            out["xmean"] = np.asarray(m["xmean"])
+            out["eigs_all"] = np.asarray(m["eigs_all"], dtype=np.float64)
+            out["thetas"] = _tails(m["eigs_all"], k)
+            out["fit_T2"] = np.asarray(m["T2"], dtype=np.float64)
+            out["fit_Q"] = np.asarray(m["Q"])
+            out["test_T2"] = np.asarray(tr[0], dtype=np.float64)
+            out["test_Q"] = np.asarray(tr[2])
+            first = False
+        for key in per:
+            per[key].append(float(m[key]))
+        preds.append(np.asarray(pr)[:, 0].astype(np.uint8))
+    out["combos"] = np.array(["|".join(c) for c in combos])
+    for key, v in per.items():
+        out[key] = np.array(v)
+    out["pred"] = np.stack(preds)
+    return out
+
+
+def make_northstar():
+    """SURVEY.md §8 north-star shape (p = 2048, k = 20) from the reference."""
+    from oracle.simca_oracle import synth_spectra
+
+    c = NS
+    X = synth_spectra(c["n_fit"] + c["n_test"], c["p"], c["k"], rank=c["rank"], seed=c["seed"],
+                      outlier_frac=c["outlier_frac"])
+    X_fit, X_test = X[:c["n_fit"]], X[c["n_fit"]:]
+    y_fit = np.zeros(c["n_fit"], dtype=np.int64)
+    out = _simca_combo_run(X_fit, y_fit, X_test, c["k"], NS_COMBOS)
+    out["config_json"] = np.array(json.dumps(c))
+    out["fit_T2"] = out["fit_T2"].astype(np.float64)
+    np.savez_compressed(os.path.join(HERE, "simca_ns.npz"), **out)
+    print("ns", {k: out[k] for k in ("T2_limit", "Q_limit")})
+
+
+def make_f64():
+    """Float64 input: the reference's PCA then runs in float64."""
+    from oracle.simca_oracle import synth_spectra
+
+    cfg = dict(n=2600, n_fit=2000, p=256, k=10, rank=24, seed=404, outlier_frac=600 / 2600)
+    X = synth_spectra(cfg["n"], cfg["p"], cfg["k"], rank=cfg["rank"], seed=cfg["seed"],
+                      outlier_frac=cfg["outlier_frac"], dtype=np.float64)
+    X_fit, X_test = X[:cfg["n_fit"]], X[cfg["n_fit"]:]
+    y_fit = np.zeros(2000, dtype=np.int64)
+    out = _simca_combo_run(X_fit, y_fit, X_test, 10, [("alt", "Fdist", "jm"), ("sim", "chi2", "chi2box"),
+                                                      ("dd", "chi2pom", "chi2pom")])
+    out["config_json"] = np.array(json.dumps(cfg))  # X regenerates from the seed (float64 synth_spectra)
+    np.savez_compressed(os.path.join(HERE, "simca_f64.npz"), **out)
+    print("f64", out["Q_limit"])
+
+
+def make_score_pins():
+    """SIMCA.score on the simca_a / simca_multi fixtures (their stored inputs)."""
+    from utils import SIMCA
+
+    out = {}
+    for name, k, mc in (("a", 4, 0), ("multi", [2, 3, 4], None)):
+        g = np.load(os.path.join(HERE, f"simca_{name}.npz"), allow_pickle=False)
+        np.random.seed(7)
+        est = SIMCA(n_components=k, model_class=mc, verbose=False)
+        with contextlib.redirect_stdout(io.StringIO()):
+            est.fit(g["X_fit"], g["y_fit"])
+            try:
+                out[f"{name}_score"] = np.float64(est.score(g["X_test"], g["y_test"]))
+                out[f"{name}_error"] = np.array("")
+            except Exception as e:  # the reference's list-class quirk can raise
+                out[f"{name}_score"] = np.float64(np.nan)
+                out[f"{name}_error"] = np.array(type(e).__name__)
+    np.savez_compressed(os.path.join(HERE, "score.npz"), **out)
+    print("score", {k: v for k, v in out.items()})
+
+
+def _extract(path, first, last, names=None):
+    """Compile the statements of a reference script whose first line lies in
+    [first, last] (any nesting depth), or the top-level class ``names``."""
+    import ast
+
+    src = open(path).read()
+    tree = ast.parse(src)
+    if names:
+        body = [n for n in tree.body if isinstance(n, ast.ClassDef) and n.name in names]
+    else:
+        body, seen = [], set()
+        for node in ast.walk(tree):
+            if isinstance(node, ast.stmt) and first <= node.lineno <= last and node.lineno not in seen:
+                if any(first <= a.lineno <= last and a is not node and node in ast.walk(a) for a in body):
+                    continue
+                body.append(node)
+                seen.add(node.lineno)
+        body.sort(key=lambda n: n.lineno)
+        # drop statements nested inside another extracted statement
+        outer = []
+        for n in body:
+            if not any(n is not o and n in list(ast.walk(o)) for o in body):
+                outer.append(n)
+        body = outer
+    mod = ast.Module(body=body, type_ignores=[])
+    return compile(mod, path, "exec")
+
+
+def _vae_a_model():
+    import torch
+    from vae_model import ConvVAE1D
+
+    L, d, kw = VAE_CONFIGS["a"]
+    g = np.load(os.path.join(HERE, "vae_a.npz"), allow_pickle=False)
+    m = ConvVAE1D(L, d, g["mean"], g["std"], **kw)
+    m.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("sd/")})
+    return m.eval(), g
+
+
+def make_vaesimca():
+    """VAESIMCA of VAE_SIMCA.py:215-382, executed alone on the vae_a network."""
+    import torch
+    from scipy import special
+
+    ns = {"np": np, "torch": torch, "special": special}
+    exec(_extract(os.path.join(REF, "VAE_SIMCA.py"), 0, 0, names={"VAESIMCA"}), ns)
+    VAESIMCA = ns["VAESIMCA"]
+    m, g = _vae_a_model()
+    cal = [(torch.from_numpy(g["x_cal"]),)]   # one batch: bit-identical to mu_cal / zhat_cal
+    test = [(torch.from_numpy(g["x_test"]),)]
+    out = {}
+    combos = []
+    for ty in ("sim", "alt", "ci", "dd"):
+        for t2 in ("perc", "Fdist", "chi2", "chi2pom"):
+            for ql in ("perc", "jm", "chi2pom"):
+                combos.append((ty, t2, ql))
+    lim = {k: [] for k in ("T2_limit", "Q_limit", "D_limit", "T2dof", "Qdof", "T2scfact", "Qscfact")}
+    preds, errs = [], []
+    for ty, t2, ql in combos:
+        vs = VAESIMCA(m, type=ty, t2lim=t2, qlim=ql, verbose=False)
+        try:
+            vs.fit_thresholds(cal, class_label=0)
+            y_pred, T2, Q = vs.predict(test)
+            info = vs._model[0]
+            for k in lim:
+                v = info[k]
+                lim[k].append(np.nan if v is None else float(v))
+            preds.append(np.asarray(y_pred, dtype=np.uint8))
+            errs.append("")
+            if "fit_T2" not in out:
+                out["fit_T2"], out["fit_Q"] = np.asarray(info["T2"]), np.asarray(info["Q"])
+                out["test_T2"], out["test_Q"] = np.asarray(T2), np.asarray(Q)
+                out["latent_mean"], out["invcovT"] = np.asarray(info["latent_mean"]), np.asarray(info["invcovT"])
+        except Exception as e:
+            for k in lim:
+                lim[k].append(np.nan)
+            preds.append(np.zeros(len(g["x_test"]), np.uint8))
+            errs.append(type(e).__name__)
+    out["combos"] = np.array(["|".join(c) for c in combos])
+    out["errors"] = np.array(errs)
+    for k, v in lim.items():
+        out[k] = np.array(v)
+    out["pred"] = np.stack(preds)
+    np.savez_compressed(os.path.join(HERE, "vaesimca.npz"), **out)
+    print("vaesimca", len(combos), "combos,", sum(1 for e in errs if e), "raise")
+
+
+class _Buffers:
+    """Stand-in for the loaded network whose buffers the f-distance block reads."""
+
+    def __init__(self, latent_mean):
+        import torch
+
+        self.latent_mean = torch.from_numpy(np.asarray(latent_mean, dtype=np.float32))
+
+
+def make_final_vaesimca():
+    """utils/final_vaesimca.py:428-436 (latent stats) and :511-533 (full-distance
+    decision), extracted statement by statement and executed on vae_a latents
+    and synthetic reconstruction errors."""
+    import scipy as sp
+    import scipy.stats  # noqa: F401
+
+    g = np.load(os.path.join(HERE, "vae_a.npz"), allow_pickle=False)
+    path = os.path.join(REF, "utils", "final_vaesimca.py")
+    rng = np.random.default_rng(55)
+    rec_cal = rng.gamma(4.0, 0.5, size=len(g["mu_cal"])).astype(np.float32)
+    q_test = rng.gamma(4.0, 0.5, size=len(g["mu_test"])).astype(np.float32)
+    q_test[60:] *= 3.0
+    ns = {"np": np, "sp": sp, "mus_train_list": [g["mu_cal"][:150], g["mu_cal"][150:]],
+          "rec_errors_list": [rec_cal[:150], rec_cal[150:]]}
+    exec(_extract(path, 428, 436), ns)
+    out = {"rec_cal": rec_cal, "q_test": q_test, "mu_train_mean": ns["mu_train_mean"], "cov_inv": ns["cov_inv"],
+           "threshold": np.float64(ns["threshold"]), "q_threshold": np.float64(ns["q_threshold"])}
+    ns2 = {"np": np, "sp": sp, "mus_test": g["mu_test"], "q_errors": q_test,
+           "vae_best": _Buffers(ns["mu_train_mean"])}
+    exec(_extract(path, 511, 533), ns2)
+    for key in ("h", "h0", "sh", "Nh", "q0", "sq", "Nq", "f", "Nf", "fcrit"):
+        out[key] = np.asarray(ns2[key])
+    out["pred_class0"] = np.asarray(ns2["pred_class0"], dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "final_vaesimca.npz"), **out)
+    print("final_vaesimca fcrit", float(out["fcrit"]), "accept", int(out["pred_class0"].sum()))
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    extra = {"ns": make_northstar, "f64": make_f64, "score": make_score_pins, "vaesimca": make_vaesimca,
+             "final": make_final_vaesimca}
+    if argv:
+        for name in argv:
+            extra[name]()
+        return
     # A: one class, spectral gap at k (SURVEY.md §8d), wavelength-correlated bands.
     # The last 100 rows carry the out-of-class band; fit on the first 1200.
     Xa_all = synth_spectra(1600, 96, 4, rank=12, seed=1234, outlier_frac=100 / 1600)
@@ -293,6 +538,8 @@ def main():
     make_qhf()
     make_vae()
     make_splits()
+    for fn in extra.values():
+        fn()
 
 
 if __name__ == "__main__":

@@ -13,7 +13,7 @@ LIB = os.path.join(REPO, "ocm-vae-simca_amd", "ocm", "libocm.so")
 
 def header_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ocm_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(ocm_\w+)\s*\(", txt, re.M)))
 
 
 def test_header_parses():
@@ -37,7 +37,7 @@ def test_binding_signatures_cover_header():
 
     assert set(_lib.SIGNATURES) == set(header_symbols())
     lib = _lib.load()
-    assert lib.ocm_abi_version() == 1
+    assert lib.ocm_abi_version() == _lib.ABI_VERSION == 2
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libocm.so not built")

@@ -16,11 +16,15 @@ def eng():
 
 
 @pytest.fixture(params=["f32", "bf16x3", "i8x3"])
-def gram_mode(request, monkeypatch):
+def gram_mode(request):
     """All Gram kernels: FP32 MFMA, the bf16×3 split on bf16 MFMA and the int8
-    digit split on integer MFMA (the default)."""
-    monkeypatch.setenv("OCM_GRAM_MODE", request.param)
-    return request.param
+    digit split on integer MFMA (the default), chosen through the explicit
+    mode argument of ocm_gram_f32_ex."""
+    from ocm import engine
+
+    prev = engine.set_gram_mode(request.param)
+    yield request.param
+    engine.set_gram_mode(prev)
 
 
 def _dev(a):
@@ -209,13 +213,15 @@ def test_rowsq_residual_broadcast_and_strided(eng):
 
 
 @pytest.mark.parametrize("n,p", [(9000, 257), (300, 2048)])
-def test_gram_i8_digit_split_edge_cases(eng, monkeypatch, n, p):
+def test_gram_i8_digit_split_edge_cases(eng, n, p):
     """i8x3 fixed-point split: per-(1536-row block, column) power-of-two scales
-    must cope with zero / constant columns, a far-off shift, a single huge
-    outlier row (it sets its block's scale), ragged chunk/block tails and
-    p not a multiple of the 128 tile."""
-    monkeypatch.setenv("OCM_GRAM_MODE", "i8x3")
-    monkeypatch.setenv("OCM_GRAM_CHUNK", "512")
+    must cope with zero / constant columns, a far-off shift, ragged
+    chunk/block tails, p not a multiple of the 128 tile, a 1e-20-scale column
+    and a single huge value (3e5 among N(0, 0.25) values).  The huge value is
+    screened by the outlier guard and added back exactly, so the other rows
+    of its block keep full precision: the error is normalised by the Gram of
+    the rows WITHOUT the outlier (an outer(d, d) over all rows would let the
+    outlier hide the loss)."""
     rng = np.random.default_rng(p)
     X = rng.standard_normal((n, p)).astype(np.float32) * np.float32(0.5)
     X[:, 3] = 0.0
@@ -225,10 +231,103 @@ def test_gram_i8_digit_split_edge_cases(eng, monkeypatch, n, p):
     X[:, -1] = np.float32(1e-20) * rng.standard_normal(n).astype(np.float32)
     Xd = _dev(X)
     shift = _dev(X[:5].mean(0).astype(np.float32))
-    G, cs = eng.gram(Xd, None, [0, n], shift)
+    G, cs = eng.gram(Xd, None, [0, n], shift, mode="i8x3", chunk_rows=512)
+    assert eng.last_gram_marks(0) >= 1
     Y = X.astype(np.float64) - shift.cpu().numpy().astype(np.float64)
     Gref = Y.T @ Y
-    d = np.sqrt(np.maximum(np.diag(Gref), 1e-300))
+    Y0 = np.delete(Y, n // 3, axis=0)
+    d = np.sqrt(np.maximum(np.einsum("ij,ij->j", Y0, Y0), 1e-300))
     err = np.abs(G[0].cpu().numpy() - Gref) / np.outer(d, d)
     assert err.max() < 2e-6, err.max()
     np.testing.assert_allclose(cs[0].cpu().numpy(), Y.sum(0), rtol=1e-6, atol=1e-6 * np.abs(Y).sum(0).max())
+
+
+def _outlier_rows(rng, n, frac, lo=100.0, hi=1000.0):
+    """Row indices spread over the matrix (one or more per 1536-row block) and
+    their scale factors in [lo, hi]."""
+    m = max(1, int(round(frac * n)))
+    idx = np.sort(rng.choice(n, m, replace=False))
+    return idx, rng.uniform(lo, hi, m)
+
+
+@pytest.mark.parametrize("frac", [0.005, 0.01])
+def test_gram_i8_outlier_rows(eng, frac):
+    """0.5–1 % of the rows scaled ×100–×1000, spread so that most 1536-row
+    blocks hold several: the guarded i8×3 Gram must match fp64 to the same
+    relative accuracy (normalised by the clean rows' scale) as on clean data,
+    and agree with the FP32-MFMA Gram."""
+    from oracle.simca_oracle import synth_spectra
+
+    rng = np.random.default_rng(int(frac * 1e4))
+    n, p = 20000, 384
+    X = synth_spectra(n, p, 8, rank=24, seed=17)
+    idx, f = _outlier_rows(rng, n, frac)
+    mu = X.mean(0)
+    X[idx] = (mu + (X[idx] - mu) * f[:, None]).astype(np.float32)
+    Xd = _dev(X)
+    shift = eng.cast_f32(eng.colmean(Xd, None, 4096))
+    G, cs = eng.gram(Xd, None, [0, n], shift, mode="i8x3")
+    marks = eng.last_gram_marks(0)
+    assert 0 < marks <= n // 8
+    Y = X.astype(np.float64) - shift.cpu().numpy().astype(np.float64)
+    Gref = Y.T @ Y
+    clean = np.setdiff1d(np.arange(n), idx)
+    d = np.sqrt(np.einsum("ij,ij->j", Y[clean], Y[clean]))
+    err = np.abs(G[0].cpu().numpy() - Gref) / np.outer(d, d)
+    assert err.max() < 1e-6, err.max()
+
+
+def test_gram_i8_clean_data_marks_nothing(eng):
+    from oracle.simca_oracle import synth_spectra
+
+    X = synth_spectra(12000, 256, 8, rank=24, seed=3, outlier_frac=0.1)
+    Xd = _dev(X)
+    shift = eng.cast_f32(eng.colmean(Xd, None, 4096))
+    eng.gram(Xd, None, [0, 12000], shift, mode="i8x3")
+    assert eng.last_gram_marks(0) == 0
+
+
+def test_gram_i8_heavy_marking_falls_back_to_f32(eng):
+    """Scale drift after the sample rows (every later row ×200): more than n/8
+    marks, so the call recomputes on FP32 MFMA; the result is still the Gram."""
+    rng = np.random.default_rng(8)
+    n, p = 12000, 192
+    X = rng.standard_normal((n, p)).astype(np.float32)
+    X[5000:] *= np.float32(200.0)
+    Xd = _dev(X)
+    shift = _dev(np.zeros(p, np.float32))
+    G, _ = eng.gram(Xd, None, [0, n], shift, mode="i8x3")
+    assert eng.last_gram_marks(0) > n // 8
+    Y = X.astype(np.float64)
+    Gref = Y.T @ Y
+    np.testing.assert_allclose(G[0].cpu().numpy(), Gref, rtol=2e-6, atol=2e-6 * np.abs(Gref).max())
+
+
+def test_gram_i8_outliers_in_segments_and_gather(eng):
+    """The fix-up adds each marked row to its own segment (CV folds) and
+    follows the row-index list."""
+    rng = np.random.default_rng(21)
+    n, p = 9000, 160
+    X = rng.standard_normal((n, p)).astype(np.float32)
+    rows = np.sort(rng.choice(n, 7000, replace=False)).astype(np.int64)
+    hot = rows[[10, 2500, 2501, 5999]]
+    X[hot] *= np.float32(500.0)
+    seg = [0, 2000, 2000, 4700, 7000]
+    Xd = _dev(X)
+    import torch
+
+    shift = torch.zeros(p, dtype=torch.float32, device="cuda")
+    G, cs = eng.gram(Xd, _dev(rows), seg, shift, mode="i8x3", chunk_rows=1536)
+    assert eng.last_gram_marks(0) > 0
+    Xs = X[rows].astype(np.float64)
+    for s in range(len(seg) - 1):
+        Y = Xs[seg[s]:seg[s + 1]]
+        ref = Y.T @ Y
+        keep = ~np.isin(rows[seg[s]:seg[s + 1]], hot)
+        d = np.sqrt(np.maximum(np.einsum("ij,ij->j", Y[keep], Y[keep]), 1e-300))
+        if Y.shape[0] == 0:
+            assert np.all(G[s].cpu().numpy() == 0)
+            continue
+        err = np.abs(G[s].cpu().numpy() - ref) / np.outer(d, d)
+        assert err.max() < 2e-6, (s, err.max())
+        np.testing.assert_allclose(cs[s].cpu().numpy(), Y.sum(0), rtol=1e-6, atol=1e-6 * np.abs(Y).sum(0).max())

@@ -94,11 +94,16 @@ def test_limits_and_decisions_all_combos(golden_dir, name):
 
 
 @pytest.mark.parametrize("name", ["simca_a.npz", "simca_b.npz"])
-def test_fit_and_limits_with_bf16x3_gram(golden_dir, name, monkeypatch):
+def test_fit_and_limits_with_bf16x3_gram(golden_dir, name):
     """The same reference parity with the Gram on the exact bf16×3 split."""
-    monkeypatch.setenv("OCM_GRAM_MODE", "bf16x3")
-    test_fit_arrays_vs_reference(golden_dir, name)
-    test_limits_and_decisions_all_combos(golden_dir, name)
+    from ocm import engine
+
+    prev = engine.set_gram_mode("bf16x3")
+    try:
+        test_fit_arrays_vs_reference(golden_dir, name)
+        test_limits_and_decisions_all_combos(golden_dir, name)
+    finally:
+        engine.set_gram_mode(prev)
 
 
 @pytest.mark.parametrize("name", ["simca_a.npz", "simca_b.npz", "simca_multi.npz"])
@@ -124,6 +129,24 @@ def test_metrics_and_score(golden_dir):
         assert int(est.metrics[0][key]) == ref[key]
     s = est.score(g["X_test"], g["y_test"])
     assert np.isfinite(s)
+
+
+def test_score_pinned_to_reference(golden_dir):
+    """SIMCA.score (utils/SIMCA.py:268-278) returns the reference's value: the
+    2-D prediction matrix and the list model_class broadcast (one class → an
+    m×m comparison, specificity 5.5 on simca_a; three classes → ValueError)."""
+    pins = _load(golden_dir, "score.npz")
+    g = _load(golden_dir, "simca_a.npz")
+    est, _, _ = _est(g)
+    est.fit(g["X_fit"], g["y_fit"])
+    with contextlib.redirect_stdout(io.StringIO()):
+        np.testing.assert_allclose(est.score(g["X_test"], g["y_test"]), pins["a_score"], rtol=1e-12)
+    gm = _load(golden_dir, "simca_multi.npz")
+    est, _, _ = _est(gm)
+    est.fit(gm["X_fit"], gm["y_fit"])
+    assert str(pins["multi_error"]) == "ValueError"
+    with contextlib.redirect_stdout(io.StringIO()), pytest.raises(ValueError):
+        est.score(gm["X_test"], gm["y_test"])
 
 
 def test_device_resident_inputs(golden_dir):

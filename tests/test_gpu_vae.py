@@ -42,6 +42,22 @@ def test_compute_q_h_f_device(golden_dir):
     np.testing.assert_allclose([qc, hc, fc], g["crit"], rtol=1e-4)
 
 
+def test_compute_q_h_f_host_tensors(golden_dir):
+    """Host tensors (the reference drivers' case) run on the device too and
+    come back as host tensors."""
+    import torch
+    import vae_model as V
+
+    g = _load(golden_dir, "qhf.npz")
+    q, h, f, qc, hc, fc = V.compute_q_h_f(torch.from_numpy(g["x"]), torch.from_numpy(g["x_rec"]),
+                                          torch.from_numpy(g["z"]))
+    assert not (q.is_cuda or h.is_cuda or f.is_cuda)
+    np.testing.assert_allclose(q.numpy(), g["q"], rtol=1e-5)
+    np.testing.assert_allclose(h.numpy(), g["h"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(f.numpy(), g["f"], rtol=1e-4)
+    np.testing.assert_allclose([qc, hc, fc], g["crit"], rtol=1e-4)
+
+
 def _model(g, dev):
     import torch
     import vae_model as V
@@ -142,6 +158,80 @@ def test_vaesimca_network_path(golden_dir, name):
         assert y_pred.shape == (len(g["x_test"]),)
     finally:
         torch.backends.cudnn.enabled = prev
+
+
+def test_vaesimca_pinned_to_reference(golden_dir):
+    """VAESIMCA vs the REFERENCE class itself (tests/golden/vaesimca.npz: the
+    class of VAE_SIMCA.py:215-382 executed alone on the vae_a network), all
+    4 × 4 × 3 type / t2lim / qlim combinations on the same latents μ, ẑ:
+    combinations the reference rejects raise here too; limits rtol 1e-5 (the
+    script centres in float32, this engine in float64), dofs exact, decisions
+    identical outside a 1e-5 band."""
+    import torch
+    from ocm.vae import VAESIMCA
+
+    pins = _load(golden_dir, "vaesimca.npz")
+    g = _load(golden_dir, "vae_a.npz")
+    dev = torch.device("cuda", 0)
+    Z, Zh = torch.from_numpy(g["mu_cal"]).to(dev), torch.from_numpy(g["zhat_cal"]).to(dev)
+    Zt, Zht = torch.from_numpy(g["mu_test"]).to(dev), torch.from_numpy(g["zhat_test"]).to(dev)
+    n_ok = 0
+    for ci, combo in enumerate(pins["combos"]):
+        ty, t2, ql = str(combo).split("|")
+        est = VAESIMCA(None, type=ty, t2lim=t2, qlim=ql, device=dev, verbose=False)
+        if str(pins["errors"][ci]):
+            with pytest.raises(Exception):
+                est.fit_latents(Z, Zh, 0)
+            continue
+        est.fit_latents(Z, Zh, 0)
+        got = est._model[0]
+        if n_ok == 0:
+            np.testing.assert_allclose(got["T2"], pins["fit_T2"], rtol=1e-5)
+            np.testing.assert_allclose(got["Q"], pins["fit_Q"], rtol=1e-6)
+        for key in ("T2_limit", "Q_limit", "D_limit"):
+            np.testing.assert_allclose(got[key], pins[key][ci], rtol=1e-5, err_msg=f"{combo} {key}")
+        for key in ("T2dof", "Qdof"):
+            ref = pins[key][ci]
+            assert (got[key] is None and np.isnan(ref)) or got[key] == ref, (combo, key)
+        y_pred, T2, Q = est.predict_latents(Zt, Zht)
+        np.testing.assert_allclose(T2, pins["test_T2"], rtol=1e-5)
+        np.testing.assert_allclose(Q, pins["test_Q"], rtol=1e-6)
+        with np.errstate(divide="ignore"):
+            if ty == "alt":
+                D = np.sqrt((T2 / got["T2_limit"]) ** 2 + (Q / got["Q_limit"]) ** 2)
+            elif ty == "dd":
+                D = T2 * got["T2dof"] / got["T2scfact"] + Q * got["Qdof"] / got["Qscfact"]
+            else:
+                D = np.maximum(T2 / got["T2_limit"], Q / got["Q_limit"])
+        band = np.abs(D - got["D_limit"]) > 1e-5 * abs(got["D_limit"])
+        np.testing.assert_array_equal(y_pred[band].astype(np.uint8), pins["pred"][ci][band], err_msg=str(combo))
+        n_ok += 1
+    assert n_ok > 30
+
+
+def test_final_vaesimca_blocks_pinned_to_reference(golden_dir):
+    """utils/final_vaesimca.py:428-436 (latent stats) and :511-533 (full-distance
+    decision) vs the reference statements executed on the vae_a latents
+    (tests/golden/final_vaesimca.npz)."""
+    import torch
+    from ocm import vae
+
+    pins = _load(golden_dir, "final_vaesimca.npz")
+    g = _load(golden_dir, "vae_a.npz")
+    dev = torch.device("cuda", 0)
+    mean, inv, thr, qthr = vae.latent_stats(torch.from_numpy(g["mu_cal"]).to(dev),
+                                            torch.from_numpy(pins["rec_cal"]).to(dev))
+    np.testing.assert_allclose(mean.cpu().numpy(), pins["mu_train_mean"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(inv.cpu().numpy(), pins["cov_inv"], rtol=1e-6,
+                               atol=1e-6 * np.abs(pins["cov_inv"]).max())
+    np.testing.assert_allclose([thr, qthr], [pins["threshold"], pins["q_threshold"]], rtol=1e-6)
+    acc, f, fcrit = vae.full_distance_decision(torch.from_numpy(g["mu_test"]).to(dev),
+                                               torch.from_numpy(pins["mu_train_mean"].astype(np.float32)).to(dev),
+                                               torch.from_numpy(pins["q_test"]).to(dev))
+    np.testing.assert_allclose(f.cpu().numpy(), pins["f"], rtol=1e-5)
+    np.testing.assert_allclose(fcrit, pins["fcrit"], rtol=1e-6)
+    band = np.abs(pins["f"] - pins["fcrit"]) > 1e-4 * pins["fcrit"]
+    np.testing.assert_array_equal(acc.cpu().numpy()[band].astype(np.uint8), pins["pred_class0"][band])
 
 
 def test_vaesimca_errors():

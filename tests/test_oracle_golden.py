@@ -148,3 +148,124 @@ def test_oracle_qhf(golden_dir):
     np.testing.assert_allclose(h, g["h"], rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(f, g["f"], rtol=1e-4)
     np.testing.assert_allclose([qc, hc, fc], g["crit"], rtol=1e-4)
+
+
+# ---------------------------------------------------------------------------
+# round 2 fixtures: north-star shape, float64 input, score(), VAESIMCA and the
+# final_vaesimca inline blocks (all produced by the reference itself)
+# ---------------------------------------------------------------------------
+
+def ns_data(g):
+    """Regenerate the stored-by-seed inputs of simca_ns.npz / simca_f64.npz."""
+    cfg = json.loads(str(g["config_json"]))
+    if "n_test" in cfg:  # north star
+        X = O.synth_spectra(cfg["n_fit"] + cfg["n_test"], cfg["p"], cfg["k"], rank=cfg["rank"], seed=cfg["seed"],
+                            outlier_frac=cfg["outlier_frac"])
+        return X[:cfg["n_fit"]], X[cfg["n_fit"]:], cfg["k"]
+    X = O.synth_spectra(cfg["n"], cfg["p"], cfg["k"], rank=cfg["rank"], seed=cfg["seed"],
+                        outlier_frac=cfg["outlier_frac"], dtype=np.float64)
+    return X[:cfg["n_fit"]], X[cfg["n_fit"]:], cfg["k"]
+
+
+def _oracle_combo_check(g, X_fit, X_test, k, lim_rtol):
+    y = np.zeros(len(X_fit), dtype=np.int64)
+    n_checked = 0
+    for ci, combo in enumerate(g["combos"]):
+        ty, t2, ql = str(combo).split("|")
+        est = O.OracleSIMCA(n_components=k, model_class=0, type=ty, t2lim=t2, qlim=ql)
+        est.fit(X_fit, y)
+        m = est._model[0]
+        if ci == 0:
+            np.testing.assert_allclose(m["xmean"], g["xmean"], rtol=1e-5, atol=1e-6)
+            np.testing.assert_allclose(m["eigs_all"][:k], g["eigs_all"][:k], rtol=1e-5)
+            np.testing.assert_allclose(m["thetas"], g["thetas"], rtol=1e-4)
+            close(m["T2"], g["fit_T2"])
+            close(m["Q"], g["fit_Q"])
+            T2, _, Q, _ = est.transform(X_test)
+            close(T2, g["test_T2"], rtol=2e-4)
+            close(Q, g["test_Q"], rtol=2e-4)
+        rt = lim_rtol if t2 not in ("perc", "chi2pom") else 1e-4
+        np.testing.assert_allclose(m["T2_limit"], g["T2_limit"][ci], rtol=rt, err_msg=f"{combo} T2_limit")
+        np.testing.assert_allclose(m["Q_limit"], g["Q_limit"][ci], rtol=1e-4, err_msg=f"{combo} Q_limit")
+        np.testing.assert_allclose(m["D_limit"], g["D_limit"][ci], rtol=1e-4, err_msg=f"{combo} D_limit")
+        pred = est.predict(X_test)[:, 0]
+        d = est.dred(X_test, 0)
+        clear = np.abs(d - m["D_limit"]) > BAND * abs(m["D_limit"])
+        np.testing.assert_array_equal(pred[clear], g["pred"][ci][clear].astype(np.float64), err_msg=str(combo))
+        n_checked += int(clear.sum())
+    assert n_checked > 0
+
+
+def test_oracle_north_star_shape(golden_dir):
+    """p = 2048, k = 20 (SURVEY.md §8 north star) against the reference run."""
+    g = _load(golden_dir, "simca_ns.npz")
+    X_fit, X_test, k = ns_data(g)
+    _oracle_combo_check(g, X_fit, X_test, k, RT_LIM)
+
+
+def test_oracle_float64_input(golden_dir):
+    g = _load(golden_dir, "simca_f64.npz")
+    X_fit, X_test, k = ns_data(g)
+    _oracle_combo_check(g, X_fit, X_test, k, RT_LIM)
+
+
+def test_oracle_score_pins(golden_dir):
+    """utils/SIMCA.py:268-278: predict(X, y_true) then the conformity metrics of
+    the 2-D prediction matrix against the LIST model_class (NumPy broadcasting:
+    one class → an m×m comparison; three classes → a broadcast error)."""
+    pins = _load(golden_dir, "score.npz")
+    g = _load(golden_dir, "simca_a.npz")
+    est = O.OracleSIMCA(n_components=int(g["c0_k"]), model_class=0)
+    est.fit(g["X_fit"], g["y_fit"])
+    pred = est.predict(g["X_test"])
+    got = O.metrics_conformity(g["y_test"], pred, est.model_class)["specificity"]
+    np.testing.assert_allclose(got, pins["a_score"])
+    assert str(pins["multi_error"]) == "ValueError"
+    gm = _load(golden_dir, "simca_multi.npz")
+    est = O.OracleSIMCA(n_components=[2, 3, 4], model_class=None)
+    est.fit(gm["X_fit"], gm["y_fit"])
+    with pytest.raises(ValueError):
+        O.metrics_conformity(gm["y_test"], est.predict(gm["X_test"]), est.model_class)
+
+
+def test_oracle_vaesimca_pinned(golden_dir):
+    """VAESIMCA (VAE_SIMCA.py:215-382) restatement vs the reference class run
+    on the vae_a network (same latents μ, ẑ as vae_a.npz)."""
+    pins = _load(golden_dir, "vaesimca.npz")
+    v = _load(golden_dir, "vae_a.npz")
+    first = True
+    for ci, combo in enumerate(pins["combos"]):
+        ty, t2, ql = str(combo).split("|")
+        err = str(pins["errors"][ci])
+        if err:
+            with pytest.raises(Exception):
+                O.vaesimca_fit(v["mu_cal"], v["zhat_cal"], type=ty, t2lim=t2, qlim=ql)
+            continue
+        mdl = O.vaesimca_fit(v["mu_cal"], v["zhat_cal"], type=ty, t2lim=t2, qlim=ql)
+        if first:
+            np.testing.assert_allclose(mdl["T2"], pins["fit_T2"], rtol=1e-9)
+            np.testing.assert_allclose(mdl["Q"], pins["fit_Q"], rtol=1e-6)
+            first = False
+        for key in ("T2_limit", "Q_limit", "D_limit"):
+            # Q is a float32 torch sum in the script (±1 ulp here): Q-derived limits to 1e-6
+            np.testing.assert_allclose(mdl[key], pins[key][ci], rtol=1e-6, err_msg=f"{combo} {key}")
+        for key in ("T2dof", "Qdof"):
+            ref = pins[key][ci]
+            assert (mdl[key] is None and np.isnan(ref)) or mdl[key] == ref, (combo, key)
+        acc, T2, Q, _ = O.vaesimca_predict(mdl, v["mu_test"], v["zhat_test"])
+        np.testing.assert_array_equal(acc.astype(np.uint8), pins["pred"][ci], err_msg=str(combo))
+
+
+def test_oracle_final_vaesimca_pinned(golden_dir):
+    """utils/final_vaesimca.py:428-436 and :511-533 (extracted statements of the
+    reference run on the vae_a latents) vs the restatement."""
+    pins = _load(golden_dir, "final_vaesimca.npz")
+    v = _load(golden_dir, "vae_a.npz")
+    mu, inv, thr, qthr = O.latent_stats(v["mu_cal"], pins["rec_cal"])
+    np.testing.assert_allclose(mu, pins["mu_train_mean"], rtol=1e-6)
+    np.testing.assert_allclose(inv, pins["cov_inv"], rtol=1e-6, atol=1e-9 * np.abs(pins["cov_inv"]).max())
+    np.testing.assert_allclose([thr, qthr], [pins["threshold"], pins["q_threshold"]], rtol=1e-6)
+    acc, f, fcrit = O.full_distance_decision(v["mu_test"], pins["mu_train_mean"].astype(np.float32), pins["q_test"])
+    np.testing.assert_allclose(f, pins["f"], rtol=1e-6)
+    np.testing.assert_allclose(fcrit, pins["fcrit"], rtol=1e-6)  # the script works in float32
+    np.testing.assert_array_equal(acc.astype(np.uint8), pins["pred_class0"])
