@@ -303,7 +303,7 @@ def main():
             "avg_launch_ms": round(gram_avg_s * 1e3, 4),
             "launches": gram_n,
         },
-        "score_kernel": {"kernel": "k_score_direct (fused projection/Q/T2, two sweeps)", "bound": "hbm",
+        "score_kernel": {"kernel": "k_score_1p (fused projection/Q/T2/decision, one HBM pass; row tile kept in registers)", "bound": "hbm",
                          "achieved_GBs": round(score_gbs, 1), "peak_GBs": HBM_PEAK_GBS,
                          "frac": round(score_gbs / HBM_PEAK_GBS, 4), "avg_launch_ms": round(score_avg_s * 1e3, 4),
                          "launches": score_n, "bytes_per_launch": n * p * 4},

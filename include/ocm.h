@@ -89,12 +89,12 @@ int ocm_colmean_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* ro
  * split into three int8 digits per value (power-of-two scale per 1536-row
  * block and column) and the six digit products of weight ≥ 254⁻² are summed
  * exactly in int32 on integer MFMA (fp32-grade Gram: max relative error
- * ≈ 5e-8 on the bench data).  Outlier guard: values above 32× their column's
+ * ≈ 5e-8 on the bench data).  Outlier guard: values above 16× their column's
  * robust sample scale (2^e ≥ median|y| over the first ≤ 4096 rows) are
  * screened out of the digits of their 32-column group and
  * added back exactly (fp64 fix-up), so one extreme row does not coarsen the
- * other rows of its block; when more than n/8 values are screened the call
- * recomputes the Gram on FP32 MFMA.  Workspace: ≈ 3 B per value for the digit
+ * other rows of its block; when more than n/8 rows are screened the call
+ * recomputes the Gram on the bf16×3 split.  Workspace: ≈ 3 B per value for the digit
  * planes plus the chunk partials (≈ 8.4 GB at 1M × 2048).
  * Replaces the SVD of the centred class matrix (utils/SIMCA.py:64-66 ->
  * sklearn _pca.py:569-584 scipy.linalg.svd gesdd): the covariance
@@ -164,6 +164,18 @@ int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
                   const double* P, const double* mu, const double* A, int32_t k, float* T_out, double* T2_out,
                   float* Q_out, const ocm_decision* dec, double* accept_out, int64_t accept_stride,
                   double* stats_out, void* stream);
+
+/* Same with A = diag(a_diag) (a_diag [dev] k doubles) — the SIMCA case: the
+ * scores are on the eigenbasis, so invcovT = pinv(cov(T)) = diag(1/λ)
+ * (utils/SIMCA.py:69).  For p ∈ {256, 512, 1024, 2048}, k ≤ 20 and 16-B
+ * aligned X / ldx this runs k_score_1p, which reads every row of X from HBM
+ * once (the row tile stays in registers between the projection and the
+ * residual); other shapes take the two-sweep kernel of ocm_score_f32.
+ * Arguments and outputs as ocm_score_f32. */
+int ocm_score_f32_diag(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
+                       const double* P, const double* mu, const double* a_diag, int32_t k, float* T_out,
+                       double* T2_out, float* Q_out, const ocm_decision* dec, double* accept_out,
+                       int64_t accept_stride, double* stats_out, void* stream);
 
 /* Reduced distances and decision from stored T2/Q (utils/SIMCA.py:76-81,
  * 109-114, 131-145).  Outputs nullable [dev]: t2red, qred, dred (m doubles),
@@ -236,6 +248,14 @@ typedef struct ocm_cv_config {
 int ocm_cv_counts(ocm_ctx* ctx, const float* T, int64_t m, int32_t k, const float* Q, const double* inv_evals,
                   const uint8_t* positive, int64_t m_split, const ocm_cv_config* cfg, int32_t ncfg,
                   uint64_t* counts_out, double* accept_out, void* stream);
+
+/* Confusion counts of one class column of a prediction matrix
+ * (utils/SIMCA.py:238-245, called from predict(X, y_true) at :146-152):
+ * accept [dev] m doubles 0/1 at stride accept_stride (the column written by
+ * ocm_score_f32*'s fused decision), positive [dev] m bytes (y_true == class).
+ * counts_out [dev] 4 uint64 {TP, TN, FP, FN}. */
+int ocm_confusion_counts(ocm_ctx* ctx, const double* accept, int64_t m, int64_t accept_stride,
+                         const uint8_t* positive, uint64_t* counts_out, void* stream);
 
 /* ---- spectral preprocessing ----
  * SNV x ← (x − mean_row)/(std_row + 1e-8) (np.std ddof 0; simca_nuts.py:47-49,

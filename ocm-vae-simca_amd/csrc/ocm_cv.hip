@@ -162,6 +162,32 @@ __global__ __launch_bounds__(256) void k_cv_counts(const float* __restrict__ T, 
     if (scount[i]) atomicAdd(&counts[i], (unsigned long long)scount[i]);
 }
 
+// {TP, TN, FP, FN} of one class column of the prediction matrix
+// (utils/SIMCA.py:238-245): accept[r·stride] ∈ {0, 1}, positive[r] = (y_true == class)
+__global__ __launch_bounds__(256) void k_confusion(const double* __restrict__ accept, int64_t m, int64_t stride,
+                                                   const uint8_t* __restrict__ positive,
+                                                   unsigned long long* __restrict__ counts) {
+  __shared__ unsigned int sc[4];
+  if (threadIdx.x < 4) sc[threadIdx.x] = 0u;
+  __syncthreads();
+  unsigned int c[4] = {0u, 0u, 0u, 0u};
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < m; r += (int64_t)gridDim.x * 256) {
+    const double a = accept[r * stride];
+    const bool pos = positive[r] != 0;
+    if (a == 1.0) ++c[pos ? 0 : 2];       // TP / FP
+    else if (a == 0.0) ++c[pos ? 3 : 1];  // FN / TN
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    unsigned int v = c[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&sc[i], v);
+  }
+  __syncthreads();
+  if (threadIdx.x < 4 && sc[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)sc[threadIdx.x]);
+}
+
 int combine_impl(const double* const* G_list, const double* const* colsum_list, const double* coef, int32_t nterm,
                  int32_t p, double* G_out, double* colsum_out, hipStream_t st) {
   const int64_t pp = (int64_t)p * p;
@@ -261,6 +287,21 @@ int ocm_cv_counts(ocm_ctx* ctx, const float* T, int64_t m, int32_t k, const floa
   if (k <= 16) OCM_CV_COUNTS(16); else if (k <= 32) OCM_CV_COUNTS(32); else OCM_CV_COUNTS(64);
 #undef OCM_CV_COUNTS
   OCM_CHECK_LAUNCH("k_cv_counts");
+  return OCM_OK;
+}
+
+int ocm_confusion_counts(ocm_ctx* ctx, const double* accept, int64_t m, int64_t accept_stride,
+                         const uint8_t* positive, uint64_t* counts_out, void* stream) {
+  OCM_REQUIRE(ctx && counts_out, "ocm_confusion_counts: NULL argument");
+  OCM_REQUIRE(m == 0 || (accept && positive), "ocm_confusion_counts: NULL argument");
+  OCM_REQUIRE(m >= 0 && accept_stride >= 1, "ocm_confusion_counts: bad shape");
+  hipStream_t st = (hipStream_t)stream;
+  OCM_HIP(hipMemsetAsync(counts_out, 0, 4 * sizeof(uint64_t), st));
+  if (m == 0) return OCM_OK;
+  const unsigned grid = (unsigned)std::min<int64_t>((m + 255) / 256, (int64_t)ctx->num_cus * 4);
+  hipLaunchKernelGGL(k_confusion, dim3(grid), dim3(256), 0, st, accept, m, accept_stride, positive,
+                     reinterpret_cast<unsigned long long*>(counts_out));
+  OCM_CHECK_LAUNCH("k_confusion");
   return OCM_OK;
 }
 

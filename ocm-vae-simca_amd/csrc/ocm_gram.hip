@@ -630,13 +630,13 @@ __global__ __launch_bounds__(256) void k_gram_small_reduce(const double* __restr
 // column maximum, so one extreme row would cost the other 1535 rows of its
 // block their precision.  k_q8_quant therefore screens every value against a
 // per-column threshold τ·2^e_j (2^e_j ≥ median|y_j| over the first ≤ 4096
-// rows, a robust scale; τ = 32; k_colexp_hist / k_q8_thresholds): a row with any value above it inside the workgroup's 32
+// rows, a robust scale; τ = 16; k_colexp_hist / k_q8_thresholds): a row with any value above it inside the workgroup's 32
 // columns is left out of those columns' scale and digits (its digits there
 // are 0) and marked in a per-row column-group bitmask.  k_gram_fixup adds the
 // marked rows' missing products exactly (fp64: y_i y_j for every pair with
 // at least one column in a marked group).  Clean data marks nothing and pays
-// one scalar read-back; heavily marked data (> n/8 marks) falls back to the
-// FP32-MFMA Gram.
+// one scalar read-back; heavily marked data (> n/8 rows) falls back to the
+// bf16×3 Gram (exact split, fp32-grade).
 //
 // Digit planes: [digit][32-row group][column P8][32 B] (the 32 B of a column
 // are its 32 rows of one group — one MFMA K-step).  The digit planes are in
@@ -660,7 +660,7 @@ struct Q8Plan {
   uint32_t* nmark;   // number of (row, column group) marks
 };
 
-constexpr float Q8TAU = 32.f;     // outlier threshold in robust column scales (2^e ≥ median|y|)
+constexpr float Q8TAU = 16.f;     // outlier threshold in robust column scales (2^e ≥ median|y|)
 constexpr int Q8GROUP = 32;       // columns per guard group (= quantiser workgroup width)
 
 __device__ __forceinline__ uint32_t q8_byte(float a, int u) { return ((uint32_t)(int)a & 0xffu) << (8 * u); }
@@ -1374,8 +1374,8 @@ int gram_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, in
 
 // i8×3 path: thresholds → quantise (one read of X, outlier screen) →
 // integer-MFMA Gram → f64 reduce → (marked rows only) exact fix-up.
-// Returns OCM_OK, or 1 when more than n/8 values were screened out: the
-// caller then recomputes the Gram on the FP32-MFMA path.
+// Returns OCM_OK, or 1 when more than n/8 rows had values screened out: the
+// caller then recomputes the Gram on the bf16×3 path.
 int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
                const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
                hipStream_t st, int64_t chunk_rows) {
@@ -1515,19 +1515,23 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     OCM_CHECK_LAUNCH("k_colblk_sum");
     OCM_CHECK_LAUNCH("k_gram_reduce");
   }
-  uint32_t marks = 1;  // capturing: the fix-up runs on device-side counts
-  if (!capturing) {
+  if (!capturing) {  // capturing: the fix-up runs on device-side counts
     const hipError_t e = hipEventSynchronize(ev);
     (void)hipEventDestroy(ev);
     if (e != hipSuccess) return ocm::fail(OCM_ERR_HIP, std::string("gram mark read-back: ") + hipGetErrorString(e));
-    marks = host[0];
-    ctx->last_gram_marks = marks;
-    if (marks == 0) return OCM_OK;
-    if ((int64_t)marks > n / 8) return 1;
+    ctx->last_gram_marks = host[0];
+    if (host[0] == 0) return OCM_OK;
   }
   hipLaunchKernelGGL(k_flag_count, dim3(nfblk), dim3(256), 0, st, flags, fw, n, fcnt);
   hipLaunchKernelGGL(k_flag_emit, dim3(nfblk), dim3(256), 0, st, flags, fw, n, fcnt, nfblk, flist, counters + 1);
   OCM_CHECK_LAUNCH("k_flag_emit");
+  if (!capturing) {
+    // the fix-up costs p²/2 fp64 FMAs per marked row: past n/8 rows the
+    // bf16×3 Gram of everything is cheaper
+    OCM_HIP(hipMemcpyAsync(host + 1, counters + 1, 4, hipMemcpyDeviceToHost, st));
+    OCM_HIP(hipStreamSynchronize(st));
+    if ((int64_t)host[1] > n / 8) return 1;
+  }
   const int nt64 = (p + FX_T - 1) / FX_T;
   for (int s0 = 0; s0 < nseg; s0 += MAXSEG) {
     const int s1 = std::min(nseg, s0 + MAXSEG);
@@ -1548,7 +1552,7 @@ int gram_dispatch(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
   if (mode == OCM_GRAM_I8X3) {
     const int rc = gram_impl8(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows);
     if (rc != 1) return rc;
-    mode = OCM_GRAM_F32;  // too many screened values: recompute on FP32 MFMA
+    mode = OCM_GRAM_BF16X3;  // too many screened rows: recompute on the exact bf16×3 split
   }
   // f32 accumulation length per partial: short chunks keep the tiles of one
   // chunk co-resident on an XCD (L2 reuse) and the tail short; the partial

@@ -17,6 +17,8 @@
 // flushed to f64 every chunk.
 #include "ocm_internal.h"
 
+#include <utility>
+
 namespace {
 
 constexpr int SW = 4;   // waves per workgroup
@@ -59,8 +61,8 @@ __device__ __forceinline__ void score_epilogue(double* tls, double* sred, const 
   double T2 = 0.0, Q = q64;
   if (own) {
     const double* trow = Tt + l31 * (KP + 1);
-    if (a_diag) {
-      for (int a = 0; a < k; ++a) T2 += trow[a] * trow[a] * A[a * k + a];
+    if (a_diag) {  // A holds the diagonal only
+      for (int a = 0; a < k; ++a) T2 += trow[a] * trow[a] * A[a];
     } else {
       for (int a = 0; a < k; ++a) {
         double s = 0.0;
@@ -274,6 +276,547 @@ __global__ __launch_bounds__(256, 2) void k_score_direct(const float* __restrict
                          Q_out, dec, acc_out, acc_stride, stat_part);
 }
 
+// ---------------------------------------------------------------------------
+// k_score_1p — single HBM pass over X (p ∈ {256, 512, 1024, 2048}, k ≤ 20,
+// diagonal A = diag(1/λ) as every SIMCA fit produces).  The default scoring
+// kernel for those shapes; k_score_direct covers the rest.
+//
+// One workgroup of four waves per CU (one wave per SIMD, 512 registers),
+// persistent over 16-row tiles.  Wave w owns columns [w·p/4, (w+1)·p/4) of a
+// tile's 16 rows and keeps them in registers from the HBM read to the
+// residual, so X is read once.  Two register tiles: V (VGPRs) holds d = x − μ
+// of the tile being scored, A (AGPRs) the raw next tile.  Sweep 1 of tile
+// t + G (G = grid) moves A into V block by block and immediately refills
+// each block of A with tile t + 2G, so one whole tile (the 128 KiB per CU an
+// HBM stream needs in flight at full rate) is always outstanding, and each
+// load has a full tile of compute to arrive.
+//   sweep 1  tᵀ += P₀·(x − μ)ᵀ on v_mfma_f32_16x16x4_f32, comps 0..15 (lane
+//            (row = l&15, q = l>>4) feeds column 16j+4q+e of its row as the B
+//            operand); comps 16..19 by VALU FMAs beside it; μ and the comps
+//            16..19 loadings live in registers in a compact form and reach
+//            each lane by DPP row broadcast inside the add / FMA;
+//   reduce   the four waves' partial t meet in LDS (one barrier per tile);
+//   sweep 2  rᵀ = dᵀ + Pᵀ·(−t)ᵀ per 16-column block (comps as K, the chain
+//            starts from the stored d = x − μ; the output lands on the lanes
+//            that hold those columns), q += r²;
+//   epilogue the wave partials of Q meet after the next barrier; T², Q, T,
+//            the fused decision and the moment partials.
+// Nothing but X (and the row indices of a gather) is read from global
+// memory inside the tile loop, and the only synchronisation is LDS + s_barrier:
+// vmcnt is in order, so any wait on another global access would also wait
+// for the tile in flight.  Rows past m are clamped to row m−1 (a valid row)
+// and their outputs dropped.  P₀ is stored [comp][16-B chunk ^ sw(comp)]:
+// conflict-free ds_read_b128 in sweep 1 and ds_read_b32 in sweep 2.
+// Numerics as k_score_direct: d = x − μ in f32, f32 MFMA partials flushed to
+// f64 every 128 columns, explicit residual.
+// ---------------------------------------------------------------------------
+namespace s1p {
+constexpr int W = 4, R = 16;
+// compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N-1
+template <class F, int... I>
+__device__ __forceinline__ void sfor_(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  sfor_(f, std::make_integer_sequence<int, N>{});
+}
+__device__ __forceinline__ int sw(int m) { return ((4 * m) ^ (2 * (m >> 2))) & 15; }
+
+// d[e] = x[e] + (lane B + e of the 16-lane DPP row of u), e = 0..3: the
+// centring of one 16-column block, x read from the AGPR tile (u = −μ in the
+// compact form).  hipcc does not fold a row_newbcast mov into an add, and pads
+// nothing inside inline asm: the leading s_nop covers a VALU write of u right
+// before (DPP read: 2 states), the trailing one the MFMAs that read d next
+// (VALU write → MFMA operand).
+template <int B>
+__device__ __forceinline__ void centre4(float u, const f32x4& x, f32x4& d) {
+  asm("v_accvgpr_read_b32 %0, %5\n\t"
+      "v_accvgpr_read_b32 %1, %6\n\t"
+      "v_accvgpr_read_b32 %2, %7\n\t"
+      "v_accvgpr_read_b32 %3, %8\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %4, %0 row_newbcast:%9 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %4, %1 row_newbcast:%10 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %2, %4, %2 row_newbcast:%11 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %3, %4, %3 row_newbcast:%12 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "s_nop 1"
+      : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3])
+      : "v"(u), "a"(x[0]), "a"(x[1]), "a"(x[2]), "a"(x[3]), "n"(B), "n"(B + 1), "n"(B + 2), "n"(B + 3));
+}
+// a float of the comps 16..19 loadings into an AGPR (an MFMA A operand only)
+__device__ __forceinline__ float to_agpr(float v) {
+  float r;
+  asm("v_accvgpr_write_b32 %0, %1" : "=a"(r) : "v"(v));
+  return r;
+}
+// 16 B of row data into an AGPR quad, not tracked by the compiler's waitcnt:
+// the consumer waits with wait_vm (vmcnt is in order)
+template <int OFF>
+__device__ __forceinline__ void load_a(f32x4& a, const float* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=a"(a) : "v"(p), "n"(OFF) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm(f32x4& a) {
+#ifdef OCM_S1P_DIAG_NOWAIT  // timing ablation only (wrong results)
+  asm volatile("" : "+a"(a));
+#else
+  asm volatile("s_waitcnt vmcnt(%1)" : "+a"(a) : "n"(N));
+#endif
+}
+// ---- hand-scheduled inner steps (VALU work placed in the MFMA gaps) ----------
+// One wave per SIMD issues in order, so VALU work only overlaps the matrix
+// pipe if it sits between the MFMAs in program order: the steps below are
+// inline asm (hipcc schedules each block's VALU after its MFMAs).  Wait states
+// inside: s_nop 1 ahead of a DPP read or MFMA operand read of a register a
+// VALU op may just have written (hipcc pads nothing inside asm); an MFMA
+// result is read by VALU only ≥ 1 MFMA issue later (≥ 32 cycles ≥ the 12
+// states an 8-pass XDL result needs), except where a trailing s_nop says so.
+//
+// Sweep-1 step: MFMAs of block j (acc += a[e]·d[e]) interleaved with the
+// centring of block j+1 (n = x + DPP-broadcast −μ, x read from AGPRs) and, for
+// EX, the comps 16..19 FMAs of block j (xs[c] += DPP-broadcast p[c] · d[e]).
+#define OCM_DPP(L) " row_newbcast:" #L " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+#define OCM_S1_CENTRE(N0, N1, N2, N3)                          \
+  "s_nop 1\n\t"                                              \
+  "v_add_f32_dpp %[n0], %[mu], %[n0]" OCM_DPP(N0)            \
+  "v_add_f32_dpp %[n1], %[mu], %[n1]" OCM_DPP(N1)            \
+  "v_add_f32_dpp %[n2], %[mu], %[n2]" OCM_DPP(N2)            \
+  "v_add_f32_dpp %[n3], %[mu], %[n3]" OCM_DPP(N3)
+#define OCM_S1_READX                                           \
+  "v_accvgpr_read_b32 %[n0], %[x0]\n\t"                      \
+  "v_accvgpr_read_b32 %[n1], %[x1]\n\t"                      \
+  "v_accvgpr_read_b32 %[n2], %[x2]\n\t"                      \
+  "v_accvgpr_read_b32 %[n3], %[x3]\n\t"
+#define OCM_S1_EXFMA(D, L)                                     \
+  "v_fmac_f32_dpp %[s0], %[p0], %[" #D "]" OCM_DPP(L)          \
+  "v_fmac_f32_dpp %[s1], %[p1], %[" #D "]" OCM_DPP(L)          \
+  "v_fmac_f32_dpp %[s2], %[p2], %[" #D "]" OCM_DPP(L)          \
+  "v_fmac_f32_dpp %[s3], %[p3], %[" #D "]" OCM_DPP(L)
+#define OCM_MFMA(ACC, A, B) "v_mfma_f32_16x16x4_f32 %[" #ACC "], %[" #A "], %[" #B "], %[" #ACC "]\n\t"
+#define OCM_S1_OPS_ACC [aA] "+v"(acA), [aB] "+v"(acB), [aC] "+v"(acC), [aD] "+v"(acD)
+#define OCM_S1_IN_AD                                                                                      \
+  [a0] "v"(a[0]), [a1] "v"(a[1]), [a2] "v"(a[2]), [a3] "v"(a[3]), [d0] "v"(d[0]), [d1] "v"(d[1]),           \
+      [d2] "v"(d[2]), [d3] "v"(d[3])
+#define OCM_S1_IN_X [x0] "a"(x[0]), [x1] "a"(x[1]), [x2] "a"(x[2]), [x3] "a"(x[3]), [mu] "v"(mu)
+#define OCM_S1_IN_P [p0] "v"(p[0]), [p1] "v"(p[1]), [p2] "v"(p[2]), [p3] "v"(p[3])
+
+template <int B>  // B = 4(j % 4): DPP lanes of block j; block j+1 uses (B + 4) % 16
+struct S1Step;
+#define OCM_S1_STEP_SPEC(B, B1, B2, B3, N0, N1, N2, N3)                                                     \
+  template <>                                                                                             \
+  struct S1Step<B> {                                                                                      \
+    /* k ≤ 16: MFMAs of block j + centring of block j+1 */                                               \
+    __device__ static __forceinline__ void next(f32x4& acA, f32x4& acB, f32x4& acC, f32x4& acD,            \
+                                                const f32x4& a, const f32x4& d, float mu, const f32x4& x,  \
+                                                f32x4& n) {                                                \
+      asm("s_nop 1\n\t" OCM_MFMA(aA, a0, d0) OCM_MFMA(aB, a1, d1) OCM_S1_READX OCM_MFMA(aC, a2, d2)        \
+              OCM_S1_CENTRE(N0, N1, N2, N3) OCM_MFMA(aD, a3, d3)                                           \
+          : OCM_S1_OPS_ACC, [n0] "=&v"(n[0]), [n1] "=&v"(n[1]), [n2] "=&v"(n[2]), [n3] "=&v"(n[3])         \
+          : OCM_S1_IN_AD, OCM_S1_IN_X);                                                                   \
+    }                                                                                                     \
+    /* k > 16: the same plus the comps 16..19 FMAs of block j */                                         \
+    __device__ static __forceinline__ void next_ex(f32x4& acA, f32x4& acB, f32x4& acC, f32x4& acD,         \
+                                                   float (&s)[4], const f32x4& a, const f32x4& d,          \
+                                                   const float (&p)[4], float mu, const f32x4& x,          \
+                                                   f32x4& n) {                                             \
+      asm("s_nop 1\n\t" OCM_MFMA(aA, a0, d0) OCM_S1_EXFMA(d0, B) OCM_MFMA(aB, a1, d1) OCM_S1_READX          \
+              OCM_S1_EXFMA(d1, B1) OCM_MFMA(aC, a2, d2) OCM_S1_EXFMA(d2, B2)                               \
+                  OCM_S1_CENTRE(N0, N1, N2, N3) OCM_MFMA(aD, a3, d3) OCM_S1_EXFMA(d3, B3)                 \
+          : OCM_S1_OPS_ACC, [s0] "+v"(s[0]), [s1] "+v"(s[1]), [s2] "+v"(s[2]), [s3] "+v"(s[3]),            \
+            [n0] "=&v"(n[0]), [n1] "=&v"(n[1]), [n2] "=&v"(n[2]), [n3] "=&v"(n[3])                         \
+          : OCM_S1_IN_AD, OCM_S1_IN_P, OCM_S1_IN_X);                                                      \
+    }                                                                                                     \
+    /* the last block of the sweep (nothing to centre) */                                                \
+    __device__ static __forceinline__ void last(f32x4& acA, f32x4& acB, f32x4& acC, f32x4& acD,            \
+                                                const f32x4& a, const f32x4& d) {                          \
+      asm("s_nop 1\n\t" OCM_MFMA(aA, a0, d0) OCM_MFMA(aB, a1, d1) OCM_MFMA(aC, a2, d2) OCM_MFMA(aD, a3, d3) \
+          : OCM_S1_OPS_ACC                                                                                \
+          : OCM_S1_IN_AD);                                                                                \
+    }                                                                                                     \
+    __device__ static __forceinline__ void last_ex(f32x4& acA, f32x4& acB, f32x4& acC, f32x4& acD,         \
+                                                   float (&s)[4], const f32x4& a, const f32x4& d,          \
+                                                   const float (&p)[4]) {                                  \
+      asm("s_nop 1\n\t" OCM_MFMA(aA, a0, d0) OCM_S1_EXFMA(d0, B) OCM_MFMA(aB, a1, d1) OCM_S1_EXFMA(d1, B1)  \
+              OCM_MFMA(aC, a2, d2) OCM_S1_EXFMA(d2, B2) OCM_MFMA(aD, a3, d3) OCM_S1_EXFMA(d3, B3)           \
+          : OCM_S1_OPS_ACC, [s0] "+v"(s[0]), [s1] "+v"(s[1]), [s2] "+v"(s[2]), [s3] "+v"(s[3])             \
+          : OCM_S1_IN_AD, OCM_S1_IN_P);                                                                   \
+    }                                                                                                     \
+  };
+OCM_S1_STEP_SPEC(0, 1, 2, 3, 4, 5, 6, 7)
+OCM_S1_STEP_SPEC(4, 5, 6, 7, 8, 9, 10, 11)
+OCM_S1_STEP_SPEC(8, 9, 10, 11, 12, 13, 14, 15)
+OCM_S1_STEP_SPEC(12, 13, 14, 15, 0, 1, 2, 3)
+#undef OCM_S1_STEP_SPEC
+
+// Sweep-2 pair step: the two MFMA chains of blocks (j, j+1) — r_u = d_u +
+// Σ_s a_u[s]·tB[s] on a VGPR accumulator each, interleaved so no MFMA waits on
+// its predecessor — with the q FMAs of the previous pair (q0 += r0p², q1 +=
+// r1p²) in the gaps.  NS = 4 or 5 steps (comps 16..19: step 4, A from AGPRs).
+#define OCM_S2_IN_COMMON                                                                                  \
+  [d0] "v"(d0), [d1] "v"(d1), [u0] "v"(a0[0]), [u1] "v"(a0[1]), [u2] "v"(a0[2]), [u3] "v"(a0[3]),           \
+      [w0] "v"(a1[0]), [w1] "v"(a1[1]), [w2] "v"(a1[2]), [w3] "v"(a1[3]), [t0] "v"(tB[0]), [t1] "v"(tB[1]),   \
+      [t2] "v"(tB[2]), [t3] "v"(tB[3])
+#define OCM_S2_IN_PREV                                                                                    \
+  [e0] "v"(r0p[0]), [e1] "v"(r0p[1]), [e2] "v"(r0p[2]), [e3] "v"(r0p[3]), [f0] "v"(r1p[0]), [f1] "v"(r1p[1]), \
+      [f2] "v"(r1p[2]), [f3] "v"(r1p[3])
+#define OCM_S2_IN_EX [u4] "a"(a0[4]), [w4] "a"(a1[4]), [t4] "v"(tB[4])
+#define OCM_S2M(R, A, T) "v_mfma_f32_16x16x4_f32 %[" #R "], %[" #A "], %[" #T "], %[" #R "]\n\t"
+#define OCM_S2M0(R, A, T, D) "v_mfma_f32_16x16x4_f32 %[" #R "], %[" #A "], %[" #T "], %[" #D "]\n\t"
+#define OCM_QF(Q, E) "v_fmac_f32_e32 %[" #Q "], %[" #E "], %[" #E "]\n\t"
+template <int NS, bool FIRST>
+__device__ __forceinline__ void s2_pair(const f32x4& d0, const f32x4& d1, const float (&a0)[5], const float (&a1)[5],
+                                        const float (&tB)[5], const f32x4& r0p, const f32x4& r1p, float& q0,
+                                        float& q1, f32x4& r0, f32x4& r1) {
+  if constexpr (FIRST && NS == 4) {
+    asm("s_nop 1\n\t" OCM_S2M0(r0, u0, t0, d0) OCM_S2M0(r1, w0, t0, d1) OCM_S2M(r0, u1, t1) OCM_S2M(r1, w1, t1)
+            OCM_S2M(r0, u2, t2) OCM_S2M(r1, w2, t2) OCM_S2M(r0, u3, t3) OCM_S2M(r1, w3, t3)
+        : [r0] "=&v"(r0), [r1] "=&v"(r1)
+        : OCM_S2_IN_COMMON);
+  } else if constexpr (FIRST) {
+    asm("s_nop 1\n\t" OCM_S2M0(r0, u0, t0, d0) OCM_S2M0(r1, w0, t0, d1) OCM_S2M(r0, u1, t1) OCM_S2M(r1, w1, t1)
+            OCM_S2M(r0, u2, t2) OCM_S2M(r1, w2, t2) OCM_S2M(r0, u3, t3) OCM_S2M(r1, w3, t3) OCM_S2M(r0, u4, t4)
+                OCM_S2M(r1, w4, t4)
+        : [r0] "=&v"(r0), [r1] "=&v"(r1)
+        : OCM_S2_IN_COMMON, OCM_S2_IN_EX);
+  } else if constexpr (NS == 4) {
+    asm("s_nop 1\n\t" OCM_S2M0(r0, u0, t0, d0) OCM_S2M0(r1, w0, t0, d1) OCM_QF(q0, e0) OCM_S2M(r0, u1, t1)
+            OCM_QF(q1, e1) OCM_S2M(r1, w1, t1) OCM_QF(q0, e2) OCM_S2M(r0, u2, t2) OCM_QF(q1, e3)
+                OCM_S2M(r1, w2, t2) OCM_QF(q0, f0) OCM_S2M(r0, u3, t3) OCM_QF(q1, f1) OCM_S2M(r1, w3, t3)
+                    OCM_QF(q0, f2) OCM_QF(q1, f3)
+        : [r0] "=&v"(r0), [r1] "=&v"(r1), [q0] "+v"(q0), [q1] "+v"(q1)
+        : OCM_S2_IN_COMMON, OCM_S2_IN_PREV);
+  } else {
+    asm("s_nop 1\n\t" OCM_S2M0(r0, u0, t0, d0) OCM_S2M0(r1, w0, t0, d1) OCM_QF(q0, e0) OCM_S2M(r0, u1, t1)
+            OCM_QF(q1, e1) OCM_S2M(r1, w1, t1) OCM_QF(q0, e2) OCM_S2M(r0, u2, t2) OCM_QF(q1, e3)
+                OCM_S2M(r1, w2, t2) OCM_QF(q0, f0) OCM_S2M(r0, u3, t3) OCM_QF(q1, f1) OCM_S2M(r1, w3, t3)
+                    OCM_QF(q0, f2) OCM_S2M(r0, u4, t4) OCM_QF(q1, f3) OCM_S2M(r1, w4, t4)
+        : [r0] "=&v"(r0), [r1] "=&v"(r1), [q0] "+v"(q0), [q1] "+v"(q1)
+        : OCM_S2_IN_COMMON, OCM_S2_IN_PREV, OCM_S2_IN_EX);
+  }
+}
+
+}  // namespace s1p
+
+template <int NJ, bool EX>
+__global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X, int64_t ldx,
+                                                     const int64_t* __restrict__ rows, int64_t m,
+                                                     const double* __restrict__ P, const double* __restrict__ mu,
+                                                     const double* __restrict__ adiag, int k,
+                                                     float* __restrict__ T_out, double* __restrict__ T2_out,
+                                                     float* __restrict__ Q_out, DecArgs dec,
+                                                     double* __restrict__ acc_out, int64_t acc_stride,
+                                                     double* __restrict__ stat_part, int64_t ntiles) {
+  using namespace s1p;
+  constexpr int PW = 16 * NJ;  // columns per wave
+  constexpr int PP = W * PW;   // p
+  constexpr int NCH = PP / 4;  // 16-B chunks per component row
+  constexpr int NS = EX ? 5 : 4;  // sweep-2 K steps (4 components each; rows ≥ k of P are zero)
+  static_assert(NJ % 4 == 0, "the chunk swizzle needs 64-column wave slices");
+  __shared__ f32x4 P0s[16 * NCH];
+  __shared__ double tpart[2][W * 20 * R];  // [buffer][wave][comp][row]
+  __shared__ double qpart[2][W * R];       // [buffer][wave][row]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ln = lane & 15, lq = lane >> 4;
+
+  // ---- prologue: loadings (f64 → f32) into LDS; μ, comps 16..19, diag(A) into registers
+  for (int e = tid; e < 16 * NCH; e += 256) {
+    const int c = e / NCH, ch = e - c * NCH;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (c < k)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = (float)P[(int64_t)c * PP + 4 * ch + u];
+    P0s[c * NCH + (ch ^ sw(c))] = v;
+  }
+  // compact DPP-row form of a per-column vector v over the wave's PW columns:
+  // register g, lane (ln, lq) holds column 16j + 4lq + e with j = 4g + ln/4,
+  // e = ln%4 — the value a lane needs for (j, e) sits in lane 4(j%4) + e of
+  // its own 16-lane row (row = lq)
+  auto compact_col = [&](int g) { return w * PW + 16 * (4 * g + (ln >> 2)) + 4 * lq + (ln & 3); };
+  float nmu[NJ / 4];  // −μ
+#pragma unroll
+  for (int g = 0; g < NJ / 4; ++g) nmu[g] = -(float)mu[compact_col(g)];
+  float p1c[EX ? NJ / 4 : 1][4];  // sweep 1: comps 16..19, compact form
+  float p1a[EX ? NJ : 1];         // sweep 2: A operand of step 4, P[16 + lq][w·PW + 16j + ln]
+  if constexpr (EX) {
+#pragma unroll
+    for (int g = 0; g < NJ / 4; ++g)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) p1c[g][c] = 16 + c < k ? (float)P[(int64_t)(16 + c) * PP + compact_col(g)] : 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      p1a[j] = to_agpr(16 + lq < k ? (float)P[(int64_t)(16 + lq) * PP + w * PW + 16 * j + ln] : 0.f);
+  }
+  double ad[5];
+#pragma unroll
+  for (int s = 0; s < 5; ++s) ad[s] = lq + 4 * s < k ? adiag[lq + 4 * s] : 0.0;
+  // sweep-1 A operand: chunk (w·PW/4 + 4j + lq) ^ sw(ln) of comp ln; the XOR
+  // only touches the low 4 bits, so j = 4a + b reads b1[b] + 16a chunks
+  int b1[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) b1[b] = ln * NCH + w * (PW / 4) + ((4 * b + lq) ^ sw(ln));
+  // sweep-2 A operand: P[c = 4s + lq][w·PW + 16j + ln] at float index
+  // 4·(c·NCH + w·PW/4 + ((4j + ln/4) ^ sw(c))) + ln%4; j = 4a + b → b2[s][b] + 64a
+  int b2[4][4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int c = 4 * s + lq;
+      b2[s][b] = 4 * (c * NCH + w * (PW / 4) + ((4 * b + (ln >> 2)) ^ sw(c))) + (ln & 3);
+    }
+  const float* p0f = reinterpret_cast<const float*>(P0s);
+
+  const int64_t G = gridDim.x;
+  // base of this lane's 16-B pieces in row `row` of the wave's column slice
+  auto col_base = [&](int64_t row) { return X + row * ldx + w * PW + 4 * lq; };
+  // row index of lane row ln in tile tt (clamped: always a valid row).  For a
+  // gather the 16 indices are read through the scalar cache (uniform
+  // addresses, lgkmcnt): a vector load here would wait, in order, for the tile in flight
+  auto index_of = [&](int64_t tt) -> int64_t {
+    if (!rows) {
+      const int64_t r = tt * R + ln;
+      return r < m ? r : m - 1;
+    }
+    int64_t v = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int64_t r = tt * R + i;
+      const int64_t ri = rows[r < m ? r : m - 1];
+      v = ln == i ? ri : v;
+    }
+    return v;
+  };
+
+  f32x4 V[NJ];  // d = x − μ of the tile being scored (VGPRs)
+  f32x4 A[NJ];  // raw x of the next tile (AGPRs, loaded by asm; waited with wait_vm)
+  double st[4] = {0.0, 0.0, 0.0, 0.0};
+  double tt[5];
+  float tB[5];
+  double T2 = 0.0, T2prev = 0.0;
+
+  // ---- sweep 1: A (raw tile) → V (d), partial t → tpart[buf]; each block of
+  // A is refilled from `pre` (the tile after next) as soon as it is read
+  auto sweep1 = [&](const float* pre, int buf) {
+    f32x4 accA = {0.f, 0.f, 0.f, 0.f}, accB = accA, accC = accA, accD = accA;
+    double t64[4] = {0.0, 0.0, 0.0, 0.0};
+    float x1[4] = {0.f, 0.f, 0.f, 0.f};
+    double x164[4] = {0.0, 0.0, 0.0, 0.0};
+    f32x4 aN = P0s[b1[0]];  // LDS operands read one 16-column block ahead
+    // A[j] was issued NJ loads before the refills of blocks ≤ j... are: the rest
+    // of its tile and the refills of blocks < j were issued after it (a few
+    // output stores may add to that, which only makes the wait earlier)
+    wait_vm<NJ - 1>(A[0]);
+    centre4<0>(nmu[0], A[0], V[0]);
+    load_a<0>(A[0], pre);
+    static_for<NJ>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      const f32x4 a = aN;
+      if constexpr (j + 1 < NJ) aN = P0s[b1[(j + 1) & 3] + 16 * ((j + 1) >> 2)];
+      using Step = S1Step<4 * (j & 3)>;
+      if constexpr (j + 1 < NJ) {
+        wait_vm<NJ - 1>(A[j + 1]);
+        if constexpr (EX)
+          Step::next_ex(accA, accB, accC, accD, x1, a, V[j], p1c[j >> 2], nmu[(j + 1) >> 2], A[j + 1], V[j + 1]);
+        else
+          Step::next(accA, accB, accC, accD, a, V[j], nmu[(j + 1) >> 2], A[j + 1], V[j + 1]);
+        load_a<64 * (j + 1)>(A[j + 1], pre);
+      } else {
+        if constexpr (EX)
+          Step::last_ex(accA, accB, accC, accD, x1, a, V[j], p1c[j >> 2]);
+        else
+          Step::last(accA, accB, accC, accD, a, V[j]);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting every block's reads
+      if constexpr ((j & 15) == 15 || j == NJ - 1) {  // f32 partials over ≤ 64 columns per chain
+        asm volatile("s_nop 11" ::: "memory");        // last MFMA result → VALU read
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          t64[i] += ((double)accA[i] + (double)accB[i]) + ((double)accC[i] + (double)accD[i]);
+          accA[i] = accB[i] = accC[i] = accD[i] = 0.f;
+          if constexpr (EX) {
+            x164[i] += (double)x1[i];
+            x1[i] = 0.f;
+          }
+        }
+      }
+    });
+    double* tp = tpart[buf];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tp[(w * 20 + 4 * lq + i) * R + ln] = t64[i];
+    if constexpr (EX) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // comps 16..19: sum over the q lanes
+        x164[u] += __shfl_xor(x164[u], 16, 64);
+        x164[u] += __shfl_xor(x164[u], 32, 64);
+      }
+      if (lq == 0)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) tp[(w * 20 + 16 + u) * R + ln] = x164[u];
+    }
+  };
+  // ---- full t of this lane's comps lq + 4s (row ln) from tpart[buf]; T², T --
+  auto compute_t = [&](int64_t t, int buf) {
+    const double* tp = tpart[buf];
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      double v = 0.0;
+      if (s < 4 || EX)
+#pragma unroll
+        for (int ww = 0; ww < W; ++ww) v += tp[(ww * 20 + lq + 4 * s) * R + ln];
+      tt[s] = v;
+    }
+    T2 = 0.0;
+#pragma unroll
+    for (int s = 0; s < 5; ++s) T2 += tt[s] * tt[s] * ad[s];
+    T2 += __shfl_xor(T2, 16, 64);
+    T2 += __shfl_xor(T2, 32, 64);
+    const int64_t row = t * R + ln;
+    if (T_out && w == 0 && row < m)
+#pragma unroll
+      for (int s = 0; s < 5; ++s)
+        if (lq + 4 * s < k) T_out[row * k + lq + 4 * s] = (float)tt[s];
+#pragma unroll
+    for (int s = 0; s < 5; ++s) tB[s] = -(float)tt[s];  // the sweep-2 chain from d ends at r = d − Pᵀt
+  };
+  // ---- sweep 2 on V (d of the tile being scored): Q partials → qpart[buf] --
+  auto sweep2 = [&](int buf) {
+    float q0 = 0.f, q1 = 0.f;
+    double q64 = 0.0;
+    float aN[2][5];  // A operands of the next block pair (LDS reads one pair ahead)
+    auto read_a = [&](auto J, float (&dst)[5]) {
+      constexpr int j = decltype(J)::value;
+#ifdef OCM_S1P_DIAG_NOLDS2  // timing ablation only (wrong results)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) dst[s] = (float)(b2[s][j & 3] + j);
+#else
+#pragma unroll
+      for (int s = 0; s < 4; ++s) dst[s] = p0f[b2[s][j & 3] + 64 * (j >> 2)];
+#endif
+      if constexpr (EX) dst[4] = p1a[j];
+      else dst[4] = 0.f;
+    };
+    read_a(std::integral_constant<int, 0>{}, aN[0]);
+    read_a(std::integral_constant<int, 1>{}, aN[1]);
+    f32x4 r0, r1;  // r of the previous pair (its q FMAs run inside the next pair's MFMAs)
+    static_for<NJ / 2>([&](auto H) {
+      constexpr int j = 2 * decltype(H)::value;
+      float a0[5], a1[5];
+#pragma unroll
+      for (int s = 0; s < 5; ++s) {
+        a0[s] = aN[0][s];
+        a1[s] = aN[1][s];
+      }
+      if constexpr (j + 2 < NJ) {
+        read_a(std::integral_constant<int, j + 2>{}, aN[0]);
+        read_a(std::integral_constant<int, j + 3>{}, aN[1]);
+      }
+      f32x4 n0, n1;
+      s2_pair<NS, j == 0>(V[j], V[j + 1], a0, a1, tB, r0, r1, q0, q1, n0, n1);
+      r0 = n0;
+      r1 = n1;
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((j & 15) == 14) {  // f32 q partials over ≤ 128 columns per accumulator
+        q64 += (double)q0 + (double)q1;
+        q0 = q1 = 0.f;
+      }
+    });
+    asm volatile("s_nop 11" ::: "memory");  // last pair's MFMA results → VALU
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      q0 = fmaf(r0[e], r0[e], q0);
+      q1 = fmaf(r1[e], r1[e], q1);
+    }
+    q64 += (double)q0 + (double)q1;
+    q64 += __shfl_xor(q64, 16, 64);
+    q64 += __shfl_xor(q64, 32, 64);
+    if (lq == 0) qpart[buf][w * R + ln] = q64;
+  };
+  // outputs of tile t from qpart[buf] (T² of t was kept in T2prev)
+  auto finish = [&](int64_t t, int buf) {
+    double Q = 0.0;
+#pragma unroll
+    for (int ww = 0; ww < W; ++ww) Q += qpart[buf][ww * R + ln];
+    const int64_t row = t * R + ln;
+    if (w == 0 && lq == 0 && row < m) {
+      const float Qf = (float)Q;
+      if (T2_out) T2_out[row] = T2prev;
+      if (Q_out) Q_out[row] = Qf;
+      if (dec.enabled) {
+        const double dr = ocm::dred_of(dec.type, T2prev * dec.t2_scale, (double)Qf * dec.q_scale);
+        acc_out[row * acc_stride] = dr < dec.dlim ? 1.0 : 0.0;
+      }
+      st[0] += T2prev;
+      st[1] += T2prev * T2prev;
+      st[2] += (double)Qf;
+      st[3] += (double)Qf * (double)Qf;
+    }
+  };
+  // LDS hand-off between the waves: no global access is waited for
+  auto lds_barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // ---- tile pipeline: tiles t_i = blockIdx.x + i·G.  An iteration scores t
+  // (sweep 2 on V), then runs sweep 1 of t + G (A → V) while tile t + 2G
+  // streams into A; past the last tile the refill re-reads a valid tile.
+  int64_t t = blockIdx.x;
+  auto clamp_tile = [&](int64_t tt) { return tt < ntiles ? tt : t; };
+  {
+    const float* p0 = col_base(index_of(t));
+    static_for<NJ>([&](auto J) { load_a<64 * decltype(J)::value>(A[decltype(J)::value], p0); });
+  }
+  sweep1(col_base(index_of(clamp_tile(t + G))), 0);
+  lds_barrier();
+  compute_t(t, 0);
+  int buf = 0;
+#ifdef OCM_S1P_STAMPS  // diagnostic build only: cycles per phase (stat_part carries them)
+  uint64_t cyc[4] = {0, 0, 0, 0};
+#define OCM_STAMP(I) { const uint64_t now_ = __builtin_amdgcn_s_memtime(); cyc[I] += now_ - last_; last_ = now_; }
+  uint64_t last_ = __builtin_amdgcn_s_memtime();
+#else
+#define OCM_STAMP(I)
+#endif
+  for (;;) {
+    const int64_t tn = t + G;
+    const bool more = tn < ntiles;
+    sweep2(buf);
+    OCM_STAMP(0)
+    if (more) sweep1(col_base(index_of(clamp_tile(tn + G))), buf ^ 1);
+    OCM_STAMP(1)
+    lds_barrier();
+    OCM_STAMP(2)
+    T2prev = T2;
+    finish(t, buf);
+    if (!more) break;
+    t = tn;
+    buf ^= 1;
+    compute_t(t, buf);
+    OCM_STAMP(3)
+  }
+#undef OCM_STAMP
+#ifdef OCM_S1P_STAMPS
+  st[0] = (double)cyc[0]; st[1] = (double)cyc[1]; st[2] = (double)cyc[2]; st[3] = (double)cyc[3];
+  if (stat_part && w == 0 && lane == 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) stat_part[(int64_t)blockIdx.x * 4 + i] = st[i];
+  return;
+#endif
+  // drain the refills past the last tile before the wave ends
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) wait_vm<0>(A[j]);
+  if (stat_part) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st[i] = wave_sum_f64(st[i]);
+    if (w == 0 && lane == 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) stat_part[(int64_t)blockIdx.x * 4 + i] = st[i];
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_stats_reduce(const double* __restrict__ part, int64_t nblk,
                                                        double* __restrict__ out) {
   // 16 waves: wave w sums column w & 3 over row slice w >> 2 (4 slices), four
@@ -331,19 +874,11 @@ __global__ void k_cast_f64_f32(const double* __restrict__ a, int64_t n, float* _
   if (i < n) b[i] = (float)a[i];
 }
 
-}  // namespace
-
-extern "C" {
-
-int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
-                  const double* P, const double* mu, const double* A, int32_t k, float* T_out, double* T2_out,
-                  float* Q_out, const ocm_decision* dec, double* accept_out, int64_t accept_stride,
-                  double* stats_out, void* stream) {
-  OCM_REQUIRE(ctx && X && P && mu && A, "ocm_score_f32: NULL argument");
-  OCM_REQUIRE(m >= 0 && p > 0 && ldx >= p, "ocm_score_f32: bad shape");
-  OCM_REQUIRE(k >= 1 && k <= 64, "ocm_score_f32: 1 <= k <= 64");
-  OCM_REQUIRE(!dec || accept_out, "ocm_score_f32: decision requires accept_out");
-  hipStream_t st = (hipStream_t)stream;
+// k_score_direct launch (any p, k ≤ 64); a_diag: A is the k-vector diag(A)
+int score_direct(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
+                 const double* P, const double* mu, const double* A, int a_diag, int32_t k, float* T_out,
+                 double* T2_out, float* Q_out, const ocm_decision* dec, double* accept_out, int64_t accept_stride,
+                 double* stats_out, hipStream_t st) {
   if (m == 0) {
     if (stats_out) OCM_HIP(hipMemsetAsync(stats_out, 0, 4 * sizeof(double), st));
     return OCM_OK;
@@ -364,7 +899,6 @@ int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
                      (int64_t)k * p, P32);
   hipLaunchKernelGGL(k_cast_f64_f32, dim3((p + 255) / 256), dim3(256), 0, st, mu, (int64_t)p, mu32);
   OCM_CHECK_LAUNCH("k_cast_f64_f32");
-  const int a_diag = 0;  // general k×k quadratic form (k² FMAs per row are negligible)
   DecArgs d{};
   if (dec) {
     d.enabled = 1;
@@ -390,6 +924,88 @@ int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
   OCM_CHECK_LAUNCH("k_score");
   if (stats_out) {
     hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, st, part, nblk, stats_out);
+    OCM_CHECK_LAUNCH("k_stats_reduce");
+  }
+  return OCM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
+                  const double* P, const double* mu, const double* A, int32_t k, float* T_out, double* T2_out,
+                  float* Q_out, const ocm_decision* dec, double* accept_out, int64_t accept_stride,
+                  double* stats_out, void* stream) {
+  OCM_REQUIRE(ctx && X && P && mu && A, "ocm_score_f32: NULL argument");
+  OCM_REQUIRE(m >= 0 && p > 0 && ldx >= p, "ocm_score_f32: bad shape");
+  OCM_REQUIRE(k >= 1 && k <= 64, "ocm_score_f32: 1 <= k <= 64");
+  OCM_REQUIRE(!dec || accept_out, "ocm_score_f32: decision requires accept_out");
+  // general k×k quadratic form (k² FMAs per row are negligible)
+  return score_direct(ctx, X, ldx, rows, m, p, P, mu, A, 0, k, T_out, T2_out, Q_out, dec, accept_out,
+                      accept_stride, stats_out, (hipStream_t)stream);
+}
+
+int ocm_score_f32_diag(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
+                       const double* P, const double* mu, const double* a_diag, int32_t k, float* T_out,
+                       double* T2_out, float* Q_out, const ocm_decision* dec, double* accept_out,
+                       int64_t accept_stride, double* stats_out, void* stream) {
+  OCM_REQUIRE(ctx && X && P && mu && a_diag, "ocm_score_f32_diag: NULL argument");
+  OCM_REQUIRE(m >= 0 && p > 0 && ldx >= p, "ocm_score_f32_diag: bad shape");
+  OCM_REQUIRE(k >= 1 && k <= 64, "ocm_score_f32_diag: 1 <= k <= 64");
+  OCM_REQUIRE(!dec || accept_out, "ocm_score_f32_diag: decision requires accept_out");
+  hipStream_t st = (hipStream_t)stream;
+  const int nj = p / 64;
+  const bool vec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+  const bool one_pass = vec && p % 64 == 0 && (nj == 4 || nj == 8 || nj == 16 || nj == 32) && k <= 20;
+  if (!one_pass)  // other shapes: the two-sweep kernel
+    return score_direct(ctx, X, ldx, rows, m, p, P, mu, a_diag, 1, k, T_out, T2_out, Q_out, dec, accept_out,
+                        accept_stride, stats_out, st);
+  if (m == 0) {
+    if (stats_out) OCM_HIP(hipMemsetAsync(stats_out, 0, 4 * sizeof(double), st));
+    return OCM_OK;
+  }
+  const int64_t ntiles = (m + s1p::R - 1) / s1p::R;
+  const int grid = (int)std::min<int64_t>(ctx->num_cus, ntiles);
+  double* part = nullptr;
+  if (stats_out) {
+    void* wsp = ocm::workspace(ctx, (size_t)grid * 4 * sizeof(double) + 256, st);
+    if (!wsp) return OCM_ERR_NOMEM;
+    part = static_cast<double*>(wsp);
+  }
+  DecArgs d{};
+  if (dec) {
+    d.enabled = 1;
+    d.type = dec->type;
+    d.t2_scale = dec->t2_scale;
+    d.q_scale = dec->q_scale;
+    d.dlim = dec->dlim;
+  }
+  {
+    ocm::TimedRegion tr(ctx, OCM_KERNEL_SCORE, st);
+#define OCM_S1P(NJ_, EX_)                                                                                    \
+  hipLaunchKernelGGL((k_score_1p<NJ_, EX_>), dim3(grid), dim3(256), 0, st, X, ldx, rows, m, P, mu, a_diag, k, \
+                     T_out, T2_out, Q_out, d, accept_out, accept_stride, part, ntiles)
+#define OCM_S1P_K(NJ_) \
+  if (k > 16)          \
+    OCM_S1P(NJ_, true); \
+  else                 \
+    OCM_S1P(NJ_, false);
+    if (nj == 32) {
+      OCM_S1P_K(32)
+    } else if (nj == 16) {
+      OCM_S1P_K(16)
+    } else if (nj == 8) {
+      OCM_S1P_K(8)
+    } else {
+      OCM_S1P_K(4)
+    }
+#undef OCM_S1P_K
+#undef OCM_S1P
+  }
+  OCM_CHECK_LAUNCH("k_score_1p");
+  if (stats_out) {
+    hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, st, part, (int64_t)grid, stats_out);
     OCM_CHECK_LAUNCH("k_stats_reduce");
   }
   return OCM_OK;

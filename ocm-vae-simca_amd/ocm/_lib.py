@@ -74,6 +74,9 @@ SIGNATURES = {
     "ocm_score_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_void_p,
                               c_i32, c_void_p, c_void_p, c_void_p, ctypes.POINTER(OcmDecision), c_void_p, c_i64,
                               c_void_p, c_void_p]),
+    "ocm_score_f32_diag": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p,
+                                   c_void_p, c_i32, c_void_p, c_void_p, c_void_p, ctypes.POINTER(OcmDecision),
+                                   c_void_p, c_i64, c_void_p, c_void_p]),
     "ocm_decide": (c_i32, [c_void_p, c_void_p, c_void_p, c_i64, ctypes.POINTER(OcmDecision), c_void_p, c_void_p,
                            c_void_p, c_void_p, c_i64, c_void_p]),
     "ocm_rowsq_residual_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i64, c_i32, c_void_p,
@@ -85,6 +88,7 @@ SIGNATURES = {
                                  ctypes.POINTER(c_f64), c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
     "ocm_cv_prefix": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_void_p, c_void_p, ctypes.POINTER(c_i32), c_i32,
                               c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ocm_confusion_counts": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_void_p]),
     "ocm_snv_savgol_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_i32, c_i32, c_i32,
                                    ctypes.POINTER(c_f64), c_void_p, c_i64, c_void_p]),
     "ocm_cv_counts": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_void_p, c_i64,

@@ -23,11 +23,15 @@ their own fold's prediction and other-class rows the LAST fold's
 (:190, 205-207), eff = √(sens·spec) (:208).
 
 Multi-GPU (``group`` given): each rank holds a contiguous row block of X
-(``row_offset``) and the full label vector.  Per-fold Grams are summed by one
-RCCL all-reduce, fold f's eigensolve runs on rank f mod W and its model is
-broadcast, every rank scores its own rows, and the confusion counts and
-training moments are all-reduced.  Same code path at W = 1 without
-collectives.
+(``row_offset``) and the full label vector.  Fold f's eigensolve runs on
+its owner rank f mod W: every rank forms its local TRAIN Gram of fold f
+(Σ_g G_g − G_f, fp64 downdating on the device) and one RCCL reduce brings
+the sum to the owner only (K reduces of p² doubles instead of K
+all-reduces); the column sums (K·p doubles) are all-reduced.  The owner
+broadcasts the fold model (P, μ, λ, θ ≈ 0.3 MB), every rank scores its own
+rows, the confusion counts and training moments are all-reduced, and the
+pooled prediction vectors travel as one device all-gather of each rank's
+row block.  Same code path at W = 1 without collectives.
 """
 from __future__ import annotations
 
@@ -197,21 +201,32 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
         G = torch.zeros((K, p, p), dtype=torch.float64, device=dev)
         cs = torch.zeros((K, p), dtype=torch.float64, device=dev)
     if distributed:
-        dist.all_reduce(G, group=group)
         dist.all_reduce(cs, group=group)
+    # local total Gram Σ_g G_g (its column sums are rebuilt from the reduced cs)
     Gt = torch.empty((p, p), dtype=torch.float64, device=dev)
     cst = torch.empty(p, dtype=torch.float64, device=dev)
     engine.gram_combine([(1.0, G[f], cs[f]) for f in range(K)], Gt, cst)
 
     # ---- per-fold eigen-models (fold f on rank f mod W, then broadcast) ----
     models = FoldModels()
+    Gtr = torch.empty((p, p), dtype=torch.float64, device=dev) if distributed else None
+    cs_tr = torch.empty(p, dtype=torch.float64, device=dev)
     for f in range(K):
         n_tr = n_target - int(folds[f].size)
         if n_tr < 2:
             raise ValueError("SIMCA needs at least 2 samples in a class")
+        owner = f % W
+        if distributed:
+            # this rank's train Gram of fold f, summed on the owner only
+            engine.gram_combine([(1.0, Gt, None), (-1.0, G[f], None)], Gtr, None)
+            dist.reduce(Gtr, dst=dist.get_global_rank(group, owner) if group is not None else owner, group=group)
         pack = torch.empty(lvmax + 3 + p + lvmax * p, dtype=torch.float64, device=dev)
-        if f % W == R:
-            C, mean = engine.cov_from_gram([(1.0, Gt, cst), (-1.0, G[f], cs[f])], shift32, n_tr)
+        if owner == R:
+            torch.sub(cst, cs[f], out=cs_tr)  # Σ_g cs_g − cs_f (p doubles)
+            if distributed:
+                C, mean = engine.cov_from_gram([(1.0, Gtr, cs_tr)], shift32, n_tr)
+            else:
+                C, mean = engine.cov_from_gram([(1.0, Gt, cst), (-1.0, G[f], cs[f])], shift32, n_tr)
             evals, evecs, theta, _ = engine.eig_topk(C, lvmax, theta_mode)
             del C
             pack[:lvmax] = evals
@@ -219,7 +234,7 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
             pack[lvmax + 3:lvmax + 3 + p] = mean
             pack[lvmax + 3 + p:] = evecs.reshape(-1)
         if distributed:
-            dist.broadcast(pack, src=dist.get_global_rank(group, f % W) if group is not None else f % W,
+            dist.broadcast(pack, src=dist.get_global_rank(group, owner) if group is not None else owner,
                            group=group)
         evals = pack[:lvmax]
         models.evals.append(evals)
@@ -230,7 +245,7 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
         models.evals_h.append(host[:lvmax])
         models.theta_h.append(host[lvmax:lvmax + 3])
         models.n_train.append(n_tr)
-    del G, cs, Gt
+    del G, cs, Gt, Gtr
 
     # ---- per-fold scoring, limits, counts ----
     ncfg = len(combos) * len(lvs)
@@ -240,7 +255,6 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
     F_cache = {}
     for f in range(K):
         mean, evecs, inv = models.mean[f], models.evecs[f], models.inv[f]
-        A = torch.diag(inv)
         n_tr = models.n_train[f]
         # training-row statistics per LV (perc / chi2pom limits)
         tr_stats = None
@@ -249,7 +263,7 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
             tr_loc = np.concatenate([loc_folds[g] for g in range(K) if g != f]) if K > 1 else np.zeros(0, np.int64)
             if tr_loc.size:
                 rows = torch.from_numpy(tr_loc).to(dev)
-                sc = engine.score(Xd, rows, int(tr_loc.size), evecs, mean, A, want_T=True, want_T2=False,
+                sc = engine.score(Xd, rows, int(tr_loc.size), evecs, mean, inv, want_T=True, want_T2=False,
                                   want_Q=True)
                 T2a, Qa, st = engine.cv_prefix(sc["T"], sc["Q"], inv, lvs, want_T2=need_pct, want_Q=need_pct,
                                                want_stats=True)
@@ -296,7 +310,7 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
         if m:
             rows = torch.from_numpy(test_loc).to(dev)
             pos = torch.from_numpy(positive_glob[test_loc + lo].astype(np.uint8)).to(dev)
-            sc = engine.score(Xd, rows, m, evecs, mean, A, want_T=True, want_T2=False, want_Q=True)
+            sc = engine.score(Xd, rows, m, evecs, mean, inv, want_T=True, want_T2=False, want_Q=True)
             cnt, acc = engine.cv_counts(sc["T"], sc["Q"], inv, pos, int(fold_loc.size), configs,
                                         want_accept=store_predictions)
             del sc
@@ -307,12 +321,20 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
             dist.all_reduce(cnt, group=group)
         counts[f] = cnt.cpu().numpy()
         if store_predictions:
-            preds_fold.append((test_loc + lo, acc.cpu().numpy()))
+            # the pooled vector (utils/CVSIMCA.py:190, 205-207): target rows
+            # take their own fold's decision, other-class rows the last fold's
+            keep = slice(0, int(fold_loc.size)) if f < K - 1 else slice(0, m)
+            preds_fold.append((torch.from_numpy(test_loc[keep]).to(dev), acc[:, keep]))
 
     # ---- aggregation (utils/CVSIMCA.py:190-222) ----
     records, by_combo = [], []
-    if store_predictions and distributed:
-        preds_fold = _gather_predictions(preds_fold, group)
+    pred_all = None
+    if store_predictions:
+        pred_loc = torch.zeros((ncfg, n_loc), dtype=torch.float64, device=dev)
+        for idx, acc in preds_fold:
+            if idx.numel():
+                pred_loc[:, idx] = acc
+        pred_all = (_gather_blocks(pred_loc, lo, n_glob, group) if distributed else pred_loc).cpu().numpy()
     for ci_, combo in enumerate(combos):
         for li, lv in enumerate(lvs):
             c = ci_ * len(lvs) + li
@@ -326,11 +348,7 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
             records.append({"params": combo.copy(), "LV": lv, "spec": spec, "sens": sens,
                             "eff": float(np.sqrt(sens * spec))})
             if store_predictions:
-                pred_vec = np.zeros(n_glob, dtype=float)
-                for f in range(K):
-                    idx, acc = preds_fold[f]
-                    pred_vec[idx] = acc[c]
-                by_combo.append({"params": combo.copy(), "LV": lv, "prediction": pred_vec})
+                by_combo.append({"params": combo.copy(), "LV": lv, "prediction": pred_all[c].copy()})
     # keep the reference's record order: combos outer, LV in the given order
     if list(lv_values) != lvs:
         order = {lv: i for i, lv in enumerate(lvs)}
@@ -360,12 +378,22 @@ def _pct_fn(arr, li, n, group, distributed):
     return pct
 
 
-def _gather_predictions(preds_fold, group):
-    """All ranks' (global row index, accept) pairs per fold → every rank."""
+def _gather_blocks(block: torch.Tensor, lo: int, n_glob: int, group) -> torch.Tensor:
+    """Every rank's (rows, n_loc) column block at global offset ``lo`` →
+    the (rows, n_glob) matrix on every rank: one all-gather of the offsets and
+    one of the blocks padded to the largest (device tensors; no host pickling)."""
     W = dist.get_world_size(group)
-    out = []
-    for idx, acc in preds_fold:
-        got = [None] * W
-        dist.all_gather_object(got, (idx, acc), group=group)
-        out.append((np.concatenate([g[0] for g in got]), np.concatenate([g[1] for g in got], axis=1)))
+    dev = block.device
+    meta = torch.tensor([lo, block.shape[1]], dtype=torch.int64, device=dev)
+    metas = [torch.empty_like(meta) for _ in range(W)]
+    dist.all_gather(metas, meta, group=group)
+    metas = [m.cpu().tolist() for m in metas]
+    width = max(n for _, n in metas)
+    pad = torch.zeros((block.shape[0], width), dtype=block.dtype, device=dev)
+    pad[:, :block.shape[1]] = block
+    parts = [torch.empty_like(pad) for _ in range(W)]
+    dist.all_gather(parts, pad, group=group)
+    out = torch.zeros((block.shape[0], n_glob), dtype=block.dtype, device=dev)
+    for (o, n), part in zip(metas, parts):
+        out[:, o:o + n] = part[:, :n]
     return out

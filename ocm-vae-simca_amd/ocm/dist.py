@@ -125,6 +125,6 @@ class ShardedSIMCA:
         if out is None:
             out = torch.empty(m, dtype=torch.float64, device=X_local.device)
         fit = self.fit_
-        engine.score(X_local, None, m, fit.P64, fit.mean64, fit.invcov, want_T2=False, want_Q=False,
+        engine.score(X_local, None, m, fit.P64, fit.mean64, fit.inv_diag, want_T2=False, want_Q=False,
                      decision=self.decision, accept_out=out, accept_stride=1)
         return out

@@ -64,6 +64,7 @@ class ClassFit:
     evals: torch.Tensor          # (k,) f64
     P64: torch.Tensor            # (k, p) f64, svd_flip sign convention (scoring operand)
     invcov: torch.Tensor         # (k, k) f64 = pinv(cov(T)) = diag(1/λ)
+    inv_diag: torch.Tensor = None  # (k,) f64: its diagonal (the scoring kernels' operand)
     thetas: tuple = (0.0, 0.0, 0.0)
     evals_host: np.ndarray = None
     T: torch.Tensor | None = None
@@ -204,8 +205,9 @@ def make_decision(type_name: str, t2_scale: float, q_scale: float, dlim: float) 
 def score(X: torch.Tensor, rows: torch.Tensor | None, m: int, P64: torch.Tensor, mean64: torch.Tensor,
           A: torch.Tensor, want_T=False, want_T2=True, want_Q=True, decision: OcmDecision | None = None,
           accept_out: torch.Tensor | None = None, accept_stride: int = 1, want_stats=False):
-    """Fused scoring (ocm_score_f32): P64 (k, p) f64 orthonormal rows, mean64 (p,) f64.
-    Returns dict of device tensors."""
+    """Fused scoring: P64 (k, p) f64 orthonormal rows, mean64 (p,) f64, A the
+    (k, k) quadratic form (ocm_score_f32) or its diagonal (k,) (ocm_score_f32_diag,
+    the single-HBM-pass kernel for the SIMCA shapes).  Returns dict of device tensors."""
     k, p = P64.shape
     dev = X.device
     out = {}
@@ -215,9 +217,10 @@ def score(X: torch.Tensor, rows: torch.Tensor | None, m: int, P64: torch.Tensor,
     st = torch.empty(4, dtype=torch.float64, device=dev) if want_stats else None
     ctx = Context.get(dev.index)
     dec_p = ctypes.byref(decision) if decision is not None else None
-    check(_lib.load().ocm_score_f32(ctx.handle, ptr(X), X.stride(0), ptr(rows), m, p, ptr(P64), ptr(mean64),
-                                    ptr(A), k, ptr(T), ptr(T2), ptr(Q), dec_p, ptr(accept_out), accept_stride,
-                                    ptr(st), _stream(dev)), "ocm_score_f32")
+    fn = "ocm_score_f32_diag" if A.dim() == 1 else "ocm_score_f32"
+    check(getattr(_lib.load(), fn)(ctx.handle, ptr(X), X.stride(0), ptr(rows), m, p, ptr(P64), ptr(mean64),
+                                   ptr(A), k, ptr(T), ptr(T2), ptr(Q), dec_p, ptr(accept_out), accept_stride,
+                                   ptr(st), _stream(dev)), fn)
     out["T"], out["T2"], out["Q"], out["stats"] = T, T2, Q, st
     return out
 
@@ -233,6 +236,17 @@ def decide(T2: torch.Tensor, Q: torch.Tensor, decision: OcmDecision, want_red=Tr
     check(_lib.load().ocm_decide(ctx.handle, ptr(T2), ptr(Q), m, ctypes.byref(decision), ptr(t2r), ptr(qr),
                                  ptr(dr), ptr(accept_out), accept_stride, _stream(dev)), "ocm_decide")
     return t2r, qr, dr
+
+
+def confusion_counts(accept: torch.Tensor, positive: torch.Tensor, stride: int = 1) -> torch.Tensor:
+    """{TP, TN, FP, FN} (int64, device) of a 0/1 prediction column ``accept``
+    (float64, read at ``stride``) against the uint8 mask ``positive``."""
+    m = positive.numel()
+    out = torch.empty(4, dtype=torch.int64, device=positive.device)
+    check(_lib.load().ocm_confusion_counts(Context.get(positive.device.index).handle, ptr(accept), m, int(stride),
+                                           ptr(positive), ptr(out), _stream(positive.device)),
+          "ocm_confusion_counts")
+    return out
 
 
 def percentile(v: torch.Tensor, pct: float) -> float:
@@ -252,7 +266,10 @@ def gram_combine(terms, G_out: torch.Tensor | None, cs_out: torch.Tensor | None)
     dev = terms[0][1].device
     p = terms[0][1].shape[-1]
     Gp = (ctypes.c_void_p * nt)(*[t[1].data_ptr() for t in terms])
-    Sp = (ctypes.c_void_p * nt)(*[t[2].data_ptr() for t in terms])
+    with_cs = all(t[2] is not None for t in terms)
+    if cs_out is not None and not with_cs:
+        raise ValueError("gram_combine: cs_out needs every term's column sums")
+    Sp = (ctypes.c_void_p * nt)(*[t[2].data_ptr() for t in terms]) if with_cs else None
     cf = (ctypes.c_double * nt)(*[float(t[0]) for t in terms])
     check(_lib.load().ocm_gram_combine(Context.get(dev.index).handle, Gp, Sp, cf, nt, p, ptr(G_out), ptr(cs_out),
                                        _stream(dev)), "ocm_gram_combine")
@@ -282,11 +299,15 @@ def cv_counts(T: torch.Tensor, Q: torch.Tensor, inv_evals: torch.Tensor, positiv
     nc = len(configs)
     counts = torch.empty((nc, 2, 4), dtype=torch.int64, device=dev)
     acc = torch.empty((nc, m), dtype=torch.float64, device=dev) if want_accept else None
-    arr = (_lib.OcmCvConfig * nc)(*[_lib.OcmCvConfig(int(lv), TYPE_CODES[ty], float(a), float(b), float(d))
-                                    for (lv, ty, a, b, d) in configs])
-    check(_lib.load().ocm_cv_counts(Context.get(dev.index).handle, ptr(T), m, k, ptr(Q), ptr(inv_evals),
-                                    ptr(positive), int(m_split), arr, nc, ptr(counts), ptr(acc), _stream(dev)),
-          "ocm_cv_counts")
+    # ≤ OCM_CV_MAXCFG configurations per launch (the kernel's LDS counters)
+    for c0 in range(0, nc, _lib.OCM_CV_MAXCFG):
+        part = configs[c0:c0 + _lib.OCM_CV_MAXCFG]
+        n = len(part)
+        arr = (_lib.OcmCvConfig * n)(*[_lib.OcmCvConfig(int(lv), TYPE_CODES[ty], float(a), float(b), float(d))
+                                       for (lv, ty, a, b, d) in part])
+        check(_lib.load().ocm_cv_counts(Context.get(dev.index).handle, ptr(T), m, k, ptr(Q), ptr(inv_evals),
+                                        ptr(positive), int(m_split), arr, n, ptr(counts[c0:]),
+                                        ptr(acc[c0:] if acc is not None else None), _stream(dev)), "ocm_cv_counts")
     return counts, acc
 
 
@@ -321,13 +342,17 @@ def rowsq_residual(x: torch.Tensor, xhat: torch.Tensor) -> torch.Tensor:
     return q
 
 
-def invcov_from_evals(evals: torch.Tensor, rcond=1e-15) -> torch.Tensor:
-    """pinv(cov(T)) for T = centred scores on the eigenbasis: cov(T) = diag(λ)
-    (utils/SIMCA.py:69 with np.linalg.pinv's rcond=1e-15 cutoff)."""
+def inv_evals(evals: torch.Tensor, rcond=1e-15) -> torch.Tensor:
+    """Diagonal of pinv(cov(T)) for T = centred scores on the eigenbasis:
+    cov(T) = diag(λ) (utils/SIMCA.py:69 with np.linalg.pinv's rcond=1e-15 cutoff)."""
     lam = evals.to(torch.float64)
     cut = rcond * lam.abs().max()
-    inv = torch.where(lam.abs() > cut, 1.0 / lam, torch.zeros_like(lam))
-    return torch.diag(inv)
+    return torch.where(lam.abs() > cut, 1.0 / lam, torch.zeros_like(lam))
+
+
+def invcov_from_evals(evals: torch.Tensor, rcond=1e-15) -> torch.Tensor:
+    """pinv(cov(T)) as the (k, k) matrix the reference stores (``invcovT``)."""
+    return torch.diag(inv_evals(evals, rcond))
 
 
 def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_mode: int,
@@ -361,12 +386,12 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
     host = torch.cat([evals, theta]).cpu().numpy()
     ev_h = host[:k]
     th = tuple(float(v) for v in host[k:k + 3])
-    invcov = invcov_from_evals(evals)
-    sc = score(X, rows, n, evecs, mean64, invcov, want_T=want_T, want_stats=True)
+    inv = inv_evals(evals)
+    sc = score(X, rows, n, evecs, mean64, inv, want_T=want_T, want_stats=True)
     stats = sc["stats"]
     if allreduce is not None:
         allreduce([stats])  # stream-ordered: no host wait
-    fit = ClassFit(k=k, n=n_total, p=p, mean64=mean64, evals=evals, P64=evecs, invcov=invcov, thetas=th,
+    fit = ClassFit(k=k, n=n_total, p=p, mean64=mean64, evals=evals, P64=evecs, invcov=torch.diag(inv), inv_diag=inv, thetas=th,
                    evals_host=ev_h, T=sc["T"], T2=sc["T2"], Q=sc["Q"], stats_dev=stats, eig_iters=iters,
                    C=C if keep_C else None)
     fit.extra["shift32"] = shift32

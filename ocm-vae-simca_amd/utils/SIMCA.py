@@ -89,7 +89,7 @@ class EnginePCA:
 
     def transform(self, X):
         Xd = engine.as_device_f32(X)
-        out = engine.score(Xd, None, Xd.shape[0], self._fit.P64, self._fit.mean64, self._fit.invcov,
+        out = engine.score(Xd, None, Xd.shape[0], self._fit.P64, self._fit.mean64, self._fit.inv_diag,
                            want_T=True, want_T2=False, want_Q=False)
         T = out["T"]
         return T if isinstance(X, torch.Tensor) else T.cpu().numpy().astype(self._dt)
@@ -106,6 +106,18 @@ def _np(t, dtype=None):
     a = t.detach().cpu().numpy()
     return a.astype(dtype) if dtype is not None and a.dtype != dtype else a
 
+
+
+def _rates(TP, TN, FP, FN):
+    """Sensitivity / specificity / accuracy / efficiency in percent from the
+    confusion counts (utils/SIMCA.py:247-266; NumPy division semantics)."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        sensitivity = TP / (TP + FN) * 100
+        specificity = TN / (TN + FP) * 100
+        accuracy = (TP + TN) / (TP + TN + FP + FN) * 100
+        efficiency = np.sqrt(sensitivity * specificity)
+    return {"sensitivity": sensitivity, "specificity": specificity, "accuracy": accuracy,
+            "efficiency": efficiency, "TP": TP, "TN": TN, "FP": FP, "FN": FN}
 
 class SIMCA(BaseEstimator, ClassifierMixin):
     def __init__(self, n_components=2, model_class=None, type: str = "alt", t2lim="Fdist", t2cl=0.95, qlim="jm",
@@ -211,7 +223,7 @@ class SIMCA(BaseEstimator, ClassifierMixin):
         cls = self.model_class[-1]
         fit = self._fits[cls]
         m = self._model[cls]
-        out = engine.score(Xd, None, Xd.shape[0], fit.P64, fit.mean64, fit.invcov)
+        out = engine.score(Xd, None, Xd.shape[0], fit.P64, fit.mean64, fit.inv_diag)
         dec = self._decision(m["T2_limit"], m["Q_limit"], m["D_limit"])
         t2r, qr, _ = engine.decide(out["T2"], out["Q"], dec)
         if isinstance(X, torch.Tensor):
@@ -230,14 +242,20 @@ class SIMCA(BaseEstimator, ClassifierMixin):
             info = self._model[cls]
             dec = self._decision(info["T2_limit"], info["Q_limit"], info["D_limit"])
             acc = pred[:, i:] if C > 1 else pred
-            engine.score(Xd, None, m, fit.P64, fit.mean64, fit.invcov, want_T2=False, want_Q=False,
+            engine.score(Xd, None, m, fit.P64, fit.mean64, fit.inv_diag, want_T2=False, want_Q=False,
                          decision=dec, accept_out=acc, accept_stride=C)
         out = pred if isinstance(X, torch.Tensor) else pred.cpu().numpy()
         if y_true is not None:
             yt = _host_labels(y_true)
-            ph = out.cpu().numpy() if isinstance(out, torch.Tensor) else out
             for i, cls in enumerate(self.model_class):
-                self.metrics[cls] = self._metrics_simca_conformity(yt, ph[:, i], cls)
+                if yt.shape == (m,):
+                    # counts on the device from the prediction column (ocm_confusion_counts)
+                    pos = torch.from_numpy(np.ascontiguousarray(yt == cls).astype(np.uint8)).to(Xd.device)
+                    cnt = engine.confusion_counts(pred[:, i:], pos, stride=C).cpu().numpy()
+                    self.metrics[cls] = _rates(*(np.int64(v) for v in cnt))
+                else:  # the reference's NumPy broadcasting semantics for odd label shapes
+                    ph = pred.cpu().numpy()
+                    self.metrics[cls] = self._metrics_simca_conformity(yt, ph[:, i], cls)
                 if self.verbose:
                     mt = self.metrics[cls]
                     print(f"Sample class {cls} = {np.sum(yt == cls)}")
@@ -252,17 +270,8 @@ class SIMCA(BaseEstimator, ClassifierMixin):
         y_true = _host_labels(y_true)
         y_pred = y_pred.cpu().numpy() if isinstance(y_pred, torch.Tensor) else np.asarray(y_pred)
         true_class = (y_true == class_index).astype(int)
-        TP = np.sum((y_pred == 1) & (true_class == 1))
-        TN = np.sum((y_pred == 0) & (true_class == 0))
-        FP = np.sum((y_pred == 1) & (true_class == 0))
-        FN = np.sum((y_pred == 0) & (true_class == 1))
-        with np.errstate(divide="ignore", invalid="ignore"):
-            sensitivity = TP / (TP + FN) * 100
-            specificity = TN / (TN + FP) * 100
-            accuracy = (TP + TN) / (TP + TN + FP + FN) * 100
-            efficiency = np.sqrt(sensitivity * specificity)
-        return {"sensitivity": sensitivity, "specificity": specificity, "accuracy": accuracy,
-                "efficiency": efficiency, "TP": TP, "TN": TN, "FP": FP, "FN": FN}
+        return _rates(np.sum((y_pred == 1) & (true_class == 1)), np.sum((y_pred == 0) & (true_class == 0)),
+                      np.sum((y_pred == 1) & (true_class == 0)), np.sum((y_pred == 0) & (true_class == 1)))
 
     def score(self, X, y):
         """utils/SIMCA.py:268-278 — returns specificity (2-D y_pred, list class index, as the reference)."""

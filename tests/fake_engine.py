@@ -82,7 +82,8 @@ def score(X, rows, m, P64, mean64, A, want_T=False, want_T2=True, want_Q=True, d
     R = Y - T @ P
     Q = (R ** 2).sum(1).astype(np.float32)
     T32 = T.astype(np.float32)
-    T2 = np.einsum("ij,jk,ik->i", T32.astype(np.float64), A.numpy(), T32.astype(np.float64))
+    Am = np.diag(A.numpy()) if A.dim() == 1 else A.numpy()
+    T2 = np.einsum("ij,jk,ik->i", T32.astype(np.float64), Am, T32.astype(np.float64))
     out = {"T": torch.from_numpy(T32) if want_T else None, "T2": torch.from_numpy(T2) if want_T2 else None,
            "Q": torch.from_numpy(Q) if want_Q else None, "stats": None}
     if want_stats:
@@ -207,11 +208,11 @@ def fit_class(X, rows, n, k, theta_mode, want_T=True, keep_C=False, shift32=None
     C, mean64 = cov_from_gram([(1.0, G[0], cs[0])], shift32, n_total)
     evals, evecs, theta, iters = eig_topk(C, k, theta_mode)
     invcov = invcov_from_evals(evals)
-    sc = score(X, rows, n, evecs, mean64, invcov, want_T=want_T, want_stats=True)
+    sc = score(X, rows, n, evecs, mean64, torch.diagonal(invcov).clone(), want_T=want_T, want_stats=True)
     stats = sc["stats"]
     if allreduce is not None:
         allreduce([stats])
     st = stats.numpy()
-    return _Fit(k=k, n=n_total, p=p, mean64=mean64, evals=evals, P64=evecs, invcov=invcov,
+    return _Fit(k=k, n=n_total, p=p, mean64=mean64, evals=evals, P64=evecs, invcov=invcov, inv_diag=torch.diagonal(invcov).clone(),
                 thetas=tuple(float(v) for v in theta.numpy()), evals_host=evals.numpy(), T=sc["T"], T2=sc["T2"],
                 Q=sc["Q"], T2_stats=(st[0], st[1]), Q_stats=(st[2], st[3]), eig_iters=iters, C=None)

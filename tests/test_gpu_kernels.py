@@ -149,6 +149,73 @@ def test_score_matches_oracle(eng, k):
     assert np.all(acc[:, 0].cpu().numpy() == 0)
 
 
+@pytest.mark.parametrize("n,p,k", [(5003, 2048, 20), (4097, 2048, 16), (1000, 1024, 17), (777, 512, 10),
+                                   (300, 256, 1), (33, 2048, 20), (1, 512, 5), (2000, 520, 20), (1500, 2048, 24)])
+def test_score_diag_matches_oracle(eng, n, p, k):
+    """ocm_score_f32_diag (A = diag(1/λ), the SIMCA case): the single-pass
+    kernel k_score_1p for p ∈ {256, 512, 1024, 2048}, k ≤ 20, and the two-sweep
+    fallback for the rest (p = 520, k = 24); ragged tails (m mod 16 ≠ 0, m < 16),
+    the row-index gather, the fused decision and the moment partials."""
+    import torch
+    from oracle.simca_oracle import project_scores, synth_spectra
+
+    X = synth_spectra(n + 64, p, min(k, 20), rank=max(k + 5, 30), seed=n + k, outlier_frac=0.1)
+    Xf = X.astype(np.float64)
+    mean = Xf.mean(0)
+    w, V = np.linalg.eigh(np.cov(Xf, rowvar=False))
+    P = V[:, ::-1][:, :k].T.copy()
+    lam = w[::-1][:k]
+    inv = 1 / lam
+    T_ref, T2_ref, Q_ref = project_scores(X[:n], P, mean, np.diag(inv))
+    Xd = _dev(X)
+    out = eng.score(Xd, None, n, _dev(P), _dev(mean), _dev(inv), want_T=True, want_stats=True)
+    np.testing.assert_allclose(out["T"].cpu().numpy(), T_ref, rtol=1e-4, atol=1e-4 * np.abs(T_ref).max())
+    np.testing.assert_allclose(out["T2"].cpu().numpy(), T2_ref, rtol=2e-5, atol=1e-6 * np.median(T2_ref))
+    np.testing.assert_allclose(out["Q"].cpu().numpy(), Q_ref, rtol=2e-5, atol=1e-6 * np.median(Q_ref))
+    q64 = Q_ref.astype(np.float64)
+    np.testing.assert_allclose(out["stats"].cpu().numpy(),
+                               [T2_ref.sum(), (T2_ref ** 2).sum(), q64.sum(), (q64 ** 2).sum()], rtol=1e-6)
+    # same as the general two-sweep kernel with the full matrix
+    full = eng.score(Xd, None, n, _dev(P), _dev(mean), _dev(np.diag(inv)), want_T=True)
+    np.testing.assert_allclose(out["Q"].cpu().numpy(), full["Q"].cpu().numpy(), rtol=2e-5,
+                               atol=1e-6 * np.median(Q_ref))
+    # gather + fused decision at a stride, T2/Q/T outputs off
+    rows = np.arange(n + 63, -1, -3)[: max(1, (n + 64) // 3)]
+    _, T2r, Qr = project_scores(X[rows], P, mean, np.diag(inv))
+    acc = torch.zeros((len(rows), 2), dtype=torch.float64, device="cuda")
+    dec = eng.make_decision("alt", 1 / np.percentile(T2r, 90), 1 / np.percentile(Qr, 90), np.sqrt(2))
+    eng.score(Xd, _dev(rows.astype(np.int64)), len(rows), _dev(P), _dev(mean), _dev(inv), want_T2=False,
+              want_Q=False, decision=dec, accept_out=acc[:, 1:], accept_stride=2)
+    d = np.sqrt((T2r * dec.t2_scale) ** 2 + (Qr.astype(np.float64) * dec.q_scale) ** 2)
+    clear = np.abs(d - np.sqrt(2)) > 1e-4
+    np.testing.assert_array_equal(acc[:, 1].cpu().numpy()[clear], (d < np.sqrt(2))[clear].astype(float))
+    assert np.all(acc[:, 0].cpu().numpy() == 0)
+
+
+@pytest.mark.parametrize("offset", [0, 1])
+def test_score_diag_strided_and_offset_rows(eng, offset):
+    """X a column slice of a wider matrix (ldx > p); offset 1 breaks the 16-B
+    alignment and takes the two-sweep kernel.  Data with a large common mean
+    (μ ≈ 50σ) checks that the centring happens before the f32 projection."""
+    from oracle.simca_oracle import project_scores
+
+    rng = np.random.default_rng(5 + offset)
+    n, p, k = 2000, 1024, 12
+    W = (rng.standard_normal((n, p + 8)) * 0.02 + 1.0).astype(np.float32)
+    W[:, :p] += (rng.standard_normal((n, k)) @ rng.standard_normal((k, p)) * 0.05).astype(np.float32)
+    X = W[:, offset:offset + p]
+    Xf = X.astype(np.float64)
+    mean = Xf.mean(0)
+    w, V = np.linalg.eigh(np.cov(Xf, rowvar=False))
+    P = V[:, ::-1][:, :k].T.copy()
+    inv = 1 / w[::-1][:k]
+    T_ref, T2_ref, Q_ref = project_scores(np.ascontiguousarray(X), P, mean, np.diag(inv))
+    Wd = _dev(W)
+    out = eng.score(Wd[:, offset:offset + p], None, n, _dev(P), _dev(mean), _dev(inv), want_T=True)
+    np.testing.assert_allclose(out["T2"].cpu().numpy(), T2_ref, rtol=2e-5, atol=1e-6 * np.median(T2_ref))
+    np.testing.assert_allclose(out["Q"].cpu().numpy(), Q_ref, rtol=2e-5, atol=1e-6 * np.median(Q_ref))
+
+
 def test_decide_types(eng):
     import torch
 
@@ -287,9 +354,10 @@ def test_gram_i8_clean_data_marks_nothing(eng):
     assert eng.last_gram_marks(0) == 0
 
 
-def test_gram_i8_heavy_marking_falls_back_to_f32(eng):
+def test_gram_i8_heavy_marking_falls_back_to_bf16x3(eng):
     """Scale drift after the sample rows (every later row ×200): more than n/8
-    marks, so the call recomputes on FP32 MFMA; the result is still the Gram."""
+    marked rows, so the call recomputes on the bf16×3 split; the result is
+    still the Gram."""
     rng = np.random.default_rng(8)
     n, p = 12000, 192
     X = rng.standard_normal((n, p)).astype(np.float32)
