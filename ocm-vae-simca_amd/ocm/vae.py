@@ -33,23 +33,65 @@ from . import engine
 __all__ = ["qhf_device", "latent_stats", "full_distance_decision", "VAESIMCA", "latent_T2"]
 
 
-def _moments(v: torch.Tensor):
-    """(mean, unbiased std, ddof-0 std) in fp64 of a device vector."""
+def _moments(v: torch.Tensor, group=None):
+    """(mean, unbiased std, ddof-0 std) in fp64 of a device vector — over the
+    concatenation of every rank's vector when ``group`` spans several ranks
+    (the reference takes these moments over the whole test
+    set).  Each rank reduces (n, mean, Σ(d − mean)²) locally, one all-gather
+    of those 3 doubles follows, and every rank combines them in rank order
+    (Chan et al.'s pairwise update): the same numbers on every rank."""
     d = v.to(torch.float64)
     n = d.numel()
-    m = d.mean()
+    m = d.mean() if n else torch.zeros((), dtype=torch.float64, device=d.device)
     ss = ((d - m) ** 2).sum()
-    out = torch.stack([m, ss]).cpu().numpy()
-    mean, s2 = float(out[0]), float(out[1])
+    if _world(group) > 1:
+        import torch.distributed as dist
+
+        loc = torch.stack([torch.tensor(float(n), dtype=torch.float64, device=d.device), m, ss])
+        parts = [torch.empty_like(loc) for _ in range(_world(group))]
+        dist.all_gather(parts, loc, group=group)
+        N, mean, s2 = 0.0, 0.0, 0.0
+        for part in parts:
+            nb, mb, sb = (float(x) for x in part.cpu().numpy())
+            if nb == 0:
+                continue
+            delta = mb - mean
+            tot = N + nb
+            mean += delta * nb / tot
+            s2 += sb + delta * delta * N * nb / tot
+            N = tot
+        n = int(N)
+    else:
+        out = torch.stack([m, ss]).cpu().numpy()
+        mean, s2 = float(out[0]), float(out[1])
     return mean, math.sqrt(s2 / (n - 1)) if n > 1 else float("nan"), math.sqrt(s2 / n)
 
 
-def _latent_cov(Z: torch.Tensor):
-    """Column mean (f64) and covariance (f64, ddof 1) of latent rows on the GPU."""
+def _world(group) -> int:
+    import torch.distributed as dist
+
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+
+
+def _latent_cov(Z: torch.Tensor, group=None):
+    """Column mean (f64) and covariance (f64, ddof 1) of latent rows on the GPU
+    (of every rank's rows: one all-reduce of the d×d Gram, Σz and n)."""
     n, d = Z.shape
     shift64 = engine.colmean(Z, None, min(n, engine.SHIFT_SAMPLE))
+    if _world(group) > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(shift64, group=group)
+        shift64 /= _world(group)
     shift32 = engine.cast_f32(shift64)
     G, cs = engine.gram(Z, None, [0, n], shift32)
+    if _world(group) > 1:
+        import torch.distributed as dist
+
+        cnt = torch.tensor([float(n)], dtype=torch.float64, device=Z.device)
+        for t in (G, cs, cnt):
+            dist.all_reduce(t, group=group)
+        n = int(round(float(cnt.item())))
     C, mean = engine.cov_from_gram([(1.0, G[0], cs[0])], shift32, n)
     return mean, C
 
@@ -81,24 +123,38 @@ def qhf_device(x: torch.Tensor, x_rec: torch.Tensor, z: torch.Tensor):
             stats.chi2.ppf(0.95, df=Nh + Nq))
 
 
-def latent_stats(mus: torch.Tensor, q_cal: torch.Tensor, ridge: float = 1e-6, pct: float = 95.0):
+def latent_stats(mus: torch.Tensor, q_cal: torch.Tensor, ridge: float = 1e-6, pct: float = 95.0, group=None):
     """utils/final_vaesimca.py:428-442: (latent mean f64, (cov + ridge·I)⁻¹ f64,
-    T² threshold, Q threshold) of the calibration latents / residuals."""
+    T² threshold, Q threshold) of the calibration latents / residuals — of
+    every rank's rows when ``group`` spans several ranks (all-reduced latent
+    Gram, distributed radix-select percentiles)."""
+    from .dist import percentile_sharded
+
     Z = engine.as_device_f32(mus)
-    mean, C = _latent_cov(Z)
+    mean, C = _latent_cov(Z, group)
     C.diagonal().add_(ridge)
     inv = engine.sym_pinv(C)  # SPD: the pseudo-inverse is the inverse (np.linalg.inv at :431)
     T2 = latent_T2(Z, mean, inv)
     qd = q_cal if q_cal.dtype in (torch.float32, torch.float64) else q_cal.to(torch.float32)
+    if _world(group) > 1:
+        import torch.distributed as dist
+
+        cnt = torch.tensor([float(Z.shape[0])], dtype=torch.float64, device=Z.device)
+        dist.all_reduce(cnt, group=group)
+        n = int(round(float(cnt.item())))
+        return mean, inv, percentile_sharded(T2, pct, n, group), percentile_sharded(qd.contiguous(), pct, n, group)
     return mean, inv, engine.percentile(T2, pct), engine.percentile(qd.contiguous(), pct)
 
 
-def full_distance_decision(mus_test: torch.Tensor, latent_mean: torch.Tensor, q: torch.Tensor, alpha=0.05):
-    """utils/final_vaesimca.py:510-533: accept (bool, device), f (f64), f_crit."""
+def full_distance_decision(mus_test: torch.Tensor, latent_mean: torch.Tensor, q: torch.Tensor, alpha=0.05,
+                           group=None):
+    """utils/final_vaesimca.py:510-533: accept (bool, device), f (f64), f_crit.
+    With ``group`` the test set is the concatenation of every rank's rows: the
+    h / q moments are global (one all-gather of 3 doubles each), the decision local."""
     Z = engine.as_device_f32(mus_test)
     h = engine.rowsq_residual(Z, engine.as_device_f32(latent_mean, Z.device).reshape(-1))
-    h0, _, sh = _moments(h)
-    q0, _, sq = _moments(q)
+    h0, _, sh = _moments(h, group)
+    q0, _, sq = _moments(q, group)
     Nh = 2 * (h0 / sh) ** 2
     Nq = 2 * (q0 / sq) ** 2
     f = h.to(torch.float64) / h0 * Nh + q.to(torch.float64) / q0 * Nq

@@ -92,6 +92,19 @@ def score(X, rows, m, P64, mean64, A, want_T=False, want_T2=True, want_Q=True, d
     return out
 
 
+def rowsq_residual(x, xhat):
+    xn = x.numpy().astype(np.float64)
+    xh = xhat.numpy().astype(np.float64).reshape(-1, xn.shape[1])
+    return torch.from_numpy(((xn - xh) ** 2).sum(1).astype(np.float32))
+
+
+def sym_pinv(A, rcond=1e-15):
+    w, V = np.linalg.eigh(A.numpy())
+    cut = rcond * np.abs(w).max()
+    inv = np.where(np.abs(w) > cut, 1.0 / np.where(w == 0, 1, w), 0.0)
+    return torch.from_numpy((V * inv) @ V.T)
+
+
 def _prefix(T, Q, inv, lv):
     t2sq = T.numpy().astype(np.float64) ** 2
     t2 = (t2sq[:, :lv] * inv.numpy()[:lv]).sum(1)
