@@ -281,34 +281,37 @@ __global__ __launch_bounds__(256, 2) void k_score_direct(const float* __restrict
 // diagonal A = diag(1/λ) as every SIMCA fit produces).  The default scoring
 // kernel for those shapes; k_score_direct covers the rest.
 //
-// One workgroup of four waves per CU (one wave per SIMD, 512 registers),
-// persistent over 16-row tiles.  Wave w owns columns [w·p/4, (w+1)·p/4) of a
-// tile's 16 rows and keeps them in registers from the HBM read to the
-// residual, so X is read once.  Two register tiles: V (VGPRs) holds d = x − μ
-// of the tile being scored, A (AGPRs) the raw next tile.  Sweep 1 of tile
-// t + G (G = grid) moves A into V block by block and immediately refills
-// each block of A with tile t + 2G, so one whole tile (the 128 KiB per CU an
-// HBM stream needs in flight at full rate) is always outstanding, and each
-// load has a full tile of compute to arrive.
-//   sweep 1  tᵀ += P₀·(x − μ)ᵀ on v_mfma_f32_16x16x4_f32, comps 0..15 (lane
-//            (row = l&15, q = l>>4) feeds column 16j+4q+e of its row as the B
-//            operand); comps 16..19 by VALU FMAs beside it; μ and the comps
-//            16..19 loadings live in registers in a compact form and reach
-//            each lane by DPP row broadcast inside the add / FMA;
+// One workgroup of four waves per CU (one wave per SIMD), persistent over
+// 16-row tiles.  Wave w owns columns [w·p/4, (w+1)·p/4) of a tile's 16 rows.
+// The raw rows stay in AGPRs from the HBM read to the residual (X is read
+// once), in two tile buffers: while tile t is finished (sweep 2) and tile
+// t + G (G = grid) starts (sweep 1), tile t + 2G streams into the registers
+// tile t frees, block by block — a whole tile (the 128 KiB per CU an HBM
+// stream needs in flight at full rate) is always outstanding and each load
+// has a full tile of compute to arrive.  The MFMAs read x straight from the
+// AGPRs: no VALU touches the data.
+//   sweep 1  tᵀ += P₀·xᵀ (comps 0..15) on v_mfma_f32_16x16x4_f32, lane (row =
+//            l&15, q = l>>4) feeding column 16j+4q+e of its row as B; comps
+//            16..19 on v_mfma_f32_4x4x1_16b_f32 (16 4×4 blocks, a quarter of
+//            the cycles: block l/4 = (q, row group), so lane (row, q) sums its
+//            own columns, reduced over q once per tile; the A operands come
+//            from one register per block by ds_bpermute); the mean is applied
+//            once per tile, t = P·x − P·μ (fp64);
 //   reduce   the four waves' partial t meet in LDS (one barrier per tile);
-//   sweep 2  rᵀ = dᵀ + Pᵀ·(−t)ᵀ per 16-column block (comps as K, the chain
-//            starts from the stored d = x − μ; the output lands on the lanes
-//            that hold those columns), q += r²;
+//   sweep 2  rᵀ = xᵀ + Pᵀ·(−t)ᵀ − μ per 16-column block: a chain of MFMAs from
+//            the AGPR tile as accumulator input (comps as K; one more step
+//            with the −μ column); q += r²;
 //   epilogue the wave partials of Q meet after the next barrier; T², Q, T,
 //            the fused decision and the moment partials.
-// Nothing but X (and the row indices of a gather) is read from global
-// memory inside the tile loop, and the only synchronisation is LDS + s_barrier:
-// vmcnt is in order, so any wait on another global access would also wait
-// for the tile in flight.  Rows past m are clamped to row m−1 (a valid row)
-// and their outputs dropped.  P₀ is stored [comp][16-B chunk ^ sw(comp)]:
-// conflict-free ds_read_b128 in sweep 1 and ds_read_b32 in sweep 2.
-// Numerics as k_score_direct: d = x − μ in f32, f32 MFMA partials flushed to
-// f64 every 128 columns, explicit residual.
+// Nothing but X (and the row indices of a gather, through the scalar cache) is
+// read from global memory inside the tile loop and the waves synchronise by
+// LDS + s_barrier only: vmcnt is in order, so any wait on another global
+// access would also wait for the tile in flight.  Rows past m are clamped to
+// row m−1 (a valid row) and their outputs dropped.  P₀ is stored
+// [comp][16-B chunk ^ sw(comp)]: conflict-free ds_read_b128 in sweep 1 and
+// ds_read_b32 in sweep 2.  Numerics: f32 MFMA products, f32 partials over ≤ 64
+// columns per chain flushed to f64; r is formed in the f32 accumulator as the
+// reference forms X − (T·P + μ) in float32 (utils/SIMCA.py:67, 105).
 // ---------------------------------------------------------------------------
 namespace s1p {
 constexpr int W = 4, R = 16;
@@ -323,179 +326,90 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 __device__ __forceinline__ int sw(int m) { return ((4 * m) ^ (2 * (m >> 2))) & 15; }
 
-// d[e] = x[e] + (lane B + e of the 16-lane DPP row of u), e = 0..3: the
-// centring of one 16-column block, x read from the AGPR tile (u = −μ in the
-// compact form).  hipcc does not fold a row_newbcast mov into an add, and pads
-// nothing inside inline asm: the leading s_nop covers a VALU write of u right
-// before (DPP read: 2 states), the trailing one the MFMAs that read d next
-// (VALU write → MFMA operand).
-template <int B>
-__device__ __forceinline__ void centre4(float u, const f32x4& x, f32x4& d) {
-  asm("v_accvgpr_read_b32 %0, %5\n\t"
-      "v_accvgpr_read_b32 %1, %6\n\t"
-      "v_accvgpr_read_b32 %2, %7\n\t"
-      "v_accvgpr_read_b32 %3, %8\n\t"
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %4, %0 row_newbcast:%9 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %1, %4, %1 row_newbcast:%10 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %2, %4, %2 row_newbcast:%11 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %3, %4, %3 row_newbcast:%12 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "s_nop 1"
-      : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3])
-      : "v"(u), "a"(x[0]), "a"(x[1]), "a"(x[2]), "a"(x[3]), "n"(B), "n"(B + 1), "n"(B + 2), "n"(B + 3));
-}
-// a float of the comps 16..19 loadings into an AGPR (an MFMA A operand only)
-__device__ __forceinline__ float to_agpr(float v) {
-  float r;
-  asm("v_accvgpr_write_b32 %0, %1" : "=a"(r) : "v"(v));
-  return r;
-}
 // 16 B of row data into an AGPR quad, not tracked by the compiler's waitcnt:
 // the consumer waits with wait_vm (vmcnt is in order)
 template <int OFF>
 __device__ __forceinline__ void load_a(f32x4& a, const float* p) {
   asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=a"(a) : "v"(p), "n"(OFF) : "memory");
 }
-template <int N>
-__device__ __forceinline__ void wait_vm(f32x4& a) {
-#ifdef OCM_S1P_DIAG_NOWAIT  // timing ablation only (wrong results)
-  asm volatile("" : "+a"(a));
+// diagnostic builds only (make exp): the refill loads of sweep 2 are skipped
+template <int OFF>
+__device__ __forceinline__ void refill_a(f32x4& a, const float* p) {
+#ifdef OCM_S1P_DIAG_NOLOAD
+  asm volatile("" : "+a"(a) : "v"(p));
 #else
-  asm volatile("s_waitcnt vmcnt(%1)" : "+a"(a) : "n"(N));
+  load_a<OFF>(a, p);
 #endif
 }
-// ---- hand-scheduled inner steps (VALU work placed in the MFMA gaps) ----------
-// One wave per SIMD issues in order, so VALU work only overlaps the matrix
-// pipe if it sits between the MFMAs in program order: the steps below are
-// inline asm (hipcc schedules each block's VALU after its MFMAs).  Wait states
-// inside: s_nop 1 ahead of a DPP read or MFMA operand read of a register a
-// VALU op may just have written (hipcc pads nothing inside asm); an MFMA
-// result is read by VALU only ≥ 1 MFMA issue later (≥ 32 cycles ≥ the 12
-// states an 8-pass XDL result needs), except where a trailing s_nop says so.
-//
-// Sweep-1 step: MFMAs of block j (acc += a[e]·d[e]) interleaved with the
-// centring of block j+1 (n = x + DPP-broadcast −μ, x read from AGPRs) and, for
-// EX, the comps 16..19 FMAs of block j (xs[c] += DPP-broadcast p[c] · d[e]).
-#define OCM_DPP(L) " row_newbcast:" #L " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-#define OCM_S1_CENTRE(N0, N1, N2, N3)                          \
-  "s_nop 1\n\t"                                              \
-  "v_add_f32_dpp %[n0], %[mu], %[n0]" OCM_DPP(N0)            \
-  "v_add_f32_dpp %[n1], %[mu], %[n1]" OCM_DPP(N1)            \
-  "v_add_f32_dpp %[n2], %[mu], %[n2]" OCM_DPP(N2)            \
-  "v_add_f32_dpp %[n3], %[mu], %[n3]" OCM_DPP(N3)
-#define OCM_S1_READX                                           \
-  "v_accvgpr_read_b32 %[n0], %[x0]\n\t"                      \
-  "v_accvgpr_read_b32 %[n1], %[x1]\n\t"                      \
-  "v_accvgpr_read_b32 %[n2], %[x2]\n\t"                      \
-  "v_accvgpr_read_b32 %[n3], %[x3]\n\t"
-#define OCM_S1_EXFMA(D, L)                                     \
-  "v_fmac_f32_dpp %[s0], %[p0], %[" #D "]" OCM_DPP(L)          \
-  "v_fmac_f32_dpp %[s1], %[p1], %[" #D "]" OCM_DPP(L)          \
-  "v_fmac_f32_dpp %[s2], %[p2], %[" #D "]" OCM_DPP(L)          \
-  "v_fmac_f32_dpp %[s3], %[p3], %[" #D "]" OCM_DPP(L)
-#define OCM_MFMA(ACC, A, B) "v_mfma_f32_16x16x4_f32 %[" #ACC "], %[" #A "], %[" #B "], %[" #ACC "]\n\t"
-#define OCM_S1_OPS_ACC [aA] "+v"(acA), [aB] "+v"(acB), [aC] "+v"(acC), [aD] "+v"(acD)
-#define OCM_S1_IN_AD                                                                                      \
-  [a0] "v"(a[0]), [a1] "v"(a[1]), [a2] "v"(a[2]), [a3] "v"(a[3]), [d0] "v"(d[0]), [d1] "v"(d[1]),           \
-      [d2] "v"(d[2]), [d3] "v"(d[3])
-#define OCM_S1_IN_X [x0] "a"(x[0]), [x1] "a"(x[1]), [x2] "a"(x[2]), [x3] "a"(x[3]), [mu] "v"(mu)
-#define OCM_S1_IN_P [p0] "v"(p[0]), [p1] "v"(p[1]), [p2] "v"(p[2]), [p3] "v"(p[3])
-
-template <int B>  // B = 4(j % 4): DPP lanes of block j; block j+1 uses (B + 4) % 16
-struct S1Step;
-#define OCM_S1_STEP_SPEC(B, B1, B2, B3, N0, N1, N2, N3)                                                     \
-  template <>                                                                                             \
-  struct S1Step<B> {                                                                                      \
-    /* k ≤ 16: MFMAs of block j + centring of block j+1 */                                               \
-    __device__ static __forceinline__ void next(f32x4& acA, f32x4& acB, f32x4& acC, f32x4& acD,            \
-                                                const f32x4& a, const f32x4& d, float mu, const f32x4& x,  \
-                                                f32x4& n) {                                                \
-      asm("s_nop 1\n\t" OCM_MFMA(aA, a0, d0) OCM_MFMA(aB, a1, d1) OCM_S1_READX OCM_MFMA(aC, a2, d2)        \
-              OCM_S1_CENTRE(N0, N1, N2, N3) OCM_MFMA(aD, a3, d3)                                           \
-          : OCM_S1_OPS_ACC, [n0] "=&v"(n[0]), [n1] "=&v"(n[1]), [n2] "=&v"(n[2]), [n3] "=&v"(n[3])         \
-          : OCM_S1_IN_AD, OCM_S1_IN_X);                                                                   \
-    }                                                                                                     \
-    /* k > 16: the same plus the comps 16..19 FMAs of block j */                                         \
-    __device__ static __forceinline__ void next_ex(f32x4& acA, f32x4& acB, f32x4& acC, f32x4& acD,         \
-                                                   float (&s)[4], const f32x4& a, const f32x4& d,          \
-                                                   const float (&p)[4], float mu, const f32x4& x,          \
-                                                   f32x4& n) {                                             \
-      asm("s_nop 1\n\t" OCM_MFMA(aA, a0, d0) OCM_S1_EXFMA(d0, B) OCM_MFMA(aB, a1, d1) OCM_S1_READX          \
-              OCM_S1_EXFMA(d1, B1) OCM_MFMA(aC, a2, d2) OCM_S1_EXFMA(d2, B2)                               \
-                  OCM_S1_CENTRE(N0, N1, N2, N3) OCM_MFMA(aD, a3, d3) OCM_S1_EXFMA(d3, B3)                 \
-          : OCM_S1_OPS_ACC, [s0] "+v"(s[0]), [s1] "+v"(s[1]), [s2] "+v"(s[2]), [s3] "+v"(s[3]),            \
-            [n0] "=&v"(n[0]), [n1] "=&v"(n[1]), [n2] "=&v"(n[2]), [n3] "=&v"(n[3])                         \
-          : OCM_S1_IN_AD, OCM_S1_IN_P, OCM_S1_IN_X);                                                      \
-    }                                                                                                     \
-    /* the last block of the sweep (nothing to centre) */                                                \
-    __device__ static __forceinline__ void last(f32x4& acA, f32x4& acB, f32x4& acC, f32x4& acD,            \
-                                                const f32x4& a, const f32x4& d) {                          \
-      asm("s_nop 1\n\t" OCM_MFMA(aA, a0, d0) OCM_MFMA(aB, a1, d1) OCM_MFMA(aC, a2, d2) OCM_MFMA(aD, a3, d3) \
-          : OCM_S1_OPS_ACC                                                                                \
-          : OCM_S1_IN_AD);                                                                                \
-    }                                                                                                     \
-    __device__ static __forceinline__ void last_ex(f32x4& acA, f32x4& acB, f32x4& acC, f32x4& acD,         \
-                                                   float (&s)[4], const f32x4& a, const f32x4& d,          \
-                                                   const float (&p)[4]) {                                  \
-      asm("s_nop 1\n\t" OCM_MFMA(aA, a0, d0) OCM_S1_EXFMA(d0, B) OCM_MFMA(aB, a1, d1) OCM_S1_EXFMA(d1, B1)  \
-              OCM_MFMA(aC, a2, d2) OCM_S1_EXFMA(d2, B2) OCM_MFMA(aD, a3, d3) OCM_S1_EXFMA(d3, B3)           \
-          : OCM_S1_OPS_ACC, [s0] "+v"(s[0]), [s1] "+v"(s[1]), [s2] "+v"(s[2]), [s3] "+v"(s[3])             \
-          : OCM_S1_IN_AD, OCM_S1_IN_P);                                                                   \
-    }                                                                                                     \
-  };
-OCM_S1_STEP_SPEC(0, 1, 2, 3, 4, 5, 6, 7)
-OCM_S1_STEP_SPEC(4, 5, 6, 7, 8, 9, 10, 11)
-OCM_S1_STEP_SPEC(8, 9, 10, 11, 12, 13, 14, 15)
-OCM_S1_STEP_SPEC(12, 13, 14, 15, 0, 1, 2, 3)
-#undef OCM_S1_STEP_SPEC
-
-// Sweep-2 pair step: the two MFMA chains of blocks (j, j+1) — r_u = d_u +
-// Σ_s a_u[s]·tB[s] on a VGPR accumulator each, interleaved so no MFMA waits on
-// its predecessor — with the q FMAs of the previous pair (q0 += r0p², q1 +=
-// r1p²) in the gaps.  NS = 4 or 5 steps (comps 16..19: step 4, A from AGPRs).
-#define OCM_S2_IN_COMMON                                                                                  \
-  [d0] "v"(d0), [d1] "v"(d1), [u0] "v"(a0[0]), [u1] "v"(a0[1]), [u2] "v"(a0[2]), [u3] "v"(a0[3]),           \
-      [w0] "v"(a1[0]), [w1] "v"(a1[1]), [w2] "v"(a1[2]), [w3] "v"(a1[3]), [t0] "v"(tB[0]), [t1] "v"(tB[1]),   \
-      [t2] "v"(tB[2]), [t3] "v"(tB[3])
-#define OCM_S2_IN_PREV                                                                                    \
-  [e0] "v"(r0p[0]), [e1] "v"(r0p[1]), [e2] "v"(r0p[2]), [e3] "v"(r0p[3]), [f0] "v"(r1p[0]), [f1] "v"(r1p[1]), \
-      [f2] "v"(r1p[2]), [f3] "v"(r1p[3])
-#define OCM_S2_IN_EX [u4] "a"(a0[4]), [w4] "a"(a1[4]), [t4] "v"(tB[4])
-#define OCM_S2M(R, A, T) "v_mfma_f32_16x16x4_f32 %[" #R "], %[" #A "], %[" #T "], %[" #R "]\n\t"
-#define OCM_S2M0(R, A, T, D) "v_mfma_f32_16x16x4_f32 %[" #R "], %[" #A "], %[" #T "], %[" #D "]\n\t"
-#define OCM_QF(Q, E) "v_fmac_f32_e32 %[" #Q "], %[" #E "], %[" #E "]\n\t"
-template <int NS, bool FIRST>
-__device__ __forceinline__ void s2_pair(const f32x4& d0, const f32x4& d1, const float (&a0)[5], const float (&a1)[5],
-                                        const float (&tB)[5], const f32x4& r0p, const f32x4& r1p, float& q0,
-                                        float& q1, f32x4& r0, f32x4& r1) {
-  if constexpr (FIRST && NS == 4) {
-    asm("s_nop 1\n\t" OCM_S2M0(r0, u0, t0, d0) OCM_S2M0(r1, w0, t0, d1) OCM_S2M(r0, u1, t1) OCM_S2M(r1, w1, t1)
-            OCM_S2M(r0, u2, t2) OCM_S2M(r1, w2, t2) OCM_S2M(r0, u3, t3) OCM_S2M(r1, w3, t3)
-        : [r0] "=&v"(r0), [r1] "=&v"(r1)
-        : OCM_S2_IN_COMMON);
-  } else if constexpr (FIRST) {
-    asm("s_nop 1\n\t" OCM_S2M0(r0, u0, t0, d0) OCM_S2M0(r1, w0, t0, d1) OCM_S2M(r0, u1, t1) OCM_S2M(r1, w1, t1)
-            OCM_S2M(r0, u2, t2) OCM_S2M(r1, w2, t2) OCM_S2M(r0, u3, t3) OCM_S2M(r1, w3, t3) OCM_S2M(r0, u4, t4)
-                OCM_S2M(r1, w4, t4)
-        : [r0] "=&v"(r0), [r1] "=&v"(r1)
-        : OCM_S2_IN_COMMON, OCM_S2_IN_EX);
-  } else if constexpr (NS == 4) {
-    asm("s_nop 1\n\t" OCM_S2M0(r0, u0, t0, d0) OCM_S2M0(r1, w0, t0, d1) OCM_QF(q0, e0) OCM_S2M(r0, u1, t1)
-            OCM_QF(q1, e1) OCM_S2M(r1, w1, t1) OCM_QF(q0, e2) OCM_S2M(r0, u2, t2) OCM_QF(q1, e3)
-                OCM_S2M(r1, w2, t2) OCM_QF(q0, f0) OCM_S2M(r0, u3, t3) OCM_QF(q1, f1) OCM_S2M(r1, w3, t3)
-                    OCM_QF(q0, f2) OCM_QF(q1, f3)
-        : [r0] "=&v"(r0), [r1] "=&v"(r1), [q0] "+v"(q0), [q1] "+v"(q1)
-        : OCM_S2_IN_COMMON, OCM_S2_IN_PREV);
-  } else {
-    asm("s_nop 1\n\t" OCM_S2M0(r0, u0, t0, d0) OCM_S2M0(r1, w0, t0, d1) OCM_QF(q0, e0) OCM_S2M(r0, u1, t1)
-            OCM_QF(q1, e1) OCM_S2M(r1, w1, t1) OCM_QF(q0, e2) OCM_S2M(r0, u2, t2) OCM_QF(q1, e3)
-                OCM_S2M(r1, w2, t2) OCM_QF(q0, f0) OCM_S2M(r0, u3, t3) OCM_QF(q1, f1) OCM_S2M(r1, w3, t3)
-                    OCM_QF(q0, f2) OCM_S2M(r0, u4, t4) OCM_QF(q1, f3) OCM_S2M(r1, w4, t4)
-        : [r0] "=&v"(r0), [r1] "=&v"(r1), [q0] "+v"(q0), [q1] "+v"(q1)
-        : OCM_S2_IN_COMMON, OCM_S2_IN_PREV, OCM_S2_IN_EX);
-  }
+template <int N>
+__device__ __forceinline__ void wait_vm(f32x4& a) {
+  asm volatile("s_waitcnt vmcnt(%1)" : "+a"(a) : "n"(N));
 }
 
+// Sweep-1 block: acc[A..D] += a[e] · x[e] (comps 0..15), and for EX acc[E,F]
+// += b[e] ⊗ x[e] on 4x4x1 blocks (comps 16..19 of this lane's row over its
+// columns).  B operands straight from the AGPR tile; four (six) interleaved
+// chains, none waits on its predecessor.  The s_nop covers a VALU/LDS write
+// of a or b right before.
+#define OCM_MF(ACC, A, B) "v_mfma_f32_16x16x4_f32 %[" #ACC "], %[" #A "], %[" #B "], %[" #ACC "]\n\t"
+#define OCM_M4(ACC, A, B) "v_mfma_f32_4x4x1_16b_f32 %[" #ACC "], %[" #A "], %[" #B "], %[" #ACC "]\n\t"
+template <bool EX>
+__device__ __forceinline__ void s1_block(f32x4& acA, f32x4& acB, f32x4& acC, f32x4& acD, f32x4& acE, f32x4& acF,
+                                         const f32x4& a, const float (&b)[4], const f32x4& x) {
+  if constexpr (EX)
+    asm("s_nop 1\n\t" OCM_M4(cE, b0, x0) OCM_MF(cA, a0, x0) OCM_M4(cF, b1, x1) OCM_MF(cB, a1, x1)
+            OCM_M4(cE, b2, x2) OCM_MF(cC, a2, x2) OCM_M4(cF, b3, x3) OCM_MF(cD, a3, x3)
+        : [cA] "+v"(acA), [cB] "+v"(acB), [cC] "+v"(acC), [cD] "+v"(acD), [cE] "+v"(acE), [cF] "+v"(acF)
+        : [a0] "v"(a[0]), [a1] "v"(a[1]), [a2] "v"(a[2]), [a3] "v"(a[3]), [b0] "v"(b[0]), [b1] "v"(b[1]),
+          [b2] "v"(b[2]), [b3] "v"(b[3]), [x0] "a"(x[0]), [x1] "a"(x[1]), [x2] "a"(x[2]), [x3] "a"(x[3]));
+  else
+    asm("s_nop 1\n\t" OCM_MF(cA, a0, x0) OCM_MF(cB, a1, x1) OCM_MF(cC, a2, x2) OCM_MF(cD, a3, x3)
+        : [cA] "+v"(acA), [cB] "+v"(acB), [cC] "+v"(acC), [cD] "+v"(acD)
+        : [a0] "v"(a[0]), [a1] "v"(a[1]), [a2] "v"(a[2]), [a3] "v"(a[3]), [x0] "a"(x[0]), [x1] "a"(x[1]),
+          [x2] "a"(x[2]), [x3] "a"(x[3]));
+}
+
+// Sweep-2 block pair (j, j+1): r_u = x_u − μ_u + Σ_s a_u[s]·tB[s], two MFMA
+// chains interleaved, in place on the AGPR tile (an MFMA's C input and result
+// share a register file).  The −μ step comes first, on a 4x4x1 MFMA (block
+// l/4, row l&3 = this lane's column 4q + (l&3); B = 1), then NS = 4 or 5 comp
+// steps.  QW: the q += r² work of the PREVIOUS pair (p0, p1, finished a whole
+// pair ago) rides in the gaps of this pair's MFMAs as groups of four
+// independent VALU ops (a dependent VALU op would stall the in-order issue
+// and with it the next MFMA); the caller refills p0, p1 afterwards.  No
+// trailing wait: the next reader of x0, x1 is the next pair's statement or
+// the drain, which opens with its own s_nop.
+#define OCM_M2(R, A, T) "v_mfma_f32_16x16x4_f32 %[" #R "], %[" #A "], %[" #T "], %[" #R "]\n\t"
+#define OCM_RD(S, P) "v_accvgpr_read_b32 %[" #S "], %[" #P "]\n\t"
+#define OCM_FM(Q, S) "v_fmac_f32_e32 %[" #Q "], %[" #S "], %[" #S "]\n\t"
+template <bool EX, bool QW>
+__device__ __forceinline__ void s2_pair(f32x4& x0, f32x4& x1, const float (&a0)[5], const float (&a1)[5], float m0,
+                                        float m1, const float (&tB)[5], float one, const f32x4& p0, const f32x4& p1,
+                                        float (&q)[4]) {
+  float s[4];
+  if constexpr (EX && QW)
+    asm volatile("s_nop 1\n\t" OCM_M4(x0, m0, on) OCM_M4(x1, m1, on) "s_nop 4\n\t" OCM_M2(x0, u0, t0) OCM_M2(x1, w0, t0) OCM_RD(s0, p00) OCM_RD(s1, p10) OCM_RD(s2, p01) OCM_RD(s3, p11) OCM_M2(x0, u1, t1) OCM_FM(q0, s0) OCM_FM(q1, s1) OCM_FM(q2, s2) OCM_FM(q3, s3) OCM_M2(x1, w1, t1) OCM_RD(s0, p02) OCM_RD(s1, p12) OCM_RD(s2, p03) OCM_RD(s3, p13) OCM_M2(x0, u2, t2) OCM_FM(q0, s0) OCM_FM(q1, s1) OCM_FM(q2, s2) OCM_FM(q3, s3) OCM_M2(x1, w2, t2) OCM_M2(x0, u3, t3) OCM_M2(x1, w3, t3) OCM_M2(x0, u4, t4) OCM_M2(x1, w4, t4)
+        : [x0] "+a"(x0), [x1] "+a"(x1), [q0] "+v"(q[0]), [q1] "+v"(q[1]), [q2] "+v"(q[2]), [q3] "+v"(q[3]), [s0] "=&v"(s[0]), [s1] "=&v"(s[1]), [s2] "=&v"(s[2]), [s3] "=&v"(s[3])
+        : [u0] "v"(a0[0]), [u1] "v"(a0[1]), [u2] "v"(a0[2]), [u3] "v"(a0[3]), [u4] "v"(a0[4]), [w0] "v"(a1[0]), [w1] "v"(a1[1]), [w2] "v"(a1[2]), [w3] "v"(a1[3]), [w4] "v"(a1[4]), [m0] "v"(m0), [m1] "v"(m1), [t0] "v"(tB[0]), [t1] "v"(tB[1]), [t2] "v"(tB[2]), [t3] "v"(tB[3]), [t4] "v"(tB[4]), [on] "v"(one), [p00] "a"(p0[0]), [p01] "a"(p0[1]), [p02] "a"(p0[2]), [p03] "a"(p0[3]), [p10] "a"(p1[0]), [p11] "a"(p1[1]), [p12] "a"(p1[2]), [p13] "a"(p1[3]));
+  else if constexpr (EX)
+    asm volatile("s_nop 1\n\t" OCM_M4(x0, m0, on) OCM_M4(x1, m1, on) "s_nop 4\n\t" OCM_M2(x0, u0, t0) OCM_M2(x1, w0, t0) OCM_M2(x0, u1, t1) OCM_M2(x1, w1, t1) OCM_M2(x0, u2, t2) OCM_M2(x1, w2, t2) OCM_M2(x0, u3, t3) OCM_M2(x1, w3, t3) OCM_M2(x0, u4, t4) OCM_M2(x1, w4, t4)
+        : [x0] "+a"(x0), [x1] "+a"(x1)
+        : [u0] "v"(a0[0]), [u1] "v"(a0[1]), [u2] "v"(a0[2]), [u3] "v"(a0[3]), [u4] "v"(a0[4]), [w0] "v"(a1[0]), [w1] "v"(a1[1]), [w2] "v"(a1[2]), [w3] "v"(a1[3]), [w4] "v"(a1[4]), [m0] "v"(m0), [m1] "v"(m1), [t0] "v"(tB[0]), [t1] "v"(tB[1]), [t2] "v"(tB[2]), [t3] "v"(tB[3]), [t4] "v"(tB[4]), [on] "v"(one));
+  else if constexpr (QW)
+    asm volatile("s_nop 1\n\t" OCM_M4(x0, m0, on) OCM_M4(x1, m1, on) "s_nop 4\n\t" OCM_M2(x0, u0, t0) OCM_M2(x1, w0, t0) OCM_RD(s0, p00) OCM_RD(s1, p10) OCM_RD(s2, p01) OCM_RD(s3, p11) OCM_M2(x0, u1, t1) OCM_FM(q0, s0) OCM_FM(q1, s1) OCM_FM(q2, s2) OCM_FM(q3, s3) OCM_M2(x1, w1, t1) OCM_RD(s0, p02) OCM_RD(s1, p12) OCM_RD(s2, p03) OCM_RD(s3, p13) OCM_M2(x0, u2, t2) OCM_FM(q0, s0) OCM_FM(q1, s1) OCM_FM(q2, s2) OCM_FM(q3, s3) OCM_M2(x1, w2, t2) OCM_M2(x0, u3, t3) OCM_M2(x1, w3, t3)
+        : [x0] "+a"(x0), [x1] "+a"(x1), [q0] "+v"(q[0]), [q1] "+v"(q[1]), [q2] "+v"(q[2]), [q3] "+v"(q[3]), [s0] "=&v"(s[0]), [s1] "=&v"(s[1]), [s2] "=&v"(s[2]), [s3] "=&v"(s[3])
+        : [u0] "v"(a0[0]), [u1] "v"(a0[1]), [u2] "v"(a0[2]), [u3] "v"(a0[3]), [w0] "v"(a1[0]), [w1] "v"(a1[1]), [w2] "v"(a1[2]), [w3] "v"(a1[3]), [m0] "v"(m0), [m1] "v"(m1), [t0] "v"(tB[0]), [t1] "v"(tB[1]), [t2] "v"(tB[2]), [t3] "v"(tB[3]), [on] "v"(one), [p00] "a"(p0[0]), [p01] "a"(p0[1]), [p02] "a"(p0[2]), [p03] "a"(p0[3]), [p10] "a"(p1[0]), [p11] "a"(p1[1]), [p12] "a"(p1[2]), [p13] "a"(p1[3]));
+  else
+    asm volatile("s_nop 1\n\t" OCM_M4(x0, m0, on) OCM_M4(x1, m1, on) "s_nop 4\n\t" OCM_M2(x0, u0, t0) OCM_M2(x1, w0, t0) OCM_M2(x0, u1, t1) OCM_M2(x1, w1, t1) OCM_M2(x0, u2, t2) OCM_M2(x1, w2, t2) OCM_M2(x0, u3, t3) OCM_M2(x1, w3, t3)
+        : [x0] "+a"(x0), [x1] "+a"(x1)
+        : [u0] "v"(a0[0]), [u1] "v"(a0[1]), [u2] "v"(a0[2]), [u3] "v"(a0[3]), [w0] "v"(a1[0]), [w1] "v"(a1[1]), [w2] "v"(a1[2]), [w3] "v"(a1[3]), [m0] "v"(m0), [m1] "v"(m1), [t0] "v"(tB[0]), [t1] "v"(tB[1]), [t2] "v"(tB[2]), [t3] "v"(tB[3]), [on] "v"(one));
+  (void)s, (void)p0, (void)p1, (void)q;
+}
+#undef OCM_MF
+#undef OCM_M4
+#undef OCM_M2
+#undef OCM_RD
+#undef OCM_FM
 }  // namespace s1p
 
 template <int NJ, bool EX>
@@ -511,16 +425,18 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
   constexpr int PW = 16 * NJ;  // columns per wave
   constexpr int PP = W * PW;   // p
   constexpr int NCH = PP / 4;  // 16-B chunks per component row
-  constexpr int NS = EX ? 5 : 4;  // sweep-2 K steps (4 components each; rows ≥ k of P are zero)
-  static_assert(NJ % 4 == 0, "the chunk swizzle needs 64-column wave slices");
+  static_assert(NJ % 4 == 0 && 2 * NJ - 1 <= 63, "64-column wave slices, vmcnt range");
   __shared__ f32x4 P0s[16 * NCH];
+  __shared__ float nmuL[PP];               // −μ (the sweep-2 μ step's A operand)
+  __shared__ double pmuL[20];              // P·μ (fp64)
   __shared__ double tpart[2][W * 20 * R];  // [buffer][wave][comp][row]
   __shared__ double qpart[2][W * R];       // [buffer][wave][row]
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ln = lane & 15, lq = lane >> 4;
 
-  // ---- prologue: loadings (f64 → f32) into LDS; μ, comps 16..19, diag(A) into registers
+  // ---- prologue: loadings (f64 → f32) and −μ into LDS, P·μ (fp64), comps
+  // 16..19 and diag(A) into registers
   for (int e = tid; e < 16 * NCH; e += 256) {
     const int c = e / NCH, ch = e - c * NCH;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -529,25 +445,18 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
       for (int u = 0; u < 4; ++u) v[u] = (float)P[(int64_t)c * PP + 4 * ch + u];
     P0s[c * NCH + (ch ^ sw(c))] = v;
   }
-  // compact DPP-row form of a per-column vector v over the wave's PW columns:
-  // register g, lane (ln, lq) holds column 16j + 4lq + e with j = 4g + ln/4,
-  // e = ln%4 — the value a lane needs for (j, e) sits in lane 4(j%4) + e of
-  // its own 16-lane row (row = lq)
-  auto compact_col = [&](int g) { return w * PW + 16 * (4 * g + (ln >> 2)) + 4 * lq + (ln & 3); };
-  float nmu[NJ / 4];  // −μ
-#pragma unroll
-  for (int g = 0; g < NJ / 4; ++g) nmu[g] = -(float)mu[compact_col(g)];
-  float p1c[EX ? NJ / 4 : 1][4];  // sweep 1: comps 16..19, compact form
-  float p1a[EX ? NJ : 1];         // sweep 2: A operand of step 4, P[16 + lq][w·PW + 16j + ln]
-  if constexpr (EX) {
-#pragma unroll
-    for (int g = 0; g < NJ / 4; ++g)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) p1c[g][c] = 16 + c < k ? (float)P[(int64_t)(16 + c) * PP + compact_col(g)] : 0.f;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-      p1a[j] = to_agpr(16 + lq < k ? (float)P[(int64_t)(16 + lq) * PP + w * PW + 16 * j + ln] : 0.f);
+  for (int c = tid; c < PP; c += 256) nmuL[c] = -(float)mu[c];
+  for (int c = w; c < 20; c += W) {  // wave w: comps w, w + 4, ...
+    double s = 0.0;
+    if (c < k)
+      for (int col = lane; col < PP; col += 64) s += P[(int64_t)c * PP + col] * mu[col];
+    s = wave_sum_f64(s);
+    if (lane == 0) pmuL[c] = s;
   }
+  float p1a[EX ? NJ : 1];  // comps 16..19: lane (ln, lq) holds P[16 + lq][w·PW + 16j + ln]
+  if constexpr (EX)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) p1a[j] = 16 + lq < k ? (float)P[(int64_t)(16 + lq) * PP + w * PW + 16 * j + ln] : 0.f;
   double ad[5];
 #pragma unroll
   for (int s = 0; s < 5; ++s) ad[s] = lq + 4 * s < k ? adiag[lq + 4 * s] : 0.0;
@@ -567,13 +476,18 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
       b2[s][b] = 4 * (c * NCH + w * (PW / 4) + ((4 * b + (ln >> 2)) ^ sw(c))) + (ln & 3);
     }
   const float* p0f = reinterpret_cast<const float*>(P0s);
+  // sweep-1 comps 16..19 operand of MFMA e: P[16 + (ln&3)][16j + 4lq + e], which
+  // p1a[j] holds on lane 16(ln&3) + 4lq + e (ds_bpermute address, bytes)
+  const int bperm = 4 * (16 * (ln & 3) + 4 * lq);
+  const float one = 1.f;  // B of the −μ step
+  __syncthreads();
 
   const int64_t G = gridDim.x;
   // base of this lane's 16-B pieces in row `row` of the wave's column slice
   auto col_base = [&](int64_t row) { return X + row * ldx + w * PW + 4 * lq; };
   // row index of lane row ln in tile tt (clamped: always a valid row).  For a
   // gather the 16 indices are read through the scalar cache (uniform
-  // addresses, lgkmcnt): a vector load here would wait, in order, for the tile in flight
+  // addresses, lgkmcnt): a vector load would wait, in order, for the tile in flight
   auto index_of = [&](int64_t tt) -> int64_t {
     if (!rows) {
       const int64_t r = tt * R + ln;
@@ -589,65 +503,58 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
     return v;
   };
 
-  f32x4 V[NJ];  // d = x − μ of the tile being scored (VGPRs)
-  f32x4 A[NJ];  // raw x of the next tile (AGPRs, loaded by asm; waited with wait_vm)
+  f32x4 XA[NJ], XB[NJ];  // two raw row tiles (AGPRs, loaded by asm, waited with wait_vm)
   double st[4] = {0.0, 0.0, 0.0, 0.0};
   double tt[5];
   float tB[5];
   double T2 = 0.0, T2prev = 0.0;
 
-  // ---- sweep 1: A (raw tile) → V (d), partial t → tpart[buf]; each block of
-  // A is refilled from `pre` (the tile after next) as soon as it is read
-  auto sweep1 = [&](const float* pre, int buf) {
-    f32x4 accA = {0.f, 0.f, 0.f, 0.f}, accB = accA, accC = accA, accD = accA;
-    double t64[4] = {0.0, 0.0, 0.0, 0.0};
-    float x1[4] = {0.f, 0.f, 0.f, 0.f};
-    double x164[4] = {0.0, 0.0, 0.0, 0.0};
-    f32x4 aN = P0s[b1[0]];  // LDS operands read one 16-column block ahead
-    // A[j] was issued NJ loads before the refills of blocks ≤ j... are: the rest
-    // of its tile and the refills of blocks < j were issued after it (a few
-    // output stores may add to that, which only makes the wait earlier)
-    wait_vm<NJ - 1>(A[0]);
-    centre4<0>(nmu[0], A[0], V[0]);
-    load_a<0>(A[0], pre);
+  // ---- sweep 1 on tile Y: partial t (uncentred) → tpart[buf] ----------------
+  auto sweep1 = [&](f32x4 (&Y)[NJ], int buf) {
+    f32x4 acA = {0.f, 0.f, 0.f, 0.f}, acB = acA, acC = acA, acD = acA, acE = acA, acF = acA;
+    double t64[4] = {0.0, 0.0, 0.0, 0.0}, x164[4] = {0.0, 0.0, 0.0, 0.0};
+    f32x4 aN = P0s[b1[0]];  // LDS / crossbar operands one block ahead
+    float bN[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (EX)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        bN[e] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(bperm + 4 * e, __builtin_bit_cast(int, p1a[0])));
     static_for<NJ>([&](auto J) {
       constexpr int j = decltype(J)::value;
       const f32x4 a = aN;
-      if constexpr (j + 1 < NJ) aN = P0s[b1[(j + 1) & 3] + 16 * ((j + 1) >> 2)];
-      using Step = S1Step<4 * (j & 3)>;
+      float b[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) b[e] = bN[e];
       if constexpr (j + 1 < NJ) {
-        wait_vm<NJ - 1>(A[j + 1]);
+        aN = P0s[b1[(j + 1) & 3] + 16 * ((j + 1) >> 2)];
         if constexpr (EX)
-          Step::next_ex(accA, accB, accC, accD, x1, a, V[j], p1c[j >> 2], nmu[(j + 1) >> 2], A[j + 1], V[j + 1]);
-        else
-          Step::next(accA, accB, accC, accD, a, V[j], nmu[(j + 1) >> 2], A[j + 1], V[j + 1]);
-        load_a<64 * (j + 1)>(A[j + 1], pre);
-      } else {
-        if constexpr (EX)
-          Step::last_ex(accA, accB, accC, accD, x1, a, V[j], p1c[j >> 2]);
-        else
-          Step::last(accA, accB, accC, accD, a, V[j]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            bN[e] = __builtin_bit_cast(float,
+                                       __builtin_amdgcn_ds_bpermute(bperm + 4 * e, __builtin_bit_cast(int, p1a[j + 1])));
       }
+      // Y[j] was issued before the rest of its tile (NJ − 1 − j loads) and
+      // the NJ refills of the other tile (stores issued since only make the
+      // wait earlier)
+      wait_vm<2 * NJ - 1 - j>(Y[j]);
+      s1_block<EX>(acA, acB, acC, acD, acE, acF, a, b, Y[j]);
       __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting every block's reads
       if constexpr ((j & 15) == 15 || j == NJ - 1) {  // f32 partials over ≤ 64 columns per chain
-        asm volatile("s_nop 11" ::: "memory");        // last MFMA result → VALU read
+        asm volatile("s_nop 11" ::: "memory");        // MFMA result → VALU read
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          t64[i] += ((double)accA[i] + (double)accB[i]) + ((double)accC[i] + (double)accD[i]);
-          accA[i] = accB[i] = accC[i] = accD[i] = 0.f;
-          if constexpr (EX) {
-            x164[i] += (double)x1[i];
-            x1[i] = 0.f;
-          }
+          t64[i] += ((double)acA[i] + (double)acB[i]) + ((double)acC[i] + (double)acD[i]);
+          x164[i] += (double)acE[i] + (double)acF[i];
+          acA[i] = acB[i] = acC[i] = acD[i] = acE[i] = acF[i] = 0.f;
         }
       }
     });
     double* tp = tpart[buf];
 #pragma unroll
     for (int i = 0; i < 4; ++i) tp[(w * 20 + 4 * lq + i) * R + ln] = t64[i];
-    if constexpr (EX) {
+    if constexpr (EX) {  // comps 16..19: lane (ln, lq) holds the partial over its column quarter lq
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {  // comps 16..19: sum over the q lanes
+      for (int u = 0; u < 4; ++u) {
         x164[u] += __shfl_xor(x164[u], 16, 64);
         x164[u] += __shfl_xor(x164[u], 32, 64);
       }
@@ -662,9 +569,11 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
       double v = 0.0;
-      if (s < 4 || EX)
+      if (s < 4 || EX) {
 #pragma unroll
         for (int ww = 0; ww < W; ++ww) v += tp[(ww * 20 + lq + 4 * s) * R + ln];
+        v -= pmuL[lq + 4 * s];  // t = P·x − P·μ
+      }
       tt[s] = v;
     }
     T2 = 0.0;
@@ -678,28 +587,23 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
       for (int s = 0; s < 5; ++s)
         if (lq + 4 * s < k) T_out[row * k + lq + 4 * s] = (float)tt[s];
 #pragma unroll
-    for (int s = 0; s < 5; ++s) tB[s] = -(float)tt[s];  // the sweep-2 chain from d ends at r = d − Pᵀt
+    for (int s = 0; s < 5; ++s) tB[s] = -(float)tt[s];  // r = x − μ + Pᵀ(−t)
   };
-  // ---- sweep 2 on V (d of the tile being scored): Q partials → qpart[buf] --
-  auto sweep2 = [&](int buf) {
-    float q0 = 0.f, q1 = 0.f;
+  // ---- sweep 2 on tile Z (raw x of the tile being scored): Q partials →
+  // qpart[buf]; each consumed block pair of Z is refilled from `pre`
+  auto sweep2 = [&](f32x4 (&Z)[NJ], const float* pre, int buf) {
+    float q[4] = {0.f, 0.f, 0.f, 0.f};
     double q64 = 0.0;
-    float aN[2][5];  // A operands of the next block pair (LDS reads one pair ahead)
-    auto read_a = [&](auto J, float (&dst)[5]) {
+    float aN[2][5], mN[2];  // A operands of the next block pair (one pair ahead)
+    auto read_a = [&](auto J, float (&dst)[5], float& mdst) {
       constexpr int j = decltype(J)::value;
-#ifdef OCM_S1P_DIAG_NOLDS2  // timing ablation only (wrong results)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) dst[s] = (float)(b2[s][j & 3] + j);
-#else
 #pragma unroll
       for (int s = 0; s < 4; ++s) dst[s] = p0f[b2[s][j & 3] + 64 * (j >> 2)];
-#endif
-      if constexpr (EX) dst[4] = p1a[j];
-      else dst[4] = 0.f;
+      dst[4] = EX ? p1a[j] : 0.f;
+      mdst = nmuL[w * PW + 16 * j + 4 * lq + (ln & 3)];  // 4x4x1 A: block l/4, row l&3
     };
-    read_a(std::integral_constant<int, 0>{}, aN[0]);
-    read_a(std::integral_constant<int, 1>{}, aN[1]);
-    f32x4 r0, r1;  // r of the previous pair (its q FMAs run inside the next pair's MFMAs)
+    read_a(std::integral_constant<int, 0>{}, aN[0], mN[0]);
+    read_a(std::integral_constant<int, 1>{}, aN[1], mN[1]);
     static_for<NJ / 2>([&](auto H) {
       constexpr int j = 2 * decltype(H)::value;
       float a0[5], a1[5];
@@ -708,27 +612,41 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
         a0[s] = aN[0][s];
         a1[s] = aN[1][s];
       }
+      const float m0 = mN[0], m1 = mN[1];
       if constexpr (j + 2 < NJ) {
-        read_a(std::integral_constant<int, j + 2>{}, aN[0]);
-        read_a(std::integral_constant<int, j + 3>{}, aN[1]);
+        read_a(std::integral_constant<int, j + 2>{}, aN[0], mN[0]);
+        read_a(std::integral_constant<int, j + 3>{}, aN[1], mN[1]);
       }
-      f32x4 n0, n1;
-      s2_pair<NS, j == 0>(V[j], V[j + 1], a0, a1, tB, r0, r1, q0, q1, n0, n1);
-      r0 = n0;
-      r1 = n1;
+      // r is formed in place of x (the tile registers are all the AGPRs there
+      // are at NJ = 32; a separate result would push tile quads into VGPRs and
+      // the compiler would copy them before their loads had landed); the
+      // previous pair's r is squared into q inside this pair's MFMA stream and
+      // only then refilled
+      if constexpr (j == 0) {
+        s2_pair<EX, false>(Z[0], Z[1], a0, a1, m0, m1, tB, one, Z[0], Z[1], q);
+      } else {
+        s2_pair<EX, true>(Z[j], Z[j + 1], a0, a1, m0, m1, tB, one, Z[j - 2], Z[j - 1], q);
+        __builtin_amdgcn_sched_barrier(0);
+        refill_a<64 * (j - 2)>(Z[j - 2], pre);
+        refill_a<64 * (j - 1)>(Z[j - 1], pre);
+        if constexpr (((j - 2) & 15) == 14) {  // f32 q partials over ≤ 16 columns each per lane
+          q64 += ((double)q[0] + (double)q[1]) + ((double)q[2] + (double)q[3]);
+          q[0] = q[1] = q[2] = q[3] = 0.f;
+        }
+      }
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr ((j & 15) == 14) {  // f32 q partials over ≤ 128 columns per accumulator
-        q64 += (double)q0 + (double)q1;
-        q0 = q1 = 0.f;
-      }
     });
-    asm volatile("s_nop 11" ::: "memory");  // last pair's MFMA results → VALU
+    // the last pair: its MFMA results → VALU reads, then its refill
+    asm volatile("s_nop 11" : "+a"(Z[NJ - 2]), "+a"(Z[NJ - 1]));
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      q0 = fmaf(r0[e], r0[e], q0);
-      q1 = fmaf(r1[e], r1[e], q1);
+      q[e & 1] = fmaf(Z[NJ - 2][e], Z[NJ - 2][e], q[e & 1]);
+      q[2 + (e & 1)] = fmaf(Z[NJ - 1][e], Z[NJ - 1][e], q[2 + (e & 1)]);
     }
-    q64 += (double)q0 + (double)q1;
+    __builtin_amdgcn_sched_barrier(0);
+    refill_a<64 * (NJ - 2)>(Z[NJ - 2], pre);
+    refill_a<64 * (NJ - 1)>(Z[NJ - 1], pre);
+    q64 += ((double)q[0] + (double)q[1]) + ((double)q[2] + (double)q[3]);
     q64 += __shfl_xor(q64, 16, 64);
     q64 += __shfl_xor(q64, 32, 64);
     if (lq == 0) qpart[buf][w * R + ln] = q64;
@@ -760,54 +678,67 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
     asm volatile("" ::: "memory");
   };
 
-  // ---- tile pipeline: tiles t_i = blockIdx.x + i·G.  An iteration scores t
-  // (sweep 2 on V), then runs sweep 1 of t + G (A → V) while tile t + 2G
-  // streams into A; past the last tile the refill re-reads a valid tile.
+  // ---- tile pipeline: tiles t_i = blockIdx.x + i·G.  step(X, Y) scores t (in
+  // X, sweep 2) while t + 2G streams into X, then sweep 1 of t + G (in Y);
+  // unrolled by two so X / Y swap roles.  Past the last tile the refills
+  // re-read a valid tile.
   int64_t t = blockIdx.x;
   auto clamp_tile = [&](int64_t tt) { return tt < ntiles ? tt : t; };
   {
     const float* p0 = col_base(index_of(t));
-    static_for<NJ>([&](auto J) { load_a<64 * decltype(J)::value>(A[decltype(J)::value], p0); });
+    const float* p1 = col_base(index_of(clamp_tile(t + G)));
+    static_for<NJ>([&](auto J) { load_a<64 * decltype(J)::value>(XA[decltype(J)::value], p0); });
+    static_for<NJ>([&](auto J) { load_a<64 * decltype(J)::value>(XB[decltype(J)::value], p1); });
   }
-  sweep1(col_base(index_of(clamp_tile(t + G))), 0);
+  sweep1(XA, 0);
   lds_barrier();
   compute_t(t, 0);
   int buf = 0;
-#ifdef OCM_S1P_STAMPS  // diagnostic build only: cycles per phase (stat_part carries them)
-  uint64_t cyc[4] = {0, 0, 0, 0};
-#define OCM_STAMP(I) { const uint64_t now_ = __builtin_amdgcn_s_memtime(); cyc[I] += now_ - last_; last_ = now_; }
-  uint64_t last_ = __builtin_amdgcn_s_memtime();
+#ifdef OCM_S1P_STAMPS  // diagnostic build (make exp): Σ cycles per phase replace the moment partials
+  double cyc[4] = {0.0, 0.0, 0.0, 0.0};
+  uint64_t c_last = __builtin_readcyclecounter();
+#define OCM_STAMP(I)                                    \
+  {                                                     \
+    const uint64_t c_now = __builtin_readcyclecounter(); \
+    cyc[I] += (double)(c_now - c_last);                  \
+    c_last = c_now;                                      \
+  }
 #else
 #define OCM_STAMP(I)
 #endif
-  for (;;) {
+  auto step = [&](f32x4 (&Xc)[NJ], f32x4 (&Yn)[NJ]) -> bool {
     const int64_t tn = t + G;
     const bool more = tn < ntiles;
-    sweep2(buf);
+    OCM_STAMP(3)
+    sweep2(Xc, col_base(index_of(clamp_tile(tn + G))), buf);
     OCM_STAMP(0)
-    if (more) sweep1(col_base(index_of(clamp_tile(tn + G))), buf ^ 1);
+    if (more) sweep1(Yn, buf ^ 1);
     OCM_STAMP(1)
     lds_barrier();
     OCM_STAMP(2)
     T2prev = T2;
     finish(t, buf);
-    if (!more) break;
+    if (!more) return false;
     t = tn;
     buf ^= 1;
     compute_t(t, buf);
-    OCM_STAMP(3)
-  }
+    return true;
+  };
 #undef OCM_STAMP
-#ifdef OCM_S1P_STAMPS
-  st[0] = (double)cyc[0]; st[1] = (double)cyc[1]; st[2] = (double)cyc[2]; st[3] = (double)cyc[3];
-  if (stat_part && w == 0 && lane == 0)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) stat_part[(int64_t)blockIdx.x * 4 + i] = st[i];
-  return;
-#endif
+  for (;;) {
+    if (!step(XA, XB)) break;
+    if (!step(XB, XA)) break;
+  }
   // drain the refills past the last tile before the wave ends
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) wait_vm<0>(A[j]);
+  for (int j = 0; j < NJ; ++j) {
+    wait_vm<0>(XA[j]);
+    wait_vm<0>(XB[j]);
+  }
+#ifdef OCM_S1P_STAMPS
+#pragma unroll
+  for (int i = 0; i < 4; ++i) st[i] = cyc[i] / 64.0;  // the wave sum below restores the wave's total
+#endif
   if (stat_part) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) st[i] = wave_sum_f64(st[i]);

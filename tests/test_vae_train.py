@@ -136,3 +136,30 @@ def test_fast_batchnorm_matches_torch(dtype, shape):
     torch.testing.assert_close(fast.running_mean, ref.running_mean, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(fast.running_var, ref.running_var, rtol=1e-3, atol=1e-4)
     assert int(fast.num_batches_tracked) == int(ref.num_batches_tracked) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+def test_c4_graph_step_with_grad_allreduce():
+    """C5's data-parallel step at the C4 network shape (cb=3, nf=3, ks=7,
+    hid=64, d=32; B=512 × L=2048, bf16): the flat-gradient RCCL all-reduce is
+    captured into the step's HIP graph (one replay per step), every .grad is a
+    view of the one buffer, and the step trains like the single-GPU graph step.
+    World size 1 (one GPU per box), in a child process: a communicator that a
+    captured graph still references is not torn down inside the test runner.
+    World 2 runs over gloo on the CPU (tests/test_vae_ddp.py)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "c4_ddp_worker.py")], capture_output=True, text=True,
+                       timeout=240, cwd=os.path.dirname(here))
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["allreduce"] and res["graphed"] and res["grads_are_views"]
+    la, lb = np.array(res["loss_ddp"]), np.array(res["loss_single"])
+    assert np.isfinite(la).all() and np.isfinite(lb).all() and res["params_finite"]
+    assert la[-5:].mean() < la[0]
+    np.testing.assert_allclose(la[-5:].mean(), lb[-5:].mean(), rtol=0.05)
