@@ -5,8 +5,10 @@ types and quirks as the reference estimator (TEAM-AIOLY/OCM-VAE-SIMCA
 ``utils/SIMCA.py:12-381``), so drivers such as ``simca_nuts.py``
 (``from utils import SIMCA`` … ``.fit`` / ``.predict`` / ``.transform`` /
 ``._model[cls]['D_limit']``) run unchanged.  The arithmetic runs on the GPU
-through ``ocm.engine`` (Gram on FP32 MFMA, fp64 eigensolver, fused
-projection/Q/T² scoring); only the scalar limits are evaluated on the host.
+through ``ocm.engine`` (Gram on int8-digit MFMA — three base-254 digits per
+value, fp32-grade, outlier rows added back exactly —, fp64 eigensolver,
+single-pass projection/Q/T² scoring); only the scalar limits are evaluated
+on the host.
 
 Inputs may be NumPy arrays (copied to HBM; results come back as NumPy, like
 the reference) or CUDA torch tensors (device-resident; ``predict`` then
@@ -21,7 +23,14 @@ Documented deviations:
   ``inverse_transform``);
 * ``eigs_all`` holds the leading k eigenvalues from the HIP eigensolver and,
   on first access only, the rest of the spectrum (a diagnostic no limit uses;
-  the θ moments come from device traces).
+  the θ moments come from device traces);
+* float64 inputs are computed in float32 on the GPU (the reference runs its
+  PCA in float64 then); limits and decisions agree at the tolerances of
+  tests/test_gpu_northstar.py::test_float64_input_vs_reference (DESIGN.md §5);
+* ``n_components`` (and a CV sweep's ``LV_max``) is at most 64 when p > 64:
+  the subspace eigensolver (ocm_eig_topk) and the scoring / CV kernels keep
+  the components in one 64-wide block and raise ``ValueError`` beyond it; the
+  reference allows any k ≤ min(n, p).
 """
 from __future__ import annotations
 

@@ -451,7 +451,8 @@ def cross_validate_simca_grid(X, y, cls_label, n_splits, LV_min=2, LV_max=10, cf
             ci = class_index if class_index is not None else last_mc
             sens = float(metrics_conformity(y, pred_vec, _ci_scalar(ci))["sensitivity"])
             records.append({"params": dict(combo), "LV": combo.get("n_components") if grid_has_nc else lv,
-                            "spec": spec, "sens": sens, "eff": float(np.sqrt(sens * spec))})
+                            "spec": spec, "sens": sens, "eff": float(np.sqrt(sens * spec)),
+                            "prediction": pred_vec})  # pooled fold predictions (store_predictions)
     key = {"eff": "eff", "spec": "spec", "sens": "sens"}[refit_metric]
     best = int(np.argmax([r[key] for r in records]))
     return {"results": records, "best_LV": records[best]["LV"], "best_score": records[best][key],
