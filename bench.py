@@ -258,13 +258,16 @@ def main():
         gram_desc = "k_gram (FP32 MFMA shifted Gram)"
         gram_peak = FP32_MFMA_PEAK_TFLOPS
         peak_basis = "FP32 MFMA dense peak; achieved counts algorithmic flops n*p*(p+1) (symmetric Gram)"
-    traffic = None
+    # HBM bytes per launch from this round's PMC passes (scripts/pmc_passes.sh →
+    # scripts/pmc_latest.py → profiles/pmc_gram_latest.json; FETCH_SIZE doubled)
+    traffic, traffic_src, score_traffic = None, None, None
     pmc = os.path.join(REPO, "profiles", "pmc_gram_latest.json")
     if os.path.exists(pmc):
         try:
             lat = json.load(open(pmc))
-            traffic = lat.get(gram_kernel, {}).get("hbm_bytes_per_launch") if "kernel" not in lat else (
-                lat["hbm_bytes_per_launch"] if lat["kernel"] == gram_kernel else None)
+            traffic = lat.get(gram_kernel, {}).get("hbm_bytes_per_launch")
+            traffic_src = lat.get(gram_kernel, {}).get("source")
+            score_traffic = lat.get("k_score_1p", {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -298,6 +301,7 @@ def main():
             "frac": round(achieved / gram_peak, 4),
             "peak_basis": peak_basis,
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "flop_per_launch": gram_flop,
             "quantise_ms": round(quant_ms / max(quant_n, 1), 4) if quant_n else None,
             "avg_launch_ms": round(gram_avg_s * 1e3, 4),
@@ -306,7 +310,7 @@ def main():
         "score_kernel": {"kernel": "k_score_1p (fused projection/Q/T2/decision, one HBM pass; row tile kept in registers)", "bound": "hbm",
                          "achieved_GBs": round(score_gbs, 1), "peak_GBs": HBM_PEAK_GBS,
                          "frac": round(score_gbs / HBM_PEAK_GBS, 4), "avg_launch_ms": round(score_avg_s * 1e3, 4),
-                         "launches": score_n, "bytes_per_launch": n * p * 4},
+                         "launches": score_n, "bytes_per_launch": n * p * 4, "traffic": score_traffic},
         "checks": {"accept_rate": round(accepted, 4), "eig_iters": result["fit"].eig_iters,
                    "T2_limit": result["T2_limit"], "Q_limit": result["Q_limit"],
                    "gram_guard_marks": engine.last_gram_marks(device.index)},

@@ -34,7 +34,7 @@ if [ "${BENCH:-0}" = 1 ]; then
   run bench 600 "0" python -u bench.py ${BENCH_ARGS:-}
 fi
 if [ "${PROF:-0}" = 1 ]; then
-  run prof 600 "0" rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-vae
+  run prof 600 "0" rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-vae
 fi
 if [ -n "${EXTRA:-}" ]; then
   # shellcheck disable=SC2086
