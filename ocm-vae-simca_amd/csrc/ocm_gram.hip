@@ -1132,13 +1132,15 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
   const float* srow = q.scale + (size_t)chunk * q.nblk * q.P8 + I + wm * 64 + lane;
   const float* scol = q.scale + (size_t)chunk * q.nblk * q.P8 + J + wn * 64 + lane;
 
+#define Q8D_LOAD_B(FB, x_, dg_, so_) \
+  FB[x_][dg_] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(rb[dg_], voff + x_ * 1024, so_, 0)
 #define Q8D_LOAD(FA, FB, STG)                                                                         \
   do {                                                                                              \
     const int so_ = (STG) * (int)gstride;                                                           \
     _Pragma("unroll") for (int x_ = 0; x_ < 2; ++x_)                                                \
     _Pragma("unroll") for (int dg_ = 0; dg_ < 3; ++dg_) {                                           \
       FA[x_][dg_] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(ra[dg_], voff + x_ * 1024, so_, 0); \
-      FB[x_][dg_] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(rb[dg_], voff + x_ * 1024, so_, 0); \
+      Q8D_LOAD_B(FB, x_, dg_, so_);                                                                 \
     }                                                                                               \
   } while (0)
 // Z: first stage of a scale block — each accumulator's first product starts
@@ -1200,9 +1202,25 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
 #define Q8D_S0 F0A, F0B, F2A, F2B
 #define Q8D_S1 F1A, F1B, F0A, F0B
 #define Q8D_S2 F2A, F2B, F1A, F1B
+// diagnostic builds only (make exp; timing, not results): NOLOAD never
+// refreshes the operands after the prologue, HALFB refreshes only A (the
+// load path's share of the kernel time)
+#ifdef OCM_G8_DIAG_NOLOAD  // diagnostic build only (make exp): operands never refreshed after the prologue
+#define Q8D_REFILL(NA, NB, STG) (void)0
+#elif defined(OCM_G8_DIAG_HALFB)  // diagnostic: B operands never refreshed (half the loads)
+#define Q8D_REFILL(NA, NB, STG)                                                                       \
+  do {                                                                                              \
+    const int so_ = (STG) * (int)gstride;                                                           \
+    _Pragma("unroll") for (int x_ = 0; x_ < 2; ++x_)                                                \
+    _Pragma("unroll") for (int dg_ = 0; dg_ < 3; ++dg_)                                             \
+      NA[x_][dg_] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(ra[dg_], voff + x_ * 1024, so_, 0); \
+  } while (0)
+#else
+#define Q8D_REFILL(NA, NB, STG) Q8D_LOAD(NA, NB, STG)
+#endif
 #define Q8D_STEP_(STG, Z, CA, CB, NA, NB)                                                             \
   do {                                                                                              \
-    Q8D_LOAD(NA, NB, min((STG) + 2, nstage3 - 1));                                                  \
+    Q8D_REFILL(NA, NB, min((STG) + 2, nstage3 - 1));                                                \
     __builtin_amdgcn_sched_barrier(0);                                                              \
     Q8D_MFMA(CA, CB, Z);                                                         \
     __builtin_amdgcn_sched_barrier(0);                                                              \
@@ -1212,8 +1230,11 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
   i32x4 F0A[2][3], F0B[2][3], F1A[2][3], F1B[2][3], F2A[2][3], F2B[2][3];
   Q8D_LOAD(F0A, F0B, 0);
   Q8D_LOAD(F1A, F1B, min(1, nstage3 - 1));
+#if defined(OCM_G8_DIAG_NOLOAD) || defined(OCM_G8_DIAG_HALFB)
+  Q8D_LOAD(F2A, F2B, min(2, nstage3 - 1));
+#endif
   for (int blk = 0; blk < nb; ++blk) {
-    // stage s0+u uses set u % 3 (s0 is a multiple of 24); the loads of stage
+    // stage s0+u uses set u % 3 (s0 is a multiple of 48); the loads of stage
     // s0+u+2 go to set (u+2) % 3.  The block's scales are fetched early (they
     // are used by the flush after the last stage).
     const int s0 = blk * Q8SPB;
@@ -1231,11 +1252,13 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
   }
 #undef Q8D_STEP
 #undef Q8D_STEP_
+#undef Q8D_REFILL
 #undef Q8D_S0
 #undef Q8D_S1
 #undef Q8D_S2
 #undef Q8D_MFMA
 #undef Q8D_LOAD
+#undef Q8D_LOAD_B
 
   float* out = part + ((size_t)chunk * ntiles + tile) * (Q8T * Q8T);
 #pragma unroll
