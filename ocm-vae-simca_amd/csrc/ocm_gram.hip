@@ -718,20 +718,37 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ 
 #pragma unroll
   for (int e = 0; e < 4; ++e) sh[e] = c0 + e < p ? shift[c0 + e] : 0.f;
   f32x4 v[16];
+  const int64_t rblk = r0 + (int64_t)b * Q8BLK;  // first row of the block
+  if (!GATHER && vec && (int64_t)Q8BLK * ldx * 4 < (1LL << 31)) {
+    // contiguous rows: one buffer descriptor over the block's valid rows, the
+    // row step in the scalar offset (one address VGPR instead of 16 64-bit
+    // row pointers); rows past r1 lie outside the descriptor and read as 0
+    const int64_t nvalid = max((int64_t)0, min(r1 - rblk, (int64_t)Q8BLK));
+    const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(X + rblk * ldx), 0, (uint32_t)(nvalid * ldx * 4), 0x00020000);
+    const int voff = (int)((16 * rs * ldx + c0) * 4);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int64_t g = rb + j;
-    const int64_t gc = g < r1 ? g : r1 - 1;  // clamped: always a valid row
-    const float* xr = X + (GATHER ? rows[gc] : gc) * ldx;
-    f32x4 x;
-    if (vec) {
-      x = *reinterpret_cast<const f32x4*>(xr + c0);
-    } else {
+    for (int j = 0; j < 16; ++j) {
+      const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_x, voff, (int)(j * ldx * 4), 0));
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] = xr[min(c0 + e, p - 1)];
+      for (int e = 0; e < 4; ++e) v[j][e] = (rb + j < r1) ? x[e] - sh[e] : 0.f;
     }
+  } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[j][e] = (g < r1 && c0 + e < p) ? x[e] - sh[e] : 0.f;
+    for (int j = 0; j < 16; ++j) {
+      const int64_t g = rb + j;
+      const int64_t gc = g < r1 ? g : r1 - 1;  // clamped: always a valid row
+      const float* xr = X + (GATHER ? rows[gc] : gc) * ldx;
+      f32x4 x;
+      if (vec) {
+        x = *reinterpret_cast<const f32x4*>(xr + c0);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = xr[min(c0 + e, p - 1)];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = (g < r1 && c0 + e < p) ? x[e] - sh[e] : 0.f;
+    }
   }
   // column sums over every row (the fix-up does not touch them)
   double cs[4] = {0.0, 0.0, 0.0, 0.0};
@@ -804,17 +821,24 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ 
   __syncthreads();
   const f32x4 mx = *reinterpret_cast<const f32x4*>(&fmax_[4 * cq]);
   i32x4 w[3][4];  // [digit][column e]
+  f32x4 inv;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     int ex = 0;
     (void)frexpf(mx[e] * (1.f / 127.f), &ex);
-    const float inv = mx[e] > 0.f ? ldexpf(1.f, -ex) : 1.f;
+    inv[e] = mx[e] > 0.f ? ldexpf(1.f, -ex) : 1.f;
+  }
+  // row quads outermost: v[4k .. 4k+3] are dead after quad k, so the digits
+  // take the registers the values free (peak ≈ 64 + 12, not 64 + 48: no spills
+  // at the 168-VGPR budget of three waves per SIMD)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
       float d1[4], d2[4], d3[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const float t = v[4 * k + u][e] * inv;  // exact (power of two), |t| ≤ 127
+        const float t = v[4 * k + u][e] * inv[e];  // exact (power of two), |t| ≤ 127
         const float a1 = rintf(t);
         const float t2 = (t - a1) * Q8BASE;
         const float a2 = rintf(t2);

@@ -435,6 +435,7 @@ def cross_validate_simca_grid(X, y, cls_label, n_splits, LV_min=2, LV_max=10, cf
             if lv is not None:
                 kw["n_components"] = lv
             pred_vec = np.zeros(X.shape[0])
+            margin = np.full(X.shape[0], np.nan)  # |dred − D_lim| / D_lim of the fold that set pred_vec
             specs, senses = [], []
             last_mc = None
             for tr, te in splits:
@@ -442,6 +443,10 @@ def cross_validate_simca_grid(X, y, cls_label, n_splits, LV_min=2, LV_max=10, cf
                 est.fit(X[tr], y[tr])
                 yp = np.ravel(est.predict(X[te]))
                 pred_vec[te] = yp
+                mc = np.atleast_1d(est.model_class)
+                if mc.size == 1:
+                    dlim = est._model[mc[0]]["D_limit"]
+                    margin[te] = np.abs(est.dred(X[te], mc[0]) - dlim) / abs(dlim)
                 ci = class_index if class_index is not None else est.model_class
                 m = metrics_conformity(y[te], yp, _ci_scalar(ci))
                 specs.append(m["specificity"])
@@ -452,7 +457,8 @@ def cross_validate_simca_grid(X, y, cls_label, n_splits, LV_min=2, LV_max=10, cf
             sens = float(metrics_conformity(y, pred_vec, _ci_scalar(ci))["sensitivity"])
             records.append({"params": dict(combo), "LV": combo.get("n_components") if grid_has_nc else lv,
                             "spec": spec, "sens": sens, "eff": float(np.sqrt(sens * spec)),
-                            "prediction": pred_vec})  # pooled fold predictions (store_predictions)
+                            "prediction": pred_vec,  # pooled fold predictions (store_predictions)
+                            "margin": margin})  # not in the reference: the decision band of each pooled row
     key = {"eff": "eff", "spec": "spec", "sens": "sens"}[refit_metric]
     best = int(np.argmax([r[key] for r in records]))
     return {"results": records, "best_LV": records[best]["LV"], "best_score": records[best][key],
