@@ -133,13 +133,19 @@ def cpu_baseline(rows, p, k, repeats=3):
 def vae_bench(device, steps, warmup, batch=512, length=2048, dtype=None):
     """Secondary metric (BASELINE.json): VAE-SIMCA train steps/s, C4 network
     (cb=3, nf=3, ks=7, hid=64, d=32) at B=512 × L=2048 in bf16,
-    one HIP-graph replay per optimizer step (ocm/vae_train.py)."""
+    one HIP-graph replay per optimizer step (ocm/vae_train.py).  Every timed
+    step takes a distinct batch of a (warmup + steps) × B synthetic set in
+    HBM.  Then SIMCA-on-latents, timed on its own (utils/final_vaesimca.py:
+    406-442, 500-533): encode + decode the training rows (eval, no grad),
+    latent statistics and the f-distance decision on libocm."""
     import torch
 
     import vae_model as V
+    from ocm import engine
+    from ocm.vae import full_distance_decision, latent_stats
     from ocm.vae_train import GraphedVAETrainer
 
-    nb = 16
+    nb = warmup + steps
     X = synth_device(batch * nb, length, 20, seed=99, device=device)
     mean = X.mean(0).cpu().numpy()
     std = X.std(0).cpu().numpy() + 1e-6
@@ -149,24 +155,59 @@ def vae_bench(device, steps, warmup, batch=512, length=2048, dtype=None):
         dtype = torch.float32 if os.environ.get("OCM_VAE_DTYPE") == "f32" else torch.bfloat16
     tr = GraphedVAETrainer(m, batch, lr=1e-3, dtype=dtype)
     for i in range(warmup):
-        tr.step(X[(i % nb) * batch:(i % nb + 1) * batch])
+        tr.step(X[i * batch:(i + 1) * batch])
     first = float(tr.out[0].item())
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(steps):
-        tr.step(X[(i % nb) * batch:(i % nb + 1) * batch])
+    for i in range(warmup, nb):
+        tr.step(X[i * batch:(i + 1) * batch])
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     loss = float(tr.out[0].item())
     finite = all(bool(torch.isfinite(p).all()) for p in m.parameters())
+
+    # SIMCA-on-latents over every training row
+    m.eval()
+    n = X.shape[0]
+    eb = 8192
+    ac = torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16)
+
+    mus = torch.empty((n, 32), dtype=torch.float32, device=device)
+    q = torch.empty(n, dtype=torch.float32, device=device)
+
+    def encode(starts):
+        with torch.no_grad(), ac:
+            for a in starts:
+                xb = X[a:min(n, a + eb)]
+                mu, _ = m.encode((xb - m.spec_mean) / m.spec_std)
+                xr = m.decode(mu).float() * m.spec_std + m.spec_mean
+                mus[a:a + xb.shape[0]] = mu.float()
+                q[a:a + xb.shape[0]] = engine.rowsq_residual(xb, xr.contiguous())
+
+    starts = list(range(0, n, eb))
+    encode(sorted({starts[0], starts[-1]}))  # kernel selection for both batch shapes (MIOpen find)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    encode(starts)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    lmean, _, t2lim, qlim = latent_stats(mus, q)
+    accept, _, fcrit = full_distance_decision(mus, lmean, q)
+    acc = float(accept.to(torch.float64).sum().item())
+    t3 = time.perf_counter()
+    m.train()
     return {"metric": "VAE-SIMCA train steps/sec", "value": round(steps / dt, 2), "unit": "steps/s",
             "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps,
             "dtype": "f32" if dtype == torch.float32 else "bf16",
             "config": {"workload": f"ConvVAE1D cb=3 nf=3 ks=7 hid=64 d=32, B={batch}, L={length}, "
-                                   "BCE-with-logits + KL, Adam, HIP-graph step",
+                                   f"BCE-with-logits + KL, Adam, HIP-graph step, {nb} distinct batches",
                        "params": sum(p.numel() for p in m.parameters())},
             "reference_cpu_steps_per_s": 2.5, "loss_after_warmup": round(first, 5), "final_loss": round(loss, 5),
-            "params_finite": finite}
+            "params_finite": finite,
+            "latents": {"rows": n, "encode_rows_per_s": round(n / (t2 - t1), 1),
+                        "encode_s": round(t2 - t1, 4), "stats_decision_s": round(t3 - t2, 4),
+                        "t2_limit": float(t2lim), "q_limit": float(qlim), "f_crit": float(fcrit),
+                        "accept_rate": round(acc / n, 4)}}
 
 
 def main():

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--rows", type=int, default=65536)
     ap.add_argument("--batches", default="512,2048,8192")
     ap.add_argument("--dtypes", default="bf16,f32")
+    ap.add_argument("--train-steps", type=int, default=0, help="HIP-graph train steps before encoding")
     args = ap.parse_args()
     import torch
 
@@ -32,7 +33,15 @@ def main():
     torch.manual_seed(0)
     X = torch.randn(args.rows, L, device=dev)
     m = V.ConvVAE1D(L, 32, torch.zeros(L).numpy(), torch.ones(L).numpy(), conv_blocks=3, n_filters=3,
-                    kernel_size=7, hidden_fc=64).to(dev).eval()
+                    kernel_size=7, hidden_fc=64).to(dev)
+    if args.train_steps:
+        from ocm.vae_train import GraphedVAETrainer
+
+        tr = GraphedVAETrainer(m, 512, lr=1e-3, dtype=torch.bfloat16)
+        for i in range(args.train_steps):
+            tr.step(X[(i % 8) * 512:(i % 8 + 1) * 512])
+        torch.cuda.synchronize()
+    m.eval()
     for dt in args.dtypes.split(","):
         for bs in (int(b) for b in args.batches.split(",")):
             ctx = torch.autocast("cuda", dtype=torch.bfloat16, enabled=(dt == "bf16"))
