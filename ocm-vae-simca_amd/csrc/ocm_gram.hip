@@ -1242,6 +1242,35 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
 #else
 #define Q8D_REFILL(NA, NB, STG) Q8D_LOAD(NA, NB, STG)
 #endif
+#if !defined(OCM_G8_BURST) && !defined(OCM_G8_DIAG_NOLOAD) && !defined(OCM_G8_DIAG_HALFB)
+  // the 12 refill loads of stage STG+2 interleaved one per two MFMAs of stage
+  // STG, in the order the next stages consume them: 399 vs 387 TF for the
+  // loads issued as one burst before the MFMAs (OCM_G8_BURST, exp builds)
+  auto step_il = [&](i32x4 (&CA)[2][3], i32x4 (&CB)[2][3], i32x4 (&NA)[2][3], i32x4 (&NB)[2][3], int stg,
+                     bool z) __attribute__((always_inline)) {
+    const int so_ = min(stg + 2, nstage3 - 1) * (int)gstride;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const int x = i / 6, r = i % 6, dg = r / 2;
+      if (r & 1)
+        NB[x][dg] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(rb[dg], voff + x * 1024, so_, 0);
+      else
+        NA[x][dg] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(ra[dg], voff + x * 1024, so_, 0);
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int j = 2 * i + jj, blk = j / 6, kind = j % 6, a = blk >> 1, c = blk & 1;
+        if (kind == 0) acc1[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(CA[a][0], CB[c][0], z ? i32x16{} : acc1[a][c], 0, 0, 0);
+        if (kind == 1) acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(CA[a][0], CB[c][1], z ? i32x16{} : acc2[a][c], 0, 0, 0);
+        if (kind == 2) acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(CA[a][1], CB[c][0], acc2[a][c], 0, 0, 0);
+        if (kind == 3) acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(CA[a][0], CB[c][2], z ? i32x16{} : acc3[a][c], 0, 0, 0);
+        if (kind == 4) acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(CA[a][2], CB[c][0], acc3[a][c], 0, 0, 0);
+        if (kind == 5) acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(CA[a][1], CB[c][1], acc3[a][c], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+#define Q8D_STEP_(STG, Z, CA, CB, NA, NB) step_il(CA, CB, NA, NB, (STG), (Z))
+#else
 #define Q8D_STEP_(STG, Z, CA, CB, NA, NB)                                                             \
   do {                                                                                              \
     Q8D_REFILL(NA, NB, min((STG) + 2, nstage3 - 1));                                                \
@@ -1249,6 +1278,7 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
     Q8D_MFMA(CA, CB, Z);                                                         \
     __builtin_amdgcn_sched_barrier(0);                                                              \
   } while (0)
+#endif
 #define Q8D_STEP(STG, Z, ...) Q8D_STEP_(STG, Z, __VA_ARGS__)
 
   i32x4 F0A[2][3], F0B[2][3], F1A[2][3], F1B[2][3], F2A[2][3], F2B[2][3];
