@@ -493,6 +493,98 @@ __global__ __launch_bounds__(64) void k_trsm_rows(const double* __restrict__ W, 
   for (int j = 0; j < BB; ++j) V[(int64_t)r * BB + j] = v[j];
 }
 
+// CholQR pass for b = 32 in ONE launch per 256-row block (4 waves): S = Σ_z
+// part[z] (the k_atb_part planes; each thread sums 4 entries, 8 planes per
+// batch of independent loads), the Cholesky S = L Lᵀ by wave 0 in registers
+// (lane i holds row i; column j's entries are read lane by lane into scalar
+// registers, v_readlane; computed
+// redundantly by every workgroup), then V = W · L⁻ᵀ one row per thread as
+// k_trsm_rows.  Replaces k_sum_planes + k_chol + k_trsm_rows (three launches)
+// by one; same arithmetic as k_chol (pivot clamp 1e-14·max diag, trailing
+// update a_il −= (a_ij/d)(a_lj/d)).
+constexpr int QB = 32, QT = 256;
+// lane l's double, wave-uniform l (two v_readlane_b32 into SGPRs: no LDS round trip)
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__global__ __launch_bounds__(QT) void k_chol_trsm32(const double* __restrict__ part, int nz,
+                                                    const double* __restrict__ W, int p, double* __restrict__ V) {
+  __shared__ double sl[QB][QB + 1];
+  __shared__ double rd[QB];
+  const int tid = threadIdx.x;
+  {
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    int z = 0;
+    for (; z + 8 <= nz; z += 8) {
+      double t[8][4];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) t[u][c] = part[(int64_t)(z + u) * QB * QB + tid + QT * c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] += t[u][c];
+    }
+    for (; z < nz; ++z)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] += part[(int64_t)z * QB * QB + tid + QT * c];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) sl[(tid + QT * c) / QB][(tid + QT * c) % QB] = acc[c];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int lane = tid, i = lane & (QB - 1);  // lanes 32..63 mirror 0..31 (results unused)
+    double a[QB];
+#pragma unroll
+    for (int c = 0; c < QB; ++c) a[c] = sl[i][c];
+    double dii = 0.0;
+#pragma unroll
+    for (int c = 0; c < QB; ++c) dii = c == i ? a[c] : dii;
+    double dmax = dii;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) dmax = fmax(dmax, __shfl_xor(dmax, o, 64));
+    if (!(dmax > 0.0)) dmax = 1.0;
+    double lrow[QB], ldiag = 1.0;
+#pragma unroll
+    for (int j = 0; j < QB; ++j) {
+      const double ajj = readlane_f64(a[j], j);
+      const double djj = sqrt(fmax(ajj, 1e-14 * dmax));
+      const double inv = 1.0 / djj;
+      const double lij = i > j ? a[j] * inv : (i == j ? djj : 0.0);
+      lrow[j] = lij;
+      ldiag = i == j ? djj : ldiag;
+#pragma unroll
+      for (int l = j + 1; l < QB; ++l) {
+        const double llj = readlane_f64(lij, l);
+        if (l <= i) a[l] -= lij * llj;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < QB) {
+#pragma unroll
+      for (int c = 0; c < QB; ++c) sl[lane][c] = lrow[c];
+      rd[lane] = 1.0 / ldiag;
+    }
+  }
+  __syncthreads();
+  const int r = blockIdx.x * QT + tid;
+  if (r >= p) return;
+  double v[QB];
+#pragma unroll
+  for (int j = 0; j < QB; ++j) {
+    double s = W[(int64_t)r * QB + j];
+#pragma unroll
+    for (int l = 0; l < j; ++l) s -= v[l] * sl[j][l];
+    v[j] = s * rd[j];
+  }
+#pragma unroll
+  for (int j = 0; j < QB; ++j) V[(int64_t)r * QB + j] = v[j];
+}
+
 __device__ __forceinline__ double hash_normal(uint64_t a) {
   // splitmix64 -> two uniforms -> Box-Muller
   auto mix = [](uint64_t z) {
@@ -816,6 +908,12 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
     OCM_CHECK_LAUNCH("k_colnormalize");
     for (int pass = 0; pass < 2; ++pass) {
       double* src = pass == 0 ? Win : Vout;
+      if (b == QB) {  // partial Grams → fused sum + Cholesky + solve
+        hipLaunchKernelGGL(k_atb_part, dim3(nblk), dim3(256), 0, st, src, src, p, b, apart);
+        hipLaunchKernelGGL(k_chol_trsm32, dim3((p + QT - 1) / QT), dim3(QT), 0, st, apart, nblk, src, p, Vout);
+        OCM_CHECK_LAUNCH("k_chol_trsm32");
+        continue;
+      }
       int rc = atb(src, src, p, b, S, apart, st);
       if (rc) return rc;
       hipLaunchKernelGGL(k_chol, dim3(1), dim3(256), 0, st, S, b, L);
@@ -835,8 +933,11 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
   // subspace converges at the same rate without the Rayleigh–Ritz step, and a
   // 32×32 Jacobi on an unconverged projection costs many sweeps (11, 5, 3 …
   // on the bench data) plus a host read of the residuals.  Rayleigh–Ritz and
-  // the convergence test start at iteration PLAIN + 1.
-  constexpr int PLAIN = 3;
+  // the convergence test start at iteration PLAIN + 1.  The subspace after
+  // iteration i is span(Cⁱ V₀) whatever rotations happen in between, so the
+  // spectra that converge at iteration 5 (the bench data, p = 2048, k = 20)
+  // need one Rayleigh–Ritz step at PLAIN = 4 instead of two at 3.
+  constexpr int PLAIN = 4;
   int it = 0;
   bool converged = false;
   for (it = 1; it <= max_iter; ++it) {

@@ -342,6 +342,18 @@ def rowsq_residual(x: torch.Tensor, xhat: torch.Tensor) -> torch.Tensor:
     return q
 
 
+_SIDE: dict = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    """One auxiliary stream per device for small D2H reads that must not wait
+    for work queued after them on the launch stream."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=key)
+    return _SIDE[key]
+
+
 def inv_evals(evals: torch.Tensor, rcond=1e-15) -> torch.Tensor:
     """Diagonal of pinv(cov(T)) for T = centred scores on the eigenbasis:
     cov(T) = diag(λ) (utils/SIMCA.py:69 with np.linalg.pinv's rcond=1e-15 cutoff)."""
@@ -381,13 +393,27 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
     C, mean64 = cov_from_gram([(1.0, G[0], cs[0])], shift32, n_total)
     del G
     evals, evecs, theta, iters = eig_topk(C, k, theta_mode)
-    # the host scalars of the eigensolve are read BEFORE the fit-set scoring is
-    # launched, so the limits (host SciPy) overlap that kernel
-    host = torch.cat([evals, theta]).cpu().numpy()
+    # The host needs λ and θ for the limits (SciPy), the device needs 1/λ for
+    # the fit-set scoring.  The scalars go to pinned memory on a side stream
+    # that waits only for the eigensolve; 1/λ and the scoring are queued on the
+    # launch stream first, so the GPU never idles while the host issues the
+    # small ops or waits for the copy, and the limits overlap the scoring.
+    inv = inv_evals(evals)
+    host_buf = torch.empty(k + 3, dtype=torch.float64, pin_memory=True)
+    eig_done = torch.cuda.Event()
+    eig_done.record()
+    side = _side_stream(X.device)
+    with torch.cuda.stream(side):
+        side.wait_event(eig_done)
+        host_buf[:k].copy_(evals, non_blocking=True)
+        host_buf[k:].copy_(theta, non_blocking=True)
+        copied = torch.cuda.Event()
+        copied.record(side)
+    sc = score(X, rows, n, evecs, mean64, inv, want_T=want_T, want_stats=True)
+    copied.synchronize()
+    host = host_buf.numpy().copy()
     ev_h = host[:k]
     th = tuple(float(v) for v in host[k:k + 3])
-    inv = inv_evals(evals)
-    sc = score(X, rows, n, evecs, mean64, inv, want_T=want_T, want_stats=True)
     stats = sc["stats"]
     if allreduce is not None:
         allreduce([stats])  # stream-ordered: no host wait
