@@ -84,6 +84,121 @@ __global__ __launch_bounds__(256) void k_snv_savgol(const float* __restrict__ X,
   }
 }
 
+// Fast path (p % 4 == 0, p ≤ 4096, window ∈ {none, 5, 15}: the drivers'
+// filters): one wave per row, four rows per workgroup.  Each lane holds the
+// float4 pieces at columns 256k + 4·lane (coalesced 1-KiB wave loads and
+// stores); the row moments are wave reductions (no LDS, no block barrier);
+// for Savitzky–Golay the SNV row goes to a wave-private LDS row and each lane
+// forms its four outputs from a (W + 3)-sample window with the interior taps
+// in registers.  Same arithmetic as k_snv_savgol: fp64 moments rounded to
+// float32, the f32 SNV division, fp64 filter sums rounded to float32.
+constexpr int PREP_SEGS_MAX = 16;  // p ≤ 4096 (the register tile holds p / 256 float4 per lane)
+template <int W, int PREP_MAXSEG>
+__global__ __launch_bounds__(256) void k_snv_sg4(const float* __restrict__ X, int64_t ldx, int64_t m, int p, int snv,
+                                                 const double* __restrict__ taps, float* __restrict__ out,
+                                                 int64_t ldo) {
+  extern __shared__ float srow4[];  // [4][p] (W > 0)
+  constexpr int H = W / 2;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  const bool valid = r < m;
+  const int nseg = (p + 255) / 256;
+  const float* xr = X + (valid ? r : 0) * ldx;
+  f32x4 x[PREP_MAXSEG];
+#pragma unroll
+  for (int k = 0; k < PREP_MAXSEG; ++k) {
+    const int c0 = 256 * k + 4 * lane;
+    x[k] = (k < nseg && c0 < p) ? *reinterpret_cast<const f32x4*>(xr + c0) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (snv) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < PREP_MAXSEG; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += (double)x[k][e];
+    const double mean = wave_sum_f64(s) / p;
+    double ss = 0.0;
+#pragma unroll
+    for (int k = 0; k < PREP_MAXSEG; ++k) {
+      const int c0 = 256 * k + 4 * lane;
+      if (k < nseg && c0 < p)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const double d = (double)x[k][e] - mean;
+          ss += d * d;
+        }
+    }
+    const float meanf = (float)mean;
+    const float sdf = (float)sqrt(wave_sum_f64(ss) / p);
+    const float den = sdf + 1e-8f;
+#pragma unroll
+    for (int k = 0; k < PREP_MAXSEG; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[k][e] = (x[k][e] - meanf) / den;
+  }
+  float* orow = out + (valid ? r : 0) * ldo;
+  if constexpr (W == 0) {
+    if (valid)
+#pragma unroll
+      for (int k = 0; k < PREP_MAXSEG; ++k) {
+        const int c0 = 256 * k + 4 * lane;
+        if (k < nseg && c0 < p) *reinterpret_cast<f32x4*>(orow + c0) = x[k];
+      }
+    return;
+  } else {
+    float* row = srow4 + (size_t)wave * p;
+#pragma unroll
+    for (int k = 0; k < PREP_MAXSEG; ++k) {
+      const int c0 = 256 * k + 4 * lane;
+      if (k < nseg && c0 < p) *reinterpret_cast<f32x4*>(row + c0) = x[k];
+    }
+    __syncthreads();
+    double ct[W];
+#pragma unroll
+    for (int t = 0; t < W; ++t) ct[t] = taps[t];  // interior taps (wave-uniform)
+    if (!valid) return;
+#pragma unroll
+    for (int k = 0; k < PREP_MAXSEG; ++k) {
+      const int j0 = 256 * k + 4 * lane;
+      if (!(k < nseg && j0 < p)) continue;
+      f32x4 o;
+      if (j0 - H >= 0 && j0 + 3 + H < p) {
+        double win[W + 3];
+#pragma unroll
+        for (int t = 0; t < W + 3; ++t) win[t] = (double)row[j0 - H + t];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          double acc = 0.0;
+#pragma unroll
+          for (int t = 0; t < W; ++t) acc += ct[t] * win[i + t];
+          o[i] = (float)acc;
+        }
+      } else {  // the first / last H outputs: the least-squares edge fits
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int j = j0 + i;
+          const double* c;
+          int start;
+          if (j < H) {
+            c = taps + W + j * W;
+            start = 0;
+          } else if (j >= p - H) {
+            c = taps + W + H * W + (j - (p - H)) * W;
+            start = p - W;
+          } else {
+            c = taps;
+            start = j - H;
+          }
+          double acc = 0.0;
+          for (int t = 0; t < W; ++t) acc += c[t] * (double)row[start + t];
+          o[i] = (float)acc;
+        }
+      }
+      *reinterpret_cast<f32x4*>(orow + j0) = o;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -106,6 +221,32 @@ int ocm_snv_savgol_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, int
     dtaps = w;
   }
   OCM_REQUIRE(m < (1LL << 31), "ocm_snv_savgol_f32: too many rows per call");
+  const bool fast = p % 4 == 0 && p <= 256 * PREP_SEGS_MAX && ldx % 4 == 0 && ldo % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(X) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
+                    (window == 0 || window == 5 || window == 15) && p >= window + 3;
+  if (fast) {
+    const dim3 g((unsigned)((m + 3) / 4));
+    const size_t lds = window > 0 ? (size_t)4 * p * sizeof(float) : 0;
+#define OCM_SG4(W_, S_) hipLaunchKernelGGL((k_snv_sg4<W_, S_>), g, dim3(256), lds, st, X, ldx, m, p, snv, dtaps, out, ldo)
+#define OCM_SG4_S(W_) \
+  if (p <= 1024)      \
+    OCM_SG4(W_, 4);   \
+  else if (p <= 2048) \
+    OCM_SG4(W_, 8);   \
+  else                \
+    OCM_SG4(W_, 16);
+    if (window == 0) {
+      OCM_SG4_S(0)
+    } else if (window == 5) {
+      OCM_SG4_S(5)
+    } else {
+      OCM_SG4_S(15)
+    }
+#undef OCM_SG4_S
+#undef OCM_SG4
+    OCM_CHECK_LAUNCH("k_snv_sg4");
+    return OCM_OK;
+  }
   hipLaunchKernelGGL(k_snv_savgol, dim3((unsigned)m), dim3(256), (size_t)p * sizeof(double), st, X, ldx, m, p, snv,
                      window, dtaps, out, ldo);
   OCM_CHECK_LAUNCH("k_snv_savgol");

@@ -53,13 +53,18 @@ def _snv_ref(x):
 @pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")
 @pytest.mark.parametrize("snv,setting", [(True, (5, 2, 1, 1.0)), (False, (15, 2, 1, 1.0)), (True, (15, 2, 1, 1.0)),
                                          (True, None), (False, (11, 4, 3, 2.0))])
-def test_snv_savgol_device(snv, setting):
+@pytest.mark.parametrize("p", [517, 2048, 1028, 36])
+def test_snv_savgol_device(snv, setting, p):
+    """p = 517: the general one-workgroup-per-row kernel; p % 4 == 0 with the
+    drivers' filters (none, w = 5, w = 15): the wave-per-row kernel, with a
+    partial last 256-column segment (1028), a tiny row (36) and a partial last
+    group of four rows (301 rows)."""
     import torch
     from ocm import preprocess
 
     rng = np.random.default_rng(3)
-    wl = np.linspace(0, 1, 517)
-    x = (1.0 + 0.4 * wl + 0.3 * np.sin(9 * wl) + 0.02 * rng.standard_normal((301, 517))).astype(np.float32)
+    wl = np.linspace(0, 1, p)
+    x = (1.0 + 0.4 * wl + 0.3 * np.sin(9 * wl) + 0.02 * rng.standard_normal((301, p))).astype(np.float32)
     ref = _snv_ref(x) if snv else x
     if setting is not None:
         w, po, d, delta = setting
