@@ -401,7 +401,7 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
     inv = inv_evals(evals)
     host_buf = torch.empty(k + 3, dtype=torch.float64, pin_memory=True)
     eig_done = torch.cuda.Event()
-    eig_done.record()
+    eig_done.record(torch.cuda.current_stream(X.device))
     side = _side_stream(X.device)
     with torch.cuda.stream(side):
         side.wait_event(eig_done)
