@@ -1,0 +1,101 @@
+"""The headline configuration itself (BASELINE.json): SIMCA fit
++ predict on 1M × 2048 fp32 spectra in HBM, k = 20, alt / Fdist / jm — the
+exact bench workload (bench.synth_device) through the drop-in ``utils.SIMCA``.
+
+The oracle cannot run at this size in seconds, so the checks are identities
+that hold for an exact PCA at any size (utils/SIMCA.py:62-99), plus a second,
+independent Gram arithmetic:
+
+* Σ_i T²_i = k·(n − 1): T² = Σ_c t_ic²/λ_c and Σ_i t_ic² = (n − 1)·λ_c;
+* Σ_i Q_i = (n − 1)·θ1: the residual sum of squares is the tail of the
+  spectrum (θ1 from the deflated trace, Q from the explicit residuals);
+* the scores are centred (Σ_i t_ic ≈ 0) and the loadings orthonormal;
+* the fused decisions equal dred < D_lim recomputed on the host from the
+  returned T² and Q (outside the 1e-4 decision band);
+* the eigenvalues, θ1..θ3 and both limits of the default i8×3 Gram agree with
+  the exact bf16×3-split Gram (a different decomposition, different MFMA
+  units) to rtol 1e-6 / 1e-5.
+"""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+N, P, K = 1_000_000, 2048, 20
+
+
+@pytest.fixture(scope="module")
+def fitted():
+    import torch
+
+    from bench import synth_device
+    from ocm import engine
+    from utils import SIMCA
+
+    dev = torch.device("cuda", 0)
+    X = synth_device(N, P, K, seed=4321, device=dev)
+    y = torch.zeros(N, dtype=torch.int64, device=dev)
+    engine.set_gram_mode("i8x3")
+    est = SIMCA(n_components=K, model_class=0, type="alt", t2lim="Fdist", qlim="jm", verbose=False).fit(X, y)
+    pred = est.predict(X)
+    yield X, y, est, pred
+    engine.set_gram_mode("i8x3")
+
+
+def test_score_identities(fitted):
+    import torch
+
+    X, _, est, _ = fitted
+    fit = est._fits[0]
+    n, k = fit.n, fit.k
+    assert (n, k) == (N, K)
+    T2 = fit.T2.to(torch.float64)
+    Q = fit.Q.to(torch.float64)
+    np.testing.assert_allclose(float(T2.sum()), k * (n - 1), rtol=2e-6)
+    np.testing.assert_allclose(float(Q.sum()), (n - 1) * fit.thetas[0], rtol=1e-5)
+    T = fit.T.to(torch.float64)
+    lam = fit.evals.to(torch.float64)
+    # centred scores: |Σ_i t_ic| far below the √(n·λ_c) scale of the column
+    assert float((T.sum(0).abs() / torch.sqrt(n * lam)).max()) < 1e-4
+    np.testing.assert_allclose((T * T).sum(0).cpu().numpy() / (n - 1), lam.cpu().numpy(), rtol=1e-5)
+    P64 = fit.P64
+    eye = P64 @ P64.T
+    assert float((eye - torch.eye(k, dtype=eye.dtype, device=eye.device)).abs().max()) < 1e-12
+
+
+def test_fused_decisions_match_host_rule(fitted):
+    import torch
+
+    X, _, est, pred = fitted
+    m = est._model[0]
+    fit = est._fits[0]
+    # predict(X) scored the same rows: T², Q of the fit pass (the same kernel, the same model)
+    t = fit.T2.to(torch.float64) / m["T2_limit"]
+    q = fit.Q.to(torch.float64) / m["Q_limit"]
+    d = torch.sqrt(t * t + q * q)
+    dl = m["D_limit"]
+    host = (d < dl).cpu().numpy()
+    got = np.asarray(pred.cpu().numpy() if hasattr(pred, "cpu") else pred).reshape(-1)
+    clear = (torch.abs(d - dl) > 1e-4 * dl).cpu().numpy()
+    assert clear.mean() > 0.99
+    np.testing.assert_array_equal(got[clear].astype(bool), host[clear])
+
+
+def test_i8x3_gram_vs_bf16x3_gram(fitted):
+    from ocm import engine
+    from utils import SIMCA
+
+    X, y, est, _ = fitted
+    a = est._fits[0]
+    engine.set_gram_mode("bf16x3")
+    try:
+        ref = SIMCA(n_components=K, model_class=0, type="alt", t2lim="Fdist", qlim="jm", verbose=False).fit(X, y)
+    finally:
+        engine.set_gram_mode("i8x3")
+    b = ref._fits[0]
+    np.testing.assert_allclose(a.evals.cpu().numpy(), b.evals.cpu().numpy(), rtol=1e-6)
+    np.testing.assert_allclose(a.thetas, b.thetas, rtol=1e-5)
+    np.testing.assert_allclose([est._model[0]["T2_limit"], est._model[0]["Q_limit"]],
+                               [ref._model[0]["T2_limit"], ref._model[0]["Q_limit"]], rtol=1e-5)
