@@ -147,6 +147,9 @@ __global__ __launch_bounds__(256) void k_snv_sg4(const float* __restrict__ X, in
     return;
   } else {
     float* row = srow4 + (size_t)wave * p;
+    // all taps (interior + both edge tables) once per workgroup, after the rows
+    double* stp = reinterpret_cast<double*>(srow4 + (size_t)4 * p + ((4 * p) & 1));
+    for (int i = threadIdx.x; i < W + 2 * H * W; i += 256) stp[i] = taps[i];
 #pragma unroll
     for (int k = 0; k < PREP_MAXSEG; ++k) {
       const int c0 = 256 * k + 4 * lane;
@@ -180,16 +183,17 @@ __global__ __launch_bounds__(256) void k_snv_sg4(const float* __restrict__ X, in
           const double* c;
           int start;
           if (j < H) {
-            c = taps + W + j * W;
+            c = stp + W + j * W;
             start = 0;
           } else if (j >= p - H) {
-            c = taps + W + H * W + (j - (p - H)) * W;
+            c = stp + W + H * W + (j - (p - H)) * W;
             start = p - W;
           } else {
-            c = taps;
+            c = stp;
             start = j - H;
           }
           double acc = 0.0;
+#pragma unroll
           for (int t = 0; t < W; ++t) acc += c[t] * (double)row[start + t];
           o[i] = (float)acc;
         }
@@ -226,7 +230,9 @@ int ocm_snv_savgol_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, int
                     (window == 0 || window == 5 || window == 15) && p >= window + 3;
   if (fast) {
     const dim3 g((unsigned)((m + 3) / 4));
-    const size_t lds = window > 0 ? (size_t)4 * p * sizeof(float) : 0;
+    const size_t lds = window > 0 ? (size_t)(4 * p + 2) * sizeof(float) +
+                                        (size_t)(window + 2 * (window / 2) * window) * sizeof(double)
+                                  : 0;
 #define OCM_SG4(W_, S_) hipLaunchKernelGGL((k_snv_sg4<W_, S_>), g, dim3(256), lds, st, X, ldx, m, p, snv, dtaps, out, ldo)
 #define OCM_SG4_S(W_) \
   if (p <= 1024)      \
