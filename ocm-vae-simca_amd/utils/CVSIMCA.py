@@ -145,6 +145,8 @@ def _fold_predictions(est, X_test, y_test):
         pred = est.predict(X_test)
     except TypeError:  # estimators whose predict needs the labels
         pred = est.predict(X_test, y_test)
+    if hasattr(pred, "detach"):  # the drop-in returns device tensors for device inputs
+        pred = pred.detach().cpu().numpy()
     return np.ravel(np.asarray(pred))
 
 

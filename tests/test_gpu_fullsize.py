@@ -99,3 +99,48 @@ def test_i8x3_gram_vs_bf16x3_gram(fitted):
     np.testing.assert_allclose(a.thetas, b.thetas, rtol=1e-5)
     np.testing.assert_allclose([est._model[0]["T2_limit"], est._model[0]["Q_limit"]],
                                [ref._model[0]["T2_limit"], ref._model[0]["Q_limit"]], rtol=1e-5)
+
+
+def test_c3_full_size_fold_engine_vs_refit_loop():
+    """C3 at its full size (1M × 2048, 10 % other-class rows with an extra
+    band, ClasswiseKFoldWithExternalVal(10), LV 20, alt/Fdist/jm): the fold
+    engine (one pass of per-fold i8×3 Grams, fp64 downdating, device counts)
+    against the generic refit loop of the reference's control flow
+    (utils/CVSIMCA.py:145-222: a fresh drop-in SIMCA fit + predict per fold on
+    the GPU).  Pooled predictions may differ only on the decision boundary."""
+    import contextlib
+    import io
+
+    import torch
+
+    import utils.CVSIMCA as CVmod
+    from bench import synth_device
+    from utils import SIMCA, ClasswiseKFoldWithExternalVal, cross_validate_simca_grid
+
+    dev = torch.device("cuda", 0)
+    n_other = N // 10
+    y = np.concatenate([np.zeros(N - n_other, np.int64), np.ones(n_other, np.int64)])
+    X = synth_device(N, P, K, 4321, dev)
+    wl = torch.linspace(0, 1, P, device=dev)
+    X[N - n_other:] += 3.0 * torch.exp(-0.5 * ((wl - 0.5) / 0.03) ** 2)
+
+    def run(fast):
+        cv = ClasswiseKFoldWithExternalVal(n_splits=10, cls_label=0)
+        saved = CVmod._fast_grid
+        if not fast:
+            CVmod._fast_grid = lambda *a, **k: (None, None)
+        try:
+            with contextlib.redirect_stdout(io.StringIO()):
+                return cross_validate_simca_grid(SIMCA(verbose=False, model_class=0), X, y, cv, LV_min=K, LV_max=K,
+                                                 param_grid={}, print_summary=False, store_predictions=True)
+        finally:
+            CVmod._fast_grid = saved
+
+    fast, slow = run(True), run(False)
+    rf, rs = fast["results"][0], slow["results"][0]
+    assert rf["LV"] == rs["LV"] == K
+    np.testing.assert_allclose([rf["spec"], rf["sens"]], [rs["spec"], rs["sens"]], atol=1e-3)
+    pf = np.asarray(fast["by_combo"][0]["prediction"])
+    ps = np.asarray(slow["by_combo"][0]["prediction"])
+    assert pf.shape == ps.shape == (N,)
+    assert int((pf != ps).sum()) <= 20, int((pf != ps).sum())
