@@ -144,3 +144,17 @@ def test_fold_engine_gloo_world2_matches_single(golden_dir, tmp_path, grid, rest
     np.testing.assert_allclose(got["spec"], [r["spec"] for r in recs], atol=1e-9)
     np.testing.assert_allclose(got["sens"], [r["sens"] for r in recs], atol=1e-9)
     np.testing.assert_array_equal(got["pred"], np.stack([b["prediction"] for b in by]))
+
+
+def test_generic_loop_accepts_tensor_predictions():
+    """The drop-in's predict returns a (m, C) tensor for tensor inputs; the
+    generic CV loop (utils/CVSIMCA.py) must pool it like the reference's
+    NumPy arrays."""
+    from utils.CVSIMCA import _fold_predictions
+
+    class Est:
+        def predict(self, X):
+            return torch.ones((X.shape[0], 1), dtype=torch.float64)
+
+    got = _fold_predictions(Est(), torch.zeros((5, 3)), np.zeros(5))
+    assert isinstance(got, np.ndarray) and got.shape == (5,) and got.sum() == 5
