@@ -182,3 +182,49 @@ def test_errors_mirror_reference():
         SIMCA(n_components=[2, 3, 4], verbose=False).fit(X, y)
     with pytest.raises(UnboundLocalError):
         SIMCA(n_components=2, model_class=0, t2lim="nope", verbose=False).fit(X, y)
+
+
+def test_device_resident_full_api(golden_dir):
+    """Every public entry point of the drop-in with device tensors (the
+    reference only sees NumPy; the drop-in keeps device inputs on the device):
+    predict with y_true (metrics), transform, score, the _model keys and the
+    pca_model facade — against the same calls on NumPy inputs."""
+    import contextlib
+    import io
+
+    import torch
+
+    g = _load(golden_dir, "simca_multi.npz")
+    Xf, yf, Xt = g["X_fit"], g["y_fit"], g["X_test"]
+    yt = g["y_test"]
+    a = _est(g)[0].fit(torch.from_numpy(Xf).cuda(), torch.from_numpy(yf).cuda())
+    b = _est(g)[0].fit(Xf, yf)
+    Xd, yd = torch.from_numpy(Xt).cuda(), torch.from_numpy(yt).cuda()
+    with contextlib.redirect_stdout(io.StringIO()):
+        pa = a.predict(Xd, y_true=yd)
+        pb = b.predict(Xt, y_true=yt)
+    np.testing.assert_array_equal(pa.cpu().numpy(), pb)
+    for cls in b.model_class:
+        for key in ("TP", "TN", "FP", "FN"):
+            assert a.metrics[cls][key] == b.metrics[cls][key]
+    ta, tb = a.transform(Xd), b.transform(Xt)
+    for u, v in zip(ta, tb):
+        np.testing.assert_allclose(u.cpu().numpy() if hasattr(u, "cpu") else u, v, rtol=1e-6)
+    # the reference's score() raises on three classes (list model_class broadcast, score.npz)
+    with contextlib.redirect_stdout(io.StringIO()), pytest.raises(ValueError):
+        a.score(Xd, yd)
+    ga = _load(golden_dir, "simca_a.npz")
+    sa = _est(ga)[0].fit(torch.from_numpy(ga["X_fit"]).cuda(), torch.from_numpy(ga["y_fit"]).cuda())
+    sb = _est(ga)[0].fit(ga["X_fit"], ga["y_fit"])
+    with contextlib.redirect_stdout(io.StringIO()):
+        np.testing.assert_allclose(sa.score(torch.from_numpy(ga["X_test"]).cuda(), torch.from_numpy(ga["y_test"]).cuda()),
+                                   sb.score(ga["X_test"], ga["y_test"]), rtol=1e-12)
+    for cls in b.model_class:
+        ma, mb = a._model[cls], b._model[cls]
+        for key in ("T2_limit", "Q_limit", "D_limit", "n_samples", "n_components"):
+            np.testing.assert_allclose(ma[key], mb[key], rtol=1e-12)
+        for key in ("xmean", "P", "T", "T2", "Q", "invcovT"):
+            u = ma[key]
+            np.testing.assert_allclose(u.cpu().numpy() if hasattr(u, "cpu") else u, mb[key], rtol=1e-5, atol=1e-7)
+        Ta = ma["pca_model"].transform(Xd)
+        np.testing.assert_allclose(Ta.cpu().numpy(), mb["pca_model"].transform(Xt), rtol=1e-5, atol=1e-6)
