@@ -1114,17 +1114,39 @@ __global__ __launch_bounds__(256) void k_gram_fixup(const float* __restrict__ X,
 // wave-private LDS.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
-                                                   float* __restrict__ part) {
+                                                   int nwg, int nblocks, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) float scl[4][2 * 64];        // wave-private: row, column scales
   __shared__ __attribute__((aligned(16))) float runl[4][4][4][64][4];  // wave-private f32 running sums
 
   const int b = blockIdx.x;
   const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
   const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
-  const int chunk = wg / ntiles;
-  const int tile = wg - chunk * ntiles;
-  int ti, tj;
-  tile_coords(tile, nt, ti, tj);
+  const int chunk = wg / nwg;
+  // 64×64 blocks packed four per workgroup: the upper triangle of 128×128
+  // tiles has 4·ntiles − nt valid blocks (a diagonal tile's strictly-lower
+  // block is its mirror), so no wave idles on a diagonal tile.  Blocks are
+  // enumerated tile by tile in triangle order: diagonal tile (0,0) (0,1) (1,1),
+  // off-diagonal tiles (0,0) (0,1) (1,0) (1,1).
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int bi = (wg - chunk * nwg) * 4 + wave;
+  if (bi >= nblocks) return;  // no barrier in this kernel
+  int ti = 0, rem = bi;
+  while (rem >= 3 + 4 * (nt - 1 - ti)) {
+    rem -= 3 + 4 * (nt - 1 - ti);
+    ++ti;
+  }
+  int tj, wm, wn;
+  if (rem < 3) {
+    tj = ti;
+    wm = rem == 2;
+    wn = rem >= 1;
+  } else {
+    rem -= 3;
+    tj = ti + 1 + (rem >> 2);
+    wm = (rem & 3) >> 1;
+    wn = rem & 1;
+  }
+  const int tile = ti * nt - ti * (ti - 1) / 2 + (tj - ti);  // triangle index (the reduce's layout)
   const int I = ti * Q8T, J = tj * Q8T;
   int s = 0;
   while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
@@ -1137,10 +1159,7 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
   const size_t gbase = (size_t)chunk * (st.chunk_rows / Q8K);
 
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
   const int l31 = lane & 31, h = lane >> 5;
-  if (ti == tj && wm > wn) return;  // strictly-lower block of a diagonal tile; no barrier to keep
   const size_t gstride = (size_t)q.P8 * 32;
   const uint32_t span = (uint32_t)((size_t)nstage3 * gstride);
   const char* cbase = q.digits + gbase * gstride;
@@ -1568,11 +1587,13 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   }
   for (size_t t = 0; t < tabs.size(); ++t) {
     const int s0 = tab_s0[t];
-    const int64_t total = (cprefix[s0 + tabs[t].nseg] - cprefix[s0]) * ntiles;
+    const int nblocks = 4 * ntiles - nt, nwg = (nblocks + 3) / 4;
+    const int64_t total = (cprefix[s0 + tabs[t].nseg] - cprefix[s0]) * nwg;
     const Q8Plan q = plan_for(s0);
     float* pg = part + (size_t)cprefix[s0] * ntiles * Q8T * Q8T;
     ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
-    hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, pg);
+    hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, nwg,
+                       nblocks, pg);
     OCM_CHECK_LAUNCH("k_gram8d");
   }
   for (int s = 0; s < nseg; ++s) {
