@@ -134,7 +134,17 @@ class GraphedVAETrainer:
                 self._body()
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # With the gradient all-reduce in the graph the process group's watchdog
+        # thread polls the warm-up collectives' events; under the default
+        # (global) capture mode such a query from another thread during the
+        # capture fails with hipErrorStreamCaptureUnsupported and the watchdog
+        # aborts the process.  Drain the warm-up work first and capture in
+        # thread-local mode, which leaves other threads' HIP calls alone.
+        mode = "global"
+        if self.allreduce:
+            torch.cuda.synchronize()
+            mode = "thread_local"
+        with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.out = self._body()
         if not self.restore:
             return
