@@ -1346,6 +1346,204 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
       }
 }
 
+#ifdef OCM_G8_LDS
+// ---------------------------------------------------------------------------
+// k_gram8s (experiment, make exp only) — the i8×3 Gram with the workgroup's
+// two 128-column panels shared through LDS.  One workgroup per 128×128 tile,
+// four waves of 64×64; each 64-row phase (two 32-row stages) of both panels
+// (48 KiB) is copied once into a 3-slot LDS ring by LDS-DMA
+// (global_load_lds_dwordx4: one 1-KiB fragment per wave-instruction, 12 per
+// wave per phase + the block's row/column scales into a 4-slot scale ring),
+// three phases ahead.  Each wave reads its fragments with ds_read_b128 one
+// stage ahead of the MFMAs that use them, one read per two MFMAs; one counted
+// vmcnt wait + one raw barrier per phase, between the two stages.  The fragment
+// image is lane-linear with the halves of column r swapped when bit 3 of r is
+// set (applied on the DMA source and on the read): conflict-free reads.
+// Measured (r02_lds, 1M × 2048): parity equal to k_gram8d (3.6e-8 vs fp64),
+// 305 TF against k_gram8d's 393 in the same process pair — halving the
+// vector-memory bytes per MFMA does not pay for the per-phase barrier; kept
+// for the next round's LDS / tile-order work, never in libocm.
+// ---------------------------------------------------------------------------
+constexpr int G8S_FRAG = 1024;
+constexpr int G8S_OPS = 2 * 2 * 3 * 4 * G8S_FRAG;  // [stage][A|B][digit][32-col block] = 48 KiB
+constexpr int G8S_NSLOT = 3;
+constexpr int G8S_SCL = 4 * 512;                   // [wave][64 row scales | 64 column scales]
+constexpr int G8S_NSCL = 4;
+
+// LDS-DMA with a scalar 64-bit base and a 32-bit per-lane offset (saddr form):
+// no per-lane 64-bit addresses to keep live across the loop
+__device__ __forceinline__ void g8s_dma16(const void* sbase, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds)
+               : "memory");
+}
+__device__ __forceinline__ void g8s_dma4(const void* sbase, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds)
+               : "memory");
+}
+
+__global__ __launch_bounds__(256, 1) void k_gram8s(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
+                                                   float* __restrict__ part) {
+  __shared__ __attribute__((aligned(1024))) char lds[G8S_NSLOT * G8S_OPS + G8S_NSCL * G8S_SCL];
+
+  const int b = blockIdx.x;
+  const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
+  const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int chunk = wg / ntiles;
+  const int tile = wg - chunk * ntiles;
+  int ti, tj;
+  tile_coords(tile, nt, ti, tj);
+  const int I = ti * Q8T, J = tj * Q8T;
+  int s = 0;
+  while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
+  const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
+  const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
+  const int nb = (int)((r1 - r0 + Q8BLK - 1) / Q8BLK);
+  constexpr int PPB = Q8SPB / 2;  // phases per scale block
+  const int nph = nb * PPB;
+  const size_t gbase = (size_t)chunk * (st.chunk_rows / Q8K);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int l31 = lane & 31, h = lane >> 5;
+  const bool skip = (ti == tj && wm > wn);  // the mirror block of a diagonal tile: computed, not stored
+  const size_t gstride = (size_t)q.P8 * 32;
+
+  // DMA role: stage (wave >> 1) of a phase, operand (wave & 1): 3 digits × 4 column blocks
+  const int sg_dma = wave >> 1, op_dma = wave & 1;
+  const uint32_t srcoff = (uint32_t)(lane >> 1) * 32 + 16 * ((lane & 1) ^ ((lane >> 4) & 1));
+  const char* dma_base = q.digits + (gbase + sg_dma) * gstride + (size_t)(op_dma ? J : I) * 32;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds);
+  const float* scl_src = q.scale + (size_t)chunk * q.nblk * q.P8;
+  const uint32_t scloff = (uint32_t)lane * 4;
+  const int srow0 = I + wm * 64, scol0 = J + wn * 64;
+
+  auto issue = [&](int ph) __attribute__((always_inline)) {
+    const int phc = min(ph, nph - 1);
+    const uint32_t sb = lds0 + (uint32_t)((ph % G8S_NSLOT) * G8S_OPS);
+    const size_t poff = (size_t)phc * 2 * gstride;
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg)
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+        g8s_dma16(dma_base + dg * q.plane + poff + x * G8S_FRAG, srcoff,
+                  sb + (((sg_dma * 2 + op_dma) * 3 + dg) * 4 + x) * G8S_FRAG);
+    const size_t so = (size_t)(phc / PPB) * q.P8;
+    const uint32_t scb = lds0 + (uint32_t)(G8S_NSLOT * G8S_OPS + (ph % G8S_NSCL) * G8S_SCL + wave * 512);
+    g8s_dma4(scl_src + so + srow0, scloff, scb);
+    g8s_dma4(scl_src + so + scol0, scloff, scb + 256);
+  };
+  const int rdoff = 16 * (2 * l31 + (h ^ ((l31 >> 3) & 1)));
+  auto frag = [&](int slot, int sg, int op, int dg, int xb) __attribute__((always_inline)) -> i32x4 {
+    return *reinterpret_cast<const i32x4*>(lds + slot * G8S_OPS + (((sg * 2 + op) * 3 + dg) * 4 + xb) * G8S_FRAG +
+                                           rdoff);
+  };
+
+  i32x16 acc1[2][2], acc2[2][2], acc3[2][2];
+  float run[2][2][16];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      acc1[a][c] = i32x16{};
+      acc2[a][c] = i32x16{};
+      acc3[a][c] = i32x16{};
+#pragma unroll
+      for (int r = 0; r < 16; ++r) run[a][c][r] = 0.f;
+    }
+  // one stage: 24 MFMAs on (CA, CB); the 12 fragments of the next stage read
+  // from LDS into (NA, NB), one per two MFMAs
+  auto half = [&](i32x4 (&CA)[2][3], i32x4 (&CB)[2][3], i32x4 (&NA)[2][3], i32x4 (&NB)[2][3], int rslot,
+                  int rsg) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const int x = i / 6, r = i % 6, dg = r / 2;
+      if (r & 1)
+        NB[x][dg] = frag(rslot, rsg, 1, dg, 2 * wn + x);
+      else
+        NA[x][dg] = frag(rslot, rsg, 0, dg, 2 * wm + x);
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int j = 2 * i + jj, blk = j / 6, kind = j % 6, a = blk >> 1, c = blk & 1;
+        if (kind == 0) acc1[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(CA[a][0], CB[c][0], acc1[a][c], 0, 0, 0);
+        if (kind == 1) acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(CA[a][0], CB[c][1], acc2[a][c], 0, 0, 0);
+        if (kind == 2) acc2[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(CA[a][1], CB[c][0], acc2[a][c], 0, 0, 0);
+        if (kind == 3) acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(CA[a][0], CB[c][2], acc3[a][c], 0, 0, 0);
+        if (kind == 4) acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(CA[a][2], CB[c][0], acc3[a][c], 0, 0, 0);
+        if (kind == 5) acc3[a][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(CA[a][1], CB[c][1], acc3[a][c], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  i32x4 R0A[2][3], R0B[2][3], R1A[2][3], R1B[2][3];
+  issue(0);
+  issue(1);
+  issue(2);
+  asm volatile("s_waitcnt vmcnt(28)\n\ts_barrier" ::: "memory");  // phase 0 landed for every wave
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg) {
+      R0A[x][dg] = frag(0, 0, 0, dg, 2 * wm + x);
+      R0B[x][dg] = frag(0, 0, 1, dg, 2 * wn + x);
+    }
+  for (int ph = 0; ph < nph; ++ph) {
+    half(R0A, R0B, R1A, R1B, ph % G8S_NSLOT, 1);
+    // this wave's DMAs of phase ph+1 are done (those of ph+2 may fly); every
+    // wave's reads of slot ph%3 are done: it takes phase ph+3
+    asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    issue(ph + 3);
+    half(R1A, R1B, R0A, R0B, (ph + 1) % G8S_NSLOT, 0);
+    if (ph % PPB == PPB - 1) {
+      constexpr float w2 = 1.f / 254.f, w3 = 1.f / (254.f * 254.f);
+      const float* scl = reinterpret_cast<const float*>(lds + G8S_NSLOT * G8S_OPS + (ph % G8S_NSCL) * G8S_SCL +
+                                                        wave * 512);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float sj = scl[64 + c * 32 + l31];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 si = *reinterpret_cast<const f32x4*>(&scl[a * 32 + 8 * g + 4 * h]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int r = 4 * g + e;
+              const float v = fmaf((float)acc3[a][c][r], w3, fmaf((float)acc2[a][c][r], w2, (float)acc1[a][c][r]));
+              run[a][c][r] = fmaf(v, si[e] * sj, run[a][c][r]);
+            }
+          }
+          acc1[a][c] = i32x16{};
+          acc2[a][c] = i32x16{};
+          acc3[a][c] = i32x16{};
+        }
+      }
+    }
+  }
+  // no LDS-DMA may still be landing when the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (skip) return;
+  float* out = part + ((size_t)chunk * ntiles + tile) * (Q8T * Q8T);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int col = wn * 64 + c * 32 + l31;
+        out[row * Q8T + col] = run[a][c][r];
+      }
+}
+#endif  // OCM_G8_LDS
+
 int gram_small(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int32_t p, const float* shift,
                const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out, hipStream_t st) {
   // chunks never straddle a segment: span = (lo, hi) row range per chunk
@@ -1592,9 +1790,16 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     const Q8Plan q = plan_for(s0);
     float* pg = part + (size_t)cprefix[s0] * ntiles * Q8T * Q8T;
     ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
+#ifdef OCM_G8_LDS
+    (void)total;
+    const int64_t total_s = (cprefix[s0 + tabs[t].nseg] - cprefix[s0]) * ntiles;
+    hipLaunchKernelGGL(k_gram8s, dim3((unsigned)total_s), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total_s, pg);
+    OCM_CHECK_LAUNCH("k_gram8s");
+#else
     hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, nwg,
                        nblocks, pg);
     OCM_CHECK_LAUNCH("k_gram8d");
+#endif
   }
   for (int s = 0; s < nseg; ++s) {
     double* Gs = G_out + (size_t)s * p * p;
