@@ -1125,26 +1125,33 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
   // 64×64 blocks packed four per workgroup: the upper triangle of 128×128
   // tiles has 4·ntiles − nt valid blocks (a diagonal tile's strictly-lower
   // block is its mirror), so no wave idles on a diagonal tile.  Blocks are
-  // enumerated tile by tile in triangle order: diagonal tile (0,0) (0,1) (1,1),
-  // off-diagonal tiles (0,0) (0,1) (1,0) (1,1).
+  // enumerated tile by tile: diagonal tile (0,0) (0,1) (1,1), off-diagonal
+  // tiles (0,0) (0,1) (1,0) (1,1).
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int bi = (wg - chunk * nwg) * 4 + wave;
   if (bi >= nblocks) return;  // no barrier in this kernel
-  int ti = 0, rem = bi;
-  while (rem >= 3 + 4 * (nt - 1 - ti)) {
-    rem -= 3 + 4 * (nt - 1 - ti);
-    ++ti;
-  }
-  int tj, wm, wn;
-  if (rem < 3) {
-    tj = ti;
-    wm = rem == 2;
-    wn = rem >= 1;
-  } else {
-    rem -= 3;
-    tj = ti + 1 + (rem >> 2);
-    wm = (rem & 3) >> 1;
-    wn = rem & 1;
+  // Tiles are visited in bands of 4 tile rows × 8 tile columns (upper
+  // triangle), so the ≈ 32 tiles an XCD runs at once share 12 panels rather
+  // than one row panel and 32 column panels: 15 % fewer bytes fetched beyond
+  // L2 and 1.5–2 % faster than the row-major triangle order (r02_band).  The
+  // walk is wave-uniform scalar work, ≤ ntiles steps at kernel start.
+  int ti = -1, tj = 0, wm = 0, wn = 0;
+  {
+    int rem = bi;
+    for (int u = 0; u < nt && ti < 0; u += 4)
+      for (int v = u; v < nt && ti < 0; v += 8)
+        for (int a = u; a < min(nt, u + 4) && ti < 0; ++a)
+          for (int c = max(v, a); c < min(nt, v + 8); ++c) {
+            const int nbk = (a == c) ? 3 : 4;
+            if (rem < nbk) {
+              ti = a;
+              tj = c;
+              wm = (a == c) ? (rem == 2) : (rem >> 1);
+              wn = (a == c) ? (rem >= 1) : (rem & 1);
+              break;
+            }
+            rem -= nbk;
+          }
   }
   const int tile = ti * nt - ti * (ti - 1) / 2 + (tj - ti);  // triangle index (the reduce's layout)
   const int I = ti * Q8T, J = tj * Q8T;
