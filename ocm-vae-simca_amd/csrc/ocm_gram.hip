@@ -1113,6 +1113,15 @@ __global__ __launch_bounds__(256) void k_gram_fixup(const float* __restrict__ X,
 // One wave per SIMD, 64×64 per wave; the scale-block flush goes through
 // wave-private LDS.
 // ---------------------------------------------------------------------------
+// band shape of the Gram's tile order (tile rows × tile columns); make exp
+// builds override it for A/B
+#ifndef OCM_G8_BAND_R
+#define OCM_G8_BAND_R 4
+#endif
+#ifndef OCM_G8_BAND_C
+#define OCM_G8_BAND_C 8
+#endif
+constexpr int G8_BAND_R = OCM_G8_BAND_R, G8_BAND_C = OCM_G8_BAND_C;
 __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
                                                    int nwg, int nblocks, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) float scl[4][2 * 64];        // wave-private: row, column scales
@@ -1138,10 +1147,10 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
   int ti = -1, tj = 0, wm = 0, wn = 0;
   {
     int rem = bi;
-    for (int u = 0; u < nt && ti < 0; u += 4)
-      for (int v = u; v < nt && ti < 0; v += 8)
-        for (int a = u; a < min(nt, u + 4) && ti < 0; ++a)
-          for (int c = max(v, a); c < min(nt, v + 8); ++c) {
+    for (int u = 0; u < nt && ti < 0; u += G8_BAND_R)
+      for (int v = u; v < nt && ti < 0; v += G8_BAND_C)
+        for (int a = u; a < min(nt, u + G8_BAND_R) && ti < 0; ++a)
+          for (int c = max(v, a); c < min(nt, v + G8_BAND_C); ++c) {
             const int nbk = (a == c) ? 3 : 4;
             if (rem < nbk) {
               ti = a;
