@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCM_ABI_VERSION 2
+#define OCM_ABI_VERSION 3
 
 #define OCM_OK 0
 #define OCM_ERR_ARG (-1)         /* invalid argument (maps to ValueError) */
@@ -140,10 +140,40 @@ int ocm_cov_from_gram(ocm_ctx* ctx, const double* const* G_list, const double* c
  * evals_out [dev] k (descending), evecs_out [dev] k×p rows = loadings with the
  * sklearn svd_flip sign (max-|entry| positive, extmath.py:895-953),
  * theta_out [dev] 3, iters_out [host, nullable].  Returns OCM_ERR_NOCONV if
- * the residual tolerance was not met within max_iter (outputs still valid). */
+ * the residual tolerance was not met within max_iter (outputs still valid).
+ * Any 1 ≤ k ≤ p: the block is k plus oversampling; beyond 64 columns the
+ * block's b×b Cholesky and Rayleigh–Ritz problems are solved on the host in
+ * fp64 (the p×b products stay on the GPU). */
 int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
                  int32_t theta_mode, double* evals_out, double* evecs_out, double* theta_out, int32_t* iters_out,
                  void* stream);
+
+/* Same, with the θ3 trace work split into `theta3_nslices` slices of which
+ * this call computes slice `theta3_slice` only: theta_out[2] is then that
+ * slice's partial sum and the caller sums the partials of every slice (the
+ * ranks of a row-sharded fit each take one slice and all-reduce θ3;
+ * SURVEY.md §8e).  theta_out[0..1] and all other outputs are complete on every
+ * slice.  ocm_eig_topk is the call with (0, 1). */
+int ocm_eig_topk_ex(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
+                    int32_t theta_mode, int32_t theta3_slice, int32_t theta3_nslices, double* evals_out,
+                    double* evecs_out, double* theta_out, int32_t* iters_out, void* stream);
+
+/* ---- row-sharded fit: one all-reduce of packed moments ----
+ * ocm_gram_pack turns a rank's shifted Gram (G, colsum about `shift`, n rows,
+ * as ocm_gram_f32 returns them) into its moments about zero, packed
+ *   packed_out[0 .. p(p+1)/2)      upper triangle (row-major) of
+ *                                  G + s·csᵀ + cs·sᵀ + n·s·sᵀ  (Σ x xᵀ)
+ *   packed_out[p(p+1)/2 .. +p)     cs + n·s                    (Σ x)
+ *   packed_out[p(p+1)/2 + p]       n
+ * so that a plain sum over ranks (one RCCL all-reduce of p(p+1)/2 + p + 1
+ * doubles) gives the moments of all rows whatever shift each rank used.
+ * ocm_cov_from_packed then forms μ = Σx/n and C = (Σ x xᵀ − n·μμᵀ)/(n−1)
+ * (np.cov / sklearn explained_variance_, utils/SIMCA.py:64-66 →
+ * _pca.py:584) with n read from the buffer on the device.  [dev] all. */
+int ocm_gram_pack(ocm_ctx* ctx, const double* G, const double* colsum, const float* shift, int64_t n, int32_t p,
+                  double* packed_out, void* stream);
+int ocm_cov_from_packed(ocm_ctx* ctx, const double* packed, int32_t p, double* C_out, double* mean_out,
+                        void* stream);
 
 /* Symmetric pseudo-inverse (eigenvalue cutoff rcond·λmax) of a small d×d
  * fp64 matrix, d ≤ 64 (np.linalg.pinv(np.cov(...)) at utils/SIMCA.py:69,
@@ -191,6 +221,15 @@ int ocm_decide(ocm_ctx* ctx, const double* T2, const float* Q, int64_t m, const 
  * row).  x [dev] m×p float32 (ldx), xhat [dev] (ldxh), q_out [dev] m floats. */
 int ocm_rowsq_residual_f32(ocm_ctx* ctx, const float* x, int64_t ldx, const float* xhat, int64_t ldxh, int64_t m,
                            int32_t p, float* q_out, void* stream);
+
+/* q_i = Σ_j (s(x_ij) − s(xhat_ij))², s(v) = clamp((v − min_j x_ij)/(max_j x_ij − min_j x_ij + eps), 0, 1):
+ * the per-sample min–max scaled reconstruction residual that
+ * utils/final_vaesimca.py:417-423 (calibration Q threshold) and :484-490
+ * (test Q) use for BCE-trained networks (eps = 1e-8 there).  Scaling in
+ * float32 in the reference's order, f64 sum.  x, xhat [dev] m×p float32
+ * (ldx, ldxh ≥ p), q_out [dev] m floats. */
+int ocm_rowsq_minmax_f32(ocm_ctx* ctx, const float* x, int64_t ldx, const float* xhat, int64_t ldxh, int64_t m,
+                         int32_t p, float eps, float* q_out, void* stream);
 
 /* b[i] = (float)a[i] — loadings / mean handed to the float32 scoring kernel. */
 int ocm_cast_f64_f32(ocm_ctx* ctx, const double* a, int64_t n, float* b, void* stream);

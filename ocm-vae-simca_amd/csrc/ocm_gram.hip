@@ -720,16 +720,20 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ 
   f32x4 v[16];
   const int64_t rblk = r0 + (int64_t)b * Q8BLK;  // first row of the block
   if (!GATHER && vec && (int64_t)Q8BLK * ldx * 4 < (1LL << 31)) {
-    // contiguous rows: one buffer descriptor over the block's valid rows, the
-    // row step in the scalar offset (one address VGPR instead of 16 64-bit
-    // row pointers); rows past r1 lie outside the descriptor and read as 0
+    // contiguous rows: one buffer descriptor over the block's valid rows (one
+    // address VGPR instead of 16 64-bit row pointers).  The whole byte offset,
+    // row step included, goes in the VECTOR offset: only voffset is checked
+    // against the descriptor's size (the scalar offset is not), so rows past
+    // r1 — a block whose valid row count is not a multiple of 16 — read as 0
+    // instead of touching memory past the end of X.
     const int64_t nvalid = max((int64_t)0, min(r1 - rblk, (int64_t)Q8BLK));
     const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(X + rblk * ldx), 0, (uint32_t)(nvalid * ldx * 4), 0x00020000);
     const int voff = (int)((16 * rs * ldx + c0) * 4);
+    const int rstep = (int)(ldx * 4);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_x, voff, (int)(j * ldx * 4), 0));
+      const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_x, voff + j * rstep, 0, 0));
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[j][e] = (rb + j < r1) ? x[e] - sh[e] : 0.f;
     }

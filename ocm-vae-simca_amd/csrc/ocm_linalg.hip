@@ -15,8 +15,10 @@
 //   * p ≤ 64 (VAE latents, tiny spectra): Jacobi on C directly.
 #include <algorithm>
 #include <cmath>
+#include <limits>
 #include <vector>
 
+#include "ocm_hostla.h"
 #include "ocm_internal.h"
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -30,14 +32,18 @@ namespace {
 //         and E symmetric: the grid is the upper triangle of tiles
 //         (blockIdx.x linear), off-diagonal tiles weighted 2
 // MODE 2: rank update  D = E − A·B, part[2wg..] = {Σ diag D, Σ D²}
+// TA: A is given transposed (A(r, kk) = A[kk·lda + r]) — the b×b projections
+// VᵀW of tall p×b blocks when b > 64 (MODE 0 only).
+// tile0 (MODE 1): first upper-triangle tile of this launch (a rank's slice of
+// the trace GEMM when the θ3 work is split over GPUs).
 // ---------------------------------------------------------------------------
 constexpr int DT = 64, DBK = 16, DPAD = 16;
 
-template <int MODE>
+template <int MODE, bool TA = false>
 __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
                                                int64_t ldb, double* __restrict__ D, int64_t ldd, int M, int N, int K,
                                                int kper, const double* __restrict__ E, int64_t lde,
-                                               double* __restrict__ part) {
+                                               double* __restrict__ part, int tile0 = 0) {
   __shared__ double As[DBK][DT + DPAD];
   __shared__ double Bs[DBK][DT + DPAD];
   __shared__ double red[8];
@@ -47,7 +53,7 @@ __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int
   double wtile = 1.0;
   if (MODE == 1) {  // linear upper-triangle index -> (bx <= by)
     const int nt = (N + DT - 1) / DT;
-    int rem = blockIdx.x;
+    int rem = blockIdx.x + tile0;
     bx = 0;
     while (rem >= nt - bx) {
       rem -= nt - bx;
@@ -73,7 +79,12 @@ __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int r = m0 + arow, kk = k0 + akc + e;
-      ra[e] = (r < M && kk < ke) ? A[(int64_t)r * lda + kk] : 0.0;
+      if (TA) {  // 64 rows × 16 k from Aᵀ: lanes walk r (contiguous in A)
+        const int r2 = m0 + (tid & 63), kk2 = k0 + (tid >> 6) * 4 + e;
+        ra[e] = (r2 < M && kk2 < ke) ? A[(int64_t)kk2 * lda + r2] : 0.0;
+      } else {
+        ra[e] = (r < M && kk < ke) ? A[(int64_t)r * lda + kk] : 0.0;
+      }
       const int kr = k0 + bk, c = n0 + bcol + e;
       rb[e] = (kr < ke && c < N) ? B[(int64_t)kr * ldb + c] : 0.0;
     }
@@ -82,7 +93,10 @@ __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int
   for (int k0 = kb; k0 < ke; k0 += DBK) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      As[akc + e][arow] = ra[e];
+      if (TA)
+        As[(tid >> 6) * 4 + e][tid & 63] = ra[e];
+      else
+        As[akc + e][arow] = ra[e];
       Bs[bk][bcol + e] = rb[e];
     }
     __syncthreads();
@@ -838,17 +852,34 @@ int trsm_rows(const double* W, const double* L, int p, int b, double* V, hipStre
   return OCM_OK;
 }
 
-}  // namespace
+// ---- wide blocks (b > 64: n_components beyond one 64-wide block) ----------
+// The b×b steps of the iteration run on the host in fp64 (b ≤ p; the p×b
+// products stay on the GPU): Cholesky of the CholQR Gram, and the projected
+// eigenproblem of Rayleigh–Ritz by Householder tridiagonalisation + implicit
+// QL with Wilkinson shifts.
 
-extern "C" {
+// S = Aᵀ B (b×b) for tall p×b row-major A, B on the fp64-MFMA GEMM (split-K planes)
+int dgemm_ta(const double* A, const double* B, int p, int b, double* S, double* planes, size_t plane_cap,
+             hipStream_t st) {
+  const int tiles = ((b + DT - 1) / DT) * ((b + DT - 1) / DT);
+  int ksplit = std::max(1, std::min(16, 256 / tiles));
+  while (ksplit > 1 && (size_t)ksplit * b * b > plane_cap) --ksplit;
+  int kper = (p + ksplit - 1) / ksplit;
+  kper = (kper + DBK - 1) / DBK * DBK;
+  const int nz = (p + kper - 1) / kper;
+  dim3 g((b + DT - 1) / DT, (b + DT - 1) / DT, nz);
+  hipLaunchKernelGGL((k_dgemm<0, true>), g, dim3(256), 0, st, A, (int64_t)b, B, (int64_t)b, planes, (int64_t)b, b, b, p,
+                     kper, nullptr, 0, nullptr, 0);
+  OCM_CHECK_LAUNCH("k_dgemm TA");
+  const int64_t plane = (int64_t)b * b;
+  hipLaunchKernelGGL(k_sum_planes, dim3((unsigned)((plane + 255) / 256)), dim3(256), 0, st, planes, nz, plane, S);
+  OCM_CHECK_LAUNCH("k_sum_planes");
+  return OCM_OK;
+}
 
-int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
-                 int32_t theta_mode, double* evals_out, double* evecs_out, double* theta_out, int32_t* iters_out,
-                 void* stream) {
-  OCM_REQUIRE(ctx && C && evals_out && evecs_out, "ocm_eig_topk: NULL argument");
-  OCM_REQUIRE(p >= 1 && k >= 1 && k <= p, "ocm_eig_topk: need 1 <= k <= p");
-  OCM_REQUIRE(theta_mode == 0 || theta_out, "ocm_eig_topk: theta_out is NULL");
-  hipStream_t st = (hipStream_t)stream;
+int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
+                  int32_t theta_mode, int32_t slice, int32_t nslices, double* evals_out, double* evecs_out,
+                  double* theta_out, int32_t* iters_out, hipStream_t st) {
   if (tol <= 0) tol = 1e-10;
   if (max_iter <= 0) max_iter = 2000;
 
@@ -863,17 +894,18 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
     hipLaunchKernelGGL(k_small_finish, dim3(1), dim3(64), 0, st, ev, Z, p, k, evals_out, evecs_out,
                        theta_mode ? theta_out : nullptr);
     OCM_CHECK_LAUNCH("k_small_finish");
+    if (theta_mode && slice != 0) OCM_HIP(hipMemsetAsync(theta_out + 2, 0, sizeof(double), st));
     if (iters_out) *iters_out = 1;
     return OCM_OK;
   }
 
-  // block size: k plus oversampling, a multiple of 16, ≤ 64 and ≤ p
+  // block size: k plus oversampling, a multiple of 16, ≤ p
   int b = ((k + std::max(8, k / 2)) + 15) / 16 * 16;
   b = std::max(b, 32);
-  if (b > JMAX) b = JMAX;
-  OCM_REQUIRE(k <= b, "ocm_eig_topk: k > 64 is not supported");
-  if (b > p) b = (p / 16) * 16;
+  if (k <= JMAX && b > JMAX) b = JMAX;
+  if (b > p) b = std::max(k, (p / 16) * 16);
   OCM_REQUIRE(b >= k && b >= 16, "ocm_eig_topk: p too small for the block path");
+  const bool wide = b > JMAX;  // host b×b steps
 
   const int ksplit = std::max(1, std::min(16, (int)(256 / std::max(1, ((p + 63) / 64) * ((b + 63) / 64)))));
   const size_t pb = (size_t)p * b, bb = (size_t)b * b;
@@ -881,7 +913,8 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
   const size_t def_blocks = (size_t)((p + DT - 1) / DT) * ((p + DT - 1) / DT);  // deflate GEMM tiles
   constexpr int TRACE_KSPLIT = 4;  // the trace GEMM's K split (the trace is linear in the K segments)
   const size_t trace_wgs = (size_t)TRACE_KSPLIT * ((p + DT - 1) / DT) * ((p + DT - 1) / DT);
-  size_t need = (6 * pb + 6 * bb + (size_t)ksplit * pb + (size_t)nblk * bb + 4 * b + 64) * sizeof(double);
+  const size_t plane_cap = std::max((size_t)ksplit * pb, wide ? 16 * bb : 0);
+  size_t need = (6 * pb + 6 * bb + plane_cap + (wide ? 0 : (size_t)nblk * bb) + 4 * b + 64) * sizeof(double);
   if (theta_mode) need += ((size_t)p * p + 4 * (size_t)k * p + 2 * def_blocks + trace_wgs + 8) * sizeof(double);
   void* w = ocm::workspace(ctx, need + 16 * 256, st);
   if (!w) return OCM_ERR_NOMEM;
@@ -897,16 +930,41 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
   double* L = cv.take<double>(bb);
   double* theta = cv.take<double>(b);
   double* res = cv.take<double>(b);
-  double* planes = cv.take<double>((size_t)ksplit * pb);
-  double* apart = cv.take<double>((size_t)nblk * bb);
-  auto* hres = static_cast<double*>(ocm::host_staging(ctx, 2 * b * sizeof(double)));
+  double* planes = cv.take<double>(plane_cap);
+  double* apart = wide ? nullptr : cv.take<double>((size_t)nblk * bb);
+  auto* hres = static_cast<double*>(ocm::host_staging(ctx, (wide ? 3 * bb + b : 2 * b) * sizeof(double)));
   if (!hres) return OCM_ERR_NOMEM;
+  double* hmat = hres + 2 * b;  // wide: b×b host staging (+ b×b result, + b values)
 
+  // wide: S = AᵀB on the device → host
+  auto proj_to_host = [&](const double* A, const double* B) -> int {
+    int rc = dgemm_ta(A, B, p, b, S, planes, plane_cap, st);
+    if (rc) return rc;
+    OCM_HIP(hipMemcpyAsync(hmat, S, bb * sizeof(double), hipMemcpyDeviceToHost, st));
+    OCM_HIP(hipStreamSynchronize(st));
+    return OCM_OK;
+  };
+
+  using ocm::host_chol_inv_t;
+  using ocm::host_sym_eig;
   auto orth = [&](double* Win, double* Vout, uint64_t seed) -> int {
     // CholQR2 on column-normalised Win; result in Vout (Win is clobbered)
     hipLaunchKernelGGL(k_colnormalize, dim3(b), dim3(256), 0, st, Win, p, b, seed);
     OCM_CHECK_LAUNCH("k_colnormalize");
     for (int pass = 0; pass < 2; ++pass) {
+      if (wide) {  // pass 0: Win → Vout; pass 1: Vout → Win → Vout (the GEMM cannot run in place)
+        double* src = pass == 0 ? Win : Vout;
+        double* dst = pass == 0 ? Vout : Win;
+        int rc = proj_to_host(src, src);
+        if (rc) return rc;
+        host_chol_inv_t(hmat, b, hmat + bb);
+        OCM_HIP(hipMemcpyAsync(L, hmat + bb, bb * sizeof(double), hipMemcpyHostToDevice, st));
+        rc = dgemm(src, b, L, b, dst, b, p, b, b, 1, nullptr, st);
+        if (rc) return rc;
+        if (pass == 1) OCM_HIP(hipMemcpyAsync(Vout, Win, pb * sizeof(double), hipMemcpyDeviceToDevice, st));
+        OCM_HIP(hipStreamSynchronize(st));  // hmat is reused by the next pass
+        continue;
+      }
       double* src = pass == 0 ? Win : Vout;
       if (b == QB) {  // partial Grams → fused sum + Cholesky + solve
         hipLaunchKernelGGL(k_atb_part, dim3(nblk), dim3(256), 0, st, src, src, p, b, apart);
@@ -921,6 +979,25 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
       rc = trsm_rows(src, L, p, b, Vout, st);
       if (rc) return rc;
     }
+    return OCM_OK;
+  };
+  // H = Vᵀ W (b×b) on the device
+  auto project = [&](const double* A, const double* B, double* out) -> int {
+    if (wide) return dgemm_ta(A, B, p, b, out, planes, plane_cap, st);
+    return atb(A, B, p, b, out, apart, st);
+  };
+  // Ritz values (theta, descending) and rotations Z of H = Vᵀ W
+  auto ritz = [&]() -> int {
+    if (!wide) {
+      int rc = project(V, W, H);
+      if (rc) return rc;
+      return jacobi(H, b, 40, theta, Z, st);
+    }
+    int rc = proj_to_host(V, W);
+    if (rc) return rc;
+    host_sym_eig(hmat, b, hmat + 2 * bb, hmat + bb);
+    OCM_HIP(hipMemcpyAsync(Z, hmat + bb, bb * sizeof(double), hipMemcpyHostToDevice, st));
+    OCM_HIP(hipMemcpyAsync(theta, hmat + 2 * bb, b * sizeof(double), hipMemcpyHostToDevice, st));
     return OCM_OK;
   };
 
@@ -948,9 +1025,7 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
       if (rc) return rc;
       continue;
     }
-    rc = atb(V, W, p, b, H, apart, st);  // H = Vᵀ W
-    if (rc) return rc;
-    rc = jacobi(H, b, 40, theta, Z, st);
+    rc = ritz();
     if (rc) return rc;
     rc = dgemm(V, b, Z, b, T1, b, p, b, b, 1, nullptr, st);  // Ritz vectors
     if (rc) return rc;
@@ -985,7 +1060,7 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
 
   if (theta_mode) {
     // H_k = V_kᵀ (C V_k): the projected block; N = V H restricted to k columns
-    rc = atb(V, W, p, b, H, apart, st);
+    rc = project(V, W, H);
     if (rc) return rc;
     // N = V_k H_k (K = k: only the leading k Ritz directions are deflated)
     rc = dgemm(V, b, H, b, Nm, b, p, b, k, 1, nullptr, st);
@@ -1001,21 +1076,24 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
     OCM_CHECK_LAUNCH("k_deflate_operands");
     const dim3 gd((p + DT - 1) / DT, (p + DT - 1) / DT, 1);
     hipLaunchKernelGGL(k_dgemm<2>, gd, dim3(256), 0, st, U, (int64_t)(2 * k), Wt, (int64_t)p, Ct, (int64_t)p, p, p,
-                       2 * k, 2 * k, C, (int64_t)p, dpart);
+                       2 * k, 2 * k, C, (int64_t)p, dpart, 0);
     OCM_CHECK_LAUNCH("k_dgemm deflate");
     hipLaunchKernelGGL(k_sum_pairs, dim3(1), dim3(256), 0, st, dpart, (int)(gd.x * gd.y), tr2);
     OCM_CHECK_LAUNCH("k_sum_pairs");
     OCM_HIP(hipMemcpyAsync(theta_out, tr2, 2 * sizeof(double), hipMemcpyDeviceToDevice, st));
-    if (theta_mode >= 2) {
-      const int nt = (p + DT - 1) / DT;
+    // this slice's share of the upper-triangle tiles of the trace GEMM
+    const int nt = (p + DT - 1) / DT;
+    const int ntri = nt * (nt + 1) / 2;
+    const int t0 = (int)((int64_t)ntri * slice / nslices), t1 = (int)((int64_t)ntri * (slice + 1) / nslices);
+    if (theta_mode >= 2 && t1 > t0) {
       // split-K: 4× the workgroups of the upper-triangle tile grid (528 tiles at p = 2048 fill the
       // chip only once), partial traces summed in a fixed order
       int kper = (p + TRACE_KSPLIT - 1) / TRACE_KSPLIT;
       kper = (kper + DBK - 1) / DBK * DBK;
       const int nz = (p + kper - 1) / kper;
-      dim3 g((unsigned)(nt * (nt + 1) / 2), 1, (unsigned)nz);
+      dim3 g((unsigned)(t1 - t0), 1, (unsigned)nz);
       hipLaunchKernelGGL(k_dgemm<1>, g, dim3(256), 0, st, Ct, (int64_t)p, Ct, (int64_t)p, nullptr, 0, p, p, p, kper, Ct,
-                         (int64_t)p, tpart);
+                         (int64_t)p, tpart, t0);
       OCM_CHECK_LAUNCH("k_dgemm trace");
       hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, tpart, (int)(g.x * g.z), theta_out + 2);
       OCM_CHECK_LAUNCH("k_sum_partials");
@@ -1024,6 +1102,32 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
     }
   }
   return converged ? OCM_OK : ocm::fail(OCM_ERR_NOCONV, "ocm_eig_topk: max_iter reached before tolerance");
+}
+
+}  // namespace
+
+extern "C" {
+
+int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
+                 int32_t theta_mode, double* evals_out, double* evecs_out, double* theta_out, int32_t* iters_out,
+                 void* stream) {
+  OCM_REQUIRE(ctx && C && evals_out && evecs_out, "ocm_eig_topk: NULL argument");
+  OCM_REQUIRE(p >= 1 && k >= 1 && k <= p, "ocm_eig_topk: need 1 <= k <= p");
+  OCM_REQUIRE(theta_mode == 0 || theta_out, "ocm_eig_topk: theta_out is NULL");
+  return eig_topk_impl(ctx, C, p, k, tol, max_iter, theta_mode, 0, 1, evals_out, evecs_out, theta_out, iters_out,
+                       (hipStream_t)stream);
+}
+
+int ocm_eig_topk_ex(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
+                    int32_t theta_mode, int32_t theta3_slice, int32_t theta3_nslices, double* evals_out,
+                    double* evecs_out, double* theta_out, int32_t* iters_out, void* stream) {
+  OCM_REQUIRE(ctx && C && evals_out && evecs_out, "ocm_eig_topk_ex: NULL argument");
+  OCM_REQUIRE(p >= 1 && k >= 1 && k <= p, "ocm_eig_topk_ex: need 1 <= k <= p");
+  OCM_REQUIRE(theta_mode == 0 || theta_out, "ocm_eig_topk_ex: theta_out is NULL");
+  OCM_REQUIRE(theta3_nslices >= 1 && theta3_slice >= 0 && theta3_slice < theta3_nslices,
+              "ocm_eig_topk_ex: need 0 <= theta3_slice < theta3_nslices");
+  return eig_topk_impl(ctx, C, p, k, tol, max_iter, theta_mode, theta3_slice, theta3_nslices, evals_out, evecs_out,
+                       theta_out, iters_out, (hipStream_t)stream);
 }
 
 int ocm_sym_pinv_f64(ocm_ctx* ctx, const double* A, int32_t d, double rcond, double* out, void* stream) {

@@ -225,14 +225,17 @@ int ocm_snv_savgol_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, int
     dtaps = w;
   }
   OCM_REQUIRE(m < (1LL << 31), "ocm_snv_savgol_f32: too many rows per call");
-  const bool fast = p % 4 == 0 && p <= 256 * PREP_SEGS_MAX && ldx % 4 == 0 && ldo % 4 == 0 &&
+  bool fast = p % 4 == 0 && p <= 256 * PREP_SEGS_MAX && ldx % 4 == 0 && ldo % 4 == 0 &&
                     (reinterpret_cast<uintptr_t>(X) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
                     (window == 0 || window == 5 || window == 15) && p >= window + 3;
+  const size_t lds = window > 0 ? (size_t)(4 * p + 2) * sizeof(float) +
+                                      (size_t)(window + 2 * (window / 2) * window) * sizeof(double)
+                                : 0;
+  int max_lds = 0;  // the wave-private rows must fit the device's LDS (160 KiB on gfx950)
+  OCM_HIP(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, ctx->device));
+  if (fast && lds > (size_t)max_lds) fast = false;
   if (fast) {
     const dim3 g((unsigned)((m + 3) / 4));
-    const size_t lds = window > 0 ? (size_t)(4 * p + 2) * sizeof(float) +
-                                        (size_t)(window + 2 * (window / 2) * window) * sizeof(double)
-                                  : 0;
 #define OCM_SG4(W_, S_) hipLaunchKernelGGL((k_snv_sg4<W_, S_>), g, dim3(256), lds, st, X, ldx, m, p, snv, dtaps, out, ldo)
 #define OCM_SG4_S(W_) \
   if (p <= 1024)      \

@@ -42,7 +42,8 @@ __device__ __forceinline__ void score_epilogue(double* tls, double* sred, const 
                                                const double* __restrict__ A, float* __restrict__ T_out,
                                                double* __restrict__ T2_out, float* __restrict__ Q_out, DecArgs dec,
                                                double* __restrict__ acc_out, int64_t acc_stride,
-                                               double* __restrict__ stat_part) {
+                                               double* __restrict__ stat_part, int ldt = 0,
+                                               const double* __restrict__ T2_in = nullptr) {
   constexpr int KP = KT * 32;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l31 = lane & 31, h = lane >> 5;
@@ -59,7 +60,9 @@ __device__ __forceinline__ void score_epilogue(double* tls, double* sred, const 
   const int64_t grow = row0 + l31;
   const bool own = (h == 0) && (grow < m);
   double T2 = 0.0, Q = q64;
+  if (ldt <= 0) ldt = k;
   if (own) {
+    if (T2_in) T2 = T2_in[grow];  // earlier component blocks (k > 64)
     const double* trow = Tt + l31 * (KP + 1);
     if (a_diag) {  // A holds the diagonal only
       for (int a = 0; a < k; ++a) T2 += trow[a] * trow[a] * A[a];
@@ -71,7 +74,7 @@ __device__ __forceinline__ void score_epilogue(double* tls, double* sred, const 
       }
     }
     if (T_out)
-      for (int a = 0; a < k; ++a) T_out[grow * k + a] = (float)trow[a];
+      for (int a = 0; a < k; ++a) T_out[grow * ldt + a] = (float)trow[a];
     if (T2_out) T2_out[grow] = T2;
     if (Q_out) Q_out[grow] = (float)Q;
     if (dec.enabled) {
@@ -121,7 +124,9 @@ __global__ __launch_bounds__(256, 2) void k_score_direct(const float* __restrict
                                                          float* __restrict__ T_out, double* __restrict__ T2_out,
                                                          float* __restrict__ Q_out, DecArgs dec,
                                                          double* __restrict__ acc_out, int64_t acc_stride,
-                                                         double* __restrict__ stat_part) {
+                                                         double* __restrict__ stat_part, int ldt,
+                                                         const double* __restrict__ T2_in, float* __restrict__ R_out,
+                                                         int64_t ldr) {
   constexpr int KP = KT * 32;
   constexpr int PS = PB + 4;  // padded LDS row: conflict-free ds_read_b128 across comps
   constexpr int MAIN_F = KP * PS + PB;
@@ -248,11 +253,23 @@ __global__ __launch_bounds__(256, 2) void k_score_direct(const float* __restrict
       // accR register 4g+e holds column 8g + 4h + e of the chunk (row lane&31)
       const int col = c0 + 8 * g + 4 * h;
       const f32x4 u = *reinterpret_cast<const f32x4*>(&Ml[col - b0]);
+      f32x4 rv;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float cm = col + e < p ? 1.f : 0.f;  // clamped loads beyond p carry data
         const float r = ((S.d[g][e] - u[e]) - accR[4 * g + e]) * cm;
+        rv[e] = r;
         qc += r * r;
+      }
+      if (R_out && grow < m) {  // the residual feeds the next component block (k > 64)
+        float* rr = R_out + grow * ldr;
+        if (VEC && col + 3 < p) {
+          *reinterpret_cast<f32x4*>(rr + col) = rv;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (col + e < p) rr[col + e] = rv[e];
+        }
       }
     }
     q64 += (double)(qc * rowmask);
@@ -273,7 +290,7 @@ __global__ __launch_bounds__(256, 2) void k_score_direct(const float* __restrict
   q64 += __shfl_xor(q64, 32, 64);
 
   score_epilogue<KT, SW>(reinterpret_cast<double*>(smem), sred, accT64, q64, row0, m, k, a_diag, A, T_out, T2_out,
-                         Q_out, dec, acc_out, acc_stride, stat_part);
+                         Q_out, dec, acc_out, acc_stride, stat_part, ldt, T2_in);
 }
 
 // ---------------------------------------------------------------------------
@@ -800,12 +817,55 @@ __global__ __launch_bounds__(256) void k_rowsq(const float* __restrict__ x, int6
   if (lane == 0) q[r] = (float)s;
 }
 
+// q_i = Σ_j (s(x_ij) − s(x̂_ij))² with s(v) = clamp((v − min_j x_ij)/(max_j x_ij − min_j x_ij + eps), 0, 1):
+// the per-sample min–max scaled residual of utils/final_vaesimca.py:417-423 /
+// 484-490 (its BCE-trained networks).  The scaling is evaluated in float32 in
+// the reference's operation order; the sum of squares in f64.  One wave per row.
+__global__ __launch_bounds__(256) void k_rowsq_minmax(const float* __restrict__ x, int64_t ldx,
+                                                      const float* __restrict__ xh, int64_t ldxh, int64_t m, int p,
+                                                      float eps, float* __restrict__ q) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= m) return;
+  const float* xr = x + r * ldx;
+  const float* hr = xh + r * ldxh;
+  float lo = INFINITY, hi = -INFINITY;
+  for (int j = lane; j < p; j += 64) {
+    const float v = xr[j];
+    lo = fminf(lo, v);
+    hi = fmaxf(hi, v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fminf(lo, __shfl_xor(lo, o, 64));
+    hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+  }
+  const float den = (hi - lo) + eps;
+  double s = 0.0;
+  for (int j = lane; j < p; j += 64) {
+    const float a = fminf(fmaxf((xr[j] - lo) / den, 0.f), 1.f);
+    const float b = fminf(fmaxf((hr[j] - lo) / den, 0.f), 1.f);
+    const float d = a - b;
+    s += (double)(d * d);
+  }
+  s = wave_sum_f64(s);
+  if (lane == 0) q[r] = (float)s;
+}
+
 __global__ void k_cast_f64_f32(const double* __restrict__ a, int64_t n, float* __restrict__ b) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) b[i] = (float)a[i];
 }
 
-// k_score_direct launch (any p, k ≤ 64); a_diag: A is the k-vector diag(A)
+// k_score_direct launch; a_diag: A is the k-vector diag(A).  k ≤ 64: one
+// launch.  k > 64 (diagonal A only): component blocks of ≤ 64 in turn, each
+// launch projecting the previous block's residual (the first block reads X and
+// subtracts μ; the residual matrix R is written by every launch but the last,
+// in place after the first), accumulating T² and writing its columns of T;
+// the last block gives Q = ‖final residual‖², the decision and the moments.
+// The loadings are orthonormal, so P_b·(y − P_aᵀt_a) = P_b·y up to rounding:
+// the same T, T², Q as one pass, in the reference's float32 residual
+// arithmetic (utils/SIMCA.py:67-68).
 int score_direct(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
                  const double* P, const double* mu, const double* A, int a_diag, int32_t k, float* T_out,
                  double* T2_out, float* Q_out, const ocm_decision* dec, double* accept_out, int64_t accept_stride,
@@ -814,22 +874,31 @@ int score_direct(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows,
     if (stats_out) OCM_HIP(hipMemsetAsync(stats_out, 0, 4 * sizeof(double), st));
     return OCM_OK;
   }
+  constexpr int KB = 64;  // components per launch
+  const int nkb = (k + KB - 1) / KB;
+  OCM_REQUIRE(nkb == 1 || a_diag, "ocm_score_f32: k > 64 needs a diagonal quadratic form (ocm_score_f32_diag)");
   const int64_t rows_per_blk = SROWS;
   const int64_t nblk = (m + rows_per_blk - 1) / rows_per_blk;
   OCM_REQUIRE(nblk < (1LL << 31), "ocm_score_f32: too many rows");
   const size_t part_bytes = stats_out ? (size_t)nblk * 4 * sizeof(double) : 0;
-  const size_t cast_bytes = ((size_t)k * p + p) * sizeof(float) + 512;
-  void* w = ocm::workspace(ctx, part_bytes + cast_bytes + 1024, st);
+  const size_t cast_bytes = ((size_t)k * p + 2 * (size_t)p) * sizeof(float) + 1024;
+  const bool need_t2 = nkb > 1 && !T2_out;  // the running T² between blocks
+  const size_t extra = nkb > 1 ? (size_t)m * p * sizeof(float) + (need_t2 ? (size_t)m * sizeof(double) : 0) + 512 : 0;
+  void* w = ocm::workspace(ctx, part_bytes + cast_bytes + extra + 1024, st);
   if (!w) return OCM_ERR_NOMEM;
   ocm::Carve cv{static_cast<char*>(w)};
   double* part = stats_out ? cv.take<double>((size_t)nblk * 4) : nullptr;
   // the f32 kernel takes f32 loadings / mean
   float* P32 = cv.take<float>((size_t)k * p);
   float* mu32 = cv.take<float>(p);
+  float* zero32 = cv.take<float>(p);
+  float* R = nkb > 1 ? cv.take<float>((size_t)m * p) : nullptr;
+  double* T2run = nkb > 1 ? (T2_out ? T2_out : cv.take<double>((size_t)m)) : T2_out;
   hipLaunchKernelGGL(k_cast_f64_f32, dim3((unsigned)(((int64_t)k * p + 255) / 256)), dim3(256), 0, st, P,
                      (int64_t)k * p, P32);
   hipLaunchKernelGGL(k_cast_f64_f32, dim3((p + 255) / 256), dim3(256), 0, st, mu, (int64_t)p, mu32);
   OCM_CHECK_LAUNCH("k_cast_f64_f32");
+  if (nkb > 1) OCM_HIP(hipMemsetAsync(zero32, 0, (size_t)p * sizeof(float), st));
   DecArgs d{};
   if (dec) {
     d.enabled = 1;
@@ -840,19 +909,32 @@ int score_direct(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows,
   }
   const bool vec = (ldx % 4 == 0) && (p % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
   dim3 g((unsigned)nblk);
-  {
+  for (int bk = 0; bk < nkb; ++bk) {
+    const int c0 = bk * KB, kb = std::min(KB, k - c0);
+    const bool first = bk == 0, last = bk == nkb - 1;
+    // input of this block: X (rows / ldx / μ) first, then the residual R (dense, μ = 0)
+    const float* Xin = first ? X : R;
+    const int64_t ldin = first ? ldx : (int64_t)p;
+    const int64_t* rin = first ? rows : nullptr;
+    const bool vin = first ? vec : (p % 4 == 0);
+    const float* muin = first ? mu32 : zero32;
+    float* Tb = T_out ? T_out + c0 : nullptr;
+    const double* Ab = A + c0;  // diagonal entries of this block (a_diag) or the whole A (nkb == 1)
+    DecArgs db = last ? d : DecArgs{};
     ocm::TimedRegion tr(ctx, OCM_KERNEL_SCORE, st);
-#define OCM_SCORE_LAUNCH(KT_, V_)                                                                          \
-  hipLaunchKernelGGL((k_score_direct<KT_, V_>), g, dim3(256), 0, st, X, ldx, rows, m, p, P32, mu32, A, k, a_diag, \
-                     T_out, T2_out, Q_out, d, accept_out, accept_stride, part)
-    if (k <= 32) {
-      if (vec) OCM_SCORE_LAUNCH(1, true); else OCM_SCORE_LAUNCH(1, false);
+#define OCM_SCORE_LAUNCH(KT_, V_)                                                                              \
+  hipLaunchKernelGGL((k_score_direct<KT_, V_>), g, dim3(256), 0, st, Xin, ldin, rin, m, p, P32 + (size_t)c0 * p, \
+                     muin, Ab, kb, a_diag, Tb, last ? T2_out : T2run, last ? Q_out : nullptr, db,             \
+                     last ? accept_out : nullptr, accept_stride, last ? part : nullptr, k,                    \
+                     first ? nullptr : T2run, last ? nullptr : R, (int64_t)p)
+    if (kb <= 32) {
+      if (vin) OCM_SCORE_LAUNCH(1, true); else OCM_SCORE_LAUNCH(1, false);
     } else {
-      if (vec) OCM_SCORE_LAUNCH(2, true); else OCM_SCORE_LAUNCH(2, false);
+      if (vin) OCM_SCORE_LAUNCH(2, true); else OCM_SCORE_LAUNCH(2, false);
     }
 #undef OCM_SCORE_LAUNCH
+    OCM_CHECK_LAUNCH("k_score");
   }
-  OCM_CHECK_LAUNCH("k_score");
   if (stats_out) {
     hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, st, part, nblk, stats_out);
     OCM_CHECK_LAUNCH("k_stats_reduce");
@@ -870,7 +952,7 @@ int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
                   double* stats_out, void* stream) {
   OCM_REQUIRE(ctx && X && P && mu && A, "ocm_score_f32: NULL argument");
   OCM_REQUIRE(m >= 0 && p > 0 && ldx >= p, "ocm_score_f32: bad shape");
-  OCM_REQUIRE(k >= 1 && k <= 64, "ocm_score_f32: 1 <= k <= 64");
+  OCM_REQUIRE(k >= 1 && k <= 64, "ocm_score_f32: 1 <= k <= 64 (larger k: ocm_score_f32_diag)");
   OCM_REQUIRE(!dec || accept_out, "ocm_score_f32: decision requires accept_out");
   // general k×k quadratic form (k² FMAs per row are negligible)
   return score_direct(ctx, X, ldx, rows, m, p, P, mu, A, 0, k, T_out, T2_out, Q_out, dec, accept_out,
@@ -883,7 +965,7 @@ int ocm_score_f32_diag(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t*
                        int64_t accept_stride, double* stats_out, void* stream) {
   OCM_REQUIRE(ctx && X && P && mu && a_diag, "ocm_score_f32_diag: NULL argument");
   OCM_REQUIRE(m >= 0 && p > 0 && ldx >= p, "ocm_score_f32_diag: bad shape");
-  OCM_REQUIRE(k >= 1 && k <= 64, "ocm_score_f32_diag: 1 <= k <= 64");
+  OCM_REQUIRE(k >= 1 && k <= p, "ocm_score_f32_diag: 1 <= k <= p");
   OCM_REQUIRE(!dec || accept_out, "ocm_score_f32_diag: decision requires accept_out");
   hipStream_t st = (hipStream_t)stream;
   const int nj = p / 64;
@@ -961,6 +1043,17 @@ int ocm_rowsq_residual_f32(ocm_ctx* ctx, const float* x, int64_t ldx, const floa
   hipLaunchKernelGGL(k_rowsq, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, ldx, xhat, ldxh, m,
                      p, q_out);
   OCM_CHECK_LAUNCH("k_rowsq");
+  return OCM_OK;
+}
+
+int ocm_rowsq_minmax_f32(ocm_ctx* ctx, const float* x, int64_t ldx, const float* xhat, int64_t ldxh, int64_t m,
+                         int32_t p, float eps, float* q_out, void* stream) {
+  OCM_REQUIRE(ctx && x && xhat && q_out, "ocm_rowsq_minmax_f32: NULL argument");
+  OCM_REQUIRE(p > 0 && ldx >= p && ldxh >= p, "ocm_rowsq_minmax_f32: bad shape");
+  if (m <= 0) return OCM_OK;
+  hipLaunchKernelGGL(k_rowsq_minmax, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, ldx, xhat,
+                     ldxh, m, p, eps, q_out);
+  OCM_CHECK_LAUNCH("k_rowsq_minmax");
   return OCM_OK;
 }
 

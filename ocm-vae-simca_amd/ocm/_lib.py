@@ -70,6 +70,10 @@ SIGNATURES = {
                                   c_void_p]),
     "ocm_eig_topk": (c_i32, [c_void_p, c_void_p, c_i32, c_i32, c_f64, c_i32, c_i32, c_void_p, c_void_p, c_void_p,
                              ctypes.POINTER(c_i32), c_void_p]),
+    "ocm_eig_topk_ex": (c_i32, [c_void_p, c_void_p, c_i32, c_i32, c_f64, c_i32, c_i32, c_i32, c_i32, c_void_p,
+                                c_void_p, c_void_p, ctypes.POINTER(c_i32), c_void_p]),
+    "ocm_gram_pack": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_i32, c_void_p, c_void_p]),
+    "ocm_cov_from_packed": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p]),
     "ocm_sym_pinv_f64": (c_i32, [c_void_p, c_void_p, c_i32, c_f64, c_void_p, c_void_p]),
     "ocm_score_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_void_p,
                               c_i32, c_void_p, c_void_p, c_void_p, ctypes.POINTER(OcmDecision), c_void_p, c_i64,
@@ -81,6 +85,8 @@ SIGNATURES = {
                            c_void_p, c_void_p, c_i64, c_void_p]),
     "ocm_rowsq_residual_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i64, c_i32, c_void_p,
                                        c_void_p]),
+    "ocm_rowsq_minmax_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i64, c_i32, ctypes.c_float,
+                                     c_void_p, c_void_p]),
     "ocm_cast_f64_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_void_p]),
     "ocm_percentile": (c_i32, [c_void_p, c_void_p, c_i32, c_i64, c_f64, ctypes.POINTER(c_f64), c_void_p]),
     "ocm_radix_hist": (c_i32, [c_void_p, c_void_p, c_i32, c_i64, ctypes.c_uint64, c_i32, c_void_p, c_void_p]),
@@ -101,7 +107,7 @@ SIGNATURES = {
                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
-ABI_VERSION = 2  # include/ocm.h OCM_ABI_VERSION
+ABI_VERSION = 3  # include/ocm.h OCM_ABI_VERSION
 
 _lib = None
 _lib_lock = threading.Lock()

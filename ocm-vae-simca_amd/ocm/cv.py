@@ -334,7 +334,14 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
         for idx, acc in preds_fold:
             if idx.numel():
                 pred_loc[:, idx] = acc
-        pred_all = (_gather_blocks(pred_loc, lo, n_glob, group) if distributed else pred_loc).cpu().numpy()
+        if distributed:
+            pred_all = _gather_blocks(pred_loc, lo, n_glob, group)
+        elif lo == 0 and n_loc == n_glob:
+            pred_all = pred_loc
+        else:  # one process holding a row block: its columns of the (ncfg, n_glob) matrix
+            pred_all = torch.zeros((ncfg, n_glob), dtype=torch.float64, device=dev)
+            pred_all[:, lo:lo + n_loc] = pred_loc
+        pred_all = pred_all.cpu().numpy()
     for ci_, combo in enumerate(combos):
         for li, lv in enumerate(lvs):
             c = ci_ * len(lvs) + li

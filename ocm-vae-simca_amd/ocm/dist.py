@@ -21,7 +21,8 @@ from . import engine, limits
 
 
 def make_allreduce(group=None):
-    """Sum (or mean) a list of device tensors across the ranks of ``group``."""
+    """Sum (or mean) a list of device tensors across the ranks of ``group``;
+    the callable carries ``rank`` / ``world`` (the θ3 slice of this rank)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return None
 
@@ -32,6 +33,8 @@ def make_allreduce(group=None):
             if op == "mean":
                 t.div_(ws)
 
+    allreduce.rank = dist.get_rank(group)
+    allreduce.world = dist.get_world_size(group)
     return allreduce
 
 
@@ -104,14 +107,16 @@ class ShardedSIMCA:
         ar = make_allreduce(self.group)
         n_local = X_local.shape[0] if n_local is None else n_local
         k = self.n_components
+        need_stats = "chi2pom" in (self.t2lim, self.qlim)  # moments feed only chi2pom limits
         self.fit_ = fit = engine.fit_class(X_local, rows, n_local, k, limits.theta_mode_for(self), want_T=self.want_T,
-                                           allreduce=ar)
+                                           allreduce=ar, need_stats=need_stats)
         n = fit.n
         T2m = limits.Moments(n, lambda: fit.T2_stats, None, lambda pct: percentile_sharded(fit.T2, pct, n, self.group))
         Qm = limits.Moments(n, lambda: fit.Q_stats, None, lambda pct: percentile_sharded(fit.Q, pct, n, self.group))
         self.T2_limit = limits.t2_limit(self, T2m, k)
         self.Q_limit = limits.q_limit(self, Qm, fit.thetas)
         self.D_limit = limits.critic_distance(self, self.T2_limit, self.Q_limit, fit.thetas, k)
+        engine._mark("limits")
         if self.type == "dd":
             self.decision = engine.make_decision("dd", self._t2dof / self._t2scfact, self._qdof / self._qscfact,
                                                  self.D_limit)

@@ -170,7 +170,12 @@ def cov_from_gram(terms, shift32: torch.Tensor, n: int):
     return C, mean
 
 
-def eig_topk(C: torch.Tensor, k: int, theta_mode: int, tol=EIG_TOL, max_iter=EIG_MAX_ITER):
+def eig_topk(C: torch.Tensor, k: int, theta_mode: int, tol=EIG_TOL, max_iter=EIG_MAX_ITER, theta3_slice=(0, 1)):
+    """Top-k eigenpairs + tail moments of C (ocm_eig_topk_ex).  Raises
+    ``OcmNotConverged`` when the Ritz residuals miss ``tol`` within ``max_iter``
+    iterations (loadings and limits from an unconverged subspace are never
+    handed on).  ``theta3_slice = (s, S)``: this call's share of the θ3 trace
+    work (the ranks of a sharded fit sum the partials)."""
     p = C.shape[0]
     dev = C.device
     evals = torch.empty(k, dtype=torch.float64, device=dev)
@@ -178,14 +183,15 @@ def eig_topk(C: torch.Tensor, k: int, theta_mode: int, tol=EIG_TOL, max_iter=EIG
     theta = torch.zeros(3, dtype=torch.float64, device=dev)
     iters = ctypes.c_int32(0)
     ctx = Context.get(dev.index)
-    rc = _lib.load().ocm_eig_topk(ctx.handle, ptr(C), p, k, tol, max_iter, theta_mode, ptr(evals), ptr(evecs),
-                                  ptr(theta), ctypes.byref(iters), _stream(dev))
+    rc = _lib.load().ocm_eig_topk_ex(ctx.handle, ptr(C), p, k, tol, max_iter, theta_mode, int(theta3_slice[0]),
+                                     int(theta3_slice[1]), ptr(evals), ptr(evecs), ptr(theta), ctypes.byref(iters),
+                                     _stream(dev))
     if rc == _lib.OCM_ERR_NOCONV:
-        import warnings
-
-        warnings.warn(f"ocm_eig_topk: not converged to tol={tol} in {max_iter} iterations", RuntimeWarning)
-    else:
-        check(rc, "ocm_eig_topk")
+        raise _lib.OcmNotConverged(
+            f"ocm_eig_topk: the leading {k} eigenpairs of the {p}x{p} covariance did not converge to tol={tol} in "
+            f"{max_iter} iterations (no usable spectral gap after component {k}); pick n_components at a gap in "
+            "the spectrum")
+    check(rc, "ocm_eig_topk_ex")
     return evals, evecs, theta, int(iters.value)
 
 
@@ -319,6 +325,8 @@ def radix_hist(v: torch.Tensor, prefix: int, shift: int, hist: torch.Tensor | No
         raise TypeError("radix_hist: float32/float64 only")
     if hist is None:
         hist = torch.empty(256, dtype=torch.int64, device=v.device)
+    if v.numel() == 0:  # a rank without values takes part in the all-reduce with zeros
+        return hist.zero_()
     check(_lib.load().ocm_radix_hist(Context.get(v.device.index).handle, ptr(v), 0 if v.dtype == torch.float64 else 1,
                                      v.numel(), ctypes.c_uint64(prefix), shift, ptr(hist), _stream(v.device)),
           "ocm_radix_hist")
@@ -329,6 +337,8 @@ def rowsq_residual(x: torch.Tensor, xhat: torch.Tensor) -> torch.Tensor:
     """q_i = Σ_j (x_ij − xhat_ij)² (float32 out, fp64 accumulation).  ``xhat``
     may be one row (shape (p,) or (1, p)): it is broadcast to every row."""
     m, p = x.shape
+    if m == 0:
+        return torch.empty(0, dtype=torch.float32, device=x.device)
     if x.stride(1) != 1:
         x = x.contiguous()
     bcast = xhat.dim() == 1 or xhat.shape[0] == 1
@@ -339,6 +349,21 @@ def rowsq_residual(x: torch.Tensor, xhat: torch.Tensor) -> torch.Tensor:
     ctx = Context.get(x.device.index)
     check(_lib.load().ocm_rowsq_residual_f32(ctx.handle, ptr(x), x.stride(0), ptr(xh), 0 if bcast else xh.stride(0),
                                              m, p, ptr(q), _stream(x.device)), "ocm_rowsq_residual_f32")
+    return q
+
+
+def rowsq_minmax(x: torch.Tensor, xhat: torch.Tensor, eps: float = 1e-8) -> torch.Tensor:
+    """Per-sample min–max scaled residual Σ_j (s(x) − s(x̂))² (float32 out):
+    utils/final_vaesimca.py:417-423, 484-490 (ocm_rowsq_minmax_f32)."""
+    m, p = x.shape
+    if m == 0:
+        return torch.empty(0, dtype=torch.float32, device=x.device)
+    x = x if x.stride(1) == 1 else x.contiguous()
+    xhat = xhat if xhat.stride(1) == 1 else xhat.contiguous()
+    q = torch.empty(m, dtype=torch.float32, device=x.device)
+    check(_lib.load().ocm_rowsq_minmax_f32(Context.get(x.device.index).handle, ptr(x), x.stride(0), ptr(xhat),
+                                           xhat.stride(0), m, p, float(eps), ptr(q), _stream(x.device)),
+          "ocm_rowsq_minmax_f32")
     return q
 
 
@@ -367,32 +392,96 @@ def invcov_from_evals(evals: torch.Tensor, rcond=1e-15) -> torch.Tensor:
     return torch.diag(inv_evals(evals, rcond))
 
 
+def gram_pack(G: torch.Tensor, cs: torch.Tensor, shift32: torch.Tensor, n: int, out: torch.Tensor | None = None):
+    """This rank's moments about zero in the packed all-reduce layout
+    (ocm_gram_pack): p(p+1)/2 + p + 1 doubles."""
+    p = shift32.shape[0]
+    if out is None:
+        out = torch.empty(p * (p + 1) // 2 + p + 1, dtype=torch.float64, device=G.device)
+    check(_lib.load().ocm_gram_pack(Context.get(G.device.index).handle, ptr(G), ptr(cs), ptr(shift32), int(n), p,
+                                    ptr(out), _stream(G.device)), "ocm_gram_pack")
+    return out
+
+
+def cov_from_packed(packed: torch.Tensor, p: int):
+    """(C, mean) from summed packed moments (ocm_cov_from_packed; n read on the device)."""
+    dev = packed.device
+    C = torch.empty((p, p), dtype=torch.float64, device=dev)
+    mean = torch.empty(p, dtype=torch.float64, device=dev)
+    check(_lib.load().ocm_cov_from_packed(Context.get(dev.index).handle, ptr(packed), p, ptr(C), ptr(mean),
+                                          _stream(dev)), "ocm_cov_from_packed")
+    return C, mean
+
+
+# ---- optional per-phase timing (bench.py): HIP events on the launch stream ----
+_phase_timer = None
+
+
+def set_phase_timer(timer):
+    """Install (or clear with None) a recorder with ``mark(name)``; the fit
+    and scoring paths then mark their phase boundaries on the launch stream."""
+    global _phase_timer
+    prev, _phase_timer = _phase_timer, timer
+    return prev
+
+
+def _mark(name: str):
+    if _phase_timer is not None:
+        _phase_timer.mark(name)
+
+
 def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_mode: int,
-              want_T=True, keep_C=False, shift32: torch.Tensor | None = None, allreduce=None) -> ClassFit:
+              want_T=True, keep_C=False, shift32: torch.Tensor | None = None, allreduce=None,
+              need_stats=True) -> ClassFit:
     """Gram → covariance → top-k eigenpairs → fit-set scores for one class.
 
-    ``allreduce`` (optional callable on a list of device tensors) sums the
-    per-rank Gram / column sums / row counts across ranks (RCCL), for row
-    shards of one class spread over GPUs."""
+    ``allreduce`` (optional callable on a list of device tensors, with the
+    rank / world size as attributes) marks a class whose rows are sharded
+    over GPUs: each rank's Gram is taken about its own sample
+    shift, packed as moments about zero (``ocm_gram_pack``) and summed in ONE
+    all-reduce; the θ3 trace work is split over the ranks and its partials
+    summed; the fit-set moments are all-reduced only when ``need_stats``."""
     p = X.shape[1]
     if k > p or k < 1:
         raise ValueError(f"n_components={k} must be in [1, {p}]")
+    _mark("start")
     if shift32 is None:
-        shift64 = colmean(X, rows, min(n, SHIFT_SAMPLE))
+        shift64 = colmean(X, rows, max(1, min(n, SHIFT_SAMPLE))) if n > 0 else torch.zeros(p, dtype=torch.float64,
+                                                                                          device=X.device)
         shift32 = cast_f32(shift64)
-        if allreduce is not None:
-            allreduce([shift32], op="mean")
-    G, cs = gram(X, rows, [0, n], shift32)
-    n_total = n
-    if allreduce is not None:
-        cnt = torch.tensor([float(n)], dtype=torch.float64, device=X.device)
-        allreduce([G, cs, cnt])
-        n_total = int(round(cnt.item()))
-    if n_total < 2:
-        raise ValueError("SIMCA needs at least 2 samples in a class")
-    C, mean64 = cov_from_gram([(1.0, G[0], cs[0])], shift32, n_total)
-    del G
-    evals, evecs, theta, iters = eig_topk(C, k, theta_mode)
+    _mark("shift")
+    slice_ = (0, 1)
+    if allreduce is None:
+        G, cs = gram(X, rows, [0, n], shift32)
+        _mark("gram")
+        n_total = n
+        if n_total < 2:
+            raise ValueError("SIMCA needs at least 2 samples in a class")
+        C, mean64 = cov_from_gram([(1.0, G[0], cs[0])], shift32, n_total)
+        del G
+        _mark("cov")
+    else:
+        if n > 0:
+            G, cs = gram(X, rows, [0, n], shift32)
+            packed = gram_pack(G[0], cs[0], shift32, n)
+            del G, cs
+        else:  # a rank without rows contributes zeros
+            packed = torch.zeros(p * (p + 1) // 2 + p + 1, dtype=torch.float64, device=X.device)
+        _mark("gram")
+        allreduce([packed])
+        _mark("allreduce")
+        C, mean64 = cov_from_packed(packed, p)
+        _mark("cov")
+        slice_ = (allreduce.rank, allreduce.world)
+        n_total = None
+    evals, evecs, theta, iters = eig_topk(C, k, theta_mode, theta3_slice=slice_)
+    if n_total is None:
+        n_total = int(round(float(packed[-1].item())))  # complete: the eigensolver synchronised
+        if n_total < 2:
+            raise ValueError("SIMCA needs at least 2 samples in a class")
+        if theta_mode >= 2 and slice_[1] > 1:
+            allreduce([theta[2:]])  # θ3 partials of the ranks' trace slices
+    _mark("eig")
     # The host needs λ and θ for the limits (SciPy), the device needs 1/λ for
     # the fit-set scoring.  The scalars go to pinned memory on a side stream
     # that waits only for the eigensolve; 1/λ and the scoring are queued on the
@@ -409,13 +498,20 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
         host_buf[k:].copy_(theta, non_blocking=True)
         copied = torch.cuda.Event()
         copied.record(side)
-    sc = score(X, rows, n, evecs, mean64, inv, want_T=want_T, want_stats=True)
+    if n > 0:
+        sc = score(X, rows, n, evecs, mean64, inv, want_T=want_T, want_stats=True)
+    else:
+        sc = {"T": torch.empty((0, k), dtype=torch.float32, device=X.device) if want_T else None,
+              "T2": torch.empty(0, dtype=torch.float64, device=X.device),
+              "Q": torch.empty(0, dtype=torch.float32, device=X.device),
+              "stats": torch.zeros(4, dtype=torch.float64, device=X.device)}
+    _mark("fit_score")
     copied.synchronize()
     host = host_buf.numpy().copy()
     ev_h = host[:k]
     th = tuple(float(v) for v in host[k:k + 3])
     stats = sc["stats"]
-    if allreduce is not None:
+    if allreduce is not None and need_stats:
         allreduce([stats])  # stream-ordered: no host wait
     fit = ClassFit(k=k, n=n_total, p=p, mean64=mean64, evals=evals, P64=evecs, invcov=torch.diag(inv), inv_diag=inv, thetas=th,
                    evals_host=ev_h, T=sc["T"], T2=sc["T2"], Q=sc["Q"], stats_dev=stats, eig_iters=iters,

@@ -75,30 +75,34 @@ def _world(group) -> int:
 
 def _latent_cov(Z: torch.Tensor, group=None):
     """Column mean (f64) and covariance (f64, ddof 1) of latent rows on the GPU
-    (of every rank's rows: one all-reduce of the d×d Gram, Σz and n)."""
+    — of every rank's rows when ``group`` spans several ranks: each rank's Gram
+    about its own sample shift, packed as moments about zero
+    (``ocm_gram_pack``) and summed in one all-reduce; a rank without rows
+    contributes zeros (nothing of it enters the mean or the shift)."""
     n, d = Z.shape
-    shift64 = engine.colmean(Z, None, min(n, engine.SHIFT_SAMPLE))
-    if _world(group) > 1:
-        import torch.distributed as dist
+    if _world(group) == 1:
+        shift32 = engine.cast_f32(engine.colmean(Z, None, min(n, engine.SHIFT_SAMPLE)))
+        G, cs = engine.gram(Z, None, [0, n], shift32)
+        C, mean = engine.cov_from_gram([(1.0, G[0], cs[0])], shift32, n)
+        return mean, C
+    import torch.distributed as dist
 
-        dist.all_reduce(shift64, group=group)
-        shift64 /= _world(group)
-    shift32 = engine.cast_f32(shift64)
-    G, cs = engine.gram(Z, None, [0, n], shift32)
-    if _world(group) > 1:
-        import torch.distributed as dist
-
-        cnt = torch.tensor([float(n)], dtype=torch.float64, device=Z.device)
-        for t in (G, cs, cnt):
-            dist.all_reduce(t, group=group)
-        n = int(round(float(cnt.item())))
-    C, mean = engine.cov_from_gram([(1.0, G[0], cs[0])], shift32, n)
+    if n > 0:
+        shift32 = engine.cast_f32(engine.colmean(Z, None, min(n, engine.SHIFT_SAMPLE)))
+        G, cs = engine.gram(Z, None, [0, n], shift32)
+        packed = engine.gram_pack(G[0], cs[0], shift32, n)
+    else:
+        packed = torch.zeros(d * (d + 1) // 2 + d + 1, dtype=torch.float64, device=Z.device)
+    dist.all_reduce(packed, group=group)
+    C, mean = engine.cov_from_packed(packed, d)
     return mean, C
 
 
 def latent_T2(Z: torch.Tensor, mean64: torch.Tensor, A: torch.Tensor) -> torch.Tensor:
     """T²_i = (z_i − μ)ᵀ A (z_i − μ) (fp64) by the SIMCA scoring kernel with P = I."""
     n, d = Z.shape
+    if n == 0:
+        return torch.empty(0, dtype=torch.float64, device=Z.device)
     eye = torch.eye(d, dtype=torch.float64, device=Z.device)
     return engine.score(Z, None, n, eye, mean64, A, want_T2=True, want_Q=False)["T2"]
 

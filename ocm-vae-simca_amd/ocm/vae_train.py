@@ -26,7 +26,6 @@ replay is still one launch.  BatchNorm statistics stay per rank, as in DDP;
 from __future__ import annotations
 
 import os
-import warnings
 
 import torch
 import torch.distributed as dist
@@ -39,8 +38,16 @@ __all__ = ["GraphedVAETrainer"]
 class GraphedVAETrainer:
     """One optimizer step per ``step(x)``; ``x`` (B, L) float32 on the device.
 
-    loss: "bce" (beta_vae_bce_loss) or "cosine" (beta_vae_cosine_loss);
-    lr / weight_decay as torch.optim.Adam (vae_bce_nut.py:155-159)."""
+    loss: "bce" (vae_model.beta_vae_bce_loss: BCE-with-logits on the
+    de-standardised output), "cosine" (beta_vae_cosine_loss), or the
+    utils/final_vaesimca.py:208-224 variants "bce_prob" (probability BCE on the
+    min-max scaled reconstruction, its "X_bce") and "euclidean" (MSE, its
+    "X_euclidean"); lr / weight_decay as torch.optim.Adam
+    (vae_bce_nut.py:155-159).  ``graph=True`` needs the runtime flag set by
+    importing ``ocm`` before torch initialises the GPU, and raises otherwise
+    (pass ``graph=False`` for eager steps)."""
+
+    LOSSES = ("bce", "cosine", "bce_prob", "euclidean")
 
     def __init__(self, model, batch: int, lr=1e-3, weight_decay=0.0, beta=1.0, loss="bce",
                  dtype=torch.bfloat16, graph=True, warmup=3, restore=True, group=None, grad_allreduce=None):
@@ -56,6 +63,8 @@ class GraphedVAETrainer:
             self._flatten_grads(dev)
             self._broadcast_state()
         self.beta = float(beta)
+        if loss not in self.LOSSES:
+            raise ValueError(f"loss must be one of {self.LOSSES}")
         self.loss = loss
         self.dtype = dtype
         # torch's fused Adam on the GPU (one multi-tensor kernel per step): 480 vs 437
@@ -71,9 +80,9 @@ class GraphedVAETrainer:
         if graph and os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") != "0":
             # the runtime's packet-capture replay races (ocm/__init__.py); the
             # flag only takes effect if set before HIP initialises
-            warnings.warn("DEBUG_CLR_GRAPH_PACKET_CAPTURE is not 0 (import ocm before torch initialises the GPU): "
-                          "HIP-graph VAE steps are unsafe on this runtime, running the step eagerly")
-            graph = False
+            raise RuntimeError("GraphedVAETrainer(graph=True): DEBUG_CLR_GRAPH_PACKET_CAPTURE is not 0, and HIP-graph "
+                               "replays race on this runtime without it (ocm/__init__.py).  Import ocm (or set the "
+                               "variable to 0) before torch initialises the GPU, or pass graph=False for eager steps")
         self.graphed = graph
         if graph:
             self._capture(warmup)
@@ -110,8 +119,12 @@ class GraphedVAETrainer:
         x_rec, mu, logvar = x_rec.float(), mu.float(), logvar.float()
         if self.loss == "bce":
             recon = V.bce_recon_term(self.x, x_rec)
-        else:
+        elif self.loss == "cosine":
             recon = V.cosine_recon_term(self.x, x_rec)
+        elif self.loss == "bce_prob":
+            recon = V.bce_prob_recon_term(self.x, x_rec)
+        else:
+            recon = V.mse_recon_term(self.x, x_rec)
         kl = V.kl_term(mu, logvar)
         total = recon + self.beta * kl
         total.backward()

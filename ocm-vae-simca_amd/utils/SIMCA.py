@@ -27,10 +27,13 @@ Documented deviations:
 * float64 inputs are computed in float32 on the GPU (the reference runs its
   PCA in float64 then); limits and decisions agree at the tolerances of
   tests/test_gpu_northstar.py::test_float64_input_vs_reference (DESIGN.md §5);
-* ``n_components`` (and a CV sweep's ``LV_max``) is at most 64 when p > 64:
-  the subspace eigensolver (ocm_eig_topk) and the scoring / CV kernels keep
-  the components in one 64-wide block and raise ``ValueError`` beyond it; the
-  reference allows any k ≤ min(n, p).
+* ``n_components`` may be any k ≤ p as in the reference; beyond 64 the
+  eigensolver's block steps run on the host in fp64 and scoring takes one
+  launch per 64 components, and a CV sweep with ``LV_max`` > 64 runs the
+  generic refit loop instead of the fold engine;
+* a fit whose leading k eigenpairs do not converge (no spectral gap after
+  component k within the iteration budget) raises ``ocm.OcmNotConverged``
+  instead of returning loadings of an unconverged subspace.
 """
 from __future__ import annotations
 
@@ -187,6 +190,7 @@ class SIMCA(BaseEstimator, ClassifierMixin):
         T2_limit = limits.t2_limit(self, T2m, k)
         Q_limit = limits.q_limit(self, Qm, fit.thetas)
         D_limit = limits.critic_distance(self, T2_limit, Q_limit, fit.thetas, k)
+        engine._mark("limits")
         dec = self._decision(T2_limit, Q_limit, D_limit)
         dt = self._out_dtype
         red = {}

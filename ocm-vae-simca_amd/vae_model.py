@@ -43,6 +43,10 @@ class ConvVAE1D(nn.Module):
     reference) and de-standardises the reconstruction.
     """
 
+    # decision thresholds travel with checkpoints (vae_model.py:29-32); the
+    # copy in utils/final_vaesimca.py:95-96 carries ("threshold", "q_threshold")
+    THRESHOLD_BUFFERS = ("threshold", "threshold_q", "threshold_h", "threshold_f")
+
     def __init__(self, input_length, latent_dim, mean, std, conv_blocks=3, n_filters=32, kernel_size=9, stride=2,
                  hidden_fc=256, activation="elu", dropout=0.0, use_batchnorm=True, beta=1.0):
         super().__init__()
@@ -51,8 +55,7 @@ class ConvVAE1D(nn.Module):
         self.beta = beta
         self.dropout = dropout
         self.use_batchnorm = use_batchnorm
-        # decision thresholds travel with checkpoints (vae_model.py:29-32)
-        for name in ("threshold", "threshold_q", "threshold_h", "threshold_f"):
+        for name in self.THRESHOLD_BUFFERS:
             self.register_buffer(name, torch.tensor(0.0))
 
         act_cls = nn.ELU if activation == "elu" else nn.GELU
@@ -154,6 +157,23 @@ def bce_recon_term(x, x_recon, eps=1e-8):
     target = ((x - lo) / (hi - lo + eps)).clamp(0.0, 1.0)
     return F.binary_cross_entropy_with_logits(x_recon.reshape(x_recon.shape[0], -1),
                                               target.reshape(target.shape[0], -1), reduction="mean")
+
+
+def _minmax_scaled(x, v, eps):
+    lo = x.min(dim=1, keepdim=True)[0]
+    hi = x.max(dim=1, keepdim=True)[0]
+    return ((v - lo) / (hi - lo + eps)).clamp(0.0, 1.0)
+
+
+def bce_prob_recon_term(x, x_recon, eps=1e-8):
+    """utils/final_vaesimca.py:213-221: probability BCE of the reconstruction
+    and the input, both min-max scaled by the input's per-sample range."""
+    return F.binary_cross_entropy(_minmax_scaled(x, x_recon, eps), _minmax_scaled(x, x, eps), reduction="mean")
+
+
+def mse_recon_term(x, x_recon):
+    """utils/final_vaesimca.py:208-209: mean squared error."""
+    return F.mse_loss(x_recon, x, reduction="mean")
 
 
 def cosine_recon_term(x, x_recon, eps=1e-8):

@@ -87,6 +87,34 @@ def pca_full(X: np.ndarray, precision: str = "exact", ncomp: int | None = None):
     return mean, ev, Vt, scores
 
 
+def covariance_chunked(X: np.ndarray, chunk: int = 32768):
+    """fp64 mean and covariance (ddof 1) of a large float32 X without an fp64
+    copy of it: Σ over row chunks of the shifted Gram YᵀY (one host dsyrk per
+    chunk, y = x − s with s the mean of the first chunk), then
+    C = (G − n·d·dᵀ)/(n − 1), μ = s + d — the covariance whose eigenpairs the
+    reference's full SVD returns (utils/SIMCA.py:64-66 → sklearn/decomposition/
+    _pca.py:569-584, explained_variance_ = S²/(n − 1)).  For the headline-size
+    (1M × 2048) parity test."""
+    n, p = X.shape
+    s = np.asarray(X[: min(n, chunk)], dtype=np.float64).mean(axis=0)
+    G = np.zeros((p, p))
+    cs = np.zeros(p)
+    for a in range(0, n, chunk):
+        Y = np.asarray(X[a:a + chunk], dtype=np.float64) - s
+        G += Y.T @ Y
+        cs += Y.sum(axis=0)
+    d = cs / n
+    return s + d, (G - n * np.outer(d, d)) / (n - 1)
+
+
+def eig_desc(C: np.ndarray):
+    """Eigenvalues (descending) and loadings rows with the svd_flip sign."""
+    w, V = np.linalg.eigh(C)
+    order = np.argsort(w)[::-1]
+    Vt, _ = svd_flip_rows(V[:, order].T)
+    return w[order], Vt
+
+
 def randomized_pca(X: np.ndarray, k: int, rng: np.random.RandomState,
                    n_oversamples: int = 10, n_iter: int | str = "auto"):
     """Restatement of the solver ``PCA(k).fit`` picks for p > 1000

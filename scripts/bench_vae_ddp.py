@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--latent-rows", type=int, default=262144, help="calibration rows encoded per rank")
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--dump", default=None, help="rank 0: save latents, Q and the SIMCA-on-latents outputs (.npz)")
     args = ap.parse_args()
 
     import ocm  # noqa: F401  (graph-capture runtime flag before the GPU initialises)
@@ -90,6 +91,7 @@ def main():
 
     for i in range(args.warmup):
         tr.step(batch(i))
+    loss0 = float(tr.out[0].item()) if args.warmup else float("nan")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -134,6 +136,12 @@ def main():
     t_stats = time.perf_counter() - t3
 
     lo, hi = shard_bounds(args.rows, rank, world)
+    if rank == 0 and args.dump:
+        import numpy as np
+
+        np.savez(args.dump, mus=mus.cpu().numpy(), q=q.cpu().numpy(), lmean=lmean.cpu().numpy(),
+                 inv=inv.cpu().numpy(), t2lim=t2lim, qlim=qlim, accept=accept.cpu().numpy(), f=f.cpu().numpy(),
+                 fcrit=fcrit, world=world)
     if rank == 0:
         print(json.dumps({
             "metric": "VAE-SIMCA DDP train samples/s", "value": round(args.steps * B * world / dt, 1),
@@ -142,7 +150,8 @@ def main():
             "config": {"workload": f"ConvVAE1D cb=3 nf=3 ks=7 hid=64 d=32, B={B}/rank, L={L}, "
                                    f"{args.rows} rows global ({hi - lo} on rank 0), grad all-reduce in the step graph",
                        "params": sum(p.numel() for p in m.parameters())},
-            "final_loss": round(loss, 5), "data_gen_s": round(t_data, 2),
+            "loss_after_warmup": round(loss0, 5), "final_loss": round(loss, 5), "data_gen_s": round(t_data, 2),
+            "params_finite": all(bool(torch.isfinite(p_).all()) for p_ in m.parameters()),
             "latents": {"rows_per_rank": nl, "encode_s": round(t_enc, 3), "stats_s": round(t_stats, 4),
                         "t2_limit": float(t2lim), "q_limit": float(qlim), "f_crit": float(fcrit),
                         "accept_rate": float(acc.item()) / (nl * world)},

@@ -63,14 +63,56 @@ def cov_from_gram(terms, shift32, n):
     return torch.from_numpy(C), torch.from_numpy(shift32.numpy().astype(np.float64) + d)
 
 
-def eig_topk(C, k, theta_mode, tol=None, max_iter=None):
-    w, V = np.linalg.eigh(C.numpy())
+def gram_pack(G, cs, shift32, n, out=None):
+    """ocm_gram_pack: moments about zero, upper triangle + Σx + n."""
+    s = shift32.numpy().astype(np.float64)
+    c = cs.numpy()
+    M = G.numpy() + np.outer(s, c) + np.outer(c, s) + n * np.outer(s, s)
+    iu = np.triu_indices(s.size)
+    return torch.from_numpy(np.concatenate([M[iu], c + n * s, [float(n)]]))
+
+
+def cov_from_packed(packed, p):
+    a = packed.numpy()
+    tri = p * (p + 1) // 2
+    M = np.zeros((p, p))
+    M[np.triu_indices(p)] = a[:tri]
+    M = M + np.triu(M, 1).T
+    n = a[-1]
+    mu = a[tri:tri + p] / n
+    return torch.from_numpy((M - n * np.outer(mu, mu)) / (n - 1)), torch.from_numpy(mu)
+
+
+def _theta3_slice(D, slice_):
+    """Σ over this slice's 64×64 upper-triangle tiles (off-diagonal ×2) of
+    (D²)∘D — the tile split of the ocm_eig_topk_ex trace GEMM."""
+    p = D.shape[0]
+    nt = (p + 63) // 64
+    tiles = [(i, j) for i in range(nt) for j in range(i, nt)]
+    s, S = slice_
+    t0, t1 = len(tiles) * s // S, len(tiles) * (s + 1) // S
+    D2 = D @ D
+    tot = 0.0
+    for i, j in tiles[t0:t1]:
+        blk = (D2[i * 64:(i + 1) * 64, j * 64:(j + 1) * 64] * D[i * 64:(i + 1) * 64, j * 64:(j + 1) * 64]).sum()
+        tot += blk if i == j else 2.0 * blk
+    return tot
+
+
+def eig_topk(C, k, theta_mode, tol=None, max_iter=None, theta3_slice=(0, 1)):
+    Cn = C.numpy()
+    w, V = np.linalg.eigh(Cn)
     w, V = w[::-1], V[:, ::-1]
     P = V[:, :k].T.copy()
     idx = np.argmax(np.abs(P), axis=1)
     P *= np.sign(P[np.arange(k), idx])[:, None]
     tail = w[k:]
     th = np.array([tail.sum(), (tail ** 2).sum(), (tail ** 3).sum()]) if theta_mode else np.zeros(3)
+    if theta_mode >= 2 and Cn.shape[0] > 64:
+        D = Cn - (V[:, :k] * w[:k]) @ V[:, :k].T
+        th[2] = _theta3_slice(D, theta3_slice)
+    elif theta_mode >= 2 and theta3_slice[0] != 0:
+        th[2] = 0.0  # p ≤ 64: slice 0 carries the whole θ3
     return torch.from_numpy(w[:k].copy()), torch.from_numpy(P), torch.from_numpy(th), 1
 
 
@@ -205,27 +247,38 @@ def invcov_from_evals(evals, rcond=1e-15):
     return torch.diag(torch.where(lam.abs() > cut, 1.0 / lam, torch.zeros_like(lam)))
 
 
-def fit_class(X, rows, n, k, theta_mode, want_T=True, keep_C=False, shift32=None, allreduce=None):
+def fit_class(X, rows, n, k, theta_mode, want_T=True, keep_C=False, shift32=None, allreduce=None, need_stats=True):
     """Same control flow and collectives as ocm.engine.fit_class."""
     p = X.shape[1]
     if shift32 is None:
         shift32 = cast_f32(colmean(X, rows, min(n, SHIFT_SAMPLE)))
-        if allreduce is not None:
-            allreduce([shift32], op="mean")
-    G, cs = gram(X, rows, [0, n], shift32)
-    n_total = n
-    if allreduce is not None:
-        cnt = torch.tensor([float(n)], dtype=torch.float64)
-        allreduce([G, cs, cnt])
-        n_total = int(round(cnt.item()))
-    C, mean64 = cov_from_gram([(1.0, G[0], cs[0])], shift32, n_total)
-    evals, evecs, theta, iters = eig_topk(C, k, theta_mode)
+    slice_ = (0, 1)
+    if allreduce is None:
+        G, cs = gram(X, rows, [0, n], shift32)
+        n_total = n
+        C, mean64 = cov_from_gram([(1.0, G[0], cs[0])], shift32, n_total)
+    else:
+        G, cs = gram(X, rows, [0, n], shift32)
+        packed = gram_pack(G[0], cs[0], shift32, n)
+        allreduce([packed])
+        C, mean64 = cov_from_packed(packed, p)
+        slice_ = (allreduce.rank, allreduce.world)
+        n_total = int(round(float(packed[-1])))
+    evals, evecs, theta, iters = eig_topk(C, k, theta_mode, theta3_slice=slice_)
+    if allreduce is not None and theta_mode >= 2 and slice_[1] > 1:
+        t3 = theta[2:].clone()
+        allreduce([t3])
+        theta[2:] = t3
     invcov = invcov_from_evals(evals)
     sc = score(X, rows, n, evecs, mean64, torch.diagonal(invcov).clone(), want_T=want_T, want_stats=True)
     stats = sc["stats"]
-    if allreduce is not None:
+    if allreduce is not None and need_stats:
         allreduce([stats])
     st = stats.numpy()
     return _Fit(k=k, n=n_total, p=p, mean64=mean64, evals=evals, P64=evecs, invcov=invcov, inv_diag=torch.diagonal(invcov).clone(),
                 thetas=tuple(float(v) for v in theta.numpy()), evals_host=evals.numpy(), T=sc["T"], T2=sc["T2"],
                 Q=sc["Q"], T2_stats=(st[0], st[1]), Q_stats=(st[2], st[3]), eig_iters=iters, C=None)
+
+
+def _mark(name):
+    """Phase marks (ocm.engine.set_phase_timer): no timer in the CPU tests."""

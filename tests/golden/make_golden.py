@@ -35,11 +35,14 @@ outputs.  They are data (inputs and expected outputs), not reference source.
 * final_vaesimca.npz — the inline latent-statistics (utils/final_vaesimca.py:
   428-436) and full-distance decision (:511-533) statements, extracted the same
   way and executed on the vae_a latents.
+* final_losses.npz   — the script's three losses (:198-224), its reconstruction
+  error Q in the X_bce (min-max scaled) and plain branches (:417-425), and the
+  seeded state_dict of its ConvVAE1D copy (:72-193).
 
 np.random.seed is set before every fit: the reference's second PCA(k) draws
 from NumPy's global RNG (SURVEY.md §8c caveat 1).
 
-    python tests/golden/make_golden.py [ns f64 score vaesimca final]   # a subset
+    python tests/golden/make_golden.py [ns f64 score vaesimca final final_losses]   # a subset
 """
 from __future__ import annotations
 
@@ -495,10 +498,57 @@ def make_final_vaesimca():
     print("final_vaesimca fcrit", float(out["fcrit"]), "accept", int(out["pred_class0"].sum()))
 
 
+def make_final_losses():
+    """utils/final_vaesimca.py: the three losses (:198-224), the calibration /
+    test reconstruction error Q in both branches (:417-425), and the state_dict
+    of the script's own ConvVAE1D copy (:72-193, seeded), each taken from the
+    script's syntax tree and executed alone."""
+    import torch
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    path = os.path.join(REF, "utils", "final_vaesimca.py")
+    ns = {"torch": torch, "F": F, "nn": nn, "np": np}
+    exec(_extract(path, 198, 224), ns)
+    rng = np.random.default_rng(77)
+    B, L, d = 48, 300, 8
+    wl = np.linspace(0, 1, L)
+    x = (1.0 + 0.5 * wl + 0.2 * rng.standard_normal((B, 1)) * np.sin(7 * wl) +
+         0.02 * rng.standard_normal((B, L))).astype(np.float32)
+    x_recon = (x + 0.08 * rng.standard_normal((B, L))).astype(np.float32)  # partly outside [min, max]
+    mu = rng.standard_normal((B, d)).astype(np.float32)
+    logvar = (0.3 * rng.standard_normal((B, d))).astype(np.float32)
+    out = {"x": x, "x_recon": x_recon, "mu": mu, "logvar": logvar}
+    t = [torch.from_numpy(a) for a in (x, x_recon, mu, logvar)]
+    for name in ("cosine", "euclidean", "bce"):
+        total, recon, kl = ns[f"beta_vae_{name}_loss"](*t, beta=0.7)
+        out[f"{name}_total"] = np.float64(total.item())
+        out[f"{name}_recon"] = np.float64(recon)
+        out[f"{name}_kl"] = np.float64(kl)
+    for loss_type in ("X_bce", "X_euclidean"):
+        ns_q = {"torch": torch, "np": np, "x": t[0], "x_rec": t[1], "loss_type": loss_type}
+        exec(_extract(path, 417, 425), ns_q)
+        out[f"rec_err_{loss_type}"] = np.asarray(ns_q["rec_err"])
+    # the script's ConvVAE1D copy: seeded init → state_dict (keys, order, values)
+    ns_m = {"torch": torch, "nn": nn, "F": F, "np": np}
+    exec(_extract(path, 0, 0, names={"ConvVAE1D"}), ns_m)
+    torch.manual_seed(5)
+    mean, std = x.mean(0), x.std(0) + 1e-3
+    m = ns_m["ConvVAE1D"](L, d, mean, std, conv_blocks=2, n_filters=3, kernel_size=5, hidden_fc=16)
+    sd = m.state_dict()
+    out["sd_keys"] = np.array(list(sd.keys()))
+    for k, v in sd.items():
+        out["sd/" + k] = v.detach().numpy()
+    out["model_cfg"] = np.array(json.dumps({"L": L, "d": d, "conv_blocks": 2, "n_filters": 3, "kernel_size": 5,
+                                            "hidden_fc": 16}))
+    np.savez_compressed(os.path.join(HERE, "final_losses.npz"), **out)
+    print("final_losses", {k: float(v) for k, v in out.items() if np.ndim(v) == 0 and k.endswith(("_total", "_recon", "_kl"))})
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     extra = {"ns": make_northstar, "f64": make_f64, "score": make_score_pins, "vaesimca": make_vaesimca,
-             "final": make_final_vaesimca}
+             "final": make_final_vaesimca, "final_losses": make_final_losses}
     if argv:
         for name in argv:
             extra[name]()

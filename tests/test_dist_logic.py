@@ -118,14 +118,17 @@ def _simca_worker(rank, world, port, path, X, bounds, cfg):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg", [dict(type="alt", t2lim="Fdist", qlim="jm"),
-                                 dict(type="dd"),
-                                 dict(type="ci", t2lim="perc", qlim="perc")])
-def test_sharded_simca_gloo_world2_matches_single(tmp_path, cfg):
+@pytest.mark.parametrize("cfg,p", [(dict(type="alt", t2lim="Fdist", qlim="jm"), 48),
+                                   (dict(type="alt", t2lim="Fdist", qlim="jm"), 160),
+                                   (dict(type="dd"), 48),
+                                   (dict(type="ci", t2lim="perc", qlim="perc"), 48)])
+def test_sharded_simca_gloo_world2_matches_single(tmp_path, cfg, p):
+    """p = 160: three 64-column tiles, so the θ3 trace tiles are split
+    between the ranks (ocm_eig_topk_ex slices) and summed by the all-reduce."""
     import ocm.dist as od
     from oracle import simca_oracle as O
 
-    X = O.synth_spectra(1500, 48, 4, rank=10, seed=3, outlier_frac=0.05)
+    X = O.synth_spectra(1500, p, 4, rank=10, seed=3, outlier_frac=0.05)
     bounds = [(0, 640), (640, 1500)]
     path = str(tmp_path / "r.npz")
     ctx = mp.get_context("spawn")

@@ -2,9 +2,12 @@
 + predict on 1M × 2048 fp32 spectra in HBM, k = 20, alt / Fdist / jm — the
 exact bench workload (bench.synth_device) through the drop-in ``utils.SIMCA``.
 
-The oracle cannot run at this size in seconds, so the checks are identities
-that hold for an exact PCA at any size (utils/SIMCA.py:62-99), plus a second,
-independent Gram arithmetic:
+Against the fp64 oracle at this size: the covariance of all 1M rows by a
+chunked host dsyrk (oracle.covariance_chunked, ≈ 4 TFLOP on the box's
+cores) and its eigh — eigenvalues, θ1..θ3, both limits, and T², Q and the
+decisions of a 100k-row sample (every 10th row) scored by the oracle.  Plus
+identities that hold for an exact PCA at any size (utils/SIMCA.py:62-99) and a
+second, independent Gram arithmetic:
 
 * Σ_i T²_i = k·(n − 1): T² = Σ_c t_ic²/λ_c and Σ_i t_ic² = (n − 1)·λ_c;
 * Σ_i Q_i = (n − 1)·θ1: the residual sum of squares is the tail of the
@@ -144,3 +147,44 @@ def test_c3_full_size_fold_engine_vs_refit_loop():
     ps = np.asarray(slow["by_combo"][0]["prediction"])
     assert pf.shape == ps.shape == (N,)
     assert int((pf != ps).sum()) <= 20, int((pf != ps).sum())
+
+
+@pytest.mark.timeout(600)
+def test_headline_vs_fp64_oracle(fitted):
+    """the headline configuration itself against the fp64
+    oracle (utils/SIMCA.py:62-99, 120-145): eigenvalues[:20] rtol 1e-6, θ1..θ3
+    and both limits rtol 1e-5, T² / Q of a 100k-row sample rtol 1e-4 and its
+    decisions outside the 1e-4 band."""
+    import math
+
+    import torch
+
+    from oracle import simca_oracle as O
+
+    X, _, est, pred = fitted
+    fit = est._fits[0]
+    m = est._model[0]
+    Xh = X.cpu().numpy()
+    mean, C = O.covariance_chunked(Xh)
+    ev, Vt = O.eig_desc(C)
+    np.testing.assert_allclose(fit.evals.cpu().numpy(), ev[:K], rtol=1e-6)
+    th = O.tail_thetas(ev, K)
+    np.testing.assert_allclose(fit.thetas, th, rtol=1e-5)
+    st = O.DDState()
+    t2l = O.t2_limit(np.zeros(N), K, "Fdist", 0.95, st)
+    ql = O.q_limit(None, th, "jm", 0.95, st)
+    np.testing.assert_allclose([m["T2_limit"], m["Q_limit"]], [t2l, ql], rtol=1e-5)
+    np.testing.assert_allclose(fit.mean64.cpu().numpy(), mean, rtol=1e-7, atol=1e-7 * np.abs(mean).max())
+    idx = np.arange(0, N, 10)
+    _, T2o, Qo = O.project_scores(Xh[idx], Vt[:K], mean, np.diag(1.0 / ev[:K]))
+    it = torch.from_numpy(idx).to(fit.T2.device)
+    T2g = fit.T2[it].cpu().numpy()
+    Qg = fit.Q[it].cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(T2g, T2o, rtol=1e-4, atol=1e-6 * np.median(T2o))
+    np.testing.assert_allclose(Qg, Qo, rtol=1e-4, atol=1e-6 * np.median(Qo))
+    d = np.sqrt((T2o / t2l) ** 2 + (Qo.astype(np.float64) / ql) ** 2)
+    dl = math.sqrt(2)
+    clear = np.abs(d - dl) > 1e-4 * dl
+    got = np.asarray(pred.cpu().numpy()).reshape(-1)[idx]
+    assert clear.mean() > 0.99
+    np.testing.assert_array_equal(got[clear].astype(bool), (d < dl)[clear])

@@ -195,3 +195,38 @@ def test_outlier_rows_limits_vs_fp64_oracle(frac, lo, hi):
     shift = engine.cast_f32(engine.colmean(Xd, None, 4096))
     engine.gram(Xd, None, [0, n], shift)
     assert 0 < engine.last_gram_marks(0)
+
+
+@pytest.mark.timeout(300)
+def test_k96_wide_block_vs_fp64_oracle():
+    """n_components beyond one 64-wide block (k = 96 at
+    p = 2048, the reference allows any k ≤ min(n, p), utils/SIMCA.py:34-40):
+    the eigensolver's 144-column block with host b×b steps, and scoring in two
+    component blocks (64 + 32), against the fp64 oracle."""
+    from oracle.simca_oracle import synth_spectra
+
+    n, p, k = 20_000, 2048, 96
+    X = synth_spectra(n + 4000, p, k, rank=140, seed=4242, outlier_frac=800 / 24_000)
+    _check_vs_oracle(X[:n], X[n:], k, [("alt", "Fdist", "jm"), ("ci", "chi2", "chi2box")])
+
+
+def test_eig_not_converged_raises():
+    """a covariance with no gap at k (a nearly flat spectrum)
+    cannot converge in a short iteration budget; the engine raises
+    OcmNotConverged instead of handing on an unconverged subspace."""
+    import torch
+
+    from ocm import OcmNotConverged, engine
+
+    p, k = 256, 20
+    rng = np.random.default_rng(9)
+    Qm, _ = np.linalg.qr(rng.standard_normal((p, p)))
+    lam = np.linspace(1.0, 0.995, p)
+    C = torch.from_numpy((Qm * lam) @ Qm.T).cuda()
+    with pytest.raises(OcmNotConverged):
+        engine.eig_topk(C, k, 2, max_iter=30)
+    # the same call with a gap converges
+    lam[:k] *= 10
+    C = torch.from_numpy((Qm * lam) @ Qm.T).cuda()
+    ev, _, _, it = engine.eig_topk(C, k, 2, max_iter=30)
+    np.testing.assert_allclose(ev.cpu().numpy(), np.sort(lam)[::-1][:k], rtol=1e-10)

@@ -53,12 +53,13 @@ def _snv_ref(x):
 @pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")
 @pytest.mark.parametrize("snv,setting", [(True, (5, 2, 1, 1.0)), (False, (15, 2, 1, 1.0)), (True, (15, 2, 1, 1.0)),
                                          (True, None), (False, (11, 4, 3, 2.0))])
-@pytest.mark.parametrize("p", [517, 2048, 1028, 36])
+@pytest.mark.parametrize("p", [517, 2048, 1028, 36, 4096])
 def test_snv_savgol_device(snv, setting, p):
     """p = 517: the general one-workgroup-per-row kernel; p % 4 == 0 with the
     drivers' filters (none, w = 5, w = 15): the wave-per-row kernel, with a
     partial last 256-column segment (1028), a tiny row (36) and a partial last
-    group of four rows (301 rows)."""
+    group of four rows (301 rows); p = 4096 (C5 spectra): 67 KB of dynamic LDS
+    at w = 15."""
     import torch
     from ocm import preprocess
 

@@ -163,3 +163,40 @@ def test_c4_graph_step_with_grad_allreduce():
     assert np.isfinite(la).all() and np.isfinite(lb).all() and res["params_finite"]
     assert la[-5:].mean() < la[0]
     np.testing.assert_allclose(la[-5:].mean(), lb[-5:].mean(), rtol=0.05)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+def test_c5_shape_rank_share_and_latent_simca(tmp_path):
+    """C5 (BASELINE.json: VAE-SIMCA DDP, 10M × 4096) at one rank's share of the
+    global matrix (10M / 8 = 1.25M rows × 4096, 20.5 GB of on-device Philox
+    shards, scripts/bench_vae_ddp.py): the L = 4096 network (1.59 M params),
+    B = 512, bf16 graphed steps, then SIMCA-on-latents on its latents
+    (utils/final_vaesimca.py:428-442, 510-533) checked against the oracle.
+    Child process: the step graph holds its resources until the process ends."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from oracle import simca_oracle as O
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    dump = str(tmp_path / "c5.npz")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(here), "scripts", "bench_vae_ddp.py"),
+                        "--rows", "1250000", "--steps", "20", "--warmup", "5", "--latent-rows", "65536",
+                        "--dump", dump], capture_output=True, text=True, timeout=300, cwd=os.path.dirname(here))
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["config"]["params"] > 1_500_000 and res["params_finite"]
+    assert np.isfinite(res["final_loss"]) and res["final_loss"] < res["loss_after_warmup"]
+    g = np.load(dump)
+    mean, inv, t2thr, qthr = O.latent_stats(g["mus"].astype(np.float64), g["q"].astype(np.float64))
+    np.testing.assert_allclose(g["lmean"], mean, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(g["inv"], inv, rtol=1e-5, atol=1e-6 * np.abs(inv).max())
+    np.testing.assert_allclose([float(g["t2lim"]), float(g["qlim"])], [t2thr, qthr], rtol=1e-5)
+    acc, f, fcrit = O.full_distance_decision(g["mus"].astype(np.float64), mean, g["q"].astype(np.float64))
+    np.testing.assert_allclose(float(g["fcrit"]), fcrit, rtol=1e-6)
+    band = np.abs(f - fcrit) > 1e-5 * fcrit
+    np.testing.assert_array_equal(g["accept"][band], acc[band])
+    assert 0.5 < res["latents"]["accept_rate"] <= 1.0
