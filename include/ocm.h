@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCM_ABI_VERSION 3
+#define OCM_ABI_VERSION 4
 
 #define OCM_OK 0
 #define OCM_ERR_ARG (-1)         /* invalid argument (maps to ValueError) */
@@ -307,6 +307,35 @@ int ocm_confusion_counts(ocm_ctx* ctx, const double* accept, int64_t m, int64_t 
  * float32 (ldx, ldo; out may not alias X).  window odd ≤ 63, p ≤ 12288. */
 int ocm_snv_savgol_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, int32_t p, int32_t snv,
                        int32_t window, const double* taps, float* out, int64_t ldo, void* stream);
+
+/* ---- float64 spectra: the PCA precision follows the input dtype ----
+ * The reference's PCA runs in the input dtype (utils/SIMCA.py:64-66 →
+ * sklearn _pca.py:544-584 on float64 X), and its scores, residuals and Q are
+ * then float64 (utils/SIMCA.py:65-71, 104-107, 127-130).  X [dev] n×p float64
+ * (ldx elements); rows as above.
+ *
+ * ocm_colmean_f64: column mean of the first n processed rows (fp64).
+ * ocm_gram_f64: per-segment shifted Gram Σ (x − s)(x − s)ᵀ and Σ (x − s) on
+ *   fp64 MFMA (v_mfma_f64_16x16x4f64), no digit split; arguments and outputs as
+ *   ocm_gram_f32 (the float shift is exact in fp64), so ocm_cov_from_gram /
+ *   ocm_gram_pack apply unchanged.
+ * ocm_score_f64_diag: t = P·(x − μ), T² = Σ t²·a_diag, Q = ‖x − μ‖² − ‖t‖²
+ *   (fp64: no cancellation issue at ≈1e-13 relative), fused decision and the
+ *   moments, as ocm_score_f32_diag; T_out m×k float64, Q_out m float64; any
+ *   1 ≤ k ≤ p (component blocks of 64 beyond that).
+ * ocm_decide_f64: ocm_decide with float64 Q. */
+int ocm_colmean_f64(ocm_ctx* ctx, const double* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                    double* mean_out, void* stream);
+int ocm_gram_f64(ocm_ctx* ctx, const double* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                 const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
+                 void* stream);
+int ocm_score_f64_diag(ocm_ctx* ctx, const double* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
+                       const double* P, const double* mu, const double* a_diag, int32_t k, double* T_out,
+                       double* T2_out, double* Q_out, const ocm_decision* dec, double* accept_out,
+                       int64_t accept_stride, double* stats_out, void* stream);
+int ocm_decide_f64(ocm_ctx* ctx, const double* T2, const double* Q, int64_t m, const ocm_decision* dec,
+                   double* t2red_out, double* qred_out, double* dred_out, double* accept_out, int64_t accept_stride,
+                   void* stream);
 
 /* ---- VAE network support (vae_model.py:37-81, BatchNorm1d in train mode) ----
  * Training-mode batch norm over (N, C, L) contiguous activations, bf16 or f32,

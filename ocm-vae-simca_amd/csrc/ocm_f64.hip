@@ -1,0 +1,526 @@
+// float64 spectra: the PCA precision follows the input dtype, as sklearn does
+// for the reference's PCA(svd_solver='full') on float64 X
+// (utils/SIMCA.py:64-66 → sklearn/decomposition/_pca.py:544-584: the SVD runs
+// in the input dtype) and as its NumPy scoring does (utils/SIMCA.py:65-71,
+// 104-107, 127-130: float64 T, X̂, residual and Q).
+//
+// k_gram_f64   shifted Gram Σ (x − s)(x − s)ᵀ on fp64 MFMA
+//              (v_mfma_f64_16x16x4f64): 128×128 upper-triangle tiles, four
+//              waves of 64×64 (4×4 blocks of 16×16, 128 accumulator VGPRs),
+//              operands loaded straight from L2/HBM four row-steps ahead (16
+//              MFMAs of 64 cycles per step hide them; no LDS, no barrier), rows
+//              split into chunks whose fp64 partials are summed in a fixed order.
+//              MFMA-bound: n·p(p+1) flops at the fp64 matrix rate.
+// k_score_f64  t = P·(x − μ) on the same MFMA (M = 16 components, N = 16
+//              spectra, K = 4 wavelengths per step), ‖x − μ‖² beside it, then
+//              Q = ‖y‖² − ‖t‖² (exact to ~1e-13 relative in fp64 — the identity
+//              the f32 kernels cannot afford), T² = Σ t²/λ, fused decision and
+//              the χ² moment partials.  One HBM pass; HBM/MFMA balanced at k ≤ 32.
+#include "ocm_internal.h"
+
+#include <algorithm>
+
+namespace {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+struct DecF64 {
+  int32_t enabled;
+  int32_t type;
+  double t2_scale, q_scale, dlim;
+};
+
+// ---------------------------------------------------------------------------
+// column mean (fp64 rows): per (column, row split) partial sums
+// ---------------------------------------------------------------------------
+__global__ void k_colsum_part_f64(const double* __restrict__ X, int64_t ldx, const int64_t* __restrict__ rows,
+                                  int64_t n, int p, int64_t rows_per_split, double* __restrict__ part) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  const int sp = blockIdx.y;
+  if (col >= p) return;
+  const int64_t a = (int64_t)sp * rows_per_split;
+  const int64_t e = min(n, a + rows_per_split);
+  double v = 0.0;
+  for (int64_t r = a; r < e; ++r) v += X[(rows ? rows[r] : r) * ldx + col];
+  part[(size_t)sp * p + col] = v;
+}
+
+__global__ void k_colsum_final_f64(const double* __restrict__ part, int nsplit, int p, double inv_n,
+                                   double* __restrict__ mean) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= p) return;
+  double v = 0.0;
+  for (int s = 0; s < nsplit; ++s) v += part[(size_t)s * p + col];
+  mean[col] = v * inv_n;
+}
+
+// ---------------------------------------------------------------------------
+// k_gram_f64
+// ---------------------------------------------------------------------------
+constexpr int GT64 = 128;  // tile edge
+constexpr int GD64 = 4;    // row-steps (of 4 rows) loaded ahead
+
+// f64 16x16x4 operand / result map (as k_dgemm): A[i][k] from lane (i = l&15,
+// k = l>>4), B[k][j] from lane (k = l>>4, j = l&15), D[i][j] in lane
+// (j = l&15) register r with i = (l>>4) + 4r.
+__global__ __launch_bounds__(256, 1) void k_gram_f64(const double* __restrict__ X, int64_t ldx,
+                                                     const int64_t* __restrict__ rows, int64_t r_begin,
+                                                     int64_t r_end, int p, const float* __restrict__ shift,
+                                                     int64_t chunk, int nt, double* __restrict__ part,
+                                                     double* __restrict__ cpart) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r16 = lane & 15, ks = lane >> 4;
+  // linear upper-triangle tile index → (ti ≤ tj)
+  int rem = blockIdx.x, ti = 0;
+  while (rem >= nt - ti) {
+    rem -= nt - ti;
+    ++ti;
+  }
+  const int tj = ti + rem;
+  const int ntiles = nt * (nt + 1) / 2;
+  const int64_t c_lo = r_begin + (int64_t)blockIdx.y * chunk;
+  const int64_t c_hi = min(r_end, c_lo + chunk);
+
+  int ci[4], cj[4];
+  double si[4], sj[4], mi[4], mj[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int gi = ti * GT64 + wm * 64 + 16 * a + r16;
+    const int gj = tj * GT64 + wn * 64 + 16 * a + r16;
+    mi[a] = gi < p ? 1.0 : 0.0;
+    mj[a] = gj < p ? 1.0 : 0.0;
+    ci[a] = gi < p ? gi : p - 1;
+    cj[a] = gj < p ? gj : p - 1;
+    si[a] = (double)shift[ci[a]];
+    sj[a] = (double)shift[cj[a]];
+  }
+  f64x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = (f64x4){0.0, 0.0, 0.0, 0.0};
+  double csum[4] = {0.0, 0.0, 0.0, 0.0};
+  const bool want_cs = cpart && ti == tj && wn == 0;
+
+  // ring of GD64 row-steps of operands (raw x and the row's validity)
+  double ra[GD64][4], rb[GD64][4], rv[GD64];
+  auto load = [&](int slot, int64_t r0) {
+    const int64_t r = r0 + ks;
+    const bool ok = r < c_hi;
+    const int64_t rr = ok ? r : c_lo;  // a valid row, masked below
+    const double* xr = X + (rows ? rows[rr] : rr) * ldx;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      ra[slot][a] = xr[ci[a]];
+      rb[slot][a] = xr[cj[a]];
+    }
+    rv[slot] = ok ? 1.0 : 0.0;
+  };
+  const int64_t nsteps = (c_hi - c_lo + 3) / 4;
+#pragma unroll
+  for (int s = 0; s < GD64; ++s)
+    if (s < nsteps) load(s, c_lo + 4 * s);
+  for (int64_t s0 = 0; s0 < nsteps; s0 += GD64) {
+#pragma unroll
+    for (int s = 0; s < GD64; ++s) {
+      if (s0 + s >= nsteps) break;
+      double ya[4], yb[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        ya[a] = (ra[s][a] - si[a]) * (rv[s] * mi[a]);
+        yb[a] = (rb[s][a] - sj[a]) * (rv[s] * mj[a]);
+      }
+      if (s0 + s + GD64 < nsteps) load(s, c_lo + 4 * (s0 + s + GD64));
+      if (want_cs)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) csum[a] += ya[a];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[a], yb[b], acc[a][b], 0, 0, 0);
+    }
+  }
+  double* tp = part + ((size_t)blockIdx.y * ntiles + blockIdx.x) * GT64 * GT64;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int il = wm * 64 + 16 * a + ks + 4 * r, jl = wn * 64 + 16 * b + r16;
+        tp[il * GT64 + jl] = acc[a][b][r];
+      }
+  if (want_cs) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      double v = csum[a];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (ks == 0) cpart[((size_t)blockIdx.y * nt + ti) * GT64 + wm * 64 + 16 * a + r16] = v;
+    }
+  }
+}
+
+// chunk partials → G (both triangles) and column sums, fixed summation order
+__global__ __launch_bounds__(256) void k_gram_f64_reduce(const double* __restrict__ part,
+                                                         const double* __restrict__ cpart, int nchunks, int nt,
+                                                         int p, double* __restrict__ G, double* __restrict__ colsum) {
+  const int ntiles = nt * (nt + 1) / 2;
+  const int tile = blockIdx.x / 64, sub = blockIdx.x % 64;
+  int rem = tile, ti = 0;
+  while (rem >= nt - ti) {
+    rem -= nt - ti;
+    ++ti;
+  }
+  const int tj = ti + rem;
+  const int e = sub * 256 + threadIdx.x;  // element of the 128×128 tile
+  const int il = e / GT64, jl = e % GT64;
+  double v = 0.0;
+  for (int c = 0; c < nchunks; ++c) v += part[((size_t)c * ntiles + tile) * GT64 * GT64 + e];
+  const int gi = ti * GT64 + il, gj = tj * GT64 + jl;
+  if (gi < p && gj < p) {
+    G[(size_t)gi * p + gj] = v;
+    G[(size_t)gj * p + gi] = v;
+  }
+  if (ti == tj && sub == 0 && threadIdx.x < GT64) {
+    const int col = ti * GT64 + threadIdx.x;
+    double s = 0.0;
+    for (int c = 0; c < nchunks; ++c) s += cpart[((size_t)c * nt + ti) * GT64 + threadIdx.x];
+    if (col < p) colsum[col] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_score_f64<NB, RB>: wave = RB blocks of 16 spectra, NB blocks of 16
+// components (kb ≤ 16·NB); lane (row r16, k-slot ks) reads wavelengths
+// c0 + 4·ks + e of its row for the four MFMA steps e of a 16-column chunk (the
+// K order is permuted identically for P and y).
+// T²_in / TT_in (nullable): T² and ‖t‖² of earlier component blocks (k > 64).
+// TT_out (nullable): running ‖t‖² for the next block; the last block writes
+// Q = ‖y‖² − ‖t‖², T², the decision and the moments.
+// ---------------------------------------------------------------------------
+template <int NB, int RB>
+__global__ __launch_bounds__(256) void k_score_f64(const double* __restrict__ X, int64_t ldx,
+                                                   const int64_t* __restrict__ rows, int64_t m, int p,
+                                                   const double* __restrict__ P, const double* __restrict__ mu,
+                                                   const double* __restrict__ a_diag, int kb,
+                                                   double* __restrict__ T_out, int64_t ldt,
+                                                   const double* __restrict__ T2_in, const double* __restrict__ TT_in,
+                                                   double* __restrict__ T2_out, double* __restrict__ TT_out,
+                                                   double* __restrict__ Q_out, DecF64 dec,
+                                                   double* __restrict__ acc_out, int64_t acc_stride,
+                                                   double* __restrict__ stat_part) {
+  __shared__ double sred[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, ks = lane >> 4;
+  const int64_t rbase = ((int64_t)blockIdx.x * 4 + wave) * (16 * RB);
+  const double* xr[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int64_t g = rbase + 16 * rb + r16;
+    const int64_t gc = g < m ? g : m - 1;
+    xr[rb] = X + (rows ? rows[gc] : gc) * ldx;
+  }
+  const double* pr[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const int c = 16 * nb + r16;
+    pr[nb] = P + (int64_t)(c < kb ? c : 0) * p;
+  }
+  double pmask[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) pmask[nb] = 16 * nb + r16 < kb ? 1.0 : 0.0;
+
+  f64x4 acc[NB][RB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) acc[nb][rb] = (f64x4){0.0, 0.0, 0.0, 0.0};
+  double yy[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) yy[rb] = 0.0;
+
+  struct Ld {
+    double x[RB][4];
+    double w[NB][4];
+    double u[4];
+  };
+  auto load = [&](Ld& L, int c0) {
+    const int c = c0 + 4 * ks;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int cc = c + e < p ? c + e : p - 1;
+      L.u[e] = c + e < p ? mu[cc] : 0.0;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) L.x[rb][e] = c + e < p ? xr[rb][cc] : 0.0;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) L.w[nb][e] = c + e < p ? pr[nb][cc] * pmask[nb] : 0.0;
+    }
+  };
+  auto comp = [&](const Ld& L) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        const double y = L.x[rb][e] - L.u[e];
+        yy[rb] += y * y;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) acc[nb][rb] = __builtin_amdgcn_mfma_f64_16x16x4f64(L.w[nb][e], y, acc[nb][rb], 0, 0, 0);
+      }
+    }
+  };
+  Ld LA, LB;
+  load(LA, 0);
+  for (int c0 = 0; c0 < p; c0 += 32) {
+    if (c0 + 16 < p) load(LB, c0 + 16);
+    comp(LA);
+    if (c0 + 32 < p) load(LA, c0 + 32);
+    if (c0 + 16 < p) comp(LB);
+  }
+
+  // lane (r16, ks) holds t for spectrum r16 of each row block, components
+  // 16·nb + ks + 4r; the four k-slot lanes of a spectrum combine by shuffles
+  double st[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int64_t g = rbase + 16 * rb + r16;
+    double t2 = 0.0, tt = 0.0;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = 16 * nb + ks + 4 * r;
+        const double t = acc[nb][rb][r];
+        if (c < kb) {
+          t2 += t * t * a_diag[c];
+          tt += t * t;
+          if (T_out && g < m) T_out[g * ldt + c] = t;
+        }
+      }
+    double y2 = yy[rb];
+    t2 += __shfl_xor(t2, 16, 64);
+    t2 += __shfl_xor(t2, 32, 64);
+    tt += __shfl_xor(tt, 16, 64);
+    tt += __shfl_xor(tt, 32, 64);
+    y2 += __shfl_xor(y2, 16, 64);
+    y2 += __shfl_xor(y2, 32, 64);
+    if (ks == 0 && g < m) {
+      if (T2_in) t2 += T2_in[g];
+      if (TT_in) tt += TT_in[g];
+      if (TT_out) {  // not the last block: carry the running sums
+        T2_out[g] = t2;
+        TT_out[g] = tt;
+      } else {
+        const double q = fmax(y2 - tt, 0.0);
+        if (T2_out) T2_out[g] = t2;
+        if (Q_out) Q_out[g] = q;
+        if (dec.enabled) {
+          const double d = ocm::dred_of(dec.type, t2 * dec.t2_scale, q * dec.q_scale);
+          acc_out[g * acc_stride] = d < dec.dlim ? 1.0 : 0.0;
+        }
+        st[0] += t2;
+        st[1] += t2 * t2;
+        st[2] += q;
+        st[3] += q * q;
+      }
+    }
+  }
+  if (stat_part) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st[i] = wave_sum_f64(st[i]);
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sred[wave * 4 + i] = st[i];
+    __syncthreads();
+    if (tid < 4)
+      stat_part[(int64_t)blockIdx.x * 4 + tid] =
+          (sred[tid] + sred[4 + tid]) + (sred[8 + tid] + sred[12 + tid]);
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_stats_reduce_f64(const double* __restrict__ part, int64_t nblk,
+                                                           double* __restrict__ out) {
+  __shared__ double red[16];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int col = w & 3, sl = w >> 2;
+  double v = 0.0;
+  for (int64_t i = (int64_t)sl * 64 + lane; i < nblk; i += 256) v += part[i * 4 + col];
+  v = wave_sum_f64(v);
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  if (threadIdx.x < 4)
+    out[threadIdx.x] = (red[threadIdx.x] + red[4 + threadIdx.x]) + (red[8 + threadIdx.x] + red[12 + threadIdx.x]);
+}
+
+__global__ void k_decide_f64(const double* __restrict__ T2, const double* __restrict__ Q, int64_t m, DecF64 dec,
+                             double* __restrict__ t2red, double* __restrict__ qred, double* __restrict__ dred,
+                             double* __restrict__ acc, int64_t acc_stride) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const double t = T2[i] * dec.t2_scale;
+  const double q = Q[i] * dec.q_scale;
+  if (t2red) t2red[i] = t;
+  if (qred) qred[i] = q;
+  const double d = ocm::dred_of(dec.type, t, q);
+  if (dred) dred[i] = d;
+  if (acc) acc[i * acc_stride] = d < dec.dlim ? 1.0 : 0.0;
+}
+
+constexpr int SF_RB = 4;  // row blocks of 16 per wave
+
+template <int NB>
+void launch_score_f64(dim3 g, hipStream_t st, const double* X, int64_t ldx, const int64_t* rows, int64_t m, int p,
+                      const double* P, const double* mu, const double* a, int kb, double* T, int64_t ldt,
+                      const double* T2_in, const double* TT_in, double* T2_out, double* TT_out, double* Q_out,
+                      DecF64 d, double* acc, int64_t acc_stride, double* part) {
+  hipLaunchKernelGGL((k_score_f64<NB, SF_RB>), g, dim3(256), 0, st, X, ldx, rows, m, p, P, mu, a, kb, T, ldt, T2_in,
+                     TT_in, T2_out, TT_out, Q_out, d, acc, acc_stride, part);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ocm_colmean_f64(ocm_ctx* ctx, const double* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                    double* mean_out, void* stream) {
+  OCM_REQUIRE(ctx && X && mean_out, "ocm_colmean_f64: NULL argument");
+  OCM_REQUIRE(n > 0 && p > 0 && ldx >= p, "ocm_colmean_f64: bad shape");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t per = 32;
+  const int nsplit = (int)std::min<int64_t>((n + per - 1) / per, 4096);
+  const int64_t rps = (n + nsplit - 1) / nsplit;
+  auto* part = static_cast<double*>(ocm::workspace(ctx, (size_t)nsplit * p * sizeof(double), st));
+  if (!part) return OCM_ERR_NOMEM;
+  hipLaunchKernelGGL(k_colsum_part_f64, dim3((p + 255) / 256, nsplit), dim3(256), 0, st, X, ldx, rows, n, p, rps, part);
+  OCM_CHECK_LAUNCH("k_colsum_part_f64");
+  hipLaunchKernelGGL(k_colsum_final_f64, dim3((p + 255) / 256), dim3(256), 0, st, part, nsplit, p, 1.0 / (double)n,
+                     mean_out);
+  OCM_CHECK_LAUNCH("k_colsum_final_f64");
+  return OCM_OK;
+}
+
+int ocm_gram_f64(ocm_ctx* ctx, const double* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                 const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
+                 void* stream) {
+  OCM_REQUIRE(ctx && X && shift && seg_offsets && G_out && colsum_out, "ocm_gram_f64: NULL argument");
+  OCM_REQUIRE(n > 0 && p > 0 && ldx >= p && nseg > 0, "ocm_gram_f64: bad shape");
+  OCM_REQUIRE(seg_offsets[0] == 0 && seg_offsets[nseg] == n, "ocm_gram_f64: seg_offsets must span [0, n]");
+  for (int s = 0; s < nseg; ++s)
+    OCM_REQUIRE(seg_offsets[s + 1] >= seg_offsets[s], "ocm_gram_f64: seg_offsets not ascending");
+  hipStream_t st = (hipStream_t)stream;
+  const int nt = (p + GT64 - 1) / GT64;
+  const int ntiles = nt * (nt + 1) / 2;
+  int64_t maxseg = 0;
+  for (int s = 0; s < nseg; ++s) maxseg = std::max(maxseg, seg_offsets[s + 1] - seg_offsets[s]);
+  // ≈ 4 workgroups per CU over all chunks; ≥ 64 rows per chunk
+  const int nchunk_max = (int)std::max<int64_t>(1, std::min<int64_t>((4 * ctx->num_cus + ntiles - 1) / ntiles,
+                                                                      (maxseg + 63) / 64));
+  const size_t part_n = (size_t)nchunk_max * ntiles * GT64 * GT64;
+  const size_t cpart_n = (size_t)nchunk_max * nt * GT64;
+  void* w = ocm::workspace(ctx, (part_n + cpart_n) * sizeof(double) + 1024, st);
+  if (!w) return OCM_ERR_NOMEM;
+  ocm::Carve cv{static_cast<char*>(w)};
+  double* part = cv.take<double>(part_n);
+  double* cpart = cv.take<double>(cpart_n);
+  for (int s = 0; s < nseg; ++s) {
+    const int64_t a = seg_offsets[s], b = seg_offsets[s + 1];
+    double* G = G_out + (size_t)s * p * p;
+    double* cs = colsum_out + (size_t)s * p;
+    if (b == a) {
+      OCM_HIP(hipMemsetAsync(G, 0, (size_t)p * p * sizeof(double), st));
+      OCM_HIP(hipMemsetAsync(cs, 0, (size_t)p * sizeof(double), st));
+      continue;
+    }
+    const int64_t len = b - a;
+    const int nch = (int)std::min<int64_t>(nchunk_max, (len + 63) / 64);
+    const int64_t chunk = ((len + nch - 1) / nch + 3) / 4 * 4;
+    const int nchunks = (int)((len + chunk - 1) / chunk);
+    {
+      ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
+      hipLaunchKernelGGL(k_gram_f64, dim3(ntiles, nchunks), dim3(256), 0, st, X, ldx, rows, a, b, p, shift, chunk, nt,
+                         part, cpart);
+    }
+    OCM_CHECK_LAUNCH("k_gram_f64");
+    hipLaunchKernelGGL(k_gram_f64_reduce, dim3(ntiles * 64), dim3(256), 0, st, part, cpart, nchunks, nt, p, G, cs);
+    OCM_CHECK_LAUNCH("k_gram_f64_reduce");
+  }
+  return OCM_OK;
+}
+
+int ocm_score_f64_diag(ocm_ctx* ctx, const double* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
+                       const double* P, const double* mu, const double* a_diag, int32_t k, double* T_out,
+                       double* T2_out, double* Q_out, const ocm_decision* dec, double* accept_out,
+                       int64_t accept_stride, double* stats_out, void* stream) {
+  OCM_REQUIRE(ctx && X && P && mu && a_diag, "ocm_score_f64_diag: NULL argument");
+  OCM_REQUIRE(m >= 0 && p > 0 && ldx >= p, "ocm_score_f64_diag: bad shape");
+  OCM_REQUIRE(k >= 1 && k <= p, "ocm_score_f64_diag: 1 <= k <= p");
+  OCM_REQUIRE(!dec || accept_out, "ocm_score_f64_diag: decision requires accept_out");
+  hipStream_t st = (hipStream_t)stream;
+  if (m == 0) {
+    if (stats_out) OCM_HIP(hipMemsetAsync(stats_out, 0, 4 * sizeof(double), st));
+    return OCM_OK;
+  }
+  const int64_t rows_per_wg = 4 * 16 * SF_RB;
+  const int64_t nblk = (m + rows_per_wg - 1) / rows_per_wg;
+  OCM_REQUIRE(nblk < (1LL << 31), "ocm_score_f64_diag: too many rows");
+  constexpr int KB = 64;
+  const int nkb = (k + KB - 1) / KB;
+  const size_t part_n = stats_out ? (size_t)nblk * 4 : 0;
+  const size_t run_n = nkb > 1 ? 2 * (size_t)m + (T2_out ? 0 : (size_t)m) : 0;
+  void* w = ocm::workspace(ctx, (part_n + run_n) * sizeof(double) + 1024, st);
+  if (!w) return OCM_ERR_NOMEM;
+  ocm::Carve cv{static_cast<char*>(w)};
+  double* part = stats_out ? cv.take<double>(part_n) : nullptr;
+  double* TTa = nkb > 1 ? cv.take<double>(m) : nullptr;
+  double* TTb = nkb > 1 ? cv.take<double>(m) : nullptr;
+  double* T2run = nkb > 1 ? (T2_out ? T2_out : cv.take<double>(m)) : T2_out;
+  DecF64 d{};
+  if (dec) d = DecF64{1, dec->type, dec->t2_scale, dec->q_scale, dec->dlim};
+  const dim3 g((unsigned)nblk);
+  for (int bk = 0; bk < nkb; ++bk) {
+    const int c0 = bk * KB, kb = std::min(KB, k - c0);
+    const bool first = bk == 0, last = bk == nkb - 1;
+    double* Tb = T_out ? T_out + c0 : nullptr;
+    const double* T2i = first ? nullptr : T2run;
+    const double* TTi = first ? nullptr : (bk % 2 ? TTa : TTb);
+    double* TTo = last ? nullptr : (bk % 2 ? TTb : TTa);
+    double* T2o = last ? T2_out : T2run;
+    DecF64 db = last ? d : DecF64{};
+    ocm::TimedRegion tr(ctx, OCM_KERNEL_SCORE, st);
+    const double* Pb = P + (size_t)c0 * p;
+    const double* ab = a_diag + c0;
+    double* acc = last ? accept_out : nullptr;
+    double* pt = last ? part : nullptr;
+    double* Qo = last ? Q_out : nullptr;
+    if (kb <= 16)
+      launch_score_f64<1>(g, st, X, ldx, rows, m, p, Pb, mu, ab, kb, Tb, k, T2i, TTi, T2o, TTo, Qo, db, acc,
+                          accept_stride, pt);
+    else if (kb <= 32)
+      launch_score_f64<2>(g, st, X, ldx, rows, m, p, Pb, mu, ab, kb, Tb, k, T2i, TTi, T2o, TTo, Qo, db, acc,
+                          accept_stride, pt);
+    else
+      launch_score_f64<4>(g, st, X, ldx, rows, m, p, Pb, mu, ab, kb, Tb, k, T2i, TTi, T2o, TTo, Qo, db, acc,
+                          accept_stride, pt);
+    OCM_CHECK_LAUNCH("k_score_f64");
+  }
+  if (stats_out) {
+    hipLaunchKernelGGL(k_stats_reduce_f64, dim3(1), dim3(1024), 0, st, part, nblk, stats_out);
+    OCM_CHECK_LAUNCH("k_stats_reduce_f64");
+  }
+  return OCM_OK;
+}
+
+int ocm_decide_f64(ocm_ctx* ctx, const double* T2, const double* Q, int64_t m, const ocm_decision* dec,
+                   double* t2red_out, double* qred_out, double* dred_out, double* accept_out, int64_t accept_stride,
+                   void* stream) {
+  OCM_REQUIRE(ctx && T2 && Q && dec, "ocm_decide_f64: NULL argument");
+  if (m <= 0) return OCM_OK;
+  DecF64 d{1, dec->type, dec->t2_scale, dec->q_scale, dec->dlim};
+  hipLaunchKernelGGL(k_decide_f64, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, T2, Q, m, d,
+                     t2red_out, qred_out, dred_out, accept_out, accept_stride);
+  OCM_CHECK_LAUNCH("k_decide_f64");
+  return OCM_OK;
+}
+
+}  // extern "C"

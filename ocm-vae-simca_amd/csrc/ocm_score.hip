@@ -470,10 +470,21 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
     s = wave_sum_f64(s);
     if (lane == 0) pmuL[c] = s;
   }
-  float p1a[EX ? NJ : 1];  // comps 16..19: lane (ln, lq) holds P[16 + lq][w·PW + 16j + ln]
+  float p1a[EX ? NJ : 1];  // comps 16..19: lane (ln, lq) holds P[16 + lq][w·PW + 16j + ln] (sweep 2)
+  // the same values with the column of lanes lq ≥ 2 XOR 8 (lane (x, c) holds
+  // column x ^ 8·(c >> 1)): the sources one half-wave's ds_bpermute reads in
+  // sweep 1 then sit on 8 distinct banks (lane mod 32) instead of 4 — with p1a
+  // as the source, lanes 16c + col and 16(c + 2) + col met on one bank: a 2-way
+  // conflict on every bpermute, 256 extra LDS cycles per wave and tile, the
+  // whole SQ_LDS_BANK_CONFLICT count of round 2 (profiles/r02n_pmc_score.json)
+  float p1b[EX ? NJ : 1];
   if constexpr (EX)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) p1a[j] = 16 + lq < k ? (float)P[(int64_t)(16 + lq) * PP + w * PW + 16 * j + ln] : 0.f;
+    for (int j = 0; j < NJ; ++j) {
+      const int64_t rowp = (int64_t)(16 + lq) * PP + w * PW + 16 * j;
+      p1a[j] = 16 + lq < k ? (float)P[rowp + ln] : 0.f;
+      p1b[j] = 16 + lq < k ? (float)P[rowp + (ln ^ (8 * (lq >> 1)))] : 0.f;
+    }
   double ad[5];
 #pragma unroll
   for (int s = 0; s < 5; ++s) ad[s] = lq + 4 * s < k ? adiag[lq + 4 * s] : 0.0;
@@ -494,8 +505,9 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
     }
   const float* p0f = reinterpret_cast<const float*>(P0s);
   // sweep-1 comps 16..19 operand of MFMA e: P[16 + (ln&3)][16j + 4lq + e], which
-  // p1a[j] holds on lane 16(ln&3) + 4lq + e (ds_bpermute address, bytes)
-  const int bperm = 4 * (16 * (ln & 3) + 4 * lq);
+  // p1b[j] holds on lane 16c + ((4lq) ^ 8(c >> 1)) + e, c = ln&3 (ds_bpermute
+  // address, bytes)
+  const int bperm = 4 * (16 * (ln & 3) + ((4 * lq) ^ (8 * ((ln & 3) >> 1))));
   const float one = 1.f;  // B of the −μ step
   __syncthreads();
 
@@ -535,7 +547,7 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
     if constexpr (EX)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        bN[e] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(bperm + 4 * e, __builtin_bit_cast(int, p1a[0])));
+        bN[e] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(bperm + 4 * e, __builtin_bit_cast(int, p1b[0])));
     static_for<NJ>([&](auto J) {
       constexpr int j = decltype(J)::value;
       const f32x4 a = aN;
@@ -548,7 +560,7 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             bN[e] = __builtin_bit_cast(float,
-                                       __builtin_amdgcn_ds_bpermute(bperm + 4 * e, __builtin_bit_cast(int, p1a[j + 1])));
+                                       __builtin_amdgcn_ds_bpermute(bperm + 4 * e, __builtin_bit_cast(int, p1b[j + 1])));
       }
       // Y[j] was issued before the rest of its tile (NJ − 1 − j loads) and
       // the NJ refills of the other tile (stores issued since only make the

@@ -99,6 +99,14 @@ SIGNATURES = {
                                    ctypes.POINTER(c_f64), c_void_p, c_i64, c_void_p]),
     "ocm_cv_counts": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_void_p, c_i64,
                               ctypes.POINTER(OcmCvConfig), c_i32, c_void_p, c_void_p, c_void_p]),
+    "ocm_colmean_f64": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p]),
+    "ocm_gram_f64": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p,
+                             ctypes.POINTER(c_i64), c_i32, c_void_p, c_void_p, c_void_p]),
+    "ocm_score_f64_diag": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p,
+                                   c_void_p, c_i32, c_void_p, c_void_p, c_void_p, ctypes.POINTER(OcmDecision),
+                                   c_void_p, c_i64, c_void_p, c_void_p]),
+    "ocm_decide_f64": (c_i32, [c_void_p, c_void_p, c_void_p, c_i64, ctypes.POINTER(OcmDecision), c_void_p,
+                               c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
     "ocm_bn_scratch_bytes": (ctypes.c_size_t, [c_i32]),
     "ocm_bn_fwd_train": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, ctypes.c_float,
                                  ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -107,7 +115,7 @@ SIGNATURES = {
                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
-ABI_VERSION = 3  # include/ocm.h OCM_ABI_VERSION
+ABI_VERSION = 4  # include/ocm.h OCM_ABI_VERSION
 
 _lib = None
 _lib_lock = threading.Lock()

@@ -54,6 +54,21 @@ def as_device_f32(X, device=None) -> torch.Tensor:
     return t
 
 
+def as_device_x(X, device=None) -> torch.Tensor:
+    """Spectra in HBM in the arithmetic the reference would use: float64 input
+    stays float64 (sklearn's PCA follows the input dtype, utils/SIMCA.py:64-66),
+    anything else becomes float32."""
+    f64 = (X.dtype == torch.float64) if isinstance(X, torch.Tensor) else (np.asarray(X).dtype == np.float64)
+    if not f64:
+        return as_device_f32(X, device)
+    require_device()
+    t = X if isinstance(X, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(X))
+    if device is None:
+        device = t.device if t.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    t = t.to(device=device, dtype=torch.float64)
+    return t if t.is_contiguous() else t.contiguous()
+
+
 @dataclass
 class ClassFit:
     """Per-class model state (device tensors + host scalars)."""
@@ -101,8 +116,9 @@ def _stream(dev):
 def colmean(X: torch.Tensor, rows: torch.Tensor | None, n: int) -> torch.Tensor:
     ctx = Context.get(X.device.index)
     out = torch.empty(X.shape[1], dtype=torch.float64, device=X.device)
-    check(_lib.load().ocm_colmean_f32(ctx.handle, ptr(X), X.stride(0), ptr(rows), n, X.shape[1], ptr(out),
-                                      _stream(X.device)), "ocm_colmean_f32")
+    fn = "ocm_colmean_f64" if X.dtype == torch.float64 else "ocm_colmean_f32"
+    check(getattr(_lib.load(), fn)(ctx.handle, ptr(X), X.stride(0), ptr(rows), n, X.shape[1], ptr(out),
+                                   _stream(X.device)), fn)
     return out
 
 
@@ -131,7 +147,8 @@ def set_gram_mode(name: str) -> str:
 
 def gram(X: torch.Tensor, rows: torch.Tensor | None, seg_offsets, shift32: torch.Tensor, mode: str | None = None,
          chunk_rows: int = 0):
-    """Per-segment shifted Gram (nseg, p, p) f64 and column sums (nseg, p)."""
+    """Per-segment shifted Gram (nseg, p, p) f64 and column sums (nseg, p).
+    float64 X takes the fp64-MFMA Gram (``mode`` does not apply)."""
     p = X.shape[1]
     seg = [int(s) for s in seg_offsets]
     nseg = len(seg) - 1
@@ -140,6 +157,10 @@ def gram(X: torch.Tensor, rows: torch.Tensor | None, seg_offsets, shift32: torch
     cs = torch.empty((nseg, p), dtype=torch.float64, device=X.device)
     arr = (ctypes.c_int64 * len(seg))(*seg)
     ctx = Context.get(X.device.index)
+    if X.dtype == torch.float64:
+        check(_lib.load().ocm_gram_f64(ctx.handle, ptr(X), X.stride(0), ptr(rows), n, p, ptr(shift32), arr, nseg,
+                                       ptr(G), ptr(cs), _stream(X.device)), "ocm_gram_f64")
+        return G, cs
     code = GRAM_MODES[mode or _gram_mode]
     check(_lib.load().ocm_gram_f32_ex(ctx.handle, ptr(X), X.stride(0), ptr(rows), n, p, ptr(shift32), arr, nseg,
                                       code, int(chunk_rows), ptr(G), ptr(cs), _stream(X.device)), "ocm_gram_f32_ex")
@@ -217,13 +238,17 @@ def score(X: torch.Tensor, rows: torch.Tensor | None, m: int, P64: torch.Tensor,
     k, p = P64.shape
     dev = X.device
     out = {}
-    T = torch.empty((m, k), dtype=torch.float32, device=dev) if want_T else None
+    f64 = X.dtype == torch.float64
+    if f64 and A.dim() != 1:
+        raise ValueError("float64 spectra are scored with a diagonal quadratic form (ocm_score_f64_diag)")
+    vdt = torch.float64 if f64 else torch.float32  # T and Q follow the input dtype (utils/SIMCA.py:65-71)
+    T = torch.empty((m, k), dtype=vdt, device=dev) if want_T else None
     T2 = torch.empty(m, dtype=torch.float64, device=dev) if want_T2 else None
-    Q = torch.empty(m, dtype=torch.float32, device=dev) if want_Q else None
+    Q = torch.empty(m, dtype=vdt, device=dev) if want_Q else None
     st = torch.empty(4, dtype=torch.float64, device=dev) if want_stats else None
     ctx = Context.get(dev.index)
     dec_p = ctypes.byref(decision) if decision is not None else None
-    fn = "ocm_score_f32_diag" if A.dim() == 1 else "ocm_score_f32"
+    fn = "ocm_score_f64_diag" if f64 else ("ocm_score_f32_diag" if A.dim() == 1 else "ocm_score_f32")
     check(getattr(_lib.load(), fn)(ctx.handle, ptr(X), X.stride(0), ptr(rows), m, p, ptr(P64), ptr(mean64),
                                    ptr(A), k, ptr(T), ptr(T2), ptr(Q), dec_p, ptr(accept_out), accept_stride,
                                    ptr(st), _stream(dev)), fn)
@@ -239,8 +264,9 @@ def decide(T2: torch.Tensor, Q: torch.Tensor, decision: OcmDecision, want_red=Tr
     qr = torch.empty(m, dtype=torch.float64, device=dev) if want_red else None
     dr = torch.empty(m, dtype=torch.float64, device=dev) if want_dred else None
     ctx = Context.get(dev.index)
-    check(_lib.load().ocm_decide(ctx.handle, ptr(T2), ptr(Q), m, ctypes.byref(decision), ptr(t2r), ptr(qr),
-                                 ptr(dr), ptr(accept_out), accept_stride, _stream(dev)), "ocm_decide")
+    fn = "ocm_decide_f64" if Q.dtype == torch.float64 else "ocm_decide"
+    check(getattr(_lib.load(), fn)(ctx.handle, ptr(T2), ptr(Q), m, ctypes.byref(decision), ptr(t2r), ptr(qr),
+                                   ptr(dr), ptr(accept_out), accept_stride, _stream(dev)), fn)
     return t2r, qr, dr
 
 

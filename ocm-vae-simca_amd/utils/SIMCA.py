@@ -24,9 +24,8 @@ Documented deviations:
 * ``eigs_all`` holds the leading k eigenvalues from the HIP eigensolver and,
   on first access only, the rest of the spectrum (a diagnostic no limit uses;
   the θ moments come from device traces);
-* float64 inputs are computed in float32 on the GPU (the reference runs its
-  PCA in float64 then); limits and decisions agree at the tolerances of
-  tests/test_gpu_northstar.py::test_float64_input_vs_reference (DESIGN.md §5);
+* float64 inputs are computed in float64 as the reference's PCA then is
+  (fp64-MFMA Gram, fp64 scoring; T, Q and ``_model`` arrays float64);
 * ``n_components`` may be any k ≤ p as in the reference; beyond 64 the
   eigensolver's block steps run on the host in fp64 and scoring takes one
   launch per 64 components, and a CV sweep with ``LV_max`` > 64 runs the
@@ -100,7 +99,7 @@ class EnginePCA:
         return self._fit.evals_host.astype(self._dt)
 
     def transform(self, X):
-        Xd = engine.as_device_f32(X)
+        Xd = engine.as_device_x(X)
         out = engine.score(Xd, None, Xd.shape[0], self._fit.P64, self._fit.mean64, self._fit.inv_diag,
                            want_T=True, want_T2=False, want_Q=False)
         T = out["T"]
@@ -168,7 +167,7 @@ class SIMCA(BaseEstimator, ClassifierMixin):
             self.qlim = "chi2pom"
 
         self._out_dtype = _out_dtype(X)
-        Xd = engine.as_device_f32(X)
+        Xd = engine.as_device_x(X)
         lab = _device_labels(classes, Xd.device)
         self._model = {}
         self._fits = {}
@@ -232,7 +231,7 @@ class SIMCA(BaseEstimator, ClassifierMixin):
     # ------------------------------------------------------------ transform
     def transform(self, X):
         """utils/SIMCA.py:101-117 — (T2, T2red, Q, Qred) of the LAST class."""
-        Xd = engine.as_device_f32(X)
+        Xd = engine.as_device_x(X)
         cls = self.model_class[-1]
         fit = self._fits[cls]
         m = self._model[cls]
@@ -246,7 +245,7 @@ class SIMCA(BaseEstimator, ClassifierMixin):
     # -------------------------------------------------------------- predict
     def predict(self, X, y_true=None):
         """utils/SIMCA.py:120-154 — (m, C) float64 of 0/1, decision fused in the scoring kernel."""
-        Xd = engine.as_device_f32(X)
+        Xd = engine.as_device_x(X)
         m = Xd.shape[0]
         C = len(self.model_class)
         pred = torch.zeros((m, C), dtype=torch.float64, device=Xd.device)

@@ -637,20 +637,26 @@ def vaesimca_predict(model: dict, Z: np.ndarray, Zhat: np.ndarray):
 
 
 def synth_spectra(n: int, p: int, k: int, rank: int = 40, seed: int = 1234, noise: float = 0.05,
-                  outlier_frac: float = 0.0, dtype=np.float32):
+                  outlier_frac: float = 0.0, dtype=np.float32, loadings: str = "bands"):
     """Rank-``rank`` spectra with a spectral gap at k plus a sloped baseline:
     scores ~ N(0, diag(s²)), s = linspace(20,8,k) ++ linspace(2,0.5,rank-k);
-    Gaussian-band loadings; σ = ``noise``.  ``outlier_frac`` of the rows get an
-    extra absorption band (≈3σ shift) so both decisions occur."""
+    Gaussian-band loadings (``loadings='bands'``; overlapping bands leave
+    fewer than ~70 independent directions at p = 2048) or orthonormal
+    N(0, 1) rows (``'random'``: full rank, the gap at any k — SURVEY.md §8d);
+    σ = ``noise``.  ``outlier_frac`` of the rows get an extra absorption band
+    (≈3σ shift) so both decisions occur."""
     rng = np.random.default_rng(seed)
     rank = min(rank, p)
     k = min(k, rank)
     s = np.concatenate([np.linspace(20, 8, k), np.linspace(2, 0.5, rank - k)])
     wl = np.linspace(0.0, 1.0, p)
-    centers = rng.uniform(0.05, 0.95, size=rank)
-    widths = rng.uniform(0.01, 0.08, size=rank)
-    L = np.exp(-0.5 * ((wl[None, :] - centers[:, None]) / widths[:, None]) ** 2)
-    L /= np.linalg.norm(L, axis=1, keepdims=True)
+    if loadings == "random":
+        L = np.linalg.qr(rng.standard_normal((p, rank)))[0].T
+    else:
+        centers = rng.uniform(0.05, 0.95, size=rank)
+        widths = rng.uniform(0.01, 0.08, size=rank)
+        L = np.exp(-0.5 * ((wl[None, :] - centers[:, None]) / widths[:, None]) ** 2)
+        L /= np.linalg.norm(L, axis=1, keepdims=True)
     S = rng.standard_normal((n, rank)) * s
     X = S @ L + noise * rng.standard_normal((n, p)) + (1.0 + 0.3 * wl)[None, :]
     if outlier_frac > 0:
