@@ -26,9 +26,11 @@ Multi-GPU (``group`` given): each rank holds a contiguous row block of X
 (``row_offset``) and the full label vector.  Fold f's eigensolve runs on
 its owner rank f mod W: every rank forms its local TRAIN Gram of fold f
 (Σ_g G_g − G_f, fp64 downdating on the device) and one RCCL reduce brings
-the sum to the owner only (K reduces of p² doubles instead of K
-all-reduces); the column sums (K·p doubles) are all-reduced.  The owner
-broadcasts the fold model (P, μ, λ, θ ≈ 0.3 MB), every rank scores its own
+the sum to the owner only (K reduces of the packed upper triangle, p(p+1)/2
++ p + 1 doubles with the fold's column sums and row count, instead of K
+all-reduces).  All K reduces are issued before any eigensolve, so the owners
+solve their folds concurrently (⌈K/W⌉ eigensolves deep).  The owners
+broadcast the fold model (P, μ, λ, θ ≈ 0.3 MB), every rank scores its own
 rows, the confusion counts and training moments are all-reduced, and the
 pooled prediction vectors travel as one device all-gather of each rank's
 row block.  Same code path at W = 1 without collectives.
@@ -202,42 +204,74 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
     else:
         G = torch.zeros((K, p, p), dtype=torch.float64, device=dev)
         cs = torch.zeros((K, p), dtype=torch.float64, device=dev)
-    if distributed:
-        dist.all_reduce(cs, group=group)
-    # local total Gram Σ_g G_g (its column sums are rebuilt from the reduced cs)
+    # local total Gram Σ_g G_g and column sums (distributed: this rank's rows
+    # only; the packed train moments below carry them to the fold owners)
     Gt = torch.empty((p, p), dtype=torch.float64, device=dev)
     cst = torch.empty(p, dtype=torch.float64, device=dev)
     engine.gram_combine([(1.0, G[f], cs[f]) for f in range(K)], Gt, cst)
 
     # ---- per-fold eigen-models (fold f on rank f mod W, then broadcast) ----
+    # Distributed: every fold's train-Gram reduce is issued before any
+    # eigensolve, so the owners solve their folds at the same time (⌈K/W⌉
+    # eigensolves deep instead of K), and the model broadcasts go out
+    # together at the end.  The reduced operand is this rank's shifted train
+    # Gram packed as its upper triangle (ocm_gram_pack about a zero shift:
+    # p(p+1)/2 + p + 1 doubles, half of p²), so C and d = Σy/n come from
+    # ocm_cov_from_packed and μ = shift + d, as ocm_cov_from_gram forms them.
     models = FoldModels()
-    Gtr = torch.empty((p, p), dtype=torch.float64, device=dev) if distributed else None
-    cs_tr = torch.empty(p, dtype=torch.float64, device=dev)
-    for f in range(K):
-        n_tr = n_target - int(folds[f].size)
-        if n_tr < 2:
-            raise ValueError("SIMCA needs at least 2 samples in a class")
-        owner = f % W
-        if distributed:
-            # this rank's train Gram of fold f, summed on the owner only
-            engine.gram_combine([(1.0, Gt, None), (-1.0, G[f], None)], Gtr, None)
-            dist.reduce(Gtr, dst=dist.get_global_rank(group, owner) if group is not None else owner, group=group)
+    n_trs = [n_target - int(folds[f].size) for f in range(K)]
+    if min(n_trs) < 2:
+        raise ValueError("SIMCA needs at least 2 samples in a class")
+
+    def gglobal(r):
+        return dist.get_global_rank(group, r) if group is not None else r
+
+    def solve(C, mean):
+        evals, evecs, theta, _ = engine.eig_topk(C, lvmax, theta_mode)
         pack = torch.empty(lvmax + 3 + p + lvmax * p, dtype=torch.float64, device=dev)
-        if owner == R:
-            torch.sub(cst, cs[f], out=cs_tr)  # Σ_g cs_g − cs_f (p doubles)
-            if distributed:
-                C, mean = engine.cov_from_gram([(1.0, Gtr, cs_tr)], shift32, n_tr)
-            else:
-                C, mean = engine.cov_from_gram([(1.0, Gt, cst), (-1.0, G[f], cs[f])], shift32, n_tr)
-            evals, evecs, theta, _ = engine.eig_topk(C, lvmax, theta_mode)
+        pack[:lvmax] = evals
+        pack[lvmax:lvmax + 3] = theta
+        pack[lvmax + 3:lvmax + 3 + p] = mean
+        pack[lvmax + 3 + p:] = evecs.reshape(-1)
+        return pack
+
+    packs = [None] * K
+    if distributed:
+        zero32 = torch.zeros(p, dtype=torch.float32, device=dev)
+        Gtr = torch.empty((p, p), dtype=torch.float64, device=dev)
+        cs_tr = torch.empty(p, dtype=torch.float64, device=dev)
+        n_loc_f = [int(f_.size) for f_ in loc_folds]
+        n_loc_t = sum(n_loc_f)
+        red, works = [], []
+        for f in range(K):
+            engine.gram_combine([(1.0, Gt, cst), (-1.0, G[f], cs[f])], Gtr, cs_tr)
+            buf = engine.gram_pack(Gtr, cs_tr, zero32, n_loc_t - n_loc_f[f])
+            red.append(buf)
+            works.append(dist.reduce(buf, dst=gglobal(f % W), group=group, async_op=True))
+        for w in works:
+            w.wait()
+        del Gtr, cs_tr
+        shift64f = shift32.to(torch.float64)
+        for f in range(R, K, W):
+            C, d = engine.cov_from_packed(red[f], p)
+            packs[f] = solve(C, d + shift64f)
             del C
-            pack[:lvmax] = evals
-            pack[lvmax:lvmax + 3] = theta
-            pack[lvmax + 3:lvmax + 3 + p] = mean
-            pack[lvmax + 3 + p:] = evecs.reshape(-1)
-        if distributed:
-            dist.broadcast(pack, src=dist.get_global_rank(group, owner) if group is not None else owner,
-                           group=group)
+        del red
+        works = []
+        for f in range(K):
+            if packs[f] is None:
+                packs[f] = torch.empty(lvmax + 3 + p + lvmax * p, dtype=torch.float64, device=dev)
+            works.append(dist.broadcast(packs[f], src=gglobal(f % W), group=group, async_op=True))
+        for w in works:
+            w.wait()
+    else:
+        for f in range(K):
+            C, mean = engine.cov_from_gram([(1.0, Gt, cst), (-1.0, G[f], cs[f])], shift32, n_trs[f])
+            packs[f] = solve(C, mean)
+            del C
+    for f in range(K):
+        n_tr = n_trs[f]
+        pack = packs[f]
         evals = pack[:lvmax]
         models.evals.append(evals)
         models.mean.append(pack[lvmax + 3:lvmax + 3 + p])
@@ -247,7 +281,7 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
         models.evals_h.append(host[:lvmax])
         models.theta_h.append(host[lvmax:lvmax + 3])
         models.n_train.append(n_tr)
-    del G, cs, Gt, Gtr
+    del G, cs, Gt, packs
 
     # ---- per-fold scoring, limits, counts ----
     ncfg = len(combos) * len(lvs)
