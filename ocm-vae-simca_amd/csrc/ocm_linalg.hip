@@ -599,6 +599,228 @@ __global__ __launch_bounds__(QT) void k_chol_trsm32(const double* __restrict__ p
   for (int j = 0; j < QB; ++j) V[(int64_t)r * QB + j] = v[j];
 }
 
+__device__ __forceinline__ double hash_normal(uint64_t a);
+
+// ---------------------------------------------------------------------------
+// CholQR of a tall p×32 fp64 block in two kinds of launch over CQ_G
+// workgroups (four waves each, 16-row blocks split evenly), instead of
+// k_colnormalize + (k_atb_part + k_chol_trsm32) per pass:
+//
+//   k_cq_gram32   S = srcᵀsrc on fp64 MFMA (v_mfma_f64_16x16x4f64), wave
+//                 partials summed in LDS, one 32×32 partial per workgroup; the
+//                 LAST workgroup to finish (a ticket on a counter) sums the
+//                 partials in workgroup order, scales the columns (r_i =
+//                 1/√S_ii: the old k_colnormalize), factors S' = D S D = L Lᵀ in
+//                 registers (lane i holds row i, v_readlane broadcasts, pivot
+//                 clamp 1e-14 as k_chol), inverts L (lane c: row c of X = L⁻¹
+//                 by back substitution) and writes M = D·Xᵀ (upper triangular),
+//                 so that src·M has orthonormal columns.  With APPLY the
+//                 launch first forms T = src·M_prev, stores it and takes the
+//                 Gram of T straight from the MFMA result registers (the C
+//                 layout is the row-contraction operand layout): the second
+//                 CholQR pass costs no extra read of T;
+//   k_cq_apply32  dst = src·M on fp64 MFMA.
+//
+// One pass: gram(W) → apply.  CholQR2: gram(W) → gram+apply(W → T) → apply(T).
+// span(src·M) = span(src) whatever the pivots (M is invertible), so a single
+// pass keeps the subspace exactly; only orthonormality depends on cond(src).
+// Operand layouts (16×16 blocks, lane l: g = l>>4, c = l&15): the Gram reads
+// src[16rb + g + 4j][16cb + c] (K-step j, both operands); the product reads
+// A = src[16rb + c][4ks + g], B = M[4ks + g][16cb + c] and yields
+// dst[16rb + g + 4r][16cb + c] in accumulator r.
+// ---------------------------------------------------------------------------
+constexpr int CQ_G = 16;  // workgroups per launch (a power of two: the ticket wraps)
+
+__device__ __forceinline__ void cq_blocks(int p, int& lo, int& hi) {
+  const int nrb = (p + 15) / 16;
+  lo = (int)((int64_t)blockIdx.x * nrb / CQ_G);
+  hi = (int)((int64_t)(blockIdx.x + 1) * nrb / CQ_G);
+}
+
+// this wave's 16-row block: dst = src · M (M rows from LDS), into o0 / o1
+__device__ __forceinline__ void cq_apply_block(const double* src, int p, int rb, const double (*sm)[33], int g, int c,
+                                               f64x4& o0, f64x4& o1) {
+  const int ra = 16 * rb + c;
+  double av[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) av[ks] = ra < p ? src[(int64_t)ra * 32 + 4 * ks + g] : 0.0;
+  o0 = f64x4{0.0, 0.0, 0.0, 0.0};
+  o1 = o0;
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    o0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], sm[4 * ks + g][c], o0, 0, 0, 0);
+    o1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], sm[4 * ks + g][16 + c], o1, 0, 0, 0);
+  }
+}
+
+template <bool APPLY>
+__global__ __launch_bounds__(256) void k_cq_gram32(double* W, int p, const double* __restrict__ Mprev, double* T,
+                                                   double* __restrict__ part, unsigned* __restrict__ ticket,
+                                                   int fix_zero, uint64_t seed, double* __restrict__ Mout) {
+  __shared__ double wpart[4][3][4][64];
+  __shared__ double sS[32][33];
+  __shared__ double sm[32][33];
+  __shared__ double rsc[32];
+  __shared__ int last, degen;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  int lo, hi;
+  cq_blocks(p, lo, hi);
+  if (APPLY) {
+    for (int e = tid; e < 32 * 32; e += 256) sm[e >> 5][e & 31] = Mprev[e];
+    __syncthreads();
+  }
+  f64x4 s00 = {0.0, 0.0, 0.0, 0.0}, s01 = s00, s11 = s00;
+  for (int rb = lo + wave; rb < hi; rb += 4) {
+    double x[2][4];
+    if (APPLY) {
+      f64x4 o0, o1;
+      cq_apply_block(W, p, rb, sm, g, c, o0, o1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * rb + g + 4 * r;
+        x[0][r] = row < p ? o0[r] : 0.0;
+        x[1][r] = row < p ? o1[r] : 0.0;
+        if (row < p) {
+          T[(int64_t)row * 32 + c] = o0[r];
+          T[(int64_t)row * 32 + 16 + c] = o1[r];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 16 * rb + g + 4 * j;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) x[cb][j] = r < p ? W[(int64_t)r * 32 + 16 * cb + c] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s00 = __builtin_amdgcn_mfma_f64_16x16x4f64(x[0][j], x[0][j], s00, 0, 0, 0);
+      s01 = __builtin_amdgcn_mfma_f64_16x16x4f64(x[0][j], x[1][j], s01, 0, 0, 0);
+      s11 = __builtin_amdgcn_mfma_f64_16x16x4f64(x[1][j], x[1][j], s11, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    wpart[wave][0][r][lane] = s00[r];
+    wpart[wave][1][r][lane] = s01[r];
+    wpart[wave][2][r][lane] = s11[r];
+  }
+  __syncthreads();
+  for (int e = tid; e < 768; e += 256) {
+    const double* w0 = &wpart[0][0][0][0];
+    part[(int64_t)blockIdx.x * 768 + e] = (w0[e] + w0[768 + e]) + (w0[1536 + e] + w0[2304 + e]);
+  }
+  __threadfence();  // this workgroup's partial is visible before its ticket
+  __syncthreads();
+  if (tid == 0) last = (atomicAdd(ticket, 1u) % CQ_G) == CQ_G - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // acquire: every partial is complete
+  for (int e = tid; e < 768; e += 256) {
+    double v = 0.0;
+    for (int wg = 0; wg < CQ_G; ++wg) v += __builtin_nontemporal_load(&part[(int64_t)wg * 768 + e]);
+    const int blk = e >> 8, r = (e >> 6) & 3, l = e & 63;
+    const int row = 16 * (blk == 2) + (l >> 4) + 4 * r, col = 16 * (blk != 0) + (l & 15);
+    sS[row][col] = v;
+    if (blk == 1) sS[col][row] = v;
+  }
+  if (tid == 0) degen = 0;
+  __syncthreads();
+  if (tid < 32) {
+    const double nrm = sqrt(sS[tid][tid]);
+    const bool zero = !(nrm > 1e-280);
+    if (zero && fix_zero) atomicOr(&degen, 1);
+    rsc[tid] = zero ? 0.0 : 1.0 / nrm;
+  }
+  __syncthreads();
+  if (degen) {
+    // rank-deficient C: a (numerically) zero column of W is replaced by the
+    // pseudo-random column k_colnormalize uses, and S is formed again here
+    // from all of W by this one workgroup (rare; the first pass only)
+    for (int cc = 0; cc < 32; ++cc) {
+      if (rsc[cc] != 0.0) continue;
+      for (int r = tid; r < p; r += 256) W[(int64_t)r * 32 + cc] = hash_normal(seed * 0x9E3779B1ull + (uint64_t)r * 131 + cc);
+    }
+    __threadfence();
+    __syncthreads();
+    for (int e = tid; e < 32 * 32; e += 256) {
+      const int i = e >> 5, j = e & 31;
+      double v = 0.0;
+      for (int r = 0; r < p; ++r) v += W[(int64_t)r * 32 + i] * W[(int64_t)r * 32 + j];
+      sS[i][j] = v;
+    }
+    __syncthreads();
+    if (tid < 32) rsc[tid] = 1.0 / sqrt(fmax(sS[tid][tid], 1e-300));
+    __syncthreads();
+  }
+  if (tid < 64) {
+    // Cholesky of S' = D S D in registers (lanes 32..63 mirror 0..31)
+    const int i = lane & 31;
+    const double ri = rsc[i];
+    double a[32];
+#pragma unroll
+    for (int cc = 0; cc < 32; ++cc) a[cc] = sS[i][cc] * ri * rsc[cc];
+    double lrow[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const double ajj = readlane_f64(a[j], j);
+      const double djj = sqrt(fmax(ajj, 1e-14));  // diag(S') = 1: clamp 1e-14 · max diag
+      const double inv = 1.0 / djj;
+      const double lij = i > j ? a[j] * inv : (i == j ? djj : 0.0);
+      lrow[j] = lij;
+#pragma unroll
+      for (int l = j + 1; l < 32; ++l) {
+        const double llj = readlane_f64(lij, l);
+        if (l <= i) a[l] -= lij * llj;
+      }
+    }
+    if (lane < 32) {
+#pragma unroll
+      for (int cc = 0; cc < 32; ++cc) sm[i][cc] = lrow[cc];
+    }
+    __builtin_amdgcn_wave_barrier();
+    // lane i: row i of X = L⁻¹ by X·L = I, columns j = 31 … 0
+    double xr[32];
+#pragma unroll
+    for (int j = 31; j >= 0; --j) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = j + 1; k < 32; ++k) s += xr[k] * sm[k][j];
+      xr[j] = j > i ? 0.0 : ((j == i ? 1.0 : 0.0) - s) / sm[j][j];
+    }
+    // M[k][i] = r_k · X[i][k]
+    if (lane < 32) {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) Mout[k * 32 + i] = rsc[k] * xr[k];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cq_apply32(const double* __restrict__ src, int p, const double* __restrict__ M,
+                                                    double* __restrict__ dst) {
+  __shared__ double sm[32][33];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  for (int e = tid; e < 32 * 32; e += 256) sm[e >> 5][e & 31] = M[e];
+  __syncthreads();
+  int lo, hi;
+  cq_blocks(p, lo, hi);
+  for (int rb = lo + wave; rb < hi; rb += 4) {
+    f64x4 o0, o1;
+    cq_apply_block(src, p, rb, sm, g, c, o0, o1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * rb + g + 4 * r;
+      if (row < p) {
+        dst[(int64_t)row * 32 + c] = o0[r];
+        dst[(int64_t)row * 32 + 16 + c] = o1[r];
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ double hash_normal(uint64_t a) {
   // splitmix64 -> two uniforms -> Box-Muller
   auto mix = [](uint64_t z) {
@@ -915,6 +1137,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   const size_t trace_wgs = (size_t)TRACE_KSPLIT * ((p + DT - 1) / DT) * ((p + DT - 1) / DT);
   const size_t plane_cap = std::max((size_t)ksplit * pb, wide ? 16 * bb : 0);
   size_t need = (6 * pb + 6 * bb + plane_cap + (wide ? 0 : (size_t)nblk * bb) + 4 * b + 64) * sizeof(double);
+  need += ((size_t)CQ_G * 768 + 2048 + 64) * sizeof(double) + 3 * 256;  // CholQR partials, M1/M2, ticket
   if (theta_mode) need += ((size_t)p * p + 4 * (size_t)k * p + 2 * def_blocks + trace_wgs + 8) * sizeof(double);
   void* w = ocm::workspace(ctx, need + 16 * 256, st);
   if (!w) return OCM_ERR_NOMEM;
@@ -932,6 +1155,10 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   double* res = cv.take<double>(b);
   double* planes = cv.take<double>(plane_cap);
   double* apart = wide ? nullptr : cv.take<double>((size_t)nblk * bb);
+  double* cq_part = cv.take<double>((size_t)CQ_G * 768);
+  double* cq_M = cv.take<double>(2048);
+  unsigned* cq_ticket = cv.take<unsigned>(64);
+  OCM_HIP(hipMemsetAsync(cq_ticket, 0, sizeof(unsigned), st));  // k_cq_gram32's tickets count from a multiple of CQ_G
   auto* hres = static_cast<double*>(ocm::host_staging(ctx, (wide ? 3 * bb + b : 2 * b) * sizeof(double)));
   if (!hres) return OCM_ERR_NOMEM;
   double* hmat = hres + 2 * b;  // wide: b×b host staging (+ b×b result, + b values)
@@ -947,8 +1174,25 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
 
   using ocm::host_chol_inv_t;
   using ocm::host_sym_eig;
-  auto orth = [&](double* Win, double* Vout, uint64_t seed) -> int {
-    // CholQR2 on column-normalised Win; result in Vout (Win is clobbered)
+  auto orth = [&](double* Win, double* Vout, uint64_t seed, int passes) -> int {
+    // CholQR (passes = 1) or CholQR2 on column-normalised Win; result in Vout
+    // (Win is clobbered).  b = 32: the whole thing in one single-workgroup launch.
+    if (!wide && b == QB) {
+      hipLaunchKernelGGL(k_cq_gram32<false>, dim3(CQ_G), dim3(256), 0, st, Win, p, nullptr, nullptr, cq_part,
+                         cq_ticket, 1, seed, cq_M);
+      OCM_CHECK_LAUNCH("k_cq_gram32");
+      const double* src = Win;
+      if (passes == 2) {  // T = Win·M1 (in place: every wave rewrites only rows it has read) + Gram of T
+        hipLaunchKernelGGL(k_cq_gram32<true>, dim3(CQ_G), dim3(256), 0, st, Win, p, cq_M, Win, cq_part, cq_ticket, 0,
+                           seed, cq_M + 1024);
+        OCM_CHECK_LAUNCH("k_cq_gram32 apply");
+        hipLaunchKernelGGL(k_cq_apply32, dim3(CQ_G), dim3(256), 0, st, src, p, cq_M + 1024, Vout);
+      } else {
+        hipLaunchKernelGGL(k_cq_apply32, dim3(CQ_G), dim3(256), 0, st, src, p, cq_M, Vout);
+      }
+      OCM_CHECK_LAUNCH("k_cq_apply32");
+      return OCM_OK;
+    }
     hipLaunchKernelGGL(k_colnormalize, dim3(b), dim3(256), 0, st, Win, p, b, seed);
     OCM_CHECK_LAUNCH("k_colnormalize");
     for (int pass = 0; pass < 2; ++pass) {
@@ -1003,7 +1247,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
 
   hipLaunchKernelGGL(k_randn, dim3((unsigned)((pb + 255) / 256)), dim3(256), 0, st, T1, (int64_t)pb, 0x5EEDull);
   OCM_CHECK_LAUNCH("k_randn");
-  int rc = orth(T1, V, 1);
+  int rc = orth(T1, V, 1, 1);  // a Gaussian block is well conditioned: one pass
   if (rc) return rc;
 
   // The first iterations are plain orthogonal iterations V ← orth(C V): the
@@ -1021,7 +1265,10 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     rc = dgemm(C, p, V, b, W, b, p, b, p, ksplit, planes, st);  // W = C V
     if (rc) return rc;
     if (it <= PLAIN && it < max_iter) {
-      rc = orth(W, V, 500 + it);  // W is not needed again (recomputed next iteration)
+      // W is not needed again (recomputed next iteration).  One CholQR pass
+      // keeps span(W) exactly; the basis that feeds Rayleigh–Ritz (the last
+      // plain iteration) gets the second pass for orthonormality to rounding.
+      rc = orth(W, V, 500 + it, it == PLAIN ? 2 : 1);
       if (rc) return rc;
       continue;
     }
@@ -1049,7 +1296,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     if (it == max_iter) break;  // keep V, W, theta consistent for the outputs
     // next basis: orth(C · Ritz vectors)
     OCM_HIP(hipMemcpyAsync(T1, W, pb * sizeof(double), hipMemcpyDeviceToDevice, st));
-    rc = orth(T1, V, 1000 + it);
+    rc = orth(T1, V, 1000 + it, 2);
     if (rc) return rc;
   }
   if (iters_out) *iters_out = std::min(it, max_iter);

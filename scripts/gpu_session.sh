@@ -35,6 +35,7 @@ if [ "${BENCH:-0}" = 1 ]; then
 fi
 if [ "${PROF:-0}" = 1 ]; then
   run prof 600 "0" rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-vae
+  rm -f "$OUT"/prof/*_kernel_trace.csv  # large; the stats file is the record
 fi
 if [ -n "${EXTRA:-}" ]; then
   # shellcheck disable=SC2086
