@@ -113,7 +113,11 @@ class GraphedVAETrainer:
                 dist.broadcast(b, src=src, group=self.group)
 
     def _body(self):
-        self.opt.zero_grad(set_to_none=False)
+        # one process: gradients set to None, so backward hands each parameter
+        # its freshly computed gradient (no per-parameter memset + accumulate
+        # kernel: 43 adds and 11 fills per step in the r03g trace); with the
+        # flat all-reduce buffer the .grad views must persist
+        self.opt.zero_grad(set_to_none=not self.allreduce)
         with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32):
             x_rec, mu, logvar = self.model(self.x)
         x_rec, mu, logvar = x_rec.float(), mu.float(), logvar.float()
