@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCM_ABI_VERSION 4
+#define OCM_ABI_VERSION 5
 
 #define OCM_OK 0
 #define OCM_ERR_ARG (-1)         /* invalid argument (maps to ValueError) */
@@ -350,15 +350,50 @@ int ocm_decide_f64(ocm_ctx* ctx, const double* T2, const double* Q, int64_t m, c
  * with NULL).  All work is stream-ordered (graph-capturable). */
 #define OCM_DTYPE_F32 0
 #define OCM_DTYPE_BF16 1
+/* act: OCM_ACT_ELU fuses the ELU (α = 1) that follows every batch norm of the
+ * VAE (vae_model.py:45-49, 75-79): y = ELU(BN(x)) forward; the backward takes
+ * the gradient of the ELU output and that output y (dz = dy·(y > 0 ? 1 : y + 1)). */
+#define OCM_ACT_NONE 0
+#define OCM_ACT_ELU 1
 size_t ocm_bn_scratch_bytes(int32_t C);
 int ocm_bn_fwd_train(ocm_ctx* ctx, int32_t dtype, const void* x, int32_t N, int32_t C, int32_t L,
                      const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
-                     float* running_var, void* y, float* save_mean, float* save_invstd, void* scratch,
+                     float* running_var, int32_t act, void* y, float* save_mean, float* save_invstd, void* scratch,
                      void* stream);
-/* dx = γ·invstd·(dy − mean(dy) − x̂·mean(dy·x̂)); dgamma = Σ dy·x̂, dbeta = Σ dy (either may be NULL). */
+/* dx = γ·invstd·(dz − mean(dz) − x̂·mean(dz·x̂)), dz = dy (act NONE) or the ELU's input gradient;
+ * dgamma = Σ dz·x̂, dbeta = Σ dz (either may be NULL); y [act ELU] the forward's output. */
 int ocm_bn_bwd(ocm_ctx* ctx, int32_t dtype, const void* x, const void* dy, int32_t N, int32_t C, int32_t L,
-               const float* gamma, const float* save_mean, const float* save_invstd, void* dx, float* dgamma,
-               float* dbeta, void* scratch, void* stream);
+               const float* gamma, const float* save_mean, const float* save_invstd, int32_t act, const void* y,
+               void* dx, float* dgamma, float* dbeta, void* scratch, void* stream);
+
+/* ---- VAE narrow convolutions (vae_model.py:37-81: Conv1d / ConvTranspose1d,
+ * 1-12 channels, kernel 7, stride 1 or 2; the layers nn.Conv1d /
+ * nn.ConvTranspose1d lower to MIOpen in the reference) ----
+ * Activations (B, C, L) contiguous, float32 or bfloat16 (dtype_*: OCM_DTYPE_*);
+ * weights, bias, gradients float32; float32 accumulation.  Stream-ordered,
+ * graph-capturable (scratch is caller-owned).
+ *
+ * ocm_conv1d, mode OCM_CONV_DOWN:  y[b][o][l] = bias[o] + Σ_i Σ_t w[o][i][t]·x[b][i][l·s + t − pad]
+ *   (Conv1d forward, w [O][I][K]; ConvTranspose1d input gradient with w its [I][O][K] weight, x = dy);
+ * mode OCM_CONV_UP:  y[b][o][j] = bias[o] + Σ_i Σ_t w[i][o][t]·x[b][i][(j + pad − t)/s] over the
+ *   terms where s divides j + pad − t (ConvTranspose1d forward, w [I][O][K]; Conv1d input gradient with
+ *   w its [O][I][K] weight read as [I][O][K] of dy's channels).  bias nullable; I ≤ 64, K ≤ 15.
+ * ocm_conv1d_wgrad: G[o][i][t] = Σ_b Σ_l P[b][o][l]·Q[b][i][l·s + t − pad], written [O][I][K]
+ *   (Conv1d: P = dy, Q = x → its [O][I][K] weight gradient; ConvTranspose1d: P = x, Q = dy → its
+ *   [I][O][K] weight gradient); psum_out [nullable] = Σ_b Σ_l P[b][o][l] (Conv1d's bias gradient).
+ *   scratch ≥ ocm_conv1d_scratch_bytes(O, I, K); fixed-order two-stage sums (deterministic).
+ * ocm_chan_sum: out[c] = Σ_b Σ_l v[b][c][l] (the bias gradient); scratch as above with O·I·K ≥ C. */
+#define OCM_CONV_DOWN 0
+#define OCM_CONV_UP 1
+size_t ocm_conv1d_scratch_bytes(int32_t O, int32_t I, int32_t K);
+int ocm_conv1d(ocm_ctx* ctx, int32_t mode, int32_t dtype_in, const void* x, int32_t B, int32_t I, int32_t Lin,
+               const float* w, const float* bias, int32_t O, int32_t Lout, int32_t K, int32_t stride, int32_t pad,
+               int32_t dtype_out, void* y, void* stream);
+int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, int32_t Lp, int32_t dtype_q,
+                     const void* Q, int32_t I, int32_t Lq, int32_t B, int32_t K, int32_t stride, int32_t pad,
+                     float* G_out, float* psum_out, void* scratch, void* stream);
+int ocm_chan_sum(ocm_ctx* ctx, int32_t dtype, const void* v, int32_t B, int32_t C, int32_t L, float* out,
+                 void* scratch, void* stream);
 
 #ifdef __cplusplus
 }

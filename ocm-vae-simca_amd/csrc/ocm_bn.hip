@@ -92,8 +92,9 @@ __global__ void k_bn_finalize(const double* __restrict__ part, int C, int64_t M,
   }
 }
 
-// grid (ceil(L / BN_T), N·C): y = (x − μ)·invstd·γ + β
-template <typename T>
+// grid (ceil(L / BN_T), N·C): y = (x − μ)·invstd·γ + β, then ELU (α = 1) when
+// fused: z > 0 ? z : exp(z) − 1 (torch's elu, evaluated in float)
+template <typename T, bool ELU>
 __global__ __launch_bounds__(BN_T) void k_bn_apply(const T* __restrict__ x, int C, int L,
                                                    const float* __restrict__ mean, const float* __restrict__ invstd,
                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -104,12 +105,24 @@ __global__ __launch_bounds__(BN_T) void k_bn_apply(const T* __restrict__ x, int 
   const float a = invstd[c] * (gamma ? gamma[c] : 1.f);
   const float b = (beta ? beta[c] : 0.f) - mean[c] * a;
   const int64_t i = (int64_t)row * L + l;
-  bn_st(y, i, fmaf(bn_ld(x, i), a, b));
+  const float z = fmaf(bn_ld(x, i), a, b);
+  bn_st(y, i, ELU ? (z > 0.f ? z : expf(z) - 1.f) : z);
 }
 
-// grid (BN_SPLIT, C): partial Σdy, Σdy·x̂
-template <typename T>
-__global__ __launch_bounds__(BN_T) void k_bn_bwd_stats(const T* __restrict__ x, const T* __restrict__ dy, int N,
+// the gradient reaching the batch norm's output: with the fused ELU, dz = dy·(y > 0 ? 1 : y + 1)
+// from the ELU output y (torch's elu_backward on the result)
+template <bool ELU, typename T>
+__device__ __forceinline__ float bn_grad(const T* dy, const T* ya, int64_t i) {
+  const float g = bn_ld(dy, i);
+  if (!ELU) return g;
+  const float v = bn_ld(ya, i);
+  return v > 0.f ? g : g * (v + 1.f);
+}
+
+// grid (BN_SPLIT, C): partial Σdz, Σdz·x̂
+template <typename T, bool ELU>
+__global__ __launch_bounds__(BN_T) void k_bn_bwd_stats(const T* __restrict__ x, const T* __restrict__ dy,
+                                                       const T* __restrict__ ya, int N,
                                                        int C, int L, const float* __restrict__ mean,
                                                        const float* __restrict__ invstd, double* __restrict__ part) {
   __shared__ double red[BN_T / 64];
@@ -120,7 +133,7 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_stats(const T* __restrict__ x, 
     const int64_t r = ((int64_t)n * C + c) * L;
     float a1 = 0.f, a2 = 0.f;
     for (int l = threadIdx.x; l < L; l += BN_T) {
-      const float g = bn_ld(dy, r + l);
+      const float g = bn_grad<ELU>(dy, ya, r + l);
       a1 += g;
       a2 = fmaf(g, (bn_ld(x, r + l) - mu) * is, a2);
     }
@@ -150,9 +163,10 @@ __global__ void k_bn_bwd_finalize(const double* __restrict__ part, int C, double
   if (dgamma) dgamma[c] = (float)s2;
 }
 
-// dx = γ·invstd·(dy − Σdy/M − x̂·Σ(dy·x̂)/M)
-template <typename T>
-__global__ __launch_bounds__(BN_T) void k_bn_bwd_apply(const T* __restrict__ x, const T* __restrict__ dy, int C,
+// dx = γ·invstd·(dz − Σdz/M − x̂·Σ(dz·x̂)/M)
+template <typename T, bool ELU>
+__global__ __launch_bounds__(BN_T) void k_bn_bwd_apply(const T* __restrict__ x, const T* __restrict__ dy,
+                                                       const T* __restrict__ ya, int C,
                                                        int L, int64_t M, const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
                                                        const float* __restrict__ gamma,
@@ -165,7 +179,7 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_apply(const T* __restrict__ x, 
   const float m1 = (float)(sums[2 * c] / (double)M), m2 = (float)(sums[2 * c + 1] / (double)M);
   const int64_t i = (int64_t)row * L + l;
   const float xh = (bn_ld(x, i) - mu) * is;
-  bn_st(dx, i, k * (bn_ld(dy, i) - m1 - xh * m2));
+  bn_st(dx, i, k * (bn_grad<ELU>(dy, ya, i) - m1 - xh * m2));
 }
 
 // scratch of one forward / backward call: per-(channel, split) partials + the
@@ -174,31 +188,37 @@ size_t bn_scratch(int C) { return ((size_t)C * BN_SPLIT * 2 + 2 * (size_t)C) * s
 
 template <typename T>
 int bn_fwd(ocm_ctx* ctx, const void* x, int N, int C, int L, const float* gamma, const float* beta, float eps,
-           float momentum, float* rmean, float* rvar, void* y, float* smean, float* sinv, void* scratch,
+           float momentum, float* rmean, float* rvar, void* y, float* smean, float* sinv, void* scratch, int act,
            hipStream_t st) {
   auto* part = static_cast<double*>(scratch ? scratch : ocm::workspace(ctx, bn_scratch(C), st));
   if (!part) return OCM_ERR_NOMEM;
   hipLaunchKernelGGL(k_bn_stats<T>, dim3(BN_SPLIT, C), dim3(BN_T), 0, st, static_cast<const T*>(x), N, C, L, part);
   hipLaunchKernelGGL(k_bn_finalize, dim3((C + 63) / 64), dim3(64), 0, st, part, C, (int64_t)N * L, eps, momentum,
                      smean, sinv, rmean, rvar);
-  hipLaunchKernelGGL(k_bn_apply<T>, dim3((L + BN_T - 1) / BN_T, N * C), dim3(BN_T), 0, st,
-                     static_cast<const T*>(x), C, L, smean, sinv, gamma, beta, static_cast<T*>(y));
+  const dim3 ga((L + BN_T - 1) / BN_T, N * C);
+  if (act == OCM_ACT_ELU)
+    hipLaunchKernelGGL((k_bn_apply<T, true>), ga, dim3(BN_T), 0, st, static_cast<const T*>(x), C, L, smean, sinv,
+                       gamma, beta, static_cast<T*>(y));
+  else
+    hipLaunchKernelGGL((k_bn_apply<T, false>), ga, dim3(BN_T), 0, st, static_cast<const T*>(x), C, L, smean, sinv,
+                       gamma, beta, static_cast<T*>(y));
   OCM_CHECK_LAUNCH("k_bn_fwd");
   return OCM_OK;
 }
 
-template <typename T>
-int bn_bwd(ocm_ctx* ctx, const void* x, const void* dy, int N, int C, int L, const float* gamma, const float* smean,
-           const float* sinv, void* dx, float* dgamma, float* dbeta, void* scratch, hipStream_t st) {
+template <typename T, bool ELU>
+int bn_bwd(ocm_ctx* ctx, const void* x, const void* dy, const void* ya, int N, int C, int L, const float* gamma,
+           const float* smean, const float* sinv, void* dx, float* dgamma, float* dbeta, void* scratch,
+           hipStream_t st) {
   auto* part = static_cast<double*>(scratch ? scratch : ocm::workspace(ctx, bn_scratch(C), st));
   if (!part) return OCM_ERR_NOMEM;
   double* sums = part + (size_t)C * BN_SPLIT * 2;
-  hipLaunchKernelGGL(k_bn_bwd_stats<T>, dim3(BN_SPLIT, C), dim3(BN_T), 0, st, static_cast<const T*>(x),
-                     static_cast<const T*>(dy), N, C, L, smean, sinv, part);
+  hipLaunchKernelGGL((k_bn_bwd_stats<T, ELU>), dim3(BN_SPLIT, C), dim3(BN_T), 0, st, static_cast<const T*>(x),
+                     static_cast<const T*>(dy), static_cast<const T*>(ya), N, C, L, smean, sinv, part);
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64), 0, st, part, C, sums, dgamma, dbeta);
-  hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3((L + BN_T - 1) / BN_T, N * C), dim3(BN_T), 0, st,
-                     static_cast<const T*>(x), static_cast<const T*>(dy), C, L, (int64_t)N * L, smean, sinv, gamma,
-                     sums, static_cast<T*>(dx));
+  hipLaunchKernelGGL((k_bn_bwd_apply<T, ELU>), dim3((L + BN_T - 1) / BN_T, N * C), dim3(BN_T), 0, st,
+                     static_cast<const T*>(x), static_cast<const T*>(dy), static_cast<const T*>(ya), C, L,
+                     (int64_t)N * L, smean, sinv, gamma, sums, static_cast<T*>(dx));
   OCM_CHECK_LAUNCH("k_bn_bwd");
   return OCM_OK;
 }
@@ -211,31 +231,40 @@ size_t ocm_bn_scratch_bytes(int32_t C) { return C > 0 ? bn_scratch(C) : 0; }
 
 int ocm_bn_fwd_train(ocm_ctx* ctx, int32_t dtype, const void* x, int32_t N, int32_t C, int32_t L,
                      const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
-                     float* running_var, void* y, float* save_mean, float* save_invstd, void* scratch,
+                     float* running_var, int32_t act, void* y, float* save_mean, float* save_invstd, void* scratch,
                      void* stream) {
   OCM_REQUIRE(ctx && x && y && save_mean && save_invstd, "ocm_bn_fwd_train: NULL argument");
   OCM_REQUIRE(N > 0 && C > 0 && L > 0, "ocm_bn_fwd_train: bad shape");
   OCM_REQUIRE(!running_mean == !running_var, "ocm_bn_fwd_train: running_mean and running_var go together");
+  OCM_REQUIRE(act == OCM_ACT_NONE || act == OCM_ACT_ELU, "ocm_bn_fwd_train: act must be OCM_ACT_NONE or OCM_ACT_ELU");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == OCM_DTYPE_F32)
     return bn_fwd<float>(ctx, x, N, C, L, gamma, beta, eps, momentum, running_mean, running_var, y, save_mean,
-                         save_invstd, scratch, st);
+                         save_invstd, scratch, act, st);
   if (dtype == OCM_DTYPE_BF16)
-    return bn_fwd<bf16_t>(ctx, x, N, C, L, gamma, beta, eps, momentum, running_mean, running_var, y,
-                                  save_mean, save_invstd, scratch, st);
+    return bn_fwd<bf16_t>(ctx, x, N, C, L, gamma, beta, eps, momentum, running_mean, running_var, y, save_mean,
+                          save_invstd, scratch, act, st);
   return ocm::fail(OCM_ERR_ARG, "ocm_bn_fwd_train: dtype must be OCM_DTYPE_F32 or OCM_DTYPE_BF16");
 }
 
 int ocm_bn_bwd(ocm_ctx* ctx, int32_t dtype, const void* x, const void* dy, int32_t N, int32_t C, int32_t L,
-               const float* gamma, const float* save_mean, const float* save_invstd, void* dx, float* dgamma,
-               float* dbeta, void* scratch, void* stream) {
+               const float* gamma, const float* save_mean, const float* save_invstd, int32_t act, const void* y,
+               void* dx, float* dgamma, float* dbeta, void* scratch, void* stream) {
   OCM_REQUIRE(ctx && x && dy && dx && save_mean && save_invstd, "ocm_bn_bwd: NULL argument");
   OCM_REQUIRE(N > 0 && C > 0 && L > 0, "ocm_bn_bwd: bad shape");
+  OCM_REQUIRE(act == OCM_ACT_NONE || (act == OCM_ACT_ELU && y), "ocm_bn_bwd: the fused ELU needs its output y");
   hipStream_t st = (hipStream_t)stream;
+  const bool elu = act == OCM_ACT_ELU;
   if (dtype == OCM_DTYPE_F32)
-    return bn_bwd<float>(ctx, x, dy, N, C, L, gamma, save_mean, save_invstd, dx, dgamma, dbeta, scratch, st);
+    return elu ? bn_bwd<float, true>(ctx, x, dy, y, N, C, L, gamma, save_mean, save_invstd, dx, dgamma, dbeta,
+                                     scratch, st)
+               : bn_bwd<float, false>(ctx, x, dy, y, N, C, L, gamma, save_mean, save_invstd, dx, dgamma, dbeta,
+                                      scratch, st);
   if (dtype == OCM_DTYPE_BF16)
-    return bn_bwd<bf16_t>(ctx, x, dy, N, C, L, gamma, save_mean, save_invstd, dx, dgamma, dbeta, scratch, st);
+    return elu ? bn_bwd<bf16_t, true>(ctx, x, dy, y, N, C, L, gamma, save_mean, save_invstd, dx, dgamma, dbeta,
+                                      scratch, st)
+               : bn_bwd<bf16_t, false>(ctx, x, dy, y, N, C, L, gamma, save_mean, save_invstd, dx, dgamma, dbeta,
+                                       scratch, st);
   return ocm::fail(OCM_ERR_ARG, "ocm_bn_bwd: dtype must be OCM_DTYPE_F32 or OCM_DTYPE_BF16");
 }
 

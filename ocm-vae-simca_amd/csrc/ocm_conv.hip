@@ -1,0 +1,327 @@
+// Narrow 1-D convolutions of the VAE (vae_model.py:37-81: Conv1d /
+// ConvTranspose1d with 1-12 channels, kernel 7, stride 1 or 2, B = 512 ×
+// L = 2048).  MIOpen lowers these to implicit-GEMM kernels plus NCHW↔NHWC
+// transposes: ≈ 19 kernels and ≈ 0.95 ms per graphed C4 training step,
+// 36 % of it (profiles/r03g_vae_step_trace.md), for a few MB of activations per
+// layer.  Here every pass is one direct kernel over the positions (the data is
+// HBM/L2-streamed once; channels and taps are a handful of FMAs per element):
+//
+//   down  y[b][o][l] = bias[o] + Σ_i Σ_t w[o][i][t] · x[b][i][l·s + t − pad]
+//         — Conv1d forward (w: [O][I][K]) and ConvTranspose1d's input gradient
+//   up    y[b][o][j] = bias[o] + Σ_i Σ_t w[i][o][t] · x[b][i][(j + pad − t)/s]
+//         (terms where s divides j + pad − t and the index is in range)
+//         — ConvTranspose1d forward (w: [I][O][K]) and Conv1d's input gradient
+//   wgrad G[o][i][t] = Σ_b Σ_l P[b][o][l] · Q[b][i][l·s + t − pad]
+//         — Conv1d: P = dy, Q = x → dW[co][ci][t];  ConvTranspose1d: P = x,
+//           Q = dy → dW[ci][co][t]; per-workgroup partials, summed in a fixed
+//           order by a second launch (deterministic)
+//   csum  Σ_b Σ_l dy[b][c][l] (the bias gradient), two-stage likewise.
+//
+// Activations (N, C, L) contiguous, float32 or bfloat16 (autocast); weights,
+// bias and gradients of them float32; accumulation float32.  Each thread of
+// down / up computes four output channels of one position (grid.y = channel
+// groups); the four channels' weights sit in LDS.
+#include <algorithm>
+
+#include "ocm_internal.h"
+
+namespace {
+
+struct bf16_t {
+  uint16_t bits;
+};
+__device__ __forceinline__ float cv_ld(const float* p, int64_t i) { return p[i]; }
+__device__ __forceinline__ float cv_ld(const bf16_t* p, int64_t i) { return __uint_as_float((uint32_t)p[i].bits << 16); }
+__device__ __forceinline__ void cv_st(float* p, int64_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void cv_st(bf16_t* p, int64_t i, float v) {
+  // round to nearest even, NaN kept quiet (torch's float → bfloat16)
+  const uint32_t u = __float_as_uint(v);
+  const uint32_t r = (u & 0x7fffffffu) > 0x7f800000u ? (u | 0x00400000u) : u + 0x7fffu + ((u >> 16) & 1u);
+  p[i].bits = (uint16_t)(r >> 16);
+}
+
+constexpr int CV_T = 256, CV_OG = 4, CV_KMAX = 15, CV_CMAX = 64;
+constexpr int WG_SPLIT = 128;   // csum partial workgroups per channel
+constexpr int WG_MAXSPLIT = 1024;  // wgrad partial workgroups per (o, i) pair, at most
+
+// down / up: grid (ceil(Lout / CV_T), ceil(O / 4), B).  KT ≥ K is the
+// compile-time tap count, so the taps of one input channel unroll and their
+// loads issue together (a runtime tap loop waits out one load latency per tap).
+template <bool UP, int KT, typename TI, typename TO>
+__global__ __launch_bounds__(CV_T) void k_conv(const TI* __restrict__ x, int I, int Lin, const float* __restrict__ w,
+                                              const float* __restrict__ bias, int O, int Lout, int K, int s, int pad,
+                                              TO* __restrict__ y) {
+  // the four output channels' weights, CV_KMAX slots per input channel (zero past K)
+  __shared__ float sw[CV_OG][CV_CMAX * CV_KMAX];
+  const int o0 = blockIdx.y * CV_OG, b = blockIdx.z;
+  for (int e = threadIdx.x; e < CV_OG * I * CV_KMAX; e += CV_T) {
+    const int u = e / (I * CV_KMAX), r = e % (I * CV_KMAX), i = r / CV_KMAX, t = r % CV_KMAX;
+    const int o = o0 + u;
+    sw[u][r] = (o < O && t < K) ? (UP ? w[((int64_t)i * O + o) * K + t] : w[((int64_t)o * I + i) * K + t]) : 0.f;
+  }
+  __syncthreads();
+  const int l = blockIdx.x * CV_T + threadIdx.x;
+  if (l >= Lout) return;
+  float acc[CV_OG];
+#pragma unroll
+  for (int u = 0; u < CV_OG; ++u) acc[u] = (bias && o0 + u < O) ? bias[o0 + u] : 0.f;
+  const TI* xb = x + (int64_t)b * I * Lin;
+  // up: the taps that reach output l are t ≡ (l + pad) mod s, input l' = (l + pad − t)/s
+  const int q0 = l + pad;
+  const int t0 = UP ? q0 % s : 0;
+  // the next input channel's taps are loaded before this channel's FMAs
+  auto taps = [&](int i, float (&v)[KT]) __attribute__((always_inline)) {
+    const TI* xr = xb + (int64_t)i * Lin;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      int j;
+      bool ok;
+      if (UP) {
+        const int tt = t0 + t * s;  // t-th tap of this output's residue class
+        j = (q0 - tt) / s;
+        ok = tt < K && q0 >= tt && j < Lin;
+      } else {
+        j = l * s + t - pad;
+        ok = t < K && j >= 0 && j < Lin;
+      }
+      v[t] = ok ? cv_ld(xr, j) : 0.f;
+    }
+  };
+  float va[KT], vb[KT];
+  taps(0, va);
+  for (int i = 0; i < I; i += 2) {
+    if (i + 1 < I) taps(i + 1, vb);
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      // raw tap of v[t] (clamped into the slot row: v[t] = 0 there)
+      const int tw = UP ? min(t0 + t * s, CV_KMAX - 1) : t;
+#pragma unroll
+      for (int u = 0; u < CV_OG; ++u) acc[u] = fmaf(sw[u][i * CV_KMAX + tw], va[t], acc[u]);
+    }
+    if (i + 1 >= I) break;
+    if (i + 2 < I) taps(i + 2, va);
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      const int tw = UP ? min(t0 + t * s, CV_KMAX - 1) : t;
+#pragma unroll
+      for (int u = 0; u < CV_OG; ++u) acc[u] = fmaf(sw[u][(i + 1) * CV_KMAX + tw], vb[t], acc[u]);
+    }
+  }
+  TO* yb = y + (int64_t)b * O * Lout;
+#pragma unroll
+  for (int u = 0; u < CV_OG; ++u)
+    if (o0 + u < O) cv_st(yb, (int64_t)(o0 + u) * Lout + l, acc[u]);
+}
+
+// wgrad: grid (split, I · ⌈O/4⌉).  Consecutive threads take consecutive
+// positions (b, l) of P (coalesced); a thread loads the K taps of Q[i] once and
+// four P channels, and accumulates the 4·K products; with WB (the Conv1d case,
+// P = dy) the i = 0 threads also sum P, the bias gradient, as tap K.  The
+// workgroup's partial sums go to part[((o·I + i)·split + x)·KS + t], KS = K + WB.
+template <int KT, bool WB, typename TP, typename TQ>
+__global__ __launch_bounds__(CV_T) void k_conv_wgrad(const TP* __restrict__ P, int O, int Lp, const TQ* __restrict__ Q,
+                                                    int I, int Lq, int B, int K, int s, int pad,
+                                                    float* __restrict__ part) {
+  constexpr int NA = KT + (WB ? 1 : 0);
+  __shared__ float red[CV_T / 64][CV_OG][NA];
+  const int i = blockIdx.y % I, o0 = (blockIdx.y / I) * CV_OG;
+  const int64_t total = (int64_t)B * Lp;
+  float acc[CV_OG][NA];  // KT ≥ K: the taps unroll with compile-time indices
+#pragma unroll
+  for (int u = 0; u < CV_OG; ++u)
+#pragma unroll
+    for (int t = 0; t < NA; ++t) acc[u][t] = 0.f;
+  for (int64_t e = (int64_t)blockIdx.x * CV_T + threadIdx.x; e < total; e += (int64_t)gridDim.x * CV_T) {
+    const int b = (int)(e / Lp), l = (int)(e - (int64_t)b * Lp);
+    const TQ* qr = Q + ((int64_t)b * I + i) * Lq;
+    const int j0 = l * s - pad;
+    float qv[KT], pv[CV_OG];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      const int j = j0 + t;
+      qv[t] = (t < K && j >= 0 && j < Lq) ? cv_ld(qr, j) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < CV_OG; ++u) pv[u] = o0 + u < O ? cv_ld(P, ((int64_t)b * O + o0 + u) * Lp + l) : 0.f;
+#pragma unroll
+    for (int u = 0; u < CV_OG; ++u) {
+#pragma unroll
+      for (int t = 0; t < KT; ++t) acc[u][t] = fmaf(pv[u], qv[t], acc[u][t]);
+      if (WB) acc[u][NA - 1] += pv[u];
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < CV_OG; ++u)
+#pragma unroll
+    for (int t = 0; t < NA; ++t) {
+      const float v = wave_sum_f32(acc[u][t]);
+      if (lane == 0) red[wv][u][t] = v;
+    }
+  __syncthreads();
+  const int KS = K + (WB ? 1 : 0);
+  for (int e = threadIdx.x; e < CV_OG * KS; e += CV_T) {
+    const int u = e / KS, t = e % KS, o = o0 + u;
+    const int ts = (WB && t == K) ? NA - 1 : t;
+    if (o < O)
+      part[(((int64_t)o * I + i) * gridDim.x + blockIdx.x) * KS + t] =
+          (red[0][u][ts] + red[1][u][ts]) + (red[2][u][ts] + red[3][u][ts]);
+  }
+}
+
+// G[(o·I + i)·K + t] = Σ_x part[((o·I + i)·split + x)·KS + t], one wave per
+// output (lane-strided partials, then the wave sum: a fixed order); with WB
+// the i = 0 slot t = K of each o is its bias gradient, db[o].
+__global__ __launch_bounds__(CV_T) void k_conv_wgrad_reduce(const float* __restrict__ part, int O, int I, int K,
+                                                           int KS, int split, float* __restrict__ G,
+                                                           float* __restrict__ db) {
+  const int wv = (blockIdx.x * CV_T + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  const int nout = O * I * KS;
+  if (wv >= nout) return;
+  const int pair = wv / KS, t = wv % KS;
+  float v = 0.f;
+  for (int xb = lane; xb < split; xb += 64) v += part[((int64_t)pair * split + xb) * KS + t];
+  v = wave_sum_f32(v);
+  if (lane) return;
+  if (t < K) G[(int64_t)pair * K + t] = v;
+  else if (pair % I == 0) db[pair / I] = v;
+}
+
+// per-channel sums of (B, C, L): grid (WG_SPLIT, C) partials, then one reduce
+template <typename T>
+__global__ __launch_bounds__(CV_T) void k_chan_sum(const T* __restrict__ v, int B, int C, int L,
+                                                  float* __restrict__ part) {
+  __shared__ float red[CV_T / 64];
+  const int c = blockIdx.y;
+  const int64_t total = (int64_t)B * L;
+  float a = 0.f;
+  for (int64_t e = (int64_t)blockIdx.x * CV_T + threadIdx.x; e < total; e += (int64_t)WG_SPLIT * CV_T) {
+    const int b = (int)(e / L), l = (int)(e % L);
+    a += cv_ld(v, ((int64_t)b * C + c) * L + l);
+  }
+  a = wave_sum_f32(a);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) part[(int64_t)c * WG_SPLIT + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void k_chan_sum_reduce(const float* __restrict__ part, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double v = 0.0;
+  for (int xb = 0; xb < WG_SPLIT; ++xb) v += part[(int64_t)c * WG_SPLIT + xb];
+  out[c] = (float)v;
+}
+
+template <bool UP, int KT>
+int launch_conv_k(int dti, int dto, const void* x, int B, int I, int Lin, const float* w, const float* bias, int O,
+                  int Lout, int K, int s, int pad, void* y, hipStream_t st) {
+  dim3 g((unsigned)((Lout + CV_T - 1) / CV_T), (unsigned)((O + CV_OG - 1) / CV_OG), (unsigned)B);
+#define OCM_CONV_L(TI, TO)                                                                                        \
+  hipLaunchKernelGGL((k_conv<UP, KT, TI, TO>), g, dim3(CV_T), 0, st, static_cast<const TI*>(x), I, Lin, w, bias, O, \
+                     Lout, K, s, pad, static_cast<TO*>(y))
+  if (dti == OCM_DTYPE_F32 && dto == OCM_DTYPE_F32) OCM_CONV_L(float, float);
+  else if (dti == OCM_DTYPE_F32) OCM_CONV_L(float, bf16_t);
+  else if (dto == OCM_DTYPE_F32) OCM_CONV_L(bf16_t, float);
+  else OCM_CONV_L(bf16_t, bf16_t);
+#undef OCM_CONV_L
+  OCM_CHECK_LAUNCH("k_conv");
+  return OCM_OK;
+}
+
+template <bool UP>
+int launch_conv(int dti, int dto, const void* x, int B, int I, int Lin, const float* w, const float* bias, int O,
+                int Lout, int K, int s, int pad, void* y, hipStream_t st) {
+  // up: KT counts the taps of one residue class, ⌈K / s⌉
+  const int kt = UP ? (K + s - 1) / s : K;
+  if (kt == 1) return launch_conv_k<UP, 1>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
+  if (kt <= 4) return launch_conv_k<UP, 4>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
+  if (kt <= 7) return launch_conv_k<UP, 7>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
+  return launch_conv_k<UP, CV_KMAX>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t ocm_conv1d_scratch_bytes(int32_t O, int32_t I, int32_t K) {
+  return (size_t)((int64_t)O * I * (K + 1) + (int64_t)(O > I ? O : I)) * WG_MAXSPLIT * sizeof(float) + 256;
+}
+
+int ocm_conv1d(ocm_ctx* ctx, int32_t mode, int32_t dtype_in, const void* x, int32_t B, int32_t I, int32_t Lin,
+               const float* w, const float* bias, int32_t O, int32_t Lout, int32_t K, int32_t stride, int32_t pad,
+               int32_t dtype_out, void* y, void* stream) {
+  OCM_REQUIRE(ctx && x && w && y, "ocm_conv1d: NULL argument");
+  OCM_REQUIRE(mode == OCM_CONV_DOWN || mode == OCM_CONV_UP, "ocm_conv1d: mode must be OCM_CONV_DOWN or OCM_CONV_UP");
+  OCM_REQUIRE(B > 0 && I > 0 && O > 0 && Lin > 0 && Lout > 0 && B <= 65535, "ocm_conv1d: bad shape");
+  OCM_REQUIRE(I <= CV_CMAX && K >= 1 && K <= CV_KMAX && stride >= 1 && pad >= 0,
+              "ocm_conv1d: channels ≤ 64, kernel ≤ 15, stride ≥ 1");
+  OCM_REQUIRE((dtype_in == OCM_DTYPE_F32 || dtype_in == OCM_DTYPE_BF16) &&
+                  (dtype_out == OCM_DTYPE_F32 || dtype_out == OCM_DTYPE_BF16),
+              "ocm_conv1d: float32 / bfloat16 activations");
+  hipStream_t st = (hipStream_t)stream;
+  return mode == OCM_CONV_DOWN ? launch_conv<false>(dtype_in, dtype_out, x, B, I, Lin, w, bias, O, Lout, K, stride, pad, y, st)
+                               : launch_conv<true>(dtype_in, dtype_out, x, B, I, Lin, w, bias, O, Lout, K, stride, pad, y, st);
+}
+
+int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, int32_t Lp, int32_t dtype_q,
+                     const void* Q, int32_t I, int32_t Lq, int32_t B, int32_t K, int32_t stride, int32_t pad,
+                     float* G_out, float* psum_out, void* scratch, void* stream) {
+  OCM_REQUIRE(ctx && P && Q && G_out && scratch, "ocm_conv1d_wgrad: NULL argument");
+  OCM_REQUIRE(B > 0 && O > 0 && I > 0 && Lp > 0 && Lq > 0 && (int64_t)I * ((O + CV_OG - 1) / CV_OG) <= 65535,
+              "ocm_conv1d_wgrad: bad shape");
+  OCM_REQUIRE(K >= 1 && K <= CV_KMAX && stride >= 1 && pad >= 0, "ocm_conv1d_wgrad: kernel ≤ 15, stride ≥ 1");
+  OCM_REQUIRE((dtype_p == OCM_DTYPE_F32 || dtype_p == OCM_DTYPE_BF16) &&
+                  (dtype_q == OCM_DTYPE_F32 || dtype_q == OCM_DTYPE_BF16),
+              "ocm_conv1d_wgrad: float32 / bfloat16 activations");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = static_cast<float*>(scratch);
+  const int groups = I * ((O + CV_OG - 1) / CV_OG);
+  // ≈ 4096 workgroups in all, so a layer with few channels still fills the chip
+  const int split = std::max(16, std::min(WG_MAXSPLIT, 4096 / groups));
+  const bool wb = psum_out != nullptr;
+  dim3 g((unsigned)split, (unsigned)groups);
+#define OCM_WG_K(KT, WB, TP, TQ)                                                                            \
+  hipLaunchKernelGGL((k_conv_wgrad<KT, WB, TP, TQ>), g, dim3(CV_T), 0, st, static_cast<const TP*>(P), O, Lp,   \
+                     static_cast<const TQ*>(Q), I, Lq, B, K, stride, pad, part)
+#define OCM_WG_L(TP, TQ)                                  \
+  do {                                                    \
+    if (K <= 7 && wb) OCM_WG_K(7, true, TP, TQ);          \
+    else if (K <= 7) OCM_WG_K(7, false, TP, TQ);          \
+    else if (wb) OCM_WG_K(CV_KMAX, true, TP, TQ);         \
+    else OCM_WG_K(CV_KMAX, false, TP, TQ);                \
+  } while (0)
+  if (dtype_p == OCM_DTYPE_F32 && dtype_q == OCM_DTYPE_F32) OCM_WG_L(float, float);
+  else if (dtype_p == OCM_DTYPE_F32) OCM_WG_L(float, bf16_t);
+  else if (dtype_q == OCM_DTYPE_F32) OCM_WG_L(bf16_t, float);
+  else OCM_WG_L(bf16_t, bf16_t);
+#undef OCM_WG_L
+#undef OCM_WG_K
+  OCM_CHECK_LAUNCH("k_conv_wgrad");
+  const int KS = K + (wb ? 1 : 0);
+  const int64_t waves = (int64_t)O * I * KS;
+  hipLaunchKernelGGL(k_conv_wgrad_reduce, dim3((unsigned)((waves * 64 + CV_T - 1) / CV_T)), dim3(CV_T), 0, st, part,
+                     O, I, K, KS, split, G_out, psum_out);
+  OCM_CHECK_LAUNCH("k_conv_wgrad_reduce");
+  return OCM_OK;
+}
+
+int ocm_chan_sum(ocm_ctx* ctx, int32_t dtype, const void* v, int32_t B, int32_t C, int32_t L, float* out,
+                 void* scratch, void* stream) {
+  OCM_REQUIRE(ctx && v && out && scratch, "ocm_chan_sum: NULL argument");
+  OCM_REQUIRE(B > 0 && C > 0 && L > 0 && C <= 65535, "ocm_chan_sum: bad shape");
+  OCM_REQUIRE(dtype == OCM_DTYPE_F32 || dtype == OCM_DTYPE_BF16, "ocm_chan_sum: float32 / bfloat16");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = static_cast<float*>(scratch);
+  dim3 g(WG_SPLIT, (unsigned)C);
+  if (dtype == OCM_DTYPE_F32)
+    hipLaunchKernelGGL(k_chan_sum<float>, g, dim3(CV_T), 0, st, static_cast<const float*>(v), B, C, L, part);
+  else
+    hipLaunchKernelGGL(k_chan_sum<bf16_t>, g, dim3(CV_T), 0, st, static_cast<const bf16_t*>(v), B, C, L, part);
+  OCM_CHECK_LAUNCH("k_chan_sum");
+  hipLaunchKernelGGL(k_chan_sum_reduce, dim3((unsigned)((C + 63) / 64)), dim3(64), 0, st, part, C, out);
+  OCM_CHECK_LAUNCH("k_chan_sum_reduce");
+  return OCM_OK;
+}
+
+}  // extern "C"

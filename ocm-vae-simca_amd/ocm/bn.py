@@ -8,16 +8,25 @@ of csrc/ocm_bn.hip instead of MIOpen's spatial BN, which handles the VAE's
 (running statistics) and host tensors use the stock module.  The kernels
 launch on the current stream, so the module is HIP-graph capturable
 (ocm/vae_train.py); their reduction scratch is caller-owned (``_scratch``).
+
+``fuse_elu()`` folds the ELU that follows every batch norm of the VAE
+(vae_model.py:45-49, 75-79) into the same kernels: the normalisation pass
+writes ELU(z), and the backward passes form the ELU's input gradient from
+the saved output on the fly (two elementwise kernels fewer per layer and
+direction).  ConvVAE1D then puts an ``nn.Identity`` where the ELU module was,
+so parameters and state_dict keys do not move.
 """
 from __future__ import annotations
 
 import torch
+import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
 from ._lib import Context, check, ptr, stream_handle
 
 _DT = {torch.float32: 0, torch.bfloat16: 1}
+ACT_NONE, ACT_ELU = 0, 1  # include/ocm.h OCM_ACT_*
 
 
 def _scratch(C: int, dev) -> torch.Tensor:
@@ -31,7 +40,7 @@ def _scratch(C: int, dev) -> torch.Tensor:
 
 class _BNTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum):
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, act):
         x = x.contiguous()
         N, C, L = x.shape
         dev = x.device
@@ -43,16 +52,17 @@ class _BNTrain(torch.autograd.Function):
         h = Context.get(dev.index).handle
         scratch = _scratch(C, dev)
         check(_lib.load().ocm_bn_fwd_train(h, _DT[x.dtype], ptr(x), N, C, L, ptr(w), ptr(b), float(eps),
-                                           float(momentum), ptr(running_mean), ptr(running_var), ptr(y),
+                                           float(momentum), ptr(running_mean), ptr(running_var), act, ptr(y),
                                            ptr(smean), ptr(sinv), ptr(scratch), stream_handle(dev)),
               "ocm_bn_fwd_train")
-        ctx.save_for_backward(x, w, smean, sinv)
+        ctx.act = act
+        ctx.save_for_backward(x, w, smean, sinv, y if act else None)
         ctx.has_w, ctx.has_b = weight is not None, bias is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w, smean, sinv = ctx.saved_tensors
+        x, w, smean, sinv, y = ctx.saved_tensors
         dy = dy.contiguous().to(x.dtype)
         N, C, L = x.shape
         dev = x.device
@@ -62,20 +72,29 @@ class _BNTrain(torch.autograd.Function):
         h = Context.get(dev.index).handle
         scratch = _scratch(C, dev)
         check(_lib.load().ocm_bn_bwd(h, _DT[x.dtype], ptr(x), ptr(dy), N, C, L, ptr(w), ptr(smean), ptr(sinv),
-                                     ptr(dx), ptr(dw), ptr(db), ptr(scratch), stream_handle(dev)), "ocm_bn_bwd")
-        return dx, dw, db, None, None, None, None
+                                     ctx.act, ptr(y), ptr(dx), ptr(dw), ptr(db), ptr(scratch), stream_handle(dev)),
+              "ocm_bn_bwd")
+        return dx, dw, db, None, None, None, None, None
 
 
 class FastBatchNorm1d(nn.BatchNorm1d):
-    """nn.BatchNorm1d with the libocm training-mode kernels on HIP tensors."""
+    """nn.BatchNorm1d with the libocm training-mode kernels on HIP tensors
+    (and, after ``fuse_elu()``, the ELU that follows it)."""
+
+    act = ACT_NONE
+
+    def fuse_elu(self):
+        self.act = ACT_ELU
+        return self
 
     def forward(self, x):
         if not (self.training and x.is_cuda and x.dim() == 3 and x.dtype in _DT) or self.momentum is None:
             # eval (running statistics), host tensors, cumulative-average momentum: the stock module
-            return super().forward(x)
+            y = super().forward(x)
+            return F.elu(y) if self.act == ACT_ELU else y
         if self.track_running_stats and self.num_batches_tracked is not None:
             self.num_batches_tracked.add_(1)
         momentum = self.momentum
         track = self.track_running_stats and self.running_mean is not None
         return _BNTrain.apply(x, self.weight, self.bias, self.running_mean if track else None,
-                              self.running_var if track else None, self.eps, momentum)
+                              self.running_var if track else None, self.eps, momentum, self.act)

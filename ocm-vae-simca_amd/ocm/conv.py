@@ -1,0 +1,128 @@
+"""Narrow Conv1d / ConvTranspose1d on libocm (ocm_conv1d / ocm_conv1d_wgrad).
+
+``FastConv1d`` and ``FastConvTranspose1d`` are ``nn.Conv1d`` /
+``nn.ConvTranspose1d`` (same parameters and state_dict keys — vae_model.py:
+37-81 builds the stock modules) whose forward on a HIP device, for the VAE's
+shapes (≤ 64 channels, kernel ≤ 15, no groups or dilation, zero padding), runs
+the direct kernels of csrc/ocm_conv.hip instead of MIOpen's implicit GEMMs and
+layout transposes (36 % of the graphed C4 step, profiles/r03g_vae_step_trace.md).
+Under bf16 autocast the activations are bf16, as torch's autocast conv would
+make them; the weights stay float32 (torch would round them to bf16 first) and
+every sum is float32.  Other shapes, host tensors and bf16 weights take the
+stock module.  All launches are on the current stream with caller-owned
+scratch, so the modules are HIP-graph capturable (ocm/vae_train.py).
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import _lib
+from ._lib import Context, check, ptr, stream_handle
+
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+DOWN, UP = 0, 1  # include/ocm.h OCM_CONV_DOWN / OCM_CONV_UP
+
+
+def _scratch(O: int, I: int, K: int, dev) -> torch.Tensor:
+    nbytes = int(_lib.load().ocm_conv1d_scratch_bytes(O, I, K))
+    return torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+
+
+def _launch(mode, x, w, bias, O, Lout, K, stride, pad, out_dtype):
+    B, I, Lin = x.shape
+    y = torch.empty((B, O, Lout), dtype=out_dtype, device=x.device)
+    check(_lib.load().ocm_conv1d(Context.get(x.device.index).handle, mode, _DT[x.dtype], ptr(x), B, I, Lin, ptr(w),
+                                 ptr(bias), O, Lout, K, stride, pad, _DT[out_dtype], ptr(y), stream_handle(x.device)),
+          "ocm_conv1d")
+    return y
+
+
+class _ConvFn(torch.autograd.Function):
+    """y = conv (transposed=False, weight [O][I][K]) or transposed conv
+    (transposed=True, weight [I][O][K]) of x (B, I, Lin)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, pad, transposed, Lout, out_dtype):
+        x = x.contiguous()
+        w = weight.detach().contiguous()
+        b = bias.detach().contiguous() if bias is not None else None
+        K = w.shape[2]
+        O = w.shape[1] if transposed else w.shape[0]
+        y = _launch(UP if transposed else DOWN, x, w, b, O, Lout, K, stride, pad, out_dtype)
+        ctx.save_for_backward(x, w)
+        ctx.conf = (stride, pad, transposed, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pad, transposed, has_bias = ctx.conf
+        dy = dy.contiguous()
+        if dy.dtype not in _DT:
+            dy = dy.float()
+        B, I, Lin = x.shape
+        _, O, Lout = dy.shape
+        K = w.shape[2]
+        dev = x.device
+        h = Context.get(dev.index).handle
+        st = stream_handle(dev)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            # the adjoint pass: Conv1d's input gradient is the "up" form of dy with
+            # its [O][I][K] weight; ConvTranspose1d's is the "down" form
+            dx = _launch(DOWN if transposed else UP, dy, w, None, I, Lin, K, stride, pad, x.dtype)
+        want_db = has_bias and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] or want_db:
+            scratch = _scratch(O, I, K, dev)
+            db = torch.empty(O, dtype=torch.float32, device=dev) if want_db else None
+            dw = torch.empty_like(w)
+            if transposed:  # dW[i][o][t] = Σ x[b][i][l] · dy[b][o][l·s + t − pad]; db = Σ dy separately
+                args = (_DT[x.dtype], ptr(x), I, Lin, _DT[dy.dtype], ptr(dy), O, Lout, B, K, stride, pad, ptr(dw),
+                        None)
+            else:  # dW[o][i][t] = Σ dy[b][o][l] · x[b][i][l·s + t − pad], db = Σ dy in the same pass
+                args = (_DT[dy.dtype], ptr(dy), O, Lout, _DT[x.dtype], ptr(x), I, Lin, B, K, stride, pad, ptr(dw),
+                        ptr(db))
+            check(_lib.load().ocm_conv1d_wgrad(h, *args, ptr(scratch), st), "ocm_conv1d_wgrad")
+            if transposed and want_db:
+                check(_lib.load().ocm_chan_sum(h, _DT[dy.dtype], ptr(dy), B, O, Lout, ptr(db), ptr(scratch), st),
+                      "ocm_chan_sum")
+            if not ctx.needs_input_grad[1]:
+                dw = None
+        return dx, dw, db, None, None, None, None, None
+
+
+def _fast_ok(mod, x) -> bool:
+    return (x.is_cuda and x.dim() == 3 and x.dtype in _DT and mod.weight.dtype == torch.float32
+            and (mod.bias is None or mod.bias.dtype == torch.float32) and mod.groups == 1
+            and mod.dilation == (1,) and mod.padding_mode == "zeros" and not isinstance(mod.padding, str)
+            and max(mod.in_channels, mod.out_channels) <= 64 and mod.kernel_size[0] <= 15)
+
+
+def _act_dtype(x):
+    if torch.is_autocast_enabled("cuda"):
+        dt = torch.get_autocast_dtype("cuda")
+        return dt if dt in _DT else x.dtype
+    return x.dtype
+
+
+class FastConv1d(nn.Conv1d):
+    """nn.Conv1d with libocm's direct kernels for the VAE's narrow shapes."""
+
+    def forward(self, x):
+        if not _fast_ok(self, x):
+            return super().forward(x)
+        K, s, pad = self.kernel_size[0], self.stride[0], self.padding[0]
+        Lout = (x.shape[-1] + 2 * pad - K) // s + 1
+        return _ConvFn.apply(x, self.weight, self.bias, s, pad, False, Lout, _act_dtype(x))
+
+
+class FastConvTranspose1d(nn.ConvTranspose1d):
+    """nn.ConvTranspose1d with libocm's direct kernels for the VAE's narrow shapes."""
+
+    def forward(self, x, output_size=None):
+        if output_size is not None or not _fast_ok(self, x):
+            return super().forward(x, output_size)
+        K, s, pad, op = self.kernel_size[0], self.stride[0], self.padding[0], self.output_padding[0]
+        Lout = (x.shape[-1] - 1) * s - 2 * pad + K + op
+        return _ConvFn.apply(x, self.weight, self.bias, s, pad, True, Lout, _act_dtype(x))

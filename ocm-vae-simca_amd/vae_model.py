@@ -3,10 +3,12 @@
 ``ConvVAE1D``, ``beta_vae_bce_loss``, ``beta_vae_cosine_loss`` and
 ``compute_q_h_f`` keep the reference's names, signatures, buffers and
 state_dict layout (a checkpoint written by either loads into the other), and
-the same seeded initialisation.  The network itself stays on PyTorch-ROCm
+the same seeded initialisation.  The network stays a PyTorch-ROCm module
 (narrow Conv1d / BN / ELU / Linear layers are launch-bound,
-not MFMA targets); the training step is captured in a HIP graph by
-``ocm.vae_train``.  The latent statistics of ``compute_q_h_f`` (residual q,
+not MFMA targets); its convolutions (``ocm.conv``) and training-mode batch
+norms (``ocm.bn``) run libocm's direct HIP kernels on the GPU instead of
+MIOpen, with the stock modules' parameters and state_dict keys; the training
+step is captured in a HIP graph by ``ocm.vae_train``.  The latent statistics of ``compute_q_h_f`` (residual q,
 leverage h) run on libocm's HIP kernels when the tensors live on the GPU
 (``ocm.vae.qhf_device``): the same Gram / pseudo-inverse / quadratic-form
 kernels as SIMCA at p = d.
@@ -18,6 +20,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ocm.bn import FastBatchNorm1d
+from ocm.conv import FastConv1d, FastConvTranspose1d
 
 __all__ = ["ConvVAE1D", "beta_vae_cosine_loss", "beta_vae_bce_loss", "compute_q_h_f"]
 
@@ -65,7 +68,7 @@ class ConvVAE1D(nn.Module):
         layers, chans, length, c_in = [], n_filters, input_length, 1
         for b in range(conv_blocks):
             s_b = 1 if b == 0 else stride
-            layers += self._block(nn.Conv1d(c_in, chans, kernel_size, stride=s_b, padding=pad), chans, act_cls)
+            layers += self._block(FastConv1d(c_in, chans, kernel_size, stride=s_b, padding=pad), chans, act_cls)
             c_in, length = chans, _conv_out_len(length, kernel_size, s_b, pad)
             chans = min(chans * 2, 1024)
         self.encoder_conv = nn.Sequential(*layers)
@@ -85,10 +88,10 @@ class ConvVAE1D(nn.Module):
         for b in range(conv_blocks):
             nxt = max(chans // 2, n_filters)
             s_b = stride if b < conv_blocks - 1 else 1
-            layers += self._block(nn.ConvTranspose1d(chans, nxt, kernel_size, stride=s_b, padding=pad,
-                                                     output_padding=s_b - 1), nxt, act_cls)
+            layers += self._block(FastConvTranspose1d(chans, nxt, kernel_size, stride=s_b, padding=pad,
+                                                      output_padding=s_b - 1), nxt, act_cls)
             chans = nxt
-        layers.append(nn.Conv1d(chans, 1, kernel_size=1))
+        layers.append(FastConv1d(chans, 1, kernel_size=1))
         self.decoder_conv = nn.Sequential(*layers)
 
         self.register_buffer("spec_mean", torch.tensor(mean, dtype=torch.float32))
@@ -99,10 +102,14 @@ class ConvVAE1D(nn.Module):
 
     def _block(self, conv: nn.Module, chans: int, act_cls) -> list:
         mods = [conv]
-        if self.use_batchnorm:
-            # nn.BatchNorm1d with libocm's training kernels on HIP tensors (same state_dict)
-            mods.append(FastBatchNorm1d(chans))
-        mods.append(act_cls())
+        if self.use_batchnorm and act_cls is nn.ELU:
+            # nn.BatchNorm1d + ELU in libocm's training kernels on HIP tensors; the
+            # Identity keeps the ELU's slot, so the state_dict keys do not move
+            mods += [FastBatchNorm1d(chans).fuse_elu(), nn.Identity()]
+        elif self.use_batchnorm:
+            mods += [FastBatchNorm1d(chans), act_cls()]
+        else:
+            mods.append(act_cls())
         if self.dropout > 0:
             mods.append(nn.Dropout(self.dropout))
         return mods

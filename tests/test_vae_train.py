@@ -140,6 +140,49 @@ def test_fast_batchnorm_matches_torch(dtype, shape):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(512, 3, 2048), (64, 12, 512), (7, 5, 33)])
+def test_fused_batchnorm_elu_matches_torch(dtype, shape):
+    """FastBatchNorm1d.fuse_elu() == nn.BatchNorm1d followed by nn.ELU: output,
+    running statistics and the input / weight / bias gradients (the ELU's
+    backward formed from the saved output inside the BN kernels).  The
+    reference runs in float32 on the same (bf16-valued) inputs: the fused
+    kernels keep z and the ELU's input gradient in float32 where torch's bf16
+    modules round both to bf16 (2⁻⁸), which moves a small channel's Σ dz·x̂ by
+    more than that rounding of the output does."""
+    from ocm.bn import FastBatchNorm1d
+
+    dev = torch.device("cuda", 0)
+    N, C, L = shape
+    g = torch.Generator(device="cpu").manual_seed(C * L + 1)
+    x0 = (0.5 + 2.0 * torch.randn(N, C, L, generator=g)).to(dev)
+    ref = torch.nn.BatchNorm1d(C).to(dev)
+    fast = FastBatchNorm1d(C).fuse_elu().to(dev)
+    with torch.no_grad():
+        ref.weight.copy_(torch.linspace(0.5, 1.5, C))
+        ref.bias.copy_(torch.linspace(-0.2, 0.3, C))
+    fast.load_state_dict(ref.state_dict())
+    xr = x0.to(dtype).float().requires_grad_(True)
+    xf = x0.to(dtype).requires_grad_(True)
+    yr, yf = torch.nn.functional.elu(ref(xr)), fast(xf)
+    gy = torch.randn(N, C, L, generator=g).to(dev).to(dtype)
+    (yr * gy.float()).sum().backward()
+    (yf.float() * gy.float()).sum().backward()
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(yf.float(), yr.float(), **tol)
+    torch.testing.assert_close(xf.grad.float(), xr.grad.float(), **tol)
+    gtol = dict(rtol=1e-2, atol=5e-3 * (N * L) ** 0.5) if dtype == torch.bfloat16 else \
+        dict(rtol=1e-3, atol=1e-2 * N * L / 1000)
+    torch.testing.assert_close(fast.weight.grad, ref.weight.grad, **gtol)
+    torch.testing.assert_close(fast.bias.grad, ref.bias.grad, **gtol)
+    torch.testing.assert_close(fast.running_mean, ref.running_mean, rtol=1e-4, atol=1e-4)
+    fast.eval()
+    ref.eval()
+    torch.testing.assert_close(fast(x0), torch.nn.functional.elu(ref(x0)))
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
 def test_c4_graph_step_with_grad_allreduce():
     """C5's data-parallel step at the C4 network shape (cb=3, nf=3, ks=7,
     hid=64, d=32; B=512 × L=2048, bf16): the flat-gradient RCCL all-reduce is
