@@ -66,9 +66,11 @@ __global__ __launch_bounds__(CV_T) void k_conv(const TI* __restrict__ x, int I, 
 #pragma unroll
   for (int u = 0; u < CV_OG; ++u) acc[u] = (bias && o0 + u < O) ? bias[o0 + u] : 0.f;
   const TI* xb = x + (int64_t)b * I * Lin;
-  // up: the taps that reach output l are t ≡ (l + pad) mod s, input l' = (l + pad − t)/s
+  // up: the taps that reach output l are t ≡ (l + pad) mod s, input l' = (l + pad − t)/s;
+  // the t-th of them is tap t0 + t·s at input jb − t (one division per thread)
   const int q0 = l + pad;
   const int t0 = UP ? q0 % s : 0;
+  const int jb = UP ? (q0 - t0) / s : 0;
   // the next input channel's taps are loaded before this channel's FMAs
   auto taps = [&](int i, float (&v)[KT]) __attribute__((always_inline)) {
     const TI* xr = xb + (int64_t)i * Lin;
@@ -78,8 +80,8 @@ __global__ __launch_bounds__(CV_T) void k_conv(const TI* __restrict__ x, int I, 
       bool ok;
       if (UP) {
         const int tt = t0 + t * s;  // t-th tap of this output's residue class
-        j = (q0 - tt) / s;
-        ok = tt < K && q0 >= tt && j < Lin;
+        j = jb - t;
+        ok = tt < K && j >= 0 && j < Lin;
       } else {
         j = l * s + t - pad;
         ok = t < K && j >= 0 && j < Lin;
@@ -125,14 +127,14 @@ __global__ __launch_bounds__(CV_T) void k_conv_wgrad(const TP* __restrict__ P, i
   constexpr int NA = KT + (WB ? 1 : 0);
   __shared__ float red[CV_T / 64][CV_OG][NA];
   const int i = blockIdx.y % I, o0 = (blockIdx.y / I) * CV_OG;
-  const int64_t total = (int64_t)B * Lp;
+  const int total = B * Lp;  // < 2³¹ (checked by the host): 32-bit position arithmetic
   float acc[CV_OG][NA];  // KT ≥ K: the taps unroll with compile-time indices
 #pragma unroll
   for (int u = 0; u < CV_OG; ++u)
 #pragma unroll
     for (int t = 0; t < NA; ++t) acc[u][t] = 0.f;
-  for (int64_t e = (int64_t)blockIdx.x * CV_T + threadIdx.x; e < total; e += (int64_t)gridDim.x * CV_T) {
-    const int b = (int)(e / Lp), l = (int)(e - (int64_t)b * Lp);
+  for (int e = blockIdx.x * CV_T + threadIdx.x; e < total; e += gridDim.x * CV_T) {
+    const int b = e / Lp, l = e - b * Lp;
     const TQ* qr = Q + ((int64_t)b * I + i) * Lq;
     const int j0 = l * s - pad;
     float qv[KT], pv[CV_OG];
@@ -193,10 +195,10 @@ __global__ __launch_bounds__(CV_T) void k_chan_sum(const T* __restrict__ v, int 
                                                   float* __restrict__ part) {
   __shared__ float red[CV_T / 64];
   const int c = blockIdx.y;
-  const int64_t total = (int64_t)B * L;
+  const int total = B * L;  // < 2³¹ (checked by the host)
   float a = 0.f;
-  for (int64_t e = (int64_t)blockIdx.x * CV_T + threadIdx.x; e < total; e += (int64_t)WG_SPLIT * CV_T) {
-    const int b = (int)(e / L), l = (int)(e % L);
+  for (int e = blockIdx.x * CV_T + threadIdx.x; e < total; e += WG_SPLIT * CV_T) {
+    const int b = e / L, l = e - b * L;
     a += cv_ld(v, ((int64_t)b * C + c) * L + l);
   }
   a = wave_sum_f32(a);
@@ -276,9 +278,12 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
               "ocm_conv1d_wgrad: float32 / bfloat16 activations");
   hipStream_t st = (hipStream_t)stream;
   float* part = static_cast<float*>(scratch);
+  OCM_REQUIRE((int64_t)B * Lp < (1LL << 31), "ocm_conv1d_wgrad: B·Lp must be < 2^31");
   const int groups = I * ((O + CV_OG - 1) / CV_OG);
-  // ≈ 4096 workgroups in all, so a layer with few channels still fills the chip
-  const int split = std::max(16, std::min(WG_MAXSPLIT, 4096 / groups));
+  // ≈ 4096 workgroups in all, so a layer with few channels still fills the chip,
+  // but ≥ 16 positions per thread (the block reductions are not free)
+  const int per16 = (int)(((int64_t)B * Lp + 16 * CV_T - 1) / (16 * CV_T));
+  const int split = std::max(1, std::min({WG_MAXSPLIT, std::max(1, 4096 / groups), per16}));
   const bool wb = psum_out != nullptr;
   dim3 g((unsigned)split, (unsigned)groups);
 #define OCM_WG_K(KT, WB, TP, TQ)                                                                            \
@@ -309,7 +314,7 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
 int ocm_chan_sum(ocm_ctx* ctx, int32_t dtype, const void* v, int32_t B, int32_t C, int32_t L, float* out,
                  void* scratch, void* stream) {
   OCM_REQUIRE(ctx && v && out && scratch, "ocm_chan_sum: NULL argument");
-  OCM_REQUIRE(B > 0 && C > 0 && L > 0 && C <= 65535, "ocm_chan_sum: bad shape");
+  OCM_REQUIRE(B > 0 && C > 0 && L > 0 && C <= 65535 && (int64_t)B * L < (1LL << 31), "ocm_chan_sum: bad shape");
   OCM_REQUIRE(dtype == OCM_DTYPE_F32 || dtype == OCM_DTYPE_BF16, "ocm_chan_sum: float32 / bfloat16");
   hipStream_t st = (hipStream_t)stream;
   float* part = static_cast<float*>(scratch);

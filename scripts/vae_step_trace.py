@@ -49,7 +49,7 @@ def run(steps: int):
     print(f"vae_step_trace: {steps} graphed steps, loss {float(tr.out[0].item()):.5f}")
 
 
-def summarize(path: str, steps: int):
+def summarize(path: str, steps: int, by_grid: bool = False):
     rows = list(csv.DictReader(open(path)))
     for r in rows:
         r["_s"], r["_e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
@@ -60,11 +60,14 @@ def summarize(path: str, steps: int):
     span_ns = rows[b]["_s"] - rows[a]["_e"]
     agg = collections.defaultdict(lambda: [0, 0])
     busy = 0
+    grid_cols = [c for c in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z", "Grid_Size") if c in win[0]] if win else []
     for r in win:
         d = r["_e"] - r["_s"]
         busy += d
-        agg[r["Kernel_Name"]][0] += 1
-        agg[r["Kernel_Name"]][1] += d
+        grid = "×".join(r[c] for c in grid_cols)
+        key = r["Kernel_Name"] if not by_grid else f"{r['Kernel_Name'][:70]} [{grid}]"
+        agg[key][0] += 1
+        agg[key][1] += d
     print(f"# C4 VAE train step (graphed, bf16, B=512, L=2048): kernel trace of {steps} replays\n")
     print(f"* kernels per step: {len(win) / steps:.1f}; wall per step (sentinel to sentinel): "
           f"{span_ns / steps / 1e3:.1f} µs; summed kernel time per step: {busy / steps / 1e3:.1f} µs\n")
@@ -76,6 +79,6 @@ def summarize(path: str, steps: int):
 
 if __name__ == "__main__":
     if sys.argv[1] == "--summarize":
-        summarize(sys.argv[2], int(sys.argv[3]))
+        summarize(sys.argv[2], int(sys.argv[3]), "--by-grid" in sys.argv[4:])
     else:
         run(int(sys.argv[1]))
