@@ -20,7 +20,7 @@
 // Activations (N, C, L) contiguous, float32 or bfloat16 (autocast); weights,
 // bias and gradients of them float32; accumulation float32.  Each thread of
 // down / up computes four output channels of one position (grid.y = channel
-// groups); the four channels' weights sit in LDS.
+// groups); the four channels' weights sit in LDS, interleaved by channel.
 #include <algorithm>
 
 #include "ocm_internal.h"
@@ -51,13 +51,19 @@ template <bool UP, int KT, typename TI, typename TO>
 __global__ __launch_bounds__(CV_T) void k_conv(const TI* __restrict__ x, int I, int Lin, const float* __restrict__ w,
                                               const float* __restrict__ bias, int O, int Lout, int K, int s, int pad,
                                               TO* __restrict__ y) {
-  // the four output channels' weights, CV_KMAX slots per input channel (zero past K)
-  __shared__ float sw[CV_OG][CV_CMAX * CV_KMAX];
+  // the four output channels' weights as [input channel][tap][channel u]: one
+  // ds_read_b128 serves the four FMAs of a tap (CV_KMAX slots, zero past K)
+  __shared__ f32x4 sw[CV_CMAX * CV_KMAX];
   const int o0 = blockIdx.y * CV_OG, b = blockIdx.z;
-  for (int e = threadIdx.x; e < CV_OG * I * CV_KMAX; e += CV_T) {
-    const int u = e / (I * CV_KMAX), r = e % (I * CV_KMAX), i = r / CV_KMAX, t = r % CV_KMAX;
-    const int o = o0 + u;
-    sw[u][r] = (o < O && t < K) ? (UP ? w[((int64_t)i * O + o) * K + t] : w[((int64_t)o * I + i) * K + t]) : 0.f;
+  for (int e = threadIdx.x; e < I * CV_KMAX; e += CV_T) {
+    const int i = e / CV_KMAX, t = e - i * CV_KMAX;
+    f32x4 wv;
+#pragma unroll
+    for (int u = 0; u < CV_OG; ++u) {
+      const int o = o0 + u;
+      wv[u] = (o < O && t < K) ? (UP ? w[((int64_t)i * O + o) * K + t] : w[((int64_t)o * I + i) * K + t]) : 0.f;
+    }
+    sw[e] = wv;
   }
   __syncthreads();
   const int l = blockIdx.x * CV_T + threadIdx.x;
@@ -97,16 +103,18 @@ __global__ __launch_bounds__(CV_T) void k_conv(const TI* __restrict__ x, int I, 
     for (int t = 0; t < KT; ++t) {
       // raw tap of v[t] (clamped into the slot row: v[t] = 0 there)
       const int tw = UP ? min(t0 + t * s, CV_KMAX - 1) : t;
+      const f32x4 wv = sw[i * CV_KMAX + tw];
 #pragma unroll
-      for (int u = 0; u < CV_OG; ++u) acc[u] = fmaf(sw[u][i * CV_KMAX + tw], va[t], acc[u]);
+      for (int u = 0; u < CV_OG; ++u) acc[u] = fmaf(wv[u], va[t], acc[u]);
     }
     if (i + 1 >= I) break;
     if (i + 2 < I) taps(i + 2, va);
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
       const int tw = UP ? min(t0 + t * s, CV_KMAX - 1) : t;
+      const f32x4 wv = sw[(i + 1) * CV_KMAX + tw];
 #pragma unroll
-      for (int u = 0; u < CV_OG; ++u) acc[u] = fmaf(sw[u][(i + 1) * CV_KMAX + tw], vb[t], acc[u]);
+      for (int u = 0; u < CV_OG; ++u) acc[u] = fmaf(wv[u], vb[t], acc[u]);
     }
   }
   TO* yb = y + (int64_t)b * O * Lout;
