@@ -339,7 +339,7 @@ int ocm_decide_f64(ocm_ctx* ctx, const double* T2, const double* Q, int64_t m, c
 
 /* ---- VAE network support (vae_model.py:37-81, BatchNorm1d in train mode) ----
  * Training-mode batch norm over (N, C, L) contiguous activations, bf16 or f32,
- * statistics per channel over N·L (torch.nn.functional.batch_norm semantics:
+ * statistics per channel over N·L < 2³¹ (torch.nn.functional.batch_norm semantics:
  * biased variance normalises, unbiased variance feeds running_var with
  * `momentum`).  Replaces the MIOpen spatial BN the reference's nn.BatchNorm1d
  * lowers to (vae_model.py:45-47, 75-77).  running_mean / running_var may both

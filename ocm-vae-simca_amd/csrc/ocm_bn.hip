@@ -15,7 +15,9 @@
 
 namespace {
 
-constexpr int BN_SPLIT = 64;   // workgroups per channel for the reductions
+constexpr int BN_SPLIT = 64;       // workgroups per channel for the reductions, at least
+constexpr int BN_SPLIT_MAX = 512;  // and at most
+constexpr int BN_U = 4;            // elements per thread per pass of the reduction kernels
 constexpr int BN_T = 256;
 
 struct bf16_t {  // raw bfloat16 storage (torch.bfloat16 bit layout)
@@ -42,45 +44,73 @@ __device__ __forceinline__ double block_sum_f64(double v, double* red) {
   return t;
 }
 
-// grid (BN_SPLIT, C): partial Σx, Σx² of channel c over its share of the N·L elements
+// split workgroups per channel for the reductions: enough to fill the chip when
+// C is small (3-channel layers), at most BN_SPLIT_MAX
+__host__ __device__ inline int bn_split(int C) {
+  const int s = 2048 / (C > 0 ? C : 1);
+  return s < BN_SPLIT ? BN_SPLIT : (s > BN_SPLIT_MAX ? BN_SPLIT_MAX : s);
+}
+
+// the n·L + l elements of channel c, BN_U per thread per pass, loads issued
+// together (clamped index + select: no branch around a load)
+template <typename T>
+__device__ __forceinline__ float bn_ld_or0(const T* p, int C, int L, int c, int e, int total) {
+  const bool ok = e < total;
+  const int ec = ok ? e : 0;
+  const int n = ec / L, l = ec - n * L;
+  const float v = bn_ld(p, ((int64_t)n * C + c) * L + l);
+  return ok ? v : 0.f;
+}
+
+// grid (split, C): partial Σx, Σx² of channel c over its share of the N·L elements
 template <typename T>
 __global__ __launch_bounds__(BN_T) void k_bn_stats(const T* __restrict__ x, int N, int C, int L,
                                                    double* __restrict__ part) {
   __shared__ double red[BN_T / 64];
-  const int c = blockIdx.y, sp = blockIdx.x;
-  double s1 = 0.0, s2 = 0.0;
-  // rows n ≡ sp (mod BN_SPLIT) of channel c, each L contiguous elements:
-  // f32 per-row partials (≤ L/BN_T terms per thread), f64 across rows
-  for (int n = sp; n < N; n += BN_SPLIT) {
-    const T* xr = x + ((int64_t)n * C + c) * L;
-    float a1 = 0.f, a2 = 0.f;
-    for (int l = threadIdx.x; l < L; l += BN_T) {
-      const float v = bn_ld(xr, l);
-      a1 += v;
-      a2 = fmaf(v, v, a2);
+  const int c = blockIdx.y, sp = blockIdx.x, split = gridDim.x;
+  const int total = N * L, step = split * BN_T;
+  float a1 = 0.f, a2 = 0.f;  // ≤ N·L / (split·BN_T) terms per thread in f32, f64 across threads
+  for (int e0 = sp * BN_T + threadIdx.x; e0 < total; e0 += BN_U * step) {
+    float v[BN_U];
+#pragma unroll
+    for (int r = 0; r < BN_U; ++r) v[r] = bn_ld_or0(x, C, L, c, e0 + r * step, total);
+#pragma unroll
+    for (int r = 0; r < BN_U; ++r) {
+      a1 += v[r];
+      a2 = fmaf(v[r], v[r], a2);
     }
-    s1 += a1;
-    s2 += a2;
   }
-  s1 = block_sum_f64(s1, red);
-  s2 = block_sum_f64(s2, red);
+  const double s1 = block_sum_f64(a1, red);
+  const double s2 = block_sum_f64(a2, red);
   if (threadIdx.x == 0) {
-    part[((size_t)c * BN_SPLIT + sp) * 2 + 0] = s1;
-    part[((size_t)c * BN_SPLIT + sp) * 2 + 1] = s2;
+    part[((size_t)c * split + sp) * 2 + 0] = s1;
+    part[((size_t)c * split + sp) * 2 + 1] = s2;
   }
 }
 
-// one thread per channel: mean / invstd and the running-stat update
-__global__ void k_bn_finalize(const double* __restrict__ part, int C, int64_t M, float eps, float momentum,
-                              float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                              float* __restrict__ running_mean, float* __restrict__ running_var) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int i = 0; i < BN_SPLIT; ++i) {
-    s1 += part[((size_t)c * BN_SPLIT + i) * 2 + 0];
-    s2 += part[((size_t)c * BN_SPLIT + i) * 2 + 1];
+// the split partials of channel c summed by one wave (lane-strided, then the
+// fixed butterfly: deterministic)
+__device__ __forceinline__ void bn_part_sum(const double* part, int c, int split, double& s1, double& s2) {
+  const int lane = threadIdx.x;
+  double a1 = 0.0, a2 = 0.0;
+  for (int i = lane; i < split; i += 64) {
+    a1 += part[((size_t)c * split + i) * 2 + 0];
+    a2 += part[((size_t)c * split + i) * 2 + 1];
   }
+  s1 = wave_sum_f64(a1);
+  s2 = wave_sum_f64(a2);
+}
+
+// grid C × one wave: mean / invstd and the running-stat update
+__global__ __launch_bounds__(64) void k_bn_finalize(const double* __restrict__ part, int C, int split, int64_t M,
+                                                    float eps, float momentum, float* __restrict__ save_mean,
+                                                    float* __restrict__ save_invstd,
+                                                    float* __restrict__ running_mean,
+                                                    float* __restrict__ running_var) {
+  const int c = blockIdx.x;
+  double s1, s2;
+  bn_part_sum(part, c, split, s1, s2);
+  if (threadIdx.x != 0) return;
   const double mean = s1 / (double)M;
   const double var = fmax(s2 / (double)M - mean * mean, 0.0);
   save_mean[c] = (float)mean;
@@ -119,44 +149,50 @@ __device__ __forceinline__ float bn_grad(const T* dy, const T* ya, int64_t i) {
   return v > 0.f ? g : g * (v + 1.f);
 }
 
-// grid (BN_SPLIT, C): partial Σdz, Σdz·x̂
+// grid (split, C): partial Σdz, Σdz·x̂
 template <typename T, bool ELU>
 __global__ __launch_bounds__(BN_T) void k_bn_bwd_stats(const T* __restrict__ x, const T* __restrict__ dy,
                                                        const T* __restrict__ ya, int N,
                                                        int C, int L, const float* __restrict__ mean,
                                                        const float* __restrict__ invstd, double* __restrict__ part) {
   __shared__ double red[BN_T / 64];
-  const int c = blockIdx.y, sp = blockIdx.x;
+  const int c = blockIdx.y, sp = blockIdx.x, split = gridDim.x;
   const float mu = mean[c], is = invstd[c];
-  double s1 = 0.0, s2 = 0.0;
-  for (int n = sp; n < N; n += BN_SPLIT) {
-    const int64_t r = ((int64_t)n * C + c) * L;
-    float a1 = 0.f, a2 = 0.f;
-    for (int l = threadIdx.x; l < L; l += BN_T) {
-      const float g = bn_grad<ELU>(dy, ya, r + l);
-      a1 += g;
-      a2 = fmaf(g, (bn_ld(x, r + l) - mu) * is, a2);
+  const int total = N * L, step = split * BN_T;
+  float a1 = 0.f, a2 = 0.f;
+  for (int e0 = sp * BN_T + threadIdx.x; e0 < total; e0 += BN_U * step) {
+    float g[BN_U], xv[BN_U];
+#pragma unroll
+    for (int r = 0; r < BN_U; ++r) {
+      g[r] = bn_ld_or0(dy, C, L, c, e0 + r * step, total);
+      xv[r] = bn_ld_or0(x, C, L, c, e0 + r * step, total);
+      if (ELU) {
+        const float v = bn_ld_or0(ya, C, L, c, e0 + r * step, total);
+        g[r] = v > 0.f ? g[r] : g[r] * (v + 1.f);
+      }
     }
-    s1 += a1;
-    s2 += a2;
+#pragma unroll
+    for (int r = 0; r < BN_U; ++r) {
+      a1 += g[r];
+      // padded elements: g = 0, so the (0 − μ)·invstd term adds nothing
+      a2 = fmaf(g[r], (xv[r] - mu) * is, a2);
+    }
   }
-  s1 = block_sum_f64(s1, red);
-  s2 = block_sum_f64(s2, red);
+  const double s1 = block_sum_f64(a1, red);
+  const double s2 = block_sum_f64(a2, red);
   if (threadIdx.x == 0) {
-    part[((size_t)c * BN_SPLIT + sp) * 2 + 0] = s1;
-    part[((size_t)c * BN_SPLIT + sp) * 2 + 1] = s2;
+    part[((size_t)c * split + sp) * 2 + 0] = s1;
+    part[((size_t)c * split + sp) * 2 + 1] = s2;
   }
 }
 
-__global__ void k_bn_bwd_finalize(const double* __restrict__ part, int C, double* __restrict__ sums,
-                                  float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int i = 0; i < BN_SPLIT; ++i) {
-    s1 += part[((size_t)c * BN_SPLIT + i) * 2 + 0];
-    s2 += part[((size_t)c * BN_SPLIT + i) * 2 + 1];
-  }
+__global__ __launch_bounds__(64) void k_bn_bwd_finalize(const double* __restrict__ part, int C, int split,
+                                                        double* __restrict__ sums, float* __restrict__ dgamma,
+                                                        float* __restrict__ dbeta) {
+  const int c = blockIdx.x;
+  double s1, s2;
+  bn_part_sum(part, c, split, s1, s2);
+  if (threadIdx.x != 0) return;
   sums[2 * c] = s1;
   sums[2 * c + 1] = s2;
   if (dbeta) dbeta[c] = (float)s1;
@@ -184,7 +220,7 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_apply(const T* __restrict__ x, 
 
 // scratch of one forward / backward call: per-(channel, split) partials + the
 // backward's channel sums
-size_t bn_scratch(int C) { return ((size_t)C * BN_SPLIT * 2 + 2 * (size_t)C) * sizeof(double); }
+size_t bn_scratch(int C) { return ((size_t)C * bn_split(C) * 2 + 2 * (size_t)C) * sizeof(double); }
 
 template <typename T>
 int bn_fwd(ocm_ctx* ctx, const void* x, int N, int C, int L, const float* gamma, const float* beta, float eps,
@@ -192,9 +228,10 @@ int bn_fwd(ocm_ctx* ctx, const void* x, int N, int C, int L, const float* gamma,
            hipStream_t st) {
   auto* part = static_cast<double*>(scratch ? scratch : ocm::workspace(ctx, bn_scratch(C), st));
   if (!part) return OCM_ERR_NOMEM;
-  hipLaunchKernelGGL(k_bn_stats<T>, dim3(BN_SPLIT, C), dim3(BN_T), 0, st, static_cast<const T*>(x), N, C, L, part);
-  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 63) / 64), dim3(64), 0, st, part, C, (int64_t)N * L, eps, momentum,
-                     smean, sinv, rmean, rvar);
+  const int split = bn_split(C);
+  hipLaunchKernelGGL(k_bn_stats<T>, dim3(split, C), dim3(BN_T), 0, st, static_cast<const T*>(x), N, C, L, part);
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(64), 0, st, part, C, split, (int64_t)N * L, eps,
+                     momentum, smean, sinv, rmean, rvar);
   const dim3 ga((L + BN_T - 1) / BN_T, N * C);
   if (act == OCM_ACT_ELU)
     hipLaunchKernelGGL((k_bn_apply<T, true>), ga, dim3(BN_T), 0, st, static_cast<const T*>(x), C, L, smean, sinv,
@@ -212,10 +249,11 @@ int bn_bwd(ocm_ctx* ctx, const void* x, const void* dy, const void* ya, int N, i
            hipStream_t st) {
   auto* part = static_cast<double*>(scratch ? scratch : ocm::workspace(ctx, bn_scratch(C), st));
   if (!part) return OCM_ERR_NOMEM;
-  double* sums = part + (size_t)C * BN_SPLIT * 2;
-  hipLaunchKernelGGL((k_bn_bwd_stats<T, ELU>), dim3(BN_SPLIT, C), dim3(BN_T), 0, st, static_cast<const T*>(x),
+  const int split = bn_split(C);
+  double* sums = part + (size_t)C * split * 2;
+  hipLaunchKernelGGL((k_bn_bwd_stats<T, ELU>), dim3(split, C), dim3(BN_T), 0, st, static_cast<const T*>(x),
                      static_cast<const T*>(dy), static_cast<const T*>(ya), N, C, L, smean, sinv, part);
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64), 0, st, part, C, sums, dgamma, dbeta);
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(C), dim3(64), 0, st, part, C, split, sums, dgamma, dbeta);
   hipLaunchKernelGGL((k_bn_bwd_apply<T, ELU>), dim3((L + BN_T - 1) / BN_T, N * C), dim3(BN_T), 0, st,
                      static_cast<const T*>(x), static_cast<const T*>(dy), static_cast<const T*>(ya), C, L,
                      (int64_t)N * L, smean, sinv, gamma, sums, static_cast<T*>(dx));
@@ -234,7 +272,7 @@ int ocm_bn_fwd_train(ocm_ctx* ctx, int32_t dtype, const void* x, int32_t N, int3
                      float* running_var, int32_t act, void* y, float* save_mean, float* save_invstd, void* scratch,
                      void* stream) {
   OCM_REQUIRE(ctx && x && y && save_mean && save_invstd, "ocm_bn_fwd_train: NULL argument");
-  OCM_REQUIRE(N > 0 && C > 0 && L > 0, "ocm_bn_fwd_train: bad shape");
+  OCM_REQUIRE(N > 0 && C > 0 && L > 0 && (int64_t)N * L < INT32_MAX, "ocm_bn_fwd_train: bad shape");
   OCM_REQUIRE(!running_mean == !running_var, "ocm_bn_fwd_train: running_mean and running_var go together");
   OCM_REQUIRE(act == OCM_ACT_NONE || act == OCM_ACT_ELU, "ocm_bn_fwd_train: act must be OCM_ACT_NONE or OCM_ACT_ELU");
   hipStream_t st = (hipStream_t)stream;
@@ -251,7 +289,7 @@ int ocm_bn_bwd(ocm_ctx* ctx, int32_t dtype, const void* x, const void* dy, int32
                const float* gamma, const float* save_mean, const float* save_invstd, int32_t act, const void* y,
                void* dx, float* dgamma, float* dbeta, void* scratch, void* stream) {
   OCM_REQUIRE(ctx && x && dy && dx && save_mean && save_invstd, "ocm_bn_bwd: NULL argument");
-  OCM_REQUIRE(N > 0 && C > 0 && L > 0, "ocm_bn_bwd: bad shape");
+  OCM_REQUIRE(N > 0 && C > 0 && L > 0 && (int64_t)N * L < INT32_MAX, "ocm_bn_bwd: bad shape");
   OCM_REQUIRE(act == OCM_ACT_NONE || (act == OCM_ACT_ELU && y), "ocm_bn_bwd: the fused ELU needs its output y");
   hipStream_t st = (hipStream_t)stream;
   const bool elu = act == OCM_ACT_ELU;

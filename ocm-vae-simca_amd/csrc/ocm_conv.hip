@@ -41,6 +41,15 @@ __device__ __forceinline__ void cv_st(bf16_t* p, int64_t i, float v) {
 }
 
 constexpr int CV_T = 256, CV_OG = 4, CV_KMAX = 15, CV_CMAX = 64;
+
+// v = ok ? p[i] : 0 without a branch: the load always runs, at an index clamped into
+// [0, n) — hipcc turns a guarded load into a branch with its own vmcnt(0) wait, so a
+// row of guarded taps would cost one memory round trip per tap
+template <typename T>
+__device__ __forceinline__ float cv_ld_or0(const T* p, int i, int n, bool ok) {
+  const float v = cv_ld(p, min(max(i, 0), n - 1));
+  return ok ? v : 0.f;
+}
 constexpr int WG_SPLIT = 128;   // csum partial workgroups per channel
 constexpr int WG_MAXSPLIT = 1024;  // wgrad partial workgroups per (o, i) pair, at most
 
@@ -92,7 +101,7 @@ __global__ __launch_bounds__(CV_T) void k_conv(const TI* __restrict__ x, int I, 
         j = l * s + t - pad;
         ok = t < K && j >= 0 && j < Lin;
       }
-      v[t] = ok ? cv_ld(xr, j) : 0.f;
+      v[t] = cv_ld_or0(xr, j, Lin, ok);
     }
   };
   float va[KT], vb[KT];
@@ -149,10 +158,15 @@ __global__ __launch_bounds__(CV_T) void k_conv_wgrad(const TP* __restrict__ P, i
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
       const int j = j0 + t;
-      qv[t] = (t < K && j >= 0 && j < Lq) ? cv_ld(qr, j) : 0.f;
+      qv[t] = cv_ld_or0(qr, j, Lq, t < K && j >= 0 && j < Lq);
     }
+    // channels past O read channel O − 1 (valid memory) and are dropped
+    const TP* pb = P + (int64_t)b * O * Lp + l;
 #pragma unroll
-    for (int u = 0; u < CV_OG; ++u) pv[u] = o0 + u < O ? cv_ld(P, ((int64_t)b * O + o0 + u) * Lp + l) : 0.f;
+    for (int u = 0; u < CV_OG; ++u) {
+      const float v = cv_ld(pb, (int64_t)min(o0 + u, O - 1) * Lp);
+      pv[u] = o0 + u < O ? v : 0.f;
+    }
 #pragma unroll
     for (int u = 0; u < CV_OG; ++u) {
 #pragma unroll
