@@ -762,12 +762,13 @@ __global__ __launch_bounds__(256) void k_cq_gram32(double* W, int p, const doubl
     double a[32];
 #pragma unroll
     for (int cc = 0; cc < 32; ++cc) a[cc] = sS[i][cc] * ri * rsc[cc];
-    double lrow[32];
+    double lrow[32], invd[32];
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
-      const double ajj = readlane_f64(a[j], j);
-      const double djj = sqrt(fmax(ajj, 1e-14));  // diag(S') = 1: clamp 1e-14 · max diag
-      const double inv = 1.0 / djj;
+      const double ajj = fmax(readlane_f64(a[j], j), 1e-14);  // diag(S') = 1: clamp 1e-14 · max diag
+      const double inv = rsqrt(ajj);
+      const double djj = ajj * inv;
+      invd[j] = inv;
       const double lij = i > j ? a[j] * inv : (i == j ? djj : 0.0);
       lrow[j] = lij;
 #pragma unroll
@@ -781,14 +782,18 @@ __global__ __launch_bounds__(256) void k_cq_gram32(double* W, int p, const doubl
       for (int cc = 0; cc < 32; ++cc) sm[i][cc] = lrow[cc];
     }
     __builtin_amdgcn_wave_barrier();
-    // lane i: row i of X = L⁻¹ by X·L = I, columns j = 31 … 0
+    // lane i: row i of X = L⁻¹ by X·L = I, columns j = 31 … 0, right-looking:
+    // once X[i][j] is known its products with row j of L go into the pending
+    // sums of columns < j (independent FMAs; the serial chain is one FMA and
+    // one multiply per column)
     double xr[32];
 #pragma unroll
-    for (int j = 31; j >= 0; --j) {
-      double s = 0.0;
+    for (int j = 0; j < 32; ++j) xr[j] = 0.0;
 #pragma unroll
-      for (int k = j + 1; k < 32; ++k) s += xr[k] * sm[k][j];
-      xr[j] = j > i ? 0.0 : ((j == i ? 1.0 : 0.0) - s) / sm[j][j];
+    for (int j = 31; j >= 0; --j) {
+      xr[j] = j > i ? 0.0 : ((j == i ? 1.0 : 0.0) - xr[j]) * invd[j];
+#pragma unroll
+      for (int jj = 0; jj < j; ++jj) xr[jj] = fma(xr[j], sm[j][jj], xr[jj]);
     }
     // M[k][i] = r_k · X[i][k]
     if (lane < 32) {
