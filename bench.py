@@ -28,7 +28,7 @@ the same way.  ``phases_ms`` is each rank's per-phase time (HIP events on
 the launch stream) from extra, untimed steps.
 
 Prints ONE JSON line (rank 0).  The `roofline` object is for the dominant
-kernel, k_gram8d: algorithmic FLOP per launch = this rank's rows × p(p+1)
+kernel, k_gram8e: algorithmic FLOP per launch = this rank's rows × p(p+1)
 (symmetric Gram) ÷ its mean duration, timed live with HIP events around every
 launch in the timed region.  `cpu_baseline` times the oracle's
 reference-precision path (float32 full SVD + randomized PCA(k) + NumPy
@@ -78,7 +78,7 @@ def parse(argv=None):
     ap.add_argument("--cv-reps", type=int, default=3)
     ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling extra run")
     ap.add_argument("--phase-steps", type=int, default=3, help="untimed steps with per-phase events (0 = off)")
-    ap.add_argument("--gram-mode", default=GRAM_MODE_DEFAULT, choices=["f32", "bf16x3", "i8x3"],
+    ap.add_argument("--gram-mode", default=GRAM_MODE_DEFAULT, choices=["f32", "bf16x3", "i8x3", "i8x3k32"],
                     help="Gram kernel: int8 digit split (default), bf16x3 split or FP32 MFMA")
     return ap.parse_args(argv)
 
@@ -429,10 +429,11 @@ def main():
     score_avg_s = score_ms / max(score_n, 1) / 1e3
     score_gbs = n * p * 4 / score_avg_s / 1e9 if score_avg_s > 0 else 0.0
 
-    gram_kernel = {"bf16x3": "k_gram3", "i8x3": "k_gram8d"}.get(args.gram_mode, "k_gram")
-    if args.gram_mode == "i8x3":
+    gram_kernel = {"bf16x3": "k_gram3", "i8x3": "k_gram8e", "i8x3k32": "k_gram8d"}.get(args.gram_mode, "k_gram")
+    if args.gram_mode in ("i8x3", "i8x3k32"):
         # fp32-grade product from 6 int8 MFMA digit products (exact int32 sums)
-        gram_desc = (f"{gram_kernel} (shifted Gram, 3 int8 digits per value, 6 i8 MFMA products per fp32 "
+        mfma = "v_mfma_i32_16x16x64_i8" if args.gram_mode == "i8x3" else "v_mfma_i32_32x32x32_i8"
+        gram_desc = (f"{gram_kernel} (shifted Gram, 3 int8 digits per value, 6 {mfma} digit products per fp32 "
                      "product, exact int32 sums)")
         gram_peak = round(I8_MFMA_PEAK_TOPS / 6, 1)
         peak_basis = "int8 MFMA dense peak / 6 (fp32-equivalent); achieved counts algorithmic fp32 flops n*p*(p+1)"

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCM_ABI_VERSION 5
+#define OCM_ABI_VERSION 6
 
 #define OCM_OK 0
 #define OCM_ERR_ARG (-1)         /* invalid argument (maps to ValueError) */
@@ -110,10 +110,14 @@ int ocm_gram_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows,
 /* Same with an explicit arithmetic mode and row-chunk length (0 = automatic):
  *   OCM_GRAM_I8X3   the default above;
  *   OCM_GRAM_F32    FP32 MFMA (v_mfma_f32_32x32x2_f32), f32 chunk partials summed in f64;
- *   OCM_GRAM_BF16X3 exact three-level bf16 split on bf16 MFMA. */
+ *   OCM_GRAM_BF16X3 exact three-level bf16 split on bf16 MFMA;
+ *   OCM_GRAM_I8X3_K32 the i8×3 Gram on v_mfma_i32_32x32x32_i8 (round 2's
+ *                   kernel) instead of the default's 16x16x64: bit-identical
+ *                   result, kept for kernel A/B. */
 #define OCM_GRAM_I8X3 0
 #define OCM_GRAM_F32 1
 #define OCM_GRAM_BF16X3 2
+#define OCM_GRAM_I8X3_K32 3
 int ocm_gram_f32_ex(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
                     const float* shift, const int64_t* seg_offsets, int32_t nseg, int32_t mode, int64_t chunk_rows,
                     double* G_out, double* colsum_out, void* stream);

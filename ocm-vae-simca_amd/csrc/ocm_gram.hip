@@ -1366,6 +1366,176 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
       }
 }
 
+// ---------------------------------------------------------------------------
+// k_gram8e — k_gram8d's work on the 16×16×64 integer MFMA
+// (v_mfma_i32_16x16x64_i8, 16 cycles) instead of 32×32×32 (32 cycles).  Same
+// digit planes, same 64×64 wave blocks packed four per workgroup, same band
+// order, same three int32 sets and f32 running sums, so the partials are bit
+// for bit those of k_gram8d (the int32 sums are exact; each element's f32
+// flushes run in the same order).  A stage is 64 rows (two 32-row digit
+// groups): lane (c, g) of a fragment holds column c (0..15) of a 16-column
+// sub-panel, bytes 16(g & 1) .. +15 of group g >> 1 — the voffset picks the
+// group, so the quantiser's layout is unchanged.  Per stage a wave loads 24
+// fragments (4 sub-panels × 3 digits for A and for B) for 96 MFMAs, one load
+// per four MFMAs, one stage ahead into the other of two register sets.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
+                                                   int nwg, int nblocks, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float scl[4][2 * 64];      // wave-private: row, column scales
+  __shared__ __attribute__((aligned(16))) float runl[4][16][64][4];  // wave-private f32 running sums
+
+  const int b = blockIdx.x;
+  const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
+  const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int chunk = wg / nwg;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int bi = (wg - chunk * nwg) * 4 + wave;
+  if (bi >= nblocks) return;  // no barrier in this kernel
+  int ti = -1, tj = 0, wm = 0, wn = 0;
+  {
+    int rem = bi;
+    for (int u = 0; u < nt && ti < 0; u += G8_BAND_R)
+      for (int v = u; v < nt && ti < 0; v += G8_BAND_C)
+        for (int a = u; a < min(nt, u + G8_BAND_R) && ti < 0; ++a)
+          for (int c = max(v, a); c < min(nt, v + G8_BAND_C); ++c) {
+            const int nbk = (a == c) ? 3 : 4;
+            if (rem < nbk) {
+              ti = a;
+              tj = c;
+              wm = (a == c) ? (rem == 2) : (rem >> 1);
+              wn = (a == c) ? (rem >= 1) : (rem & 1);
+              break;
+            }
+            rem -= nbk;
+          }
+  }
+  const int tile = ti * nt - ti * (ti - 1) / 2 + (tj - ti);
+  const int I = ti * Q8T, J = tj * Q8T;
+  int s = 0;
+  while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
+  const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
+  const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
+  const int nb = (int)((r1 - r0 + Q8BLK - 1) / Q8BLK);
+  constexpr int SPB = Q8BLK / 64;  // 64-row stages per scale block (24)
+  const int nstage = nb * SPB;
+  const size_t gbase = (size_t)chunk * (st.chunk_rows / Q8K);
+
+  const int lane = threadIdx.x & 63;
+  const int l15 = lane & 15, g4 = lane >> 4;
+  const size_t gstride = (size_t)q.P8 * 32;
+  const uint32_t span = (uint32_t)((size_t)nb * Q8SPB * gstride);
+  const char* cbase = q.digits + gbase * gstride;
+  __amdgpu_buffer_rsrc_t ra[3], rb[3];
+#pragma unroll
+  for (int dg = 0; dg < 3; ++dg) {
+    ra[dg] = __builtin_amdgcn_make_buffer_rsrc((void*)(cbase + dg * q.plane + (size_t)(I + wm * 64) * 32), 0, span,
+                                               0x00020000);
+    rb[dg] = __builtin_amdgcn_make_buffer_rsrc((void*)(cbase + dg * q.plane + (size_t)(J + wn * 64) * 32), 0, span,
+                                               0x00020000);
+  }
+  // sub-panel x of the wave's 64 columns: column 16x + l15, group g4 >> 1, half g4 & 1
+  const int voff = (g4 >> 1) * (int)gstride + l15 * 32 + (g4 & 1) * 16;
+  const int sstride = 2 * (int)gstride;
+  const float* srow = q.scale + (size_t)chunk * q.nblk * q.P8 + I + wm * 64 + lane;
+  const float* scol = q.scale + (size_t)chunk * q.nblk * q.P8 + J + wn * 64 + lane;
+
+  i32x4 acc1[4][4], acc2[4][4], acc3[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      acc1[a][c] = i32x4{};
+      acc2[a][c] = i32x4{};
+      acc3[a][c] = i32x4{};
+      *reinterpret_cast<f32x4*>(&runl[wave][a * 4 + c][lane][0]) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  float SR = 0.f, SC = 0.f;
+  auto flush = [&]() __attribute__((always_inline)) {
+    constexpr float w2 = 1.f / 254.f, w3 = 1.f / (254.f * 254.f);
+    scl[wave][lane] = SR;  // wave-private: LDS is in order within the wave
+    scl[wave][64 + lane] = SC;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      // row scales of registers 0..3: rows 16a + 4g4 + 0..3
+      const f32x4 si = *reinterpret_cast<const f32x4*>(&scl[wave][a * 16 + 4 * g4]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float sj = scl[wave][64 + c * 16 + l15];
+        f32x4* rp = reinterpret_cast<f32x4*>(&runl[wave][a * 4 + c][lane][0]);
+        f32x4 rv = *rp;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = fmaf((float)acc3[a][c][e], w3, fmaf((float)acc2[a][c][e], w2, (float)acc1[a][c][e]));
+          rv[e] = fmaf(v, si[e] * sj, rv[e]);
+        }
+        *rp = rv;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // fragment load i (0..23) of a stage, in the order the stage's MFMAs first
+  // use them: A0, B0, B1, B2, B3, A1, A2, A3 (three digits each)
+  auto load_frag = [&](i32x4 (&FA)[4][3], i32x4 (&FB)[4][3], int i, int so) __attribute__((always_inline)) {
+    const int grp = i / 3, dg = i % 3;
+    if (grp >= 1 && grp <= 4)
+      FB[grp - 1][dg] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(rb[dg], voff + (grp - 1) * 512, so, 0);
+    else {
+      const int x = grp == 0 ? 0 : grp - 4;
+      FA[x][dg] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(ra[dg], voff + x * 512, so, 0);
+    }
+  };
+  // one stage: 96 MFMAs on (CA, CB), sub-blocks row-major, six products each;
+  // the 24 loads of the next stage into (NA, NB), one per four MFMAs
+  auto step = [&](i32x4 (&CA)[4][3], i32x4 (&CB)[4][3], i32x4 (&NA)[4][3], i32x4 (&NB)[4][3], int stg,
+                  bool z) __attribute__((always_inline)) {
+    const int so = min(stg + 1, nstage - 1) * sstride;
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      load_frag(NA, NB, i, so);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int j = 4 * i + jj, blk = j / 6, kind = j % 6, a = blk >> 2, c = blk & 3;
+        if (kind == 0) acc1[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(CA[a][0], CB[c][0], z ? i32x4{} : acc1[a][c], 0, 0, 0);
+        if (kind == 1) acc2[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(CA[a][0], CB[c][1], z ? i32x4{} : acc2[a][c], 0, 0, 0);
+        if (kind == 2) acc2[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(CA[a][1], CB[c][0], acc2[a][c], 0, 0, 0);
+        if (kind == 3) acc3[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(CA[a][0], CB[c][2], z ? i32x4{} : acc3[a][c], 0, 0, 0);
+        if (kind == 4) acc3[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(CA[a][2], CB[c][0], acc3[a][c], 0, 0, 0);
+        if (kind == 5) acc3[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(CA[a][1], CB[c][1], acc3[a][c], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  i32x4 F0A[4][3], F0B[4][3], F1A[4][3], F1B[4][3];
+#pragma unroll
+  for (int i = 0; i < 24; ++i) load_frag(F0A, F0B, i, 0);
+  for (int blk = 0; blk < nb; ++blk) {
+    const int s0 = blk * SPB;
+#pragma unroll
+    for (int u = 0; u < SPB; u += 2) {
+      step(F0A, F0B, F1A, F1B, s0 + u, u == 0);
+      if (u == 0) {
+        SR = srow[(size_t)blk * q.P8];
+        SC = scol[(size_t)blk * q.P8];
+      }
+      step(F1A, F1B, F0A, F0B, s0 + u + 1, false);
+    }
+    flush();
+  }
+
+  float* out = part + ((size_t)chunk * ntiles + tile) * (Q8T * Q8T);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wm * 64 + a * 16 + 4 * g4 + e;
+        const int col = wn * 64 + c * 16 + l15;
+        out[row * Q8T + col] = runl[wave][a * 4 + c][lane][e];
+      }
+}
+
 #ifdef OCM_G8_LDS
 // ---------------------------------------------------------------------------
 // k_gram8s (experiment, make exp only) — the i8×3 Gram with the workgroup's
@@ -1692,7 +1862,7 @@ int gram_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, in
 // caller then recomputes the Gram on the bf16×3 path.
 int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
                const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
-               hipStream_t st, int64_t chunk_rows) {
+               hipStream_t st, int64_t chunk_rows, bool k32) {
   const int P8 = (int)ocm::align_up((size_t)p, Q8T);
   const int nt = P8 / Q8T;
   const int ntiles = nt * (nt + 1) / 2;
@@ -1816,9 +1986,13 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     hipLaunchKernelGGL(k_gram8s, dim3((unsigned)total_s), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total_s, pg);
     OCM_CHECK_LAUNCH("k_gram8s");
 #else
-    hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, nwg,
-                       nblocks, pg);
-    OCM_CHECK_LAUNCH("k_gram8d");
+    if (!k32)
+      hipLaunchKernelGGL(k_gram8e, dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, nwg,
+                         nblocks, pg);
+    else
+      hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, nwg,
+                         nblocks, pg);
+    OCM_CHECK_LAUNCH("k_gram8d/8e");
 #endif
   }
   for (int s = 0; s < nseg; ++s) {
@@ -1872,8 +2046,9 @@ int gram_dispatch(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
                   const float* shift, const int64_t* seg_offsets, int32_t nseg, int32_t mode, int64_t chunk_rows,
                   double* G_out, double* colsum_out, hipStream_t st) {
   if (p <= SMALL_P) return gram_small(ctx, X, ldx, rows, p, shift, seg_offsets, nseg, G_out, colsum_out, st);
-  if (mode == OCM_GRAM_I8X3) {
-    const int rc = gram_impl8(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows);
+  if (mode == OCM_GRAM_I8X3 || mode == OCM_GRAM_I8X3_K32) {
+    const int rc = gram_impl8(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows,
+                              mode == OCM_GRAM_I8X3_K32);
     if (rc != 1) return rc;
     mode = OCM_GRAM_BF16X3;  // too many screened rows: recompute on the exact bf16×3 split
   }
@@ -1918,7 +2093,8 @@ int ocm_gram_f32_ex(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* ro
   OCM_REQUIRE(ctx && X && shift && seg_offsets && G_out && colsum_out, "ocm_gram_f32: NULL argument");
   OCM_REQUIRE(n > 0 && p > 0 && ldx >= p && nseg > 0, "ocm_gram_f32: bad shape");
   OCM_REQUIRE(seg_offsets[0] == 0 && seg_offsets[nseg] == n, "ocm_gram_f32: seg_offsets must span [0, n]");
-  OCM_REQUIRE(mode == OCM_GRAM_I8X3 || mode == OCM_GRAM_F32 || mode == OCM_GRAM_BF16X3, "ocm_gram_f32: bad mode");
+  OCM_REQUIRE(mode == OCM_GRAM_I8X3 || mode == OCM_GRAM_F32 || mode == OCM_GRAM_BF16X3 || mode == OCM_GRAM_I8X3_K32,
+              "ocm_gram_f32: bad mode");
   for (int s = 0; s < nseg; ++s)
     OCM_REQUIRE(seg_offsets[s + 1] >= seg_offsets[s], "ocm_gram_f32: seg_offsets not ascending");
   return gram_dispatch(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, mode, chunk_rows, G_out, colsum_out,

@@ -121,7 +121,7 @@ SIGNATURES = {
     "ocm_chan_sum": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
 }
 
-ABI_VERSION = 5  # include/ocm.h OCM_ABI_VERSION
+ABI_VERSION = 6  # include/ocm.h OCM_ABI_VERSION
 
 _lib = None
 _lib_lock = threading.Lock()

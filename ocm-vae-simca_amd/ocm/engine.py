@@ -130,7 +130,7 @@ def cast_f32(a: torch.Tensor) -> torch.Tensor:
     return out
 
 
-GRAM_MODES = {"i8x3": 0, "f32": 1, "bf16x3": 2}  # include/ocm.h OCM_GRAM_*
+GRAM_MODES = {"i8x3": 0, "f32": 1, "bf16x3": 2, "i8x3k32": 3}  # include/ocm.h OCM_GRAM_*
 _gram_mode = "i8x3"
 
 

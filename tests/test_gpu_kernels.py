@@ -15,11 +15,12 @@ def eng():
     return engine
 
 
-@pytest.fixture(params=["f32", "bf16x3", "i8x3"])
+@pytest.fixture(params=["f32", "bf16x3", "i8x3", "i8x3k32"])
 def gram_mode(request):
     """All Gram kernels: FP32 MFMA, the bf16×3 split on bf16 MFMA and the int8
-    digit split on integer MFMA (the default), chosen through the explicit
-    mode argument of ocm_gram_f32_ex."""
+    digit split on integer MFMA (the default; on the 32x32x32 and on the
+    16x16x64 instruction), chosen through the explicit mode argument of
+    ocm_gram_f32_ex."""
     from ocm import engine
 
     prev = engine.set_gram_mode(request.param)
@@ -307,6 +308,27 @@ def test_gram_i8_digit_split_edge_cases(eng, n, p):
     err = np.abs(G[0].cpu().numpy() - Gref) / np.outer(d, d)
     assert err.max() < 2e-6, err.max()
     np.testing.assert_allclose(cs[0].cpu().numpy(), Y.sum(0), rtol=1e-6, atol=1e-6 * np.abs(Y).sum(0).max())
+
+
+@pytest.mark.parametrize("n,p,chunk", [(20000, 2048, 0), (9000, 257, 512), (5000, 300, 4608)])
+def test_gram_i8_kernels_bit_identical(eng, n, p, chunk):
+    """k_gram8e (16x16x64, the default) and k_gram8d (32x32x32) sum the same exact int32
+    digit products and flush them to f32 in the same order: the Grams are
+    bit for bit equal, with segments, a gather list and outlier rows."""
+    import torch
+
+    rng = np.random.default_rng(p + n)
+    X = (rng.standard_normal((n, p)) * rng.uniform(0.1, 3, p) + 1.0).astype(np.float32)
+    X[n // 5] *= np.float32(800.0)  # one screened row (exact fix-up in both)
+    Xd = _dev(X)
+    shift = eng.cast_f32(eng.colmean(Xd, None, 4096))
+    rows = _dev(np.sort(rng.choice(n, n - 100, replace=False)).astype(np.int64))
+    m = n - 100
+    for r, seg in ((None, [0, n]), (rows, [0, m // 3, m // 3, m])):
+        Ga, ca = eng.gram(Xd, r, seg, shift, mode="i8x3", chunk_rows=chunk)
+        Gb, cb = eng.gram(Xd, r, seg, shift, mode="i8x3k32", chunk_rows=chunk)
+        assert torch.equal(Ga, Gb)
+        assert torch.equal(ca, cb)
 
 
 def _outlier_rows(rng, n, frac, lo=100.0, hi=1000.0):
