@@ -16,6 +16,7 @@
 // consecutive tiles of one row chunk land on one XCD and share its L2.
 //   GT = 256 (default): 8 waves, BK = 16, 64 KiB LDS, 128 accumulators/lane.
 //   GT = 128:           4 waves, BK = 32, 64 KiB LDS,  64 accumulators/lane.
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -1368,17 +1369,24 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
 
 // ---------------------------------------------------------------------------
 // k_gram8e — k_gram8d's work on the 16×16×64 integer MFMA
-// (v_mfma_i32_16x16x64_i8, 16 cycles) instead of 32×32×32 (32 cycles).  Same
-// digit planes, same 64×64 wave blocks packed four per workgroup, same band
-// order, same three int32 sets and f32 running sums, so the partials are bit
-// for bit those of k_gram8d (the int32 sums are exact; each element's f32
-// flushes run in the same order).  A stage is 64 rows (two 32-row digit
+// (v_mfma_i32_16x16x64_i8, 16 cycles) instead of 32×32×32 (32 cycles): 419
+// vs 386 TF in one process (r03q; the chip holds a higher clock on the
+// 16×16 shape).  Same digit planes, 64×64 wave blocks, band order, three
+// int32 sets and f32 running sums, so the partials are bit for bit those of
+// k_gram8d (the int32 sums are exact; each element's f32 flushes run in the
+// same order).  Default launch: a workgroup is one tile's four blocks
+// (off-diagonal tiles first, then the diagonal ones packed) and its waves
+// meet at a barrier every two stages — a fragment is then loaded by two
+// waves of one CU at about the same time and the L1 serves one of them
+// (the L2 → CU path is the limit: at full MFMA rate a CU would take 64 B/clk
+// of fragments from it).  A stage is 64 rows (two 32-row digit
 // groups): lane (c, g) of a fragment holds column c (0..15) of a 16-column
 // sub-panel, bytes 16(g & 1) .. +15 of group g >> 1 — the voffset picks the
 // group, so the quantiser's layout is unchanged.  Per stage a wave loads 24
 // fragments (4 sub-panels × 3 digits for A and for B) for 96 MFMAs, one load
 // per four MFMAs, one stage ahead into the other of two register sets.
 // ---------------------------------------------------------------------------
+template <bool ALIGNED, int SYNC>
 __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
                                                    int nwg, int nblocks, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) float scl[4][2 * 64];      // wave-private: row, column scales
@@ -1389,10 +1397,43 @@ __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt
   const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
   const int chunk = wg / nwg;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int bi = (wg - chunk * nwg) * 4 + wave;
-  if (bi >= nblocks) return;  // no barrier in this kernel
+  int bi = (wg - chunk * nwg) * 4 + wave;
+  // SYNC > 0: a workgroup barrier every SYNC stages keeps the four waves in
+  // step, so the second wave's load of a shared panel fragment finds it in
+  // the CU's L1; a wave past the last block then computes a copy of the last
+  // block (never stored) instead of leaving
+  const bool dead = bi >= nblocks;
+  if (dead && SYNC == 0) return;
+  if (dead) bi = nblocks - 1;
   int ti = -1, tj = 0, wm = 0, wn = 0;
-  {
+  if (ALIGNED) {
+    // off-diagonal tiles first, in band order, four blocks each: a
+    // workgroup's four waves are one tile's four blocks, so each A and B
+    // panel fragment is fetched by two waves of the same CU (the L1 serves the
+    // second); then the nt diagonal tiles, three blocks each, packed
+    const int noff = 4 * (ntiles - nt);
+    if (bi < noff) {
+      int rem = bi >> 2;
+      wm = (bi >> 1) & 1;
+      wn = bi & 1;
+      for (int u = 0; u < nt && ti < 0; u += G8_BAND_R)
+        for (int v = u; v < nt && ti < 0; v += G8_BAND_C)
+          for (int a = u; a < min(nt, u + G8_BAND_R) && ti < 0; ++a)
+            for (int c = max(v, a + 1); c < min(nt, v + G8_BAND_C); ++c) {
+              if (rem == 0) {
+                ti = a;
+                tj = c;
+                break;
+              }
+              --rem;
+            }
+    } else {
+      const int d = (bi - noff) / 3, r = (bi - noff) - 3 * d;
+      ti = tj = d;
+      wm = (r == 2);
+      wn = (r >= 1);
+    }
+  } else {
     int rem = bi;
     for (int u = 0; u < nt && ti < 0; u += G8_BAND_R)
       for (int v = u; v < nt && ti < 0; v += G8_BAND_C)
@@ -1504,6 +1545,7 @@ __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (SYNC > 0 && stg % SYNC == SYNC - 1) __builtin_amdgcn_s_barrier();
   };
 
   i32x4 F0A[4][3], F0B[4][3], F1A[4][3], F1B[4][3];
@@ -1523,6 +1565,7 @@ __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt
     flush();
   }
 
+  if (dead) return;
   float* out = part + ((size_t)chunk * ntiles + tile) * (Q8T * Q8T);
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -1973,6 +2016,15 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     OCM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     OCM_HIP(hipEventRecord(ev, st));
   }
+  // k_gram8e's block order and wave sync: tile-aligned workgroups with a
+  // barrier every two stages (default: 437 TF against 417 for the packed
+  // walk without barriers, r03s); OCM_GRAM8_ORDER = packed | aligned | sync1
+  // picks the others for kernel A/B (same result bits)
+  const char* ord = getenv("OCM_GRAM8_ORDER");
+  int order = 3;
+  if (ord && !strcmp(ord, "packed")) order = 0;
+  if (ord && !strcmp(ord, "aligned")) order = 1;
+  if (ord && !strcmp(ord, "sync1")) order = 2;
   for (size_t t = 0; t < tabs.size(); ++t) {
     const int s0 = tab_s0[t];
     const int nblocks = 4 * ntiles - nt, nwg = (nblocks + 3) / 4;
@@ -1986,9 +2038,14 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     hipLaunchKernelGGL(k_gram8s, dim3((unsigned)total_s), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total_s, pg);
     OCM_CHECK_LAUNCH("k_gram8s");
 #else
-    if (!k32)
-      hipLaunchKernelGGL(k_gram8e, dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, nwg,
-                         nblocks, pg);
+#define G8E_LAUNCH(A_, S_)                                                                                   \
+  hipLaunchKernelGGL((k_gram8e<A_, S_>), dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, \
+                     nwg, nblocks, pg)
+    if (!k32 && order == 0) G8E_LAUNCH(false, 0);
+    else if (!k32 && order == 1) G8E_LAUNCH(true, 0);
+    else if (!k32 && order == 2) G8E_LAUNCH(true, 1);
+    else if (!k32 && order == 3) G8E_LAUNCH(true, 2);
+#undef G8E_LAUNCH
     else
       hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, nwg,
                          nblocks, pg);

@@ -4,7 +4,9 @@
 TFLOP/s (symmetric count n·p(p+1)) per mode/chunk and the max relative error
 of each mode against an fp64 Gram of a row sample.
 
-    python scripts/bench_gram.py [--variants i8x3:0,f32:0,bf16x3:0] [--outliers 0.005]
+    python scripts/bench_gram.py [--variants i8x3:0,f32:0,bf16x3:0,i8x3:0:packed] [--outliers 0.005]
+
+A third field sets OCM_GRAM8_ORDER for that variant (k_gram8e block order).
 """
 import argparse
 import os
@@ -20,7 +22,7 @@ def main():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--p", type=int, default=2048)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="i8x3:0,bf16x3:0,f32:0", help="mode:chunk_rows (0 = automatic)")
+    ap.add_argument("--variants", default="i8x3:0,bf16x3:0,f32:0", help="mode:chunk_rows[:order] (0 = automatic)")
     ap.add_argument("--outliers", type=float, default=0.0, help="fraction of rows scaled x100..x1000")
     args = ap.parse_args()
     import torch
@@ -39,11 +41,15 @@ def main():
         X[idx] = mu + (X[idx] - mu) * (100 + 900 * torch.rand(m, 1, generator=g, device=dev))
     shift = engine.cast_f32(engine.colmean(X, None, 4096))
     ctx = Context.get(0)
-    variants = [(v.split(":")[0], int(v.split(":")[1])) for v in args.variants.split(",")]
-    res = {f"{m}:{c}": [] for m, c in variants}
+    variants = [(v.split(":")[0], int(v.split(":")[1]), (v.split(":") + [""])[2]) for v in args.variants.split(",")]
+    res = {f"{m}:{c}:{o}": [] for m, c, o in variants}
     flop = args.rows * args.p * (args.p + 1)
     for _ in range(args.rounds):
-        for mode, chunk in variants:
+        for mode, chunk, order in variants:
+            if order:
+                os.environ["OCM_GRAM8_ORDER"] = order
+            else:
+                os.environ.pop("OCM_GRAM8_ORDER", None)
             engine.gram(X, None, [0, args.rows], shift, mode=mode, chunk_rows=chunk)  # warm (workspace)
             torch.cuda.synchronize()
             ctx.read_timing(0)
@@ -51,12 +57,13 @@ def main():
             engine.gram(X, None, [0, args.rows], shift, mode=mode, chunk_rows=chunk)
             ctx.set_timing(False)
             ms, _ = ctx.read_timing(0)
-            res[f"{mode}:{chunk}"].append(flop / (ms / 1e3) / 1e12)
+            res[f"{mode}:{chunk}:{order}"].append(flop / (ms / 1e3) / 1e12)
     print("guard marks (last i8x3 call):", engine.last_gram_marks(0))
     ns = min(args.rows, 65536)
     Y = X[:ns].double() - shift.double()
     Gref = Y.T @ Y
-    for mode in sorted({m for m, _ in variants}):
+    os.environ.pop("OCM_GRAM8_ORDER", None)
+    for mode in sorted({m for m, _, _ in variants}):
         Gm, _ = engine.gram(X, None, [0, ns], shift, mode=mode)
         err = ((Gm[0] - Gref).abs().max() / Gref.abs().max()).item()
         print(f"{mode:8s} sample Gram max rel err vs fp64: {err:.2e}")
