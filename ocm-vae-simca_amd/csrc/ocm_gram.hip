@@ -1581,6 +1581,228 @@ __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt
 
 #ifdef OCM_G8_LDS
 // ---------------------------------------------------------------------------
+// k_gram8x (experiment, make exp only: OCM_GRAM8_ORDER=lds) — k_gram8e with
+// the panels shared through LDS.  Measured (r03u, r03v): bit-identical, 362–367
+// TF against the default launch's 439–445 in the same processes, with the
+// partner reads as one burst or split — not kept.  One workgroup per
+// 128×128 tile (off-diagonal tiles in band order, then the diagonal ones; a
+// diagonal tile's mirror wave loads and stages its share but computes
+// nothing).  Waves (wm, wn) and (wm, 1−wn) need the same A panel, (wm, wn)
+// and (1−wm, wn) the same B panel: each wave loads only half of its 24
+// fragments per 64-row stage from global memory (A sub-panels 2wn, 2wn+1 and
+// B sub-panels 2wm, 2wm+1: its "own" 12), writes them to a two-slot LDS ring
+// and reads the other 12 from its partners' slots, so the L2 → CU traffic is
+// halved.  Stage t: read the partners' fragments of t (written before the
+// barrier that ended stage t−1); the 24 MFMAs of own × own sub-blocks cover
+// that read; the own loads of stage t+2 go out one per MFMA group, and the
+// own fragments of t+1 (loaded during t−1) are written to the other slot
+// during the last 72 MFMAs; lgkmcnt(0) + barrier.  Sub-block indices are kept
+// relative (own first): actual sub-panel = relative ^ (2·wn) for A and
+// ^ (2·wm) for B, applied to the load offsets and the output positions only.
+// Same exact int32 sets and f32 flush order as k_gram8d/8e: bit-identical.
+// ---------------------------------------------------------------------------
+constexpr int G8X_FRAG = 1024, G8X_WSLOT = 12 * G8X_FRAG, G8X_SLOT = 4 * G8X_WSLOT;
+__global__ __launch_bounds__(256, 1) void k_gram8x(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
+                                                   float* __restrict__ part) {
+  __shared__ __attribute__((aligned(1024))) char ring[2 * G8X_SLOT];     // 96 KiB
+  __shared__ __attribute__((aligned(16))) float runl[4][16][64][4];      // 64 KiB: wave-private f32 running sums
+
+  const int b = blockIdx.x;
+  const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
+  const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int chunk = wg / ntiles;
+  const int tix = wg - chunk * ntiles;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int ti = -1, tj = 0;
+  if (tix < ntiles - nt) {
+    int rem = tix;
+    for (int u = 0; u < nt && ti < 0; u += G8_BAND_R)
+      for (int v = u; v < nt && ti < 0; v += G8_BAND_C)
+        for (int a = u; a < min(nt, u + G8_BAND_R) && ti < 0; ++a)
+          for (int c = max(v, a + 1); c < min(nt, v + G8_BAND_C); ++c) {
+            if (rem == 0) {
+              ti = a;
+              tj = c;
+              break;
+            }
+            --rem;
+          }
+  } else {
+    ti = tj = tix - (ntiles - nt);
+  }
+  const bool mirror = (ti == tj) && wm == 1 && wn == 0;  // a diagonal tile's strictly-lower block
+  const int tile = ti * nt - ti * (ti - 1) / 2 + (tj - ti);
+  const int I = ti * Q8T, J = tj * Q8T;
+  int s = 0;
+  while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
+  const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
+  const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
+  const int nb = (int)((r1 - r0 + Q8BLK - 1) / Q8BLK);
+  constexpr int SPB = Q8BLK / 64;  // 64-row stages per scale block (24, a multiple of 3)
+  const int nstage = nb * SPB;
+  const size_t gbase = (size_t)chunk * (st.chunk_rows / Q8K);
+
+  const int lane = threadIdx.x & 63;
+  const int l15 = lane & 15, g4 = lane >> 4;
+  const size_t gstride = (size_t)q.P8 * 32;
+  const uint32_t span = (uint32_t)((size_t)nb * Q8SPB * gstride);
+  const char* cbase = q.digits + gbase * gstride;
+  __amdgpu_buffer_rsrc_t ra[3], rb[3];
+#pragma unroll
+  for (int dg = 0; dg < 3; ++dg) {
+    ra[dg] = __builtin_amdgcn_make_buffer_rsrc((void*)(cbase + dg * q.plane + (size_t)(I + wm * 64) * 32), 0, span,
+                                               0x00020000);
+    rb[dg] = __builtin_amdgcn_make_buffer_rsrc((void*)(cbase + dg * q.plane + (size_t)(J + wn * 64) * 32), 0, span,
+                                               0x00020000);
+  }
+  // own sub-panels: A 2wn + j, B 2wm + j (j = 0, 1)
+  const int voff = (g4 >> 1) * (int)gstride + l15 * 32 + (g4 & 1) * 16;
+  const int voffA = voff + 2 * wn * 512, voffB = voff + 2 * wm * 512;
+  const int sstride = 2 * (int)gstride;
+  const float* srow = q.scale + (size_t)chunk * q.nblk * q.P8 + I + wm * 64 + lane;
+  const float* scol = q.scale + (size_t)chunk * q.nblk * q.P8 + J + wn * 64 + lane;
+  // LDS: own fragment i of slot u at ring + u·SLOT + wave·WSLOT + i·FRAG;
+  // partner A fragments from wave ^ 1 (its own A, indices 0..5), partner B
+  // from wave ^ 2 (its own B, indices 6..11)
+  char* const wr_base = ring + wave * G8X_WSLOT + lane * 16;
+  const char* const rdA_base = ring + (wave ^ 1) * G8X_WSLOT + lane * 16;
+  const char* const rdB_base = ring + (wave ^ 2) * G8X_WSLOT + 6 * G8X_FRAG + lane * 16;
+
+  i32x4 acc1[4][4], acc2[4][4], acc3[4][4];  // [relative a][relative c]
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      acc1[a][c] = i32x4{};
+      acc2[a][c] = i32x4{};
+      acc3[a][c] = i32x4{};
+      *reinterpret_cast<f32x4*>(&runl[wave][a * 4 + c][lane][0]) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  float SR = 0.f, SC = 0.f;
+  auto flush = [&]() __attribute__((always_inline)) {
+    constexpr float w2 = 1.f / 254.f, w3 = 1.f / (254.f * 254.f);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int aa = a ^ (2 * wn);  // actual sub-panel: rows 16aa + 4g4 + e
+      f32x4 si;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) si[e] = __shfl(SR, aa * 16 + 4 * g4 + e);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float sj = __shfl(SC, (c ^ (2 * wm)) * 16 + l15);
+        f32x4* rp = reinterpret_cast<f32x4*>(&runl[wave][a * 4 + c][lane][0]);
+        f32x4 rv = *rp;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = fmaf((float)acc3[a][c][e], w3, fmaf((float)acc2[a][c][e], w2, (float)acc1[a][c][e]));
+          rv[e] = fmaf(v, si[e] * sj, rv[e]);
+        }
+        *rp = rv;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // own fragment i (0..5: A j = i / 3, 6..11: B j = (i − 6) / 3; digit i % 3)
+  auto gload = [&](i32x4 (&OA)[2][3], i32x4 (&OB)[2][3], int i, int so) __attribute__((always_inline)) {
+    const int j = (i % 6) / 3, dg = i % 3;
+    if (i < 6)
+      OA[j][dg] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(ra[dg], voffA + j * 512, so, 0);
+    else
+      OB[j][dg] = (i32x4)__builtin_amdgcn_raw_buffer_load_b128(rb[dg], voffB + j * 512, so, 0);
+  };
+  auto mfma6 = [&](const i32x4 (&A)[3], const i32x4 (&B)[3], int a, int c, bool z) __attribute__((always_inline)) {
+    acc1[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[0], z ? i32x4{} : acc1[a][c], 0, 0, 0);
+    acc2[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[1], z ? i32x4{} : acc2[a][c], 0, 0, 0);
+    acc2[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B[0], acc2[a][c], 0, 0, 0);
+    acc3[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[2], z ? i32x4{} : acc3[a][c], 0, 0, 0);
+    acc3[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2], B[0], acc3[a][c], 0, 0, 0);
+    acc3[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B[1], acc3[a][c], 0, 0, 0);
+  };
+  i32x4 PA[2][3], PB[2][3];  // partner fragments of the current stage
+  // stage t: CUR = own(t), NXT = own(t+1) (landed, staged to LDS during t),
+  // FUT = own(t+2) (loaded during t)
+  auto step = [&](i32x4 (&CA)[2][3], i32x4 (&CB)[2][3], i32x4 (&NA)[2][3], i32x4 (&NB)[2][3], i32x4 (&FA)[2][3],
+                  i32x4 (&FB)[2][3], int stg, bool z) __attribute__((always_inline)) {
+    const int rs = (stg & 1) * G8X_SLOT, ws = ((stg + 1) & 1) * G8X_SLOT;
+    const int so = min(stg + 2, nstage - 1) * sstride;
+    // partner B (used from the second quarter) first, partner A (third
+    // quarter) two sub-blocks later: the LDS read burst is spread
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int dg = 0; dg < 3; ++dg)
+        PB[j][dg] = *reinterpret_cast<const i32x4*>(rdB_base + rs + (j * 3 + dg) * G8X_FRAG);
+    // 16 sub-blocks in four quarters: own × own, own × partner, partner × own, partner × partner
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int qd = g >> 2, a = g & 1 ? 1 : 0, c = (g >> 1) & 1;
+      if (g == 2) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int dg = 0; dg < 3; ++dg)
+            PA[j][dg] = *reinterpret_cast<const i32x4*>(rdA_base + rs + (j * 3 + dg) * G8X_FRAG);
+      }
+      if (g < 12) gload(FA, FB, g, so);
+      if (g >= 4) {
+        const int i = g - 4;  // 12 staging writes over the last 12 sub-blocks
+        const int jj = (i % 6) / 3, dg = i % 3;
+        *reinterpret_cast<i32x4*>(wr_base + ws + i * G8X_FRAG) = i < 6 ? NA[jj][dg] : NB[jj][dg];
+      }
+      if (!mirror) {
+        if (qd == 0) mfma6(CA[a], CB[c], a, c, z);
+        if (qd == 1) mfma6(CA[a], PB[c], a, 2 + c, z);
+        if (qd == 2) mfma6(PA[a], CB[c], 2 + a, c, z);
+        if (qd == 3) mfma6(PA[a], PB[c], 2 + a, 2 + c, z);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+
+  i32x4 O0A[2][3], O0B[2][3], O1A[2][3], O1B[2][3], O2A[2][3], O2B[2][3];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) gload(O0A, O0B, i, 0);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) gload(O1A, O1B, i, min(1, nstage - 1) * sstride);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const int jj = (i % 6) / 3, dg = i % 3;
+    *reinterpret_cast<i32x4*>(wr_base + i * G8X_FRAG) = i < 6 ? O0A[jj][dg] : O0B[jj][dg];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  for (int blk = 0; blk < nb; ++blk) {
+    const int s0 = blk * SPB;
+#pragma unroll
+    for (int u = 0; u < SPB; u += 3) {
+      step(O0A, O0B, O1A, O1B, O2A, O2B, s0 + u, u == 0);
+      if (u == 0) {
+        SR = srow[(size_t)blk * q.P8];
+        SC = scol[(size_t)blk * q.P8];
+      }
+      step(O1A, O1B, O2A, O2B, O0A, O0B, s0 + u + 1, false);
+      step(O2A, O2B, O0A, O0B, O1A, O1B, s0 + u + 2, false);
+    }
+    if (!mirror) flush();
+  }
+  if (mirror) return;
+  float* out = part + ((size_t)chunk * ntiles + tile) * (Q8T * Q8T);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wm * 64 + (a ^ (2 * wn)) * 16 + 4 * g4 + e;
+        const int col = wn * 64 + (c ^ (2 * wm)) * 16 + l15;
+        out[row * Q8T + col] = runl[wave][a * 4 + c][lane][e];
+      }
+}
+#endif  // OCM_G8_LDS
+
+#ifdef OCM_G8_LDS
+// ---------------------------------------------------------------------------
 // k_gram8s (experiment, make exp only) — the i8×3 Gram with the workgroup's
 // two 128-column panels shared through LDS.  One workgroup per 128×128 tile,
 // four waves of 64×64; each 64-row phase (two 32-row stages) of both panels
@@ -2025,6 +2247,9 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   if (ord && !strcmp(ord, "packed")) order = 0;
   if (ord && !strcmp(ord, "aligned")) order = 1;
   if (ord && !strcmp(ord, "sync1")) order = 2;
+#ifdef OCM_G8_LDS
+  if (ord && !strcmp(ord, "lds")) order = 4;
+#endif
   for (size_t t = 0; t < tabs.size(); ++t) {
     const int s0 = tab_s0[t];
     const int nblocks = 4 * ntiles - nt, nwg = (nblocks + 3) / 4;
@@ -2046,6 +2271,13 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     else if (!k32 && order == 2) G8E_LAUNCH(true, 1);
     else if (!k32 && order == 3) G8E_LAUNCH(true, 2);
 #undef G8E_LAUNCH
+#ifdef OCM_G8_LDS
+    else if (!k32 && order == 4) {
+      const int64_t total_x = (cprefix[s0 + tabs[t].nseg] - cprefix[s0]) * ntiles;
+      hipLaunchKernelGGL(k_gram8x, dim3((unsigned)total_x), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total_x,
+                         pg);
+    }
+#endif
     else
       hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, nwg,
                          nblocks, pg);
