@@ -81,6 +81,8 @@ int ocm_ctx_destroy(ocm_ctx* ctx) {
   if (!ctx) return OCM_OK;
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
+  for (auto e : ctx->fork_ev) (void)hipEventDestroy(e);
   for (auto& v : ctx->ev)
     for (auto& pr : v) ctx->ev_pool.push_back(pr);
   for (auto& pr : ctx->ev_pool) {

@@ -694,7 +694,7 @@ template <bool GATHER>
 __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ X, int64_t ldx,
                                                       const int64_t* __restrict__ rows, int p,
                                                       const float* __restrict__ shift, SegTable st, Q8Plan q,
-                                                      double* __restrict__ colblk) {
+                                                      double* __restrict__ colblk, int cb0) {
   constexpr int QC = Q8QC;
   __shared__ __attribute__((aligned(16))) char stage[Q8SPB * QC * 32];  // one digit plane: 24 KiB
   __shared__ __attribute__((aligned(16))) float wmax[Q8QS][QC];
@@ -702,7 +702,8 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ 
   __shared__ float pmax[8][QC];
   __shared__ double psum[8][QC];
   __shared__ __attribute__((aligned(16))) float fmax_[QC];
-  const int chunk = blockIdx.x / q.nblk, b = blockIdx.x - chunk * q.nblk;
+  const int gbk = blockIdx.x + cb0;  // (chunk, block) of the call's chunk range
+  const int chunk = gbk / q.nblk, b = gbk - chunk * q.nblk;
   const int tid = threadIdx.x;
   const int cq = tid & 7, rs = tid >> 3;
   const int cg0 = blockIdx.y * QC;      // first column of the workgroup
@@ -1388,16 +1389,16 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
 // ---------------------------------------------------------------------------
 template <bool ALIGNED, int SYNC>
 __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
-                                                   int nwg, int nblocks, float* __restrict__ part) {
+                                                   int nwg, int nblocks, float* __restrict__ part, int chunk0) {
   __shared__ __attribute__((aligned(16))) float scl[4][2 * 64];      // wave-private: row, column scales
   __shared__ __attribute__((aligned(16))) float runl[4][16][64][4];  // wave-private f32 running sums
 
   const int b = blockIdx.x;
   const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
   const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
-  const int chunk = wg / nwg;
+  const int cl = wg / nwg, chunk = chunk0 + cl;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int bi = (wg - chunk * nwg) * 4 + wave;
+  int bi = (wg - cl * nwg) * 4 + wave;
   // SYNC > 0: a workgroup barrier every SYNC stages keeps the four waves in
   // step, so the second wave's load of a shared panel fragment finds it in
   // the CU's L1; a wave past the last block then computes a copy of the last
@@ -2214,30 +2215,9 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     q.nmark = counters;
     return q;
   };
-  {
-    ocm::TimedRegion tq(ctx, OCM_KERNEL_QUANT, st);
-    for (size_t t = 0; t < tabs.size(); ++t) {
-      const int s0 = tab_s0[t];
-      const int64_t gchunks = cprefix[s0 + tabs[t].nseg] - cprefix[s0];
-      const Q8Plan q = plan_for(s0);
-      double* col_g = colpart + (size_t)cprefix[s0] * nblk * P8;
-      dim3 gq((unsigned)(gchunks * nblk), (unsigned)(P8 / Q8QC));
-      if (rows)
-        hipLaunchKernelGGL(k_q8_quant<true>, gq, dim3(Q8QT), 0, st, X, ldx, rows, p, shift, tabs[t], q, col_g);
-      else
-        hipLaunchKernelGGL(k_q8_quant<false>, gq, dim3(Q8QT), 0, st, X, ldx, rows, p, shift, tabs[t], q, col_g);
-    }
-    OCM_CHECK_LAUNCH("k_q8_quant");
-  }
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   OCM_HIP(hipStreamIsCapturing(st, &cap));
   const bool capturing = cap != hipStreamCaptureStatusNone;
-  if (!capturing) OCM_HIP(hipMemcpyAsync(host, counters, 4, hipMemcpyDeviceToHost, st));
-  hipEvent_t ev = nullptr;
-  if (!capturing) {
-    OCM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    OCM_HIP(hipEventRecord(ev, st));
-  }
   // k_gram8e's block order and wave sync: tile-aligned workgroups with a
   // barrier every two stages (default: 437 TF against 417 for the packed
   // walk without barriers, r03s); OCM_GRAM8_ORDER = packed | aligned | sync1
@@ -2249,40 +2229,108 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   if (ord && !strcmp(ord, "sync1")) order = 2;
 #ifdef OCM_G8_LDS
   if (ord && !strcmp(ord, "lds")) order = 4;
+  if (ord && !strcmp(ord, "lds32")) order = 5;
 #endif
-  for (size_t t = 0; t < tabs.size(); ++t) {
+  // Quantiser / Gram overlap: the chunks are cut into `pieces` ranges; the
+  // quantiser (HBM-bound) of range i+1 runs on a side stream while the Gram
+  // (bound by the L2 → CU operand path) of range i runs on the launch stream.
+  // OCM_GRAM8_PIECES overrides the count (1 = no overlap); never while the
+  // stream is being captured.
+  int pieces = 1;
+  if (const char* pv = getenv("OCM_GRAM8_PIECES")) pieces = std::max(1, atoi(pv));
+  if (capturing || k32 || tabs.size() != 1) pieces = 1;
+  if (pieces > 1) {
+    const int64_t gch = cprefix[tab_s0[0] + tabs[0].nseg] - cprefix[tab_s0[0]];
+    pieces = (int)std::min<int64_t>(pieces, gch / 2);
+    if (pieces < 2) pieces = 1;
+  }
+  hipStream_t qs = st;  // the quantiser's stream
+  std::vector<hipEvent_t> qev;
+  if (pieces > 1) {
+    if (!ctx->side) OCM_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+    qs = ctx->side;
+    while ((int)ctx->fork_ev.size() < pieces + 1) {
+      hipEvent_t e;
+      OCM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ctx->fork_ev.push_back(e);
+    }
+    qev.assign(ctx->fork_ev.begin(), ctx->fork_ev.begin() + pieces + 1);
+    OCM_HIP(hipEventRecord(qev[pieces], st));  // everything queued before this call
+    OCM_HIP(hipStreamWaitEvent(qs, qev[pieces], 0));
+  }
+  const int nblocks = 4 * ntiles - nt, nwg = (nblocks + 3) / 4;
+  auto quantise = [&](size_t t, int64_t c0, int64_t c1) {
     const int s0 = tab_s0[t];
-    const int nblocks = 4 * ntiles - nt, nwg = (nblocks + 3) / 4;
-    const int64_t total = (cprefix[s0 + tabs[t].nseg] - cprefix[s0]) * nwg;
+    const Q8Plan q = plan_for(s0);
+    double* col_g = colpart + (size_t)cprefix[s0] * nblk * P8;
+    dim3 gq((unsigned)((c1 - c0) * nblk), (unsigned)(P8 / Q8QC));
+    ocm::TimedRegion tq(ctx, OCM_KERNEL_QUANT, qs);
+    if (rows)
+      hipLaunchKernelGGL(k_q8_quant<true>, gq, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g,
+                         (int)(c0 * nblk));
+    else
+      hipLaunchKernelGGL(k_q8_quant<false>, gq, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g,
+                         (int)(c0 * nblk));
+  };
+  auto gram = [&](size_t t, int64_t c0, int64_t c1) {
+    const int s0 = tab_s0[t];
+    const int64_t total = (c1 - c0) * nwg;
     const Q8Plan q = plan_for(s0);
     float* pg = part + (size_t)cprefix[s0] * ntiles * Q8T * Q8T;
     ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
-#ifdef OCM_G8_LDS
-    (void)total;
-    const int64_t total_s = (cprefix[s0 + tabs[t].nseg] - cprefix[s0]) * ntiles;
-    hipLaunchKernelGGL(k_gram8s, dim3((unsigned)total_s), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total_s, pg);
-    OCM_CHECK_LAUNCH("k_gram8s");
-#else
 #define G8E_LAUNCH(A_, S_)                                                                                   \
   hipLaunchKernelGGL((k_gram8e<A_, S_>), dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, \
-                     nwg, nblocks, pg)
+                     nwg, nblocks, pg, (int)c0)
     if (!k32 && order == 0) G8E_LAUNCH(false, 0);
     else if (!k32 && order == 1) G8E_LAUNCH(true, 0);
     else if (!k32 && order == 2) G8E_LAUNCH(true, 1);
     else if (!k32 && order == 3) G8E_LAUNCH(true, 2);
 #undef G8E_LAUNCH
 #ifdef OCM_G8_LDS
-    else if (!k32 && order == 4) {
-      const int64_t total_x = (cprefix[s0 + tabs[t].nseg] - cprefix[s0]) * ntiles;
-      hipLaunchKernelGGL(k_gram8x, dim3((unsigned)total_x), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total_x,
-                         pg);
+    else if (!k32 && order >= 4) {
+      const int64_t total_x = (c1 - c0) * ntiles;
+      if (order == 4)
+        hipLaunchKernelGGL(k_gram8x, dim3((unsigned)total_x), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total_x,
+                           pg);
+      else
+        hipLaunchKernelGGL(k_gram8s, dim3((unsigned)total_x), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total_x,
+                           pg);
     }
 #endif
     else
       hipLaunchKernelGGL(k_gram8d, dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, nwg,
                          nblocks, pg);
+  };
+  // all quantiser launches first (or, with pieces, range by range on the side
+  // stream), then the mark count is read back while the Gram runs
+  hipEvent_t ev = nullptr;
+  if (!capturing) OCM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  if (pieces == 1) {
+    for (size_t t = 0; t < tabs.size(); ++t) quantise(t, 0, cprefix[tab_s0[t] + tabs[t].nseg] - cprefix[tab_s0[t]]);
+    OCM_CHECK_LAUNCH("k_q8_quant");
+    if (!capturing) {
+      OCM_HIP(hipMemcpyAsync(host, counters, 4, hipMemcpyDeviceToHost, st));
+      OCM_HIP(hipEventRecord(ev, st));
+    }
+    for (size_t t = 0; t < tabs.size(); ++t) gram(t, 0, cprefix[tab_s0[t] + tabs[t].nseg] - cprefix[tab_s0[t]]);
     OCM_CHECK_LAUNCH("k_gram8d/8e");
-#endif
+  } else {
+    const int64_t gch = cprefix[tab_s0[0] + tabs[0].nseg] - cprefix[tab_s0[0]];
+    std::vector<int64_t> cut(pieces + 1);
+    for (int i = 0; i <= pieces; ++i) cut[i] = gch * i / pieces;
+    for (int i = 0; i < pieces; ++i) {
+      quantise(0, cut[i], cut[i + 1]);
+      OCM_HIP(hipEventRecord(qev[i], qs));
+    }
+    OCM_CHECK_LAUNCH("k_q8_quant");
+    OCM_HIP(hipMemcpyAsync(host, counters, 4, hipMemcpyDeviceToHost, qs));
+    OCM_HIP(hipEventRecord(ev, qs));
+    for (int i = 0; i < pieces; ++i) {
+      OCM_HIP(hipStreamWaitEvent(st, qev[i], 0));
+      gram(0, cut[i], cut[i + 1]);
+    }
+    OCM_CHECK_LAUNCH("k_gram8e");
+    OCM_HIP(hipStreamWaitEvent(st, ev, 0));  // the read-back is done before the workspace is reused
   }
   for (int s = 0; s < nseg; ++s) {
     double* Gs = G_out + (size_t)s * p * p;

@@ -23,6 +23,9 @@ struct ocm_ctx {
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[OCM_TIMED_KERNELS];
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+  // side stream + events of the quantiser / Gram overlap (created on first use)
+  hipStream_t side = nullptr;
+  std::vector<hipEvent_t> fork_ev;
 };
 
 namespace ocm {

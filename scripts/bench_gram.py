@@ -6,7 +6,9 @@ of each mode against an fp64 Gram of a row sample.
 
     python scripts/bench_gram.py [--variants i8x3:0,f32:0,bf16x3:0,i8x3:0:packed] [--outliers 0.005]
 
-A third field sets OCM_GRAM8_ORDER for that variant (k_gram8e block order).
+A third field sets OCM_GRAM8_ORDER for that variant (k_gram8e block order),
+a fourth OCM_GRAM8_PIECES (quantiser / Gram overlap).  "wall" is the whole
+call (guard, quantiser, Gram, reduce) between two device synchronisations.
 """
 import argparse
 import os
@@ -41,35 +43,46 @@ def main():
         X[idx] = mu + (X[idx] - mu) * (100 + 900 * torch.rand(m, 1, generator=g, device=dev))
     shift = engine.cast_f32(engine.colmean(X, None, 4096))
     ctx = Context.get(0)
-    variants = [(v.split(":")[0], int(v.split(":")[1]), (v.split(":") + [""])[2]) for v in args.variants.split(",")]
-    res = {f"{m}:{c}:{o}": [] for m, c, o in variants}
+    import time
+
+    variants = [(v.split(":")[0], int(v.split(":")[1]), (v.split(":") + ["", ""])[2], (v.split(":") + ["", ""])[3])
+                for v in args.variants.split(",")]
+    res = {f"{m}:{c}:{o}:{pc}": [] for m, c, o, pc in variants}
+    wall = {k: [] for k in res}
     flop = args.rows * args.p * (args.p + 1)
     for _ in range(args.rounds):
-        for mode, chunk, order in variants:
-            if order:
-                os.environ["OCM_GRAM8_ORDER"] = order
-            else:
-                os.environ.pop("OCM_GRAM8_ORDER", None)
+        for mode, chunk, order, pcs in variants:
+            for var, val in (("OCM_GRAM8_ORDER", order), ("OCM_GRAM8_PIECES", pcs)):
+                if val:
+                    os.environ[var] = val
+                else:
+                    os.environ.pop(var, None)
             engine.gram(X, None, [0, args.rows], shift, mode=mode, chunk_rows=chunk)  # warm (workspace)
             torch.cuda.synchronize()
             ctx.read_timing(0)
             ctx.set_timing(True)
+            t0 = time.perf_counter()
             engine.gram(X, None, [0, args.rows], shift, mode=mode, chunk_rows=chunk)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
             ctx.set_timing(False)
             ms, _ = ctx.read_timing(0)
-            res[f"{mode}:{chunk}:{order}"].append(flop / (ms / 1e3) / 1e12)
+            res[f"{mode}:{chunk}:{order}:{pcs}"].append(flop / (ms / 1e3) / 1e12)
+            wall[f"{mode}:{chunk}:{order}:{pcs}"].append((t1 - t0) * 1e3)
     print("guard marks (last i8x3 call):", engine.last_gram_marks(0))
     ns = min(args.rows, 65536)
     Y = X[:ns].double() - shift.double()
     Gref = Y.T @ Y
     os.environ.pop("OCM_GRAM8_ORDER", None)
-    for mode in sorted({m for m, _, _ in variants}):
+    os.environ.pop("OCM_GRAM8_PIECES", None)
+    for mode in sorted({m for m, _, _, _ in variants}):
         Gm, _ = engine.gram(X, None, [0, ns], shift, mode=mode)
         err = ((Gm[0] - Gref).abs().max() / Gref.abs().max()).item()
         print(f"{mode:8s} sample Gram max rel err vs fp64: {err:.2e}")
     for key, vals in res.items():
-        print(f"{key:16s} TFLOP/s median {sorted(vals)[len(vals) // 2]:7.2f}  all {[round(v, 1) for v in vals]}",
-              flush=True)
+        w = sorted(wall[key])
+        print(f"{key:18s} TFLOP/s median {sorted(vals)[len(vals) // 2]:7.2f}  all {[round(v, 1) for v in vals]}  "
+              f"wall ms median {w[len(w) // 2]:7.3f}", flush=True)
 
 
 if __name__ == "__main__":
