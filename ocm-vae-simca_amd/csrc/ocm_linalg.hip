@@ -14,6 +14,7 @@
 //     against the leading eigenvalues;
 //   * p ≤ 64 (VAE latents, tiny spectra): Jacobi on C directly.
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <limits>
 #include <vector>
@@ -156,6 +157,94 @@ __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// W = C·V for a 32-column block (the subspace iteration's product, b = 32):
+// two workgroups of eight waves per 16 rows of C, each a half of K, each wave
+// a sixteenth of K in 32-column groups.  Lane (i, g) holds C[r0 + i][k0 + 8g
+// .. k0 + 8g + 7] (64 contiguous bytes) and V rows k0 + 8g + s, columns i and
+// 16 + i; MFMA s of a group pairs K-slot g with column k0 + 8g + s for both
+// operands (v_mfma_f64_16x16x4f64).  The eight wave partials meet in LDS in a
+// fixed order; the second workgroup of a row block to finish (a parity
+// ticket per row block) adds the first one's partial: half 0 + half 1 in
+// either case, so the result does not depend on which finishes first.  One
+// launch instead of the generic 64×64-tile GEMM (half its columns idle at
+// b = 32) plus a split-K plane sum: 16 µs against 19 + 6 µs (r03y).  The
+// publish is one agent-scope release by one lane (a __threadfence() in every
+// thread measured 77 µs per launch).
+// ---------------------------------------------------------------------------
+constexpr int CV_W = 8;  // waves per workgroup
+__global__ __launch_bounds__(512) void k_cv32(const double* __restrict__ C, int p, const double* __restrict__ V,
+                                            double* __restrict__ W, double* __restrict__ part,
+                                            unsigned* __restrict__ ticket) {
+  __shared__ double red[CV_W][16 * 33];
+  __shared__ int last;
+  const int rb = blockIdx.x >> 1, half = blockIdx.x & 1;
+  const int r0 = rb * 16;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int i = lane & 15, g = lane >> 4;
+  const int kslice = (p + 2 * CV_W * 32 - 1) / (2 * CV_W * 32) * 32;
+  const int kb = (half * CV_W + wave) * kslice;
+  const int ke = min(p, kb + kslice);
+  const double* crow = C + (int64_t)min(r0 + i, p - 1) * p;
+  f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = acc0;
+  // (loading the next group before this group's MFMAs measured 18.1 vs 16.1 µs)
+  for (int k0 = kb; k0 < ke; k0 += 32) {
+    double a[8], b0[8], b1[8];
+    const int kk0 = k0 + 8 * g;
+    if (k0 + 32 <= ke) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        a[s] = crow[kk0 + s];
+        b0[s] = V[(int64_t)(kk0 + s) * 32 + i];
+        b1[s] = V[(int64_t)(kk0 + s) * 32 + 16 + i];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int kk = kk0 + s;
+        const bool ok = kk < ke;
+        a[s] = ok ? crow[kk] : 0.0;
+        b0[s] = ok ? V[(int64_t)kk * 32 + i] : 0.0;
+        b1[s] = ok ? V[(int64_t)kk * 32 + 16 + i] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b0[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b1[s], acc1, 0, 0, 0);
+    }
+  }
+  // f64 16x16x4 C/D map: col = lane&15, row = (lane>>4) + 4*reg
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[wave][(g + 4 * r) * 33 + i] = acc0[r];
+    red[wave][(g + 4 * r) * 33 + 16 + i] = acc1[r];
+  }
+  __syncthreads();
+  const int orow = tid >> 5, ocol = tid & 31;
+  double v = 0.0;
+#pragma unroll
+  for (int w = 0; w < CV_W; ++w) v += red[w][orow * 33 + ocol];
+  part[(int64_t)blockIdx.x * 512 + tid] = v;
+  // publish: every wave drains its stores, then one agent-scope release and
+  // the ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = (__hip_atomic_fetch_add(&ticket[rb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u) == 1u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  const double o = part[(int64_t)(blockIdx.x ^ 1) * 512 + tid];
+  if (r0 + orow < p) W[(int64_t)(r0 + orow) * 32 + ocol] = half == 0 ? v + o : o + v;
 }
 
 // sum of split-K planes: D[i] = Σ_z P[z][i]
@@ -1041,6 +1130,7 @@ int dgemm(const double* A, int64_t lda, const double* B, int64_t ldb, double* D,
 }
 
 int jacobi(const double* A, int n, int max_sweeps, double* ev, double* Z, hipStream_t st) {
+  // n = 32: the block kernel (0.95 ms per fit against 1.19 with the one-wave k_jacobi<32, 64>, r03z)
   if (n == 32)
     hipLaunchKernelGGL(k_jacobi_blk<32>, dim3(1), dim3(256), 0, st, A, max_sweeps, ev, Z, nullptr);
   else if (n == 48)
@@ -1143,6 +1233,8 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   const size_t plane_cap = std::max((size_t)ksplit * pb, wide ? 16 * bb : 0);
   size_t need = (6 * pb + 6 * bb + plane_cap + (wide ? 0 : (size_t)nblk * bb) + 4 * b + 64) * sizeof(double);
   need += ((size_t)CQ_G * 768 + 2048 + 64) * sizeof(double) + 3 * 256;  // CholQR partials, M1/M2, ticket
+  const int cv_rb = (p + 15) / 16;  // k_cv32 row blocks
+  need += ((size_t)cv_rb * 2 * 512) * sizeof(double) + (size_t)cv_rb * sizeof(unsigned) + 2 * 256;
   if (theta_mode) need += ((size_t)p * p + 4 * (size_t)k * p + 2 * def_blocks + trace_wgs + 8) * sizeof(double);
   void* w = ocm::workspace(ctx, need + 16 * 256, st);
   if (!w) return OCM_ERR_NOMEM;
@@ -1164,6 +1256,9 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   double* cq_M = cv.take<double>(2048);
   unsigned* cq_ticket = cv.take<unsigned>(64);
   OCM_HIP(hipMemsetAsync(cq_ticket, 0, sizeof(unsigned), st));  // k_cq_gram32's tickets count from a multiple of CQ_G
+  double* cv_part = cv.take<double>((size_t)cv_rb * 2 * 512);
+  unsigned* cv_ticket = cv.take<unsigned>(cv_rb);
+  OCM_HIP(hipMemsetAsync(cv_ticket, 0, (size_t)cv_rb * sizeof(unsigned), st));  // parity tickets start even
   auto* hres = static_cast<double*>(ocm::host_staging(ctx, (wide ? 3 * bb + b : 2 * b) * sizeof(double)));
   if (!hres) return OCM_ERR_NOMEM;
   double* hmat = hres + 2 * b;  // wide: b×b host staging (+ b×b result, + b values)
@@ -1267,8 +1362,13 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   int it = 0;
   bool converged = false;
   for (it = 1; it <= max_iter; ++it) {
-    rc = dgemm(C, p, V, b, W, b, p, b, p, ksplit, planes, st);  // W = C V
-    if (rc) return rc;
+    if (!wide && b == 32) {  // W = C V
+      hipLaunchKernelGGL(k_cv32, dim3(2 * cv_rb), dim3(512), 0, st, C, p, V, W, cv_part, cv_ticket);
+      OCM_CHECK_LAUNCH("k_cv32");
+    } else {
+      rc = dgemm(C, p, V, b, W, b, p, b, p, ksplit, planes, st);
+      if (rc) return rc;
+    }
     if (it <= PLAIN && it < max_iter) {
       // W is not needed again (recomputed next iteration).  One CholQR pass
       // keeps span(W) exactly; the basis that feeds Rayleigh–Ritz (the last
