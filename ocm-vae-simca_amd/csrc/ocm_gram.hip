@@ -1387,7 +1387,7 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
 // fragments (4 sub-panels × 3 digits for A and for B) for 96 MFMAs, one load
 // per four MFMAs, one stage ahead into the other of two register sets.
 // ---------------------------------------------------------------------------
-template <bool ALIGNED, int SYNC>
+template <bool ALIGNED, int SYNC, bool FRONT = false>
 __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
                                                    int nwg, int nblocks, float* __restrict__ part, int chunk0) {
   __shared__ __attribute__((aligned(16))) float scl[4][2 * 64];      // wave-private: row, column scales
@@ -1531,12 +1531,15 @@ __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt
   auto step = [&](i32x4 (&CA)[4][3], i32x4 (&CB)[4][3], i32x4 (&NA)[4][3], i32x4 (&NB)[4][3], int stg,
                   bool z) __attribute__((always_inline)) {
     const int so = min(stg + 1, nstage - 1) * sstride;
+    // FRONT: the 24 loads one per two MFMAs over the first half of the stage
+    // (more time to land) instead of one per four over the whole stage
+    constexpr int GRP = FRONT ? 48 : 24, PER = 96 / GRP;
 #pragma unroll
-    for (int i = 0; i < 24; ++i) {
-      load_frag(NA, NB, i, so);
+    for (int i = 0; i < GRP; ++i) {
+      if (i < 24) load_frag(NA, NB, i, so);
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int j = 4 * i + jj, blk = j / 6, kind = j % 6, a = blk >> 2, c = blk & 3;
+      for (int jj = 0; jj < PER; ++jj) {
+        const int j = PER * i + jj, blk = j / 6, kind = j % 6, a = blk >> 2, c = blk & 3;
         if (kind == 0) acc1[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(CA[a][0], CB[c][0], z ? i32x4{} : acc1[a][c], 0, 0, 0);
         if (kind == 1) acc2[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(CA[a][0], CB[c][1], z ? i32x4{} : acc2[a][c], 0, 0, 0);
         if (kind == 2) acc2[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(CA[a][1], CB[c][0], acc2[a][c], 0, 0, 0);
@@ -2227,6 +2230,7 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   if (ord && !strcmp(ord, "packed")) order = 0;
   if (ord && !strcmp(ord, "aligned")) order = 1;
   if (ord && !strcmp(ord, "sync1")) order = 2;
+  if (ord && !strcmp(ord, "front")) order = 6;
 #ifdef OCM_G8_LDS
   if (ord && !strcmp(ord, "lds")) order = 4;
   if (ord && !strcmp(ord, "lds32")) order = 5;
@@ -2281,13 +2285,18 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
 #define G8E_LAUNCH(A_, S_)                                                                                   \
   hipLaunchKernelGGL((k_gram8e<A_, S_>), dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, \
                      nwg, nblocks, pg, (int)c0)
+#define G8E_LAUNCH3(A_, S_, F_)                                                                                      \
+  hipLaunchKernelGGL((k_gram8e<A_, S_, F_>), dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles,         \
+                     (int)total, nwg, nblocks, pg, (int)c0)
     if (!k32 && order == 0) G8E_LAUNCH(false, 0);
     else if (!k32 && order == 1) G8E_LAUNCH(true, 0);
     else if (!k32 && order == 2) G8E_LAUNCH(true, 1);
     else if (!k32 && order == 3) G8E_LAUNCH(true, 2);
+    else if (!k32 && order == 6) G8E_LAUNCH3(true, 2, true);
 #undef G8E_LAUNCH
+#undef G8E_LAUNCH3
 #ifdef OCM_G8_LDS
-    else if (!k32 && order >= 4) {
+    else if (!k32 && order >= 4 && order <= 5) {
       const int64_t total_x = (c1 - c0) * ntiles;
       if (order == 4)
         hipLaunchKernelGGL(k_gram8x, dim3((unsigned)total_x), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total_x,

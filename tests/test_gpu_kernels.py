@@ -310,7 +310,7 @@ def test_gram_i8_digit_split_edge_cases(eng, n, p):
     np.testing.assert_allclose(cs[0].cpu().numpy(), Y.sum(0), rtol=1e-6, atol=1e-6 * np.abs(Y).sum(0).max())
 
 
-@pytest.mark.parametrize("env", [{}, {"OCM_GRAM8_ORDER": "packed"}, {"OCM_GRAM8_ORDER": "sync1"},
+@pytest.mark.parametrize("env", [{}, {"OCM_GRAM8_ORDER": "packed"}, {"OCM_GRAM8_ORDER": "sync1"}, {"OCM_GRAM8_ORDER": "front"},
                                  {"OCM_GRAM8_PIECES": "3"}, {"OCM_GRAM8_PIECES": "1"}])
 @pytest.mark.parametrize("n,p,chunk", [(20000, 2048, 0), (9000, 257, 512), (5000, 300, 4608)])
 def test_gram_i8_kernels_bit_identical(eng, n, p, chunk, env, monkeypatch):
