@@ -1531,8 +1531,8 @@ __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt
   auto step = [&](i32x4 (&CA)[4][3], i32x4 (&CB)[4][3], i32x4 (&NA)[4][3], i32x4 (&NB)[4][3], int stg,
                   bool z) __attribute__((always_inline)) {
     const int so = min(stg + 1, nstage - 1) * sstride;
-    // FRONT: the 24 loads one per two MFMAs over the first half of the stage
-    // (more time to land) instead of one per four over the whole stage
+    // FRONT (A/B only): the 24 loads one per two MFMAs over the first half of
+    // the stage instead of one per four over the whole stage — 392 vs 439 TF
     constexpr int GRP = FRONT ? 48 : 24, PER = 96 / GRP;
 #pragma unroll
     for (int i = 0; i < GRP; ++i) {
