@@ -2231,6 +2231,8 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   if (ord && !strcmp(ord, "aligned")) order = 1;
   if (ord && !strcmp(ord, "sync1")) order = 2;
   if (ord && !strcmp(ord, "front")) order = 6;
+  if (ord && !strcmp(ord, "sync4")) order = 7;
+  if (ord && !strcmp(ord, "sync3")) order = 8;
 #ifdef OCM_G8_LDS
   if (ord && !strcmp(ord, "lds")) order = 4;
   if (ord && !strcmp(ord, "lds32")) order = 5;
@@ -2293,6 +2295,8 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     else if (!k32 && order == 2) G8E_LAUNCH(true, 1);
     else if (!k32 && order == 3) G8E_LAUNCH(true, 2);
     else if (!k32 && order == 6) G8E_LAUNCH3(true, 2, true);
+    else if (!k32 && order == 7) G8E_LAUNCH(true, 4);
+    else if (!k32 && order == 8) G8E_LAUNCH(true, 3);
 #undef G8E_LAUNCH
 #undef G8E_LAUNCH3
 #ifdef OCM_G8_LDS
