@@ -72,7 +72,7 @@ int ocm_ctx_reserve(ocm_ctx* ctx, size_t bytes);
  * ocm_ctx_read_timing waits for the recorded events, returns the summed
  * duration (ms) and launch count of kernel `kernel_id`, and clears them. */
 #define OCM_TIMED_KERNELS 3
-#define OCM_KERNEL_GRAM 0  /* the Gram main kernel (k_gram8d / k_gram3 / k_gram) */
+#define OCM_KERNEL_GRAM 0  /* the Gram main kernel (k_gram8e / k_gram8d / k_gram3 / k_gram) */
 #define OCM_KERNEL_SCORE 1 /* k_score: fused projection / Q / T² kernel */
 #define OCM_KERNEL_QUANT 2 /* k_q8_quant: int8 digit split feeding k_gram8d */
 int ocm_ctx_set_timing(ocm_ctx* ctx, int enable);

@@ -690,7 +690,7 @@ __device__ __forceinline__ int q8_qslot(int P) { return P ^ ((P >> 3) & 7); }
 constexpr int Q8QC = 32;                   // columns per quantiser workgroup
 constexpr int Q8QS = Q8BLK / 16;           // 16-row slices per block (96)
 constexpr int Q8QT = Q8QS * (Q8QC / 4);    // threads (768)
-template <bool GATHER>
+template <bool GATHER, int CG = 1>
 __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ X, int64_t ldx,
                                                       const int64_t* __restrict__ rows, int p,
                                                       const float* __restrict__ shift, SegTable st, Q8Plan q,
@@ -702,12 +702,13 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ 
   __shared__ float pmax[8][QC];
   __shared__ double psum[8][QC];
   __shared__ __attribute__((aligned(16))) float fmax_[QC];
-  const int gbk = blockIdx.x + cb0;  // (chunk, block) of the call's chunk range
+  // CG > 1 (A/B): CG neighbouring 32-column groups of one row block on
+  // consecutive workgroups (they run at the same time on other CUs), so each
+  // row's CG·128 bytes are read close in time
+  const int gbk = (int)(blockIdx.x / CG) + cb0;  // (chunk, block) of the call's chunk range
   const int chunk = gbk / q.nblk, b = gbk - chunk * q.nblk;
   const int tid = threadIdx.x;
   const int cq = tid & 7, rs = tid >> 3;
-  const int cg0 = blockIdx.y * QC;      // first column of the workgroup
-  const int c0 = cg0 + 4 * cq;          // first of this thread's 4 columns
   int s = 0;
   while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
   const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
@@ -715,6 +716,8 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ 
   // blocks past the chunk's rows are written too (zero digits, scale 1): the
   // Gram kernels read whole blocks
   const int64_t rb = r0 + (int64_t)b * Q8BLK + 16 * rs;
+  const int cg0 = (int)(blockIdx.y * CG + blockIdx.x % CG) * QC;  // first column of the workgroup
+  const int c0 = cg0 + 4 * cq;                                    // first of this thread's 4 columns
   const bool vec = (ldx % 4 == 0) && (c0 + 3 < p) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
   f32x4 sh;
 #pragma unroll
@@ -2251,6 +2254,9 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     if (pieces < 2) pieces = 1;
   }
   hipStream_t qs = st;  // the quantiser's stream
+  int qcg = 1;          // OCM_Q8_CG = 2 | 4: column groups per quantiser workgroup (A/B; contiguous rows only)
+  if (const char* qv = getenv("OCM_Q8_CG")) qcg = atoi(qv);
+  if (rows || (qcg != 2 && qcg != 4)) qcg = 1;
   std::vector<hipEvent_t> qev;
   if (pieces > 1) {
     if (!ctx->side) OCM_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
@@ -2269,10 +2275,17 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     const int s0 = tab_s0[t];
     const Q8Plan q = plan_for(s0);
     double* col_g = colpart + (size_t)cprefix[s0] * nblk * P8;
-    dim3 gq((unsigned)((c1 - c0) * nblk), (unsigned)(P8 / Q8QC));
+    const int cgw = qcg;  // column groups per quantiser workgroup (P8 / 32 is a multiple of 4)
+    dim3 gq((unsigned)((c1 - c0) * nblk * cgw), (unsigned)(P8 / Q8QC / cgw));
     ocm::TimedRegion tq(ctx, OCM_KERNEL_QUANT, qs);
     if (rows)
       hipLaunchKernelGGL(k_q8_quant<true>, gq, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g,
+                         (int)(c0 * nblk));
+    else if (cgw == 4)
+      hipLaunchKernelGGL((k_q8_quant<false, 4>), gq, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g,
+                         (int)(c0 * nblk));
+    else if (cgw == 2)
+      hipLaunchKernelGGL((k_q8_quant<false, 2>), gq, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g,
                          (int)(c0 * nblk));
     else
       hipLaunchKernelGGL(k_q8_quant<false>, gq, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g,

@@ -7,7 +7,8 @@ of each mode against an fp64 Gram of a row sample.
     python scripts/bench_gram.py [--variants i8x3:0,f32:0,bf16x3:0,i8x3:0:packed] [--outliers 0.005]
 
 A third field sets OCM_GRAM8_ORDER for that variant (k_gram8e block order),
-a fourth OCM_GRAM8_PIECES (quantiser / Gram overlap).  "wall" is the whole
+a fourth OCM_GRAM8_PIECES (quantiser / Gram overlap), a fifth OCM_Q8_CG
+(column groups per quantiser row block on consecutive workgroups).  "wall" is the whole
 call (guard, quantiser, Gram, reduce) between two device synchronisations.
 """
 import argparse
@@ -15,6 +16,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+QUANT_ID = 2  # include/ocm.h OCM_KERNEL_QUANT
 sys.path.insert(0, os.path.join(REPO, "ocm-vae-simca_amd"))
 sys.path.insert(0, REPO)
 
@@ -45,14 +47,16 @@ def main():
     ctx = Context.get(0)
     import time
 
-    variants = [(v.split(":")[0], int(v.split(":")[1]), (v.split(":") + ["", ""])[2], (v.split(":") + ["", ""])[3])
-                for v in args.variants.split(",")]
-    res = {f"{m}:{c}:{o}:{pc}": [] for m, c, o, pc in variants}
+    variants = [tuple(v.split(":")[:2]) + tuple((v.split(":") + ["", "", ""])[2:5]) for v in args.variants.split(",")]
+    variants = [(m, int(c), o, pc, cg) for m, c, o, pc, cg in variants]
+    res = {":".join(map(str, v)): [] for v in variants}
     wall = {k: [] for k in res}
+    quant = {k: [] for k in res}
     flop = args.rows * args.p * (args.p + 1)
     for _ in range(args.rounds):
-        for mode, chunk, order, pcs in variants:
-            for var, val in (("OCM_GRAM8_ORDER", order), ("OCM_GRAM8_PIECES", pcs)):
+        for mode, chunk, order, pcs, qcg in variants:
+            key = ":".join(map(str, (mode, chunk, order, pcs, qcg)))
+            for var, val in (("OCM_GRAM8_ORDER", order), ("OCM_GRAM8_PIECES", pcs), ("OCM_Q8_CG", qcg)):
                 if val:
                     os.environ[var] = val
                 else:
@@ -60,6 +64,7 @@ def main():
             engine.gram(X, None, [0, args.rows], shift, mode=mode, chunk_rows=chunk)  # warm (workspace)
             torch.cuda.synchronize()
             ctx.read_timing(0)
+            ctx.read_timing(QUANT_ID)
             ctx.set_timing(True)
             t0 = time.perf_counter()
             engine.gram(X, None, [0, args.rows], shift, mode=mode, chunk_rows=chunk)
@@ -67,22 +72,26 @@ def main():
             t1 = time.perf_counter()
             ctx.set_timing(False)
             ms, _ = ctx.read_timing(0)
-            res[f"{mode}:{chunk}:{order}:{pcs}"].append(flop / (ms / 1e3) / 1e12)
-            wall[f"{mode}:{chunk}:{order}:{pcs}"].append((t1 - t0) * 1e3)
+            qms, _ = ctx.read_timing(QUANT_ID)
+            res[key].append(flop / (ms / 1e3) / 1e12)
+            wall[key].append((t1 - t0) * 1e3)
+            quant[key].append(qms)
     print("guard marks (last i8x3 call):", engine.last_gram_marks(0))
     ns = min(args.rows, 65536)
     Y = X[:ns].double() - shift.double()
     Gref = Y.T @ Y
     os.environ.pop("OCM_GRAM8_ORDER", None)
     os.environ.pop("OCM_GRAM8_PIECES", None)
-    for mode in sorted({m for m, _, _, _ in variants}):
+    os.environ.pop("OCM_Q8_CG", None)
+    for mode in sorted({v[0] for v in variants}):
         Gm, _ = engine.gram(X, None, [0, ns], shift, mode=mode)
         err = ((Gm[0] - Gref).abs().max() / Gref.abs().max()).item()
         print(f"{mode:8s} sample Gram max rel err vs fp64: {err:.2e}")
     for key, vals in res.items():
         w = sorted(wall[key])
+        qq = sorted(quant[key])
         print(f"{key:18s} TFLOP/s median {sorted(vals)[len(vals) // 2]:7.2f}  all {[round(v, 1) for v in vals]}  "
-              f"wall ms median {w[len(w) // 2]:7.3f}", flush=True)
+              f"wall ms median {w[len(w) // 2]:7.3f}  quantise ms median {qq[len(qq) // 2]:6.3f}", flush=True)
 
 
 if __name__ == "__main__":
