@@ -1539,7 +1539,11 @@ __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt
     constexpr int GRP = FRONT ? 48 : 24, PER = 96 / GRP;
 #pragma unroll
     for (int i = 0; i < GRP; ++i) {
+#ifndef OCM_G8E_DIAG_NOLOAD  // diagnostic build only (make exp): operands never refreshed (timing, not results)
       if (i < 24) load_frag(NA, NB, i, so);
+#else
+      (void)so;
+#endif
 #pragma unroll
       for (int jj = 0; jj < PER; ++jj) {
         const int j = PER * i + jj, blk = j / 6, kind = j % 6, a = blk >> 2, c = blk & 3;
