@@ -1398,8 +1398,10 @@ __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt
 
   const int b = blockIdx.x;
   const int q8 = total_wg / 8, r8 = total_wg % 8, x8 = b % 8;
-  const int wg = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
-  const int cl = wg / nwg, chunk = chunk0 + cl;
+  // XCD-aware remap (each XCD a contiguous range of chunks); chunk0 < 0 (A/B
+  // only): dispatch order, the eight XCDs on neighbouring tiles of one chunk
+  const int wg = chunk0 < 0 ? b : (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + b / 8;
+  const int cl = wg / nwg, chunk = (chunk0 < 0 ? 0 : chunk0) + cl;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int bi = (wg - cl * nwg) * 4 + wave;
   // SYNC > 0: a workgroup barrier every SYNC stages keeps the four waves in
@@ -2240,6 +2242,8 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   if (ord && !strcmp(ord, "front")) order = 6;
   if (ord && !strcmp(ord, "sync4")) order = 7;
   if (ord && !strcmp(ord, "sync3")) order = 8;
+  const char* xr = getenv("OCM_GRAM8_XCD");  // "0": no XCD remap (A/B)
+  const bool no_remap = xr && !strcmp(xr, "0");
 #ifdef OCM_G8_LDS
   if (ord && !strcmp(ord, "lds")) order = 4;
   if (ord && !strcmp(ord, "lds32")) order = 5;
@@ -2303,7 +2307,7 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
 #define G8E_LAUNCH(A_, S_)                                                                                   \
   hipLaunchKernelGGL((k_gram8e<A_, S_>), dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, \
-                     nwg, nblocks, pg, (int)c0)
+                     nwg, nblocks, pg, (no_remap && c0 == 0) ? -1 : (int)c0)
 #define G8E_LAUNCH3(A_, S_, F_)                                                                                      \
   hipLaunchKernelGGL((k_gram8e<A_, S_, F_>), dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles,         \
                      (int)total, nwg, nblocks, pg, (int)c0)

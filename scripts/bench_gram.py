@@ -8,7 +8,8 @@ of each mode against an fp64 Gram of a row sample.
 
 A third field sets OCM_GRAM8_ORDER for that variant (k_gram8e block order),
 a fourth OCM_GRAM8_PIECES (quantiser / Gram overlap), a fifth OCM_Q8_CG
-(column groups per quantiser row block on consecutive workgroups).  "wall" is the whole
+(column groups per quantiser row block on consecutive workgroups), a sixth
+OCM_GRAM8_XCD (0: no XCD remap of the Gram workgroups).  "wall" is the whole
 call (guard, quantiser, Gram, reduce) between two device synchronisations.
 """
 import argparse
@@ -47,16 +48,17 @@ def main():
     ctx = Context.get(0)
     import time
 
-    variants = [tuple(v.split(":")[:2]) + tuple((v.split(":") + ["", "", ""])[2:5]) for v in args.variants.split(",")]
-    variants = [(m, int(c), o, pc, cg) for m, c, o, pc, cg in variants]
+    variants = [tuple(v.split(":")[:2]) + tuple((v.split(":") + ["", "", "", ""])[2:6]) for v in args.variants.split(",")]
+    variants = [(m, int(c), o, pc, cg, xr) for m, c, o, pc, cg, xr in variants]
     res = {":".join(map(str, v)): [] for v in variants}
     wall = {k: [] for k in res}
     quant = {k: [] for k in res}
     flop = args.rows * args.p * (args.p + 1)
     for _ in range(args.rounds):
-        for mode, chunk, order, pcs, qcg in variants:
-            key = ":".join(map(str, (mode, chunk, order, pcs, qcg)))
-            for var, val in (("OCM_GRAM8_ORDER", order), ("OCM_GRAM8_PIECES", pcs), ("OCM_Q8_CG", qcg)):
+        for mode, chunk, order, pcs, qcg, xr in variants:
+            key = ":".join(map(str, (mode, chunk, order, pcs, qcg, xr)))
+            for var, val in (("OCM_GRAM8_ORDER", order), ("OCM_GRAM8_PIECES", pcs), ("OCM_Q8_CG", qcg),
+                             ("OCM_GRAM8_XCD", xr)):
                 if val:
                     os.environ[var] = val
                 else:
@@ -83,6 +85,7 @@ def main():
     os.environ.pop("OCM_GRAM8_ORDER", None)
     os.environ.pop("OCM_GRAM8_PIECES", None)
     os.environ.pop("OCM_Q8_CG", None)
+    os.environ.pop("OCM_GRAM8_XCD", None)
     for mode in sorted({v[0] for v in variants}):
         Gm, _ = engine.gram(X, None, [0, ns], shift, mode=mode)
         err = ((Gm[0] - Gref).abs().max() / Gref.abs().max()).item()

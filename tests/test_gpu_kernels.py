@@ -312,7 +312,7 @@ def test_gram_i8_digit_split_edge_cases(eng, n, p):
 
 @pytest.mark.parametrize("env", [{}, {"OCM_GRAM8_ORDER": "packed"}, {"OCM_GRAM8_ORDER": "sync1"}, {"OCM_GRAM8_ORDER": "front"},
                                  {"OCM_GRAM8_PIECES": "3"}, {"OCM_GRAM8_PIECES": "1"},
-                                 {"OCM_Q8_CG": "4"}, {"OCM_Q8_CG": "2"}])
+                                 {"OCM_Q8_CG": "4"}, {"OCM_Q8_CG": "2"}, {"OCM_GRAM8_XCD": "0"}])
 @pytest.mark.parametrize("n,p,chunk", [(20000, 2048, 0), (9000, 257, 512), (5000, 300, 4608)])
 def test_gram_i8_kernels_bit_identical(eng, n, p, chunk, env, monkeypatch):
     """k_gram8e (16x16x64: the default launch, the OCM_GRAM8_ORDER variants,
