@@ -206,8 +206,8 @@ __global__ __launch_bounds__(256) void k_score_f64(const double* __restrict__ X,
                                                    const double* __restrict__ P, const double* __restrict__ mu,
                                                    const double* __restrict__ a_diag, int kb,
                                                    double* __restrict__ T_out, int64_t ldt,
-                                                   const double* __restrict__ T2_in, const double* __restrict__ TT_in,
-                                                   double* __restrict__ T2_out, double* __restrict__ TT_out,
+                                                   const double* T2_in, const double* TT_in,  // alias T2_out / TT_out
+                                                   double* T2_out, double* TT_out,
                                                    double* __restrict__ Q_out, DecF64 dec,
                                                    double* __restrict__ acc_out, int64_t acc_stride,
                                                    double* __restrict__ stat_part) {

@@ -2231,11 +2231,17 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   OCM_HIP(hipStreamIsCapturing(st, &cap));
   const bool capturing = cap != hipStreamCaptureStatusNone;
   // k_gram8e's block order and wave sync: tile-aligned workgroups with a
-  // barrier every two stages (default: 437 TF against 417 for the packed
-  // walk without barriers, r03s); OCM_GRAM8_ORDER = packed | aligned | sync1
-  // picks the others for kernel A/B (same result bits)
-  const char* ord = getenv("OCM_GRAM8_ORDER");
+  // barrier every two stages (437 TF against 417 for the packed walk without
+  // barriers, r03s).  The product library launches only that variant; the
+  // A/B selectors (OCM_GRAM8_ORDER = packed | aligned | sync1 | front | sync4
+  // | sync3, OCM_GRAM8_XCD, OCM_GRAM8_PIECES, OCM_Q8_CG) exist only in
+  // `make exp` builds (OCM_EXP_SELECTORS), which the product never loads.
   int order = 3;
+  bool no_remap = false;
+  int pieces = 1;
+  int qcg = 1;  // column groups per quantiser workgroup
+#ifdef OCM_EXP_SELECTORS
+  const char* ord = getenv("OCM_GRAM8_ORDER");
   if (ord && !strcmp(ord, "packed")) order = 0;
   if (ord && !strcmp(ord, "aligned")) order = 1;
   if (ord && !strcmp(ord, "sync1")) order = 2;
@@ -2243,18 +2249,17 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   if (ord && !strcmp(ord, "sync4")) order = 7;
   if (ord && !strcmp(ord, "sync3")) order = 8;
   const char* xr = getenv("OCM_GRAM8_XCD");  // "0": no XCD remap (A/B)
-  const bool no_remap = xr && !strcmp(xr, "0");
+  no_remap = xr && !strcmp(xr, "0");
 #ifdef OCM_G8_LDS
   if (ord && !strcmp(ord, "lds")) order = 4;
   if (ord && !strcmp(ord, "lds32")) order = 5;
 #endif
-  // Quantiser / Gram overlap: the chunks are cut into `pieces` ranges; the
-  // quantiser (HBM-bound) of range i+1 runs on a side stream while the Gram
-  // (bound by the L2 → CU operand path) of range i runs on the launch stream.
-  // OCM_GRAM8_PIECES overrides the count (1 = no overlap); never while the
-  // stream is being captured.
-  int pieces = 1;
+  // Quantiser / Gram overlap (measured: no gain): the chunks are
+  // cut into `pieces` ranges; the quantiser of range i+1 runs on a side stream
+  // while the Gram of range i runs on the launch stream.
   if (const char* pv = getenv("OCM_GRAM8_PIECES")) pieces = std::max(1, atoi(pv));
+  if (const char* qv = getenv("OCM_Q8_CG")) qcg = atoi(qv);
+#endif
   if (capturing || k32 || tabs.size() != 1) pieces = 1;
   if (pieces > 1) {
     const int64_t gch = cprefix[tab_s0[0] + tabs[0].nseg] - cprefix[tab_s0[0]];
@@ -2262,8 +2267,6 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     if (pieces < 2) pieces = 1;
   }
   hipStream_t qs = st;  // the quantiser's stream
-  int qcg = 1;          // OCM_Q8_CG = 2 | 4: column groups per quantiser workgroup (A/B; contiguous rows only)
-  if (const char* qv = getenv("OCM_Q8_CG")) qcg = atoi(qv);
   if (rows || (qcg != 2 && qcg != 4)) qcg = 1;
   std::vector<hipEvent_t> qev;
   if (pieces > 1) {
@@ -2289,12 +2292,14 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     if (rows)
       hipLaunchKernelGGL(k_q8_quant<true>, gq, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g,
                          (int)(c0 * nblk));
+#ifdef OCM_EXP_SELECTORS
     else if (cgw == 4)
       hipLaunchKernelGGL((k_q8_quant<false, 4>), gq, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g,
                          (int)(c0 * nblk));
     else if (cgw == 2)
       hipLaunchKernelGGL((k_q8_quant<false, 2>), gq, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g,
                          (int)(c0 * nblk));
+#endif
     else
       hipLaunchKernelGGL(k_q8_quant<false>, gq, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g,
                          (int)(c0 * nblk));
@@ -2311,13 +2316,15 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
 #define G8E_LAUNCH3(A_, S_, F_)                                                                                      \
   hipLaunchKernelGGL((k_gram8e<A_, S_, F_>), dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles,         \
                      (int)total, nwg, nblocks, pg, (int)c0)
-    if (!k32 && order == 0) G8E_LAUNCH(false, 0);
+    if (!k32 && order == 3) G8E_LAUNCH(true, 2);
+#ifdef OCM_EXP_SELECTORS
+    else if (!k32 && order == 0) G8E_LAUNCH(false, 0);
     else if (!k32 && order == 1) G8E_LAUNCH(true, 0);
     else if (!k32 && order == 2) G8E_LAUNCH(true, 1);
-    else if (!k32 && order == 3) G8E_LAUNCH(true, 2);
     else if (!k32 && order == 6) G8E_LAUNCH3(true, 2, true);
     else if (!k32 && order == 7) G8E_LAUNCH(true, 4);
     else if (!k32 && order == 8) G8E_LAUNCH(true, 3);
+#endif
 #undef G8E_LAUNCH
 #undef G8E_LAUNCH3
 #ifdef OCM_G8_LDS

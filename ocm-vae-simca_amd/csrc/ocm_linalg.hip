@@ -1228,9 +1228,15 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   const size_t pb = (size_t)p * b, bb = (size_t)b * b;
   const int nblk = (p + 63) / 64;
   const size_t def_blocks = (size_t)((p + DT - 1) / DT) * ((p + DT - 1) / DT);  // deflate GEMM tiles
-  // the trace GEMM's K split (the trace is linear in the K segments); OCM_TRACE_KSPLIT overrides it (A/B)
+  // the trace GEMM's K split (the trace is linear in the K segments; the
+  // split fixes the fp64 summation order, so the product library never
+  // changes it — `make exp` builds read OCM_TRACE_KSPLIT for A/B)
+#ifdef OCM_EXP_SELECTORS
   static const int trace_ks_env = getenv("OCM_TRACE_KSPLIT") ? atoi(getenv("OCM_TRACE_KSPLIT")) : 0;
   const int TRACE_KSPLIT = trace_ks_env >= 1 && trace_ks_env <= 16 ? trace_ks_env : 4;
+#else
+  constexpr int TRACE_KSPLIT = 4;
+#endif
   const size_t trace_wgs = (size_t)TRACE_KSPLIT * ((p + DT - 1) / DT) * ((p + DT - 1) / DT);
   const size_t plane_cap = std::max((size_t)ksplit * pb, wide ? 16 * bb : 0);
   size_t need = (6 * pb + 6 * bb + plane_cap + (wide ? 0 : (size_t)nblk * bb) + 4 * b + 64) * sizeof(double);

@@ -40,10 +40,10 @@ template <int KT, int NW>
 __device__ __forceinline__ void score_epilogue(double* tls, double* sred, const double (&accT64)[KT][16], double q64,
                                                int64_t row0, int64_t m, int k, int a_diag,
                                                const double* __restrict__ A, float* __restrict__ T_out,
-                                               double* __restrict__ T2_out, float* __restrict__ Q_out, DecArgs dec,
+                                               double* T2_out, float* __restrict__ Q_out, DecArgs dec,
                                                double* __restrict__ acc_out, int64_t acc_stride,
                                                double* __restrict__ stat_part, int ldt = 0,
-                                               const double* __restrict__ T2_in = nullptr) {
+                                               const double* T2_in = nullptr) {
   constexpr int KP = KT * 32;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l31 = lane & 31, h = lane >> 5;
@@ -117,15 +117,18 @@ __device__ __forceinline__ void score_epilogue(double* tls, double* sred, const 
 constexpr int PB = 256;  // columns per LDS loadings block
 
 template <int KT, bool VEC>
-__global__ __launch_bounds__(256, 2) void k_score_direct(const float* __restrict__ X, int64_t ldx,
+// X and R_out (and T2_in / T2_out) alias for the component blocks after the
+// first (k > 64: the residual is projected in place), so they carry no
+// __restrict__
+__global__ __launch_bounds__(256, 2) void k_score_direct(const float* X, int64_t ldx,
                                                          const int64_t* __restrict__ rows, int64_t m, int p,
                                                          const float* __restrict__ P, const float* __restrict__ mu,
                                                          const double* __restrict__ A, int k, int a_diag,
-                                                         float* __restrict__ T_out, double* __restrict__ T2_out,
+                                                         float* __restrict__ T_out, double* T2_out,
                                                          float* __restrict__ Q_out, DecArgs dec,
                                                          double* __restrict__ acc_out, int64_t acc_stride,
                                                          double* __restrict__ stat_part, int ldt,
-                                                         const double* __restrict__ T2_in, float* __restrict__ R_out,
+                                                         const double* T2_in, float* R_out,
                                                          int64_t ldr) {
   constexpr int KP = KT * 32;
   constexpr int PS = PB + 4;  // padded LDS row: conflict-free ds_read_b128 across comps

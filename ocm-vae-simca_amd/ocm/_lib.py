@@ -15,6 +15,13 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OCM_LIB", os.path.join(_HERE, "libocm.so"))
+# `make exp` builds (csrc/build/exp/) carry diagnostic variants, some of which
+# give wrong results on purpose (load-path ablations): they are loaded only
+# when the A/B scripts ask for it explicitly
+if os.sep + os.path.join("build", "exp") + os.sep in os.path.abspath(LIB_PATH) and \
+        os.environ.get("OCM_ALLOW_EXP_LIB") != "1":
+    raise ImportError(f"OCM_LIB={LIB_PATH} is a `make exp` diagnostic build; set OCM_ALLOW_EXP_LIB=1 to load it "
+                      "(A/B scripts only, never the product path)")
 
 OCM_OK = 0
 OCM_ERR_ARG = -1

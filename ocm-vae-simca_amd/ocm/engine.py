@@ -456,6 +456,21 @@ def _mark(name: str):
         _phase_timer.mark(name)
 
 
+def common_shift(X: torch.Tensor, rows: torch.Tensor | None, n: int, allreduce) -> torch.Tensor:
+    """The Gram shift every rank of a sharded fit uses (f32): the mean of the
+    ranks' sample means (ranks without rows do not count), one all-reduce of
+    p + 1 doubles.  One shift for all ranks means the summed moments stay
+    centred to O(σ) and C is formed as (G − c cᵀ/n)/(n − 1) about it, never
+    as (M − n μμᵀ)/(n − 1) about zero (which would cancel |μ|²/λ_tail)."""
+    p = X.shape[1]
+    buf = torch.zeros(p + 1, dtype=torch.float64, device=X.device)
+    if n > 0:
+        buf[:p] = colmean(X, rows, max(1, min(n, SHIFT_SAMPLE)))
+        buf[p] = 1.0
+    allreduce([buf])
+    return cast_f32(buf[:p] / buf[p].clamp_min(1.0))
+
+
 def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_mode: int,
               want_T=True, keep_C=False, shift32: torch.Tensor | None = None, allreduce=None,
               need_stats=True) -> ClassFit:
@@ -463,15 +478,18 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
 
     ``allreduce`` (optional callable on a list of device tensors, with the
     rank / world size as attributes) marks a class whose rows are sharded
-    over GPUs: each rank's Gram is taken about its own sample
-    shift, packed as moments about zero (``ocm_gram_pack``) and summed in ONE
-    all-reduce; the θ3 trace work is split over the ranks and its partials
-    summed; the fit-set moments are all-reduced only when ``need_stats``."""
+    over GPUs: every rank's Gram is taken about one common
+    shift (``common_shift``), packed as its upper triangle (``ocm_gram_pack``
+    about a zero shift) and summed in ONE all-reduce; the θ3 trace work is
+    split over the ranks and its partials summed; the fit-set moments are
+    all-reduced only when ``need_stats``."""
     p = X.shape[1]
     if k > p or k < 1:
         raise ValueError(f"n_components={k} must be in [1, {p}]")
     _mark("start")
-    if shift32 is None:
+    if shift32 is None and allreduce is not None:
+        shift32 = common_shift(X, rows, n, allreduce)
+    elif shift32 is None:
         shift64 = colmean(X, rows, max(1, min(n, SHIFT_SAMPLE))) if n > 0 else torch.zeros(p, dtype=torch.float64,
                                                                                           device=X.device)
         shift32 = cast_f32(shift64)
@@ -487,16 +505,18 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
         del G
         _mark("cov")
     else:
+        zero32 = torch.zeros(p, dtype=torch.float32, device=X.device)
         if n > 0:
             G, cs = gram(X, rows, [0, n], shift32)
-            packed = gram_pack(G[0], cs[0], shift32, n)
+            packed = gram_pack(G[0], cs[0], zero32, n)  # moments of y = x − shift
             del G, cs
         else:  # a rank without rows contributes zeros
             packed = torch.zeros(p * (p + 1) // 2 + p + 1, dtype=torch.float64, device=X.device)
         _mark("gram")
         allreduce([packed])
         _mark("allreduce")
-        C, mean64 = cov_from_packed(packed, p)
+        C, d = cov_from_packed(packed, p)
+        mean64 = d + shift32.to(torch.float64)
         _mark("cov")
         slice_ = (allreduce.rank, allreduce.world)
         n_total = None
@@ -526,10 +546,11 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
         copied.record(side)
     if n > 0:
         sc = score(X, rows, n, evecs, mean64, inv, want_T=want_T, want_stats=True)
-    else:
-        sc = {"T": torch.empty((0, k), dtype=torch.float32, device=X.device) if want_T else None,
+    else:  # T and Q in the dtype the other ranks' scoring produces (utils/SIMCA.py:65-71)
+        vdt = torch.float64 if X.dtype == torch.float64 else torch.float32
+        sc = {"T": torch.empty((0, k), dtype=vdt, device=X.device) if want_T else None,
               "T2": torch.empty(0, dtype=torch.float64, device=X.device),
-              "Q": torch.empty(0, dtype=torch.float32, device=X.device),
+              "Q": torch.empty(0, dtype=vdt, device=X.device),
               "stats": torch.zeros(4, dtype=torch.float64, device=X.device)}
     _mark("fit_score")
     copied.synchronize()

@@ -75,10 +75,10 @@ def _world(group) -> int:
 
 def _latent_cov(Z: torch.Tensor, group=None):
     """Column mean (f64) and covariance (f64, ddof 1) of latent rows on the GPU
-    — of every rank's rows when ``group`` spans several ranks: each rank's Gram
-    about its own sample shift, packed as moments about zero
-    (``ocm_gram_pack``) and summed in one all-reduce; a rank without rows
-    contributes zeros (nothing of it enters the mean or the shift)."""
+    — of every rank's rows when ``group`` spans several ranks: every rank's
+    Gram about one common shift (``engine.common_shift``), packed as its upper
+    triangle (``ocm_gram_pack``) and summed in one all-reduce; a rank without
+    rows contributes zeros (nothing of it enters the mean or the shift)."""
     n, d = Z.shape
     if _world(group) == 1:
         shift32 = engine.cast_f32(engine.colmean(Z, None, min(n, engine.SHIFT_SAMPLE)))
@@ -87,15 +87,19 @@ def _latent_cov(Z: torch.Tensor, group=None):
         return mean, C
     import torch.distributed as dist
 
+    def allreduce(ts):
+        for t in ts:
+            dist.all_reduce(t, group=group)
+
+    shift32 = engine.common_shift(Z, None, n, allreduce)
     if n > 0:
-        shift32 = engine.cast_f32(engine.colmean(Z, None, min(n, engine.SHIFT_SAMPLE)))
         G, cs = engine.gram(Z, None, [0, n], shift32)
-        packed = engine.gram_pack(G[0], cs[0], shift32, n)
+        packed = engine.gram_pack(G[0], cs[0], torch.zeros_like(shift32), n)
     else:
         packed = torch.zeros(d * (d + 1) // 2 + d + 1, dtype=torch.float64, device=Z.device)
     dist.all_reduce(packed, group=group)
-    C, mean = engine.cov_from_packed(packed, d)
-    return mean, C
+    C, dvec = engine.cov_from_packed(packed, d)
+    return dvec + shift32.to(torch.float64), C
 
 
 def latent_T2(Z: torch.Tensor, mean64: torch.Tensor, A: torch.Tensor) -> torch.Tensor:

@@ -9,7 +9,7 @@ O=gpurun_out/${TAG:-gram}; mkdir -p "$O"
 for L in ${LIBS:-product}; do
 for V in ${VARIANTS:-i8x3:0}; do
   N=${L}_$(echo "$V" | tr ':' '_')
-  if [ "$L" = product ]; then unset OCM_LIB; else export OCM_LIB=$PWD/ocm-vae-simca_amd/csrc/build/exp/libocm_$L.so; fi
+  if [ "$L" = product ]; then unset OCM_LIB; else export OCM_ALLOW_EXP_LIB=1 OCM_LIB=$PWD/ocm-vae-simca_amd/csrc/build/exp/libocm_$L.so; fi
   echo "== $N"
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$O/$N" -o p --output-format csv \
     -- python3 scripts/bench_gram.py --variants "$V" --rounds 2 > "$O/$N.log" 2>&1 || { echo "variant $V failed"; exit 1; }

@@ -11,7 +11,7 @@ tail -3 "$O/test.log"
 timeout -k 10 300 python3 -u scripts/bench_score.py --k ${KS:-16,20} --reps 10 --kernels diag > "$O/score.log" 2>&1 || exit 2
 grep '^{' "$O/score.log"
 if [ -f ocm-vae-simca_amd/csrc/build/exp/libocm_stamps.so ]; then
-  OCM_STAMPS=1 OCM_LIB=$PWD/ocm-vae-simca_amd/csrc/build/exp/libocm_stamps.so timeout -k 10 200 python3 scripts/bench_score.py \
+  OCM_STAMPS=1 OCM_ALLOW_EXP_LIB=1 OCM_LIB=$PWD/ocm-vae-simca_amd/csrc/build/exp/libocm_stamps.so timeout -k 10 200 python3 scripts/bench_score.py \
     --k ${KS:-16,20} --kernels diag --reps 3 --tag stamps > "$O/stamps.log" 2>&1 || exit 3
   grep '^{' "$O/stamps.log"
 fi

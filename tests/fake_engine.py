@@ -247,10 +247,23 @@ def invcov_from_evals(evals, rcond=1e-15):
     return torch.diag(torch.where(lam.abs() > cut, 1.0 / lam, torch.zeros_like(lam)))
 
 
+def common_shift(X, rows, n, allreduce):
+    """ocm.engine.common_shift: the mean of the ranks' sample means."""
+    p = X.shape[1]
+    buf = torch.zeros(p + 1, dtype=torch.float64)
+    if n > 0:
+        buf[:p] = colmean(X, rows, max(1, min(n, SHIFT_SAMPLE)))
+        buf[p] = 1.0
+    allreduce([buf])
+    return cast_f32(buf[:p] / buf[p].clamp_min(1.0))
+
+
 def fit_class(X, rows, n, k, theta_mode, want_T=True, keep_C=False, shift32=None, allreduce=None, need_stats=True):
     """Same control flow and collectives as ocm.engine.fit_class."""
     p = X.shape[1]
-    if shift32 is None:
+    if shift32 is None and allreduce is not None:
+        shift32 = common_shift(X, rows, n, allreduce)
+    elif shift32 is None:
         shift32 = cast_f32(colmean(X, rows, min(n, SHIFT_SAMPLE)))
     slice_ = (0, 1)
     if allreduce is None:
@@ -259,9 +272,10 @@ def fit_class(X, rows, n, k, theta_mode, want_T=True, keep_C=False, shift32=None
         C, mean64 = cov_from_gram([(1.0, G[0], cs[0])], shift32, n_total)
     else:
         G, cs = gram(X, rows, [0, n], shift32)
-        packed = gram_pack(G[0], cs[0], shift32, n)
+        packed = gram_pack(G[0], cs[0], torch.zeros_like(shift32), n)
         allreduce([packed])
-        C, mean64 = cov_from_packed(packed, p)
+        C, d = cov_from_packed(packed, p)
+        mean64 = d + shift32.to(torch.float64)
         slice_ = (allreduce.rank, allreduce.world)
         n_total = int(round(float(packed[-1])))
     evals, evecs, theta, iters = eig_topk(C, k, theta_mode, theta3_slice=slice_)

@@ -310,18 +310,12 @@ def test_gram_i8_digit_split_edge_cases(eng, n, p):
     np.testing.assert_allclose(cs[0].cpu().numpy(), Y.sum(0), rtol=1e-6, atol=1e-6 * np.abs(Y).sum(0).max())
 
 
-@pytest.mark.parametrize("env", [{}, {"OCM_GRAM8_ORDER": "packed"}, {"OCM_GRAM8_ORDER": "sync1"}, {"OCM_GRAM8_ORDER": "front"},
-                                 {"OCM_GRAM8_PIECES": "3"}, {"OCM_GRAM8_PIECES": "1"},
-                                 {"OCM_Q8_CG": "4"}, {"OCM_Q8_CG": "2"}, {"OCM_GRAM8_XCD": "0"}])
 @pytest.mark.parametrize("n,p,chunk", [(20000, 2048, 0), (9000, 257, 512), (5000, 300, 4608)])
-def test_gram_i8_kernels_bit_identical(eng, n, p, chunk, env, monkeypatch):
-    """k_gram8e (16x16x64: the default launch, the OCM_GRAM8_ORDER variants,
-    the quantiser / Gram overlap in pieces or none) and k_gram8d (32x32x32)
-    sum the same exact int32 digit products and flush them to f32 in the same
-    order: the Grams are bit for bit equal, with segments, a gather list and
-    outlier rows."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+def test_gram_i8_kernels_bit_identical(eng, n, p, chunk):
+    """k_gram8e (16x16x64, the default launch) and k_gram8d (32x32x32) sum the
+    same exact int32 digit products and flush them to f32 in the same order:
+    the Grams are bit for bit equal, with segments, a gather list and outlier
+    rows.  (The A/B launch variants of k_gram8e live in `make exp` builds only.)"""
     import torch
 
     rng = np.random.default_rng(p + n)

@@ -8,8 +8,9 @@ p = 2048 wavelengths, k = 20 components, default i8×3 Gram.
 * on outlier-bearing data (0.5–1 % of rows scaled ×100–×1000, spread over the
   1536-row scale blocks) against the fp64 oracle: the i8×3 outlier guard must
   keep θ-based (jm) and F limits and the decisions;
-* float64 input: the drop-in computes in float32 on the GPU
-  (documented downcast) and is compared with the reference's float64 run.
+* float64 input: the drop-in computes in float64 on the GPU (fp64-MFMA Gram,
+  fp64 scoring, as sklearn's PCA follows the input dtype) and is compared
+  with the reference's float64 run.
 
 Tolerances: T², Q rtol 1e-4 with an absolute floor of
 1e-5·median; limits rtol 1e-5 (percentile / moment limits 1e-4); decisions
@@ -108,9 +109,9 @@ def test_theta_tail_sums_at_north_star(golden_dir):
 
 
 def test_float64_input_vs_reference(golden_dir):
-    """float64 X.  The reference then runs its PCA in float64; the
-    drop-in downcasts to float32 on the GPU — limits, T²/Q and
-    decisions still agree at the stated tolerances."""
+    """float64 X.  The reference then runs its PCA in float64, and so does the
+    drop-in (k_gram_f64 + k_score_f64, T and Q returned as float64): limits,
+    T²/Q and decisions agree at the stated tolerances."""
     g = _load(golden_dir, "simca_f64.npz")
     X_fit, X_test, k = _regen(g)
     assert X_fit.dtype == np.float64
