@@ -75,6 +75,7 @@ def parse(argv=None):
     ap.add_argument("--no-vae", action="store_true", help="skip the secondary VAE train-steps/s measurement")
     ap.add_argument("--vae-steps", type=int, default=200)
     ap.add_argument("--no-cv", action="store_true", help="skip the C3 10-fold CV line")
+    ap.add_argument("--no-prep", action="store_true", help="skip the preprocessing + fit + score extra line")
     ap.add_argument("--cv-reps", type=int, default=3)
     ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling extra run")
     ap.add_argument("--phase-steps", type=int, default=3, help="untimed steps with per-phase events (0 = off)")
@@ -362,6 +363,56 @@ def run_simca(args, rk, n_total):
     return out
 
 
+def run_prep(args, rk, n_total):
+    """the drivers' preprocessing before SIMCA, two ways, on
+    the same raw rows: the eager pass (``snv_savgol``: X′ written to HBM) then
+    fit + predict on X′, against the lazy view (``lazy=True``: the transform
+    runs in the Gram quantiser's and the scoring kernel's load paths, X′ never
+    exists).  Settings: simca_nuts.py:47-52 (SNV, w 5, p 2, deriv 1) and
+    simca_new_cheese.py:37-39 (w 15, p 2, deriv 1, no SNV)."""
+    import torch
+
+    from ocm import _lib, preprocess
+    from ocm.prepview import materialised_count
+    from ocm.synth import shard_bounds, spectra_shard
+    from utils import SIMCA
+
+    p, k = args.p, args.k
+    lo, hi = shard_bounds(n_total, rk.rank, rk.world)
+    X = spectra_shard(n_total, p, rk.rank, rk.world, rk.device, seed=DATA_SEED, k=k)
+    y = torch.zeros(hi - lo, dtype=torch.int64, device=rk.device)
+    ctx = _lib.Context.get(rk.device.index)
+    out = {"metric": "spectra/s, preprocessing + SIMCA fit + predict", "rows": n_total, "p": p, "k": k}
+    for name, (snv, w) in {"nuts_snv_sg5_d1": (True, 5), "cheese_sg15_d1": (False, 15)}.items():
+        res = {}
+        for mode in ("materialised", "fused"):
+            def step():
+                Xp = preprocess.snv_savgol(X, w, 2, 1, 1.0, snv=snv, lazy=(mode == "fused"))
+                model = SIMCA(n_components=k, model_class=0, type="alt", t2lim="Fdist", qlim="jm", verbose=False)
+                model.fit(Xp, y)
+                return model.predict(Xp)
+
+            step()
+            c0 = materialised_count(rk.device.index)
+            for kid in range(3):
+                ctx.read_timing(kid)
+            ctx.set_timing(True)
+            dt = _timed(rk, step, args.steps, 0)
+            ctx.set_timing(False)
+            t = {nm: ctx.read_timing(kid) for kid, nm in enumerate(("gram", "score", "quant"))}
+            res[mode] = {"ms_per_step": round(dt / args.steps * 1e3, 3),
+                         "value": round(n_total * args.steps / dt, 1),
+                         "quantise_ms": round(t["quant"][0] / max(t["quant"][1], 1), 4),
+                         "score_ms": round(t["score"][0] / max(t["score"][1], 1), 4),
+                         "gram_ms": round(t["gram"][0] / max(t["gram"][1], 1), 4)}
+            if mode == "fused":
+                res[mode]["materialised_views"] = materialised_count(rk.device.index) - c0
+        out[name] = res
+    del X, y
+    torch.cuda.empty_cache()
+    return out
+
+
 def run_cv(args, rk, n_total, folds=10, lv=20):
     """C3: class-wise 10-fold CV (ClasswiseKFoldWithExternalVal(10, cls_label=0),
     utils/CVSIMCA.py:54-80) of n_total spectra, every 10th row another class
@@ -511,6 +562,11 @@ def main():
         out["weak"] = {"scaling": "weak", "rows_per_gpu": weak["n_local"], "rows_total": args.rows * rk.world,
                        "value": round(args.rows * rk.world * args.steps / weak["seconds"], 1), "unit": "spectra/s",
                        "ms_per_step": round(weak["seconds"] / args.steps * 1e3, 3)}
+    if rk.world == 1 and not args.no_prep:
+        try:
+            out["prep_fit_score"] = run_prep(args, rk, args.rows)
+        except Exception as e:  # report, never fail the primary number
+            out["prep_fit_score"] = {"error": repr(e)}
     if not args.no_cv:
         try:
             out["cv"] = run_cv(args, rk, args.rows if args.scaling == "strong" else args.rows * rk.world)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCM_ABI_VERSION 6
+#define OCM_ABI_VERSION 7
 
 #define OCM_OK 0
 #define OCM_ERR_ARG (-1)         /* invalid argument (maps to ValueError) */
@@ -311,6 +311,63 @@ int ocm_confusion_counts(ocm_ctx* ctx, const double* accept, int64_t m, int64_t 
  * float32 (ldx, ldo; out may not alias X).  window odd ≤ 63, p ≤ 12288. */
 int ocm_snv_savgol_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, int32_t p, int32_t snv,
                        int32_t window, const double* taps, float* out, int64_t ldo, void* stream);
+
+/* ---- preprocessing in the load path (lazy view) ----
+ * The drivers run SNV then Savitzky–Golay right before SIMCA
+ * (simca_nuts.py:47-52, simca_new_cheese.py:37-38, utils/data_utils.py:57-61).
+ * An ocm_prep describes that transform and the *_prep kernels apply it to each
+ * row as they load it, so the preprocessed matrix X′ never exists in HBM.
+ * Row r, column j, float32 arithmetic identical in every kernel (the Gram,
+ * the scores and ocm_prep_apply_f32 see bit-identical values):
+ *   u_c = x_c − m_r when snv and deriv == 0, else u_c = x_c
+ *   window == 0:                 a = u_j
+ *   interior, odd deriv:         a = Σ_{t=1..H} c_{H+t}·(u_{j+t} − u_{j−t})   (c antisymmetric)
+ *   interior, deriv 0:           a = c_H·u_j + Σ_{t=1..H} c_{H+t}·(u_{j+t} + u_{j−t})
+ *   interior, even deriv ≥ 2:    a = Σ_{t=1..H} c_{H+t}·((u_{j+t} − u_j) + (u_{j−t} − u_j))
+ *   edges (j < H or j ≥ p − H):  a = Σ_t e_{j,t}·(u_{s+t} − [deriv ≥ 1]·u_j), s = 0 or p − window
+ *   y_j = a·s_r when snv, else a
+ * (fmaf chains in t order from 0; H = window/2; (m_r, s_r) = (mean_r,
+ * 1/(std_r + 1e-8)) from ocm_prep_rowstats_f32).  Savitzky–Golay maps a
+ * constant to 0 for deriv ≥ 1 and to itself for deriv 0, so y = SG(SNV(x))
+ * up to float32 rounding, with the row mean cancelling exactly in the
+ * drivers' deriv-1 filters; differences of neighbouring samples keep a large
+ * baseline from costing precision. */
+typedef struct ocm_prep {
+  int32_t window;        /* 0 (SNV only) or odd 3..31 */
+  int32_t deriv;         /* Savitzky–Golay derivative order (0 when window == 0) */
+  int32_t snv;           /* 1: apply the SNV row statistics */
+  int32_t pad_;
+  const float* taps;     /* [dev] window + 2·H·window floats: interior c, left-edge rows, right-edge rows
+                            (ocm/preprocess.py savgol_taps); NULL when window == 0 */
+  const float* rowstat;  /* [dev] (m_r, s_r) per row of X, indexed like X (gather lists index it too);
+                            NULL when snv == 0 */
+} ocm_prep;
+
+/* rowstat_out [dev] m×2 floats: m_r = mean (fp64, rounded), s_r = 1/(std_r + 1e-8) (np.std ddof 0)
+ * of each row of X — the one read-only pre-pass the SNV needs. */
+int ocm_prep_rowstats_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, int32_t p, float* rowstat_out,
+                          void* stream);
+/* out [dev] m×p (ldo) = the preprocessed rows X[rows[i]] (rows nullable): the materialised view, for
+ * shapes and modes the fused kernels do not cover and for tests. */
+int ocm_prep_apply_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
+                       const ocm_prep* prep, float* out, int64_t ldo, void* stream);
+/* ocm_colmean_f32 / ocm_gram_f32_ex / ocm_score_f32_diag on the preprocessed rows, read raw from X.
+ * The default i8×3 Gram applies the transform in its quantiser (halo columns staged through LDS) and
+ * k_score_1p applies it to each row tile in registers as the tile arrives (p ∈ {256, 512, 1024, 2048},
+ * window ∈ {0, 5, 15}, p % 4 == 0); other shapes, windows and Gram modes materialise the preprocessed
+ * rows in a temporary device buffer first. */
+int ocm_colmean_f32_prep(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                         const ocm_prep* prep, double* mean_out, void* stream);
+int ocm_gram_f32_prep(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                      const float* shift, const int64_t* seg_offsets, int32_t nseg, int32_t mode,
+                      int64_t chunk_rows, const ocm_prep* prep, double* G_out, double* colsum_out, void* stream);
+/* Number of times this context materialised a lazy view (the fallback paths above), for tests and
+ * diagnostics: 0 after any call on the fused paths. */
+int ocm_prep_materialised(ocm_ctx* ctx, int64_t* count_out);
+int ocm_score_f32_diag_prep(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
+                            const ocm_prep* prep, const double* P, const double* mu, const double* a_diag, int32_t k,
+                            float* T_out, double* T2_out, float* Q_out, const ocm_decision* dec,
+                            double* accept_out, int64_t accept_stride, double* stats_out, void* stream);
 
 /* ---- float64 spectra: the PCA precision follows the input dtype ----
  * The reference's PCA runs in the input dtype (utils/SIMCA.py:64-66 →

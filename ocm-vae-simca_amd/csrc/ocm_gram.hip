@@ -24,6 +24,20 @@
 
 namespace {
 
+// One value of the (possibly preprocessed) row `r` of X: the sample kernels
+// (shift, outlier thresholds) and the exact fix-up read through this.
+__device__ __forceinline__ float load_y(const float* __restrict__ X, int64_t ldx, int64_t r, int col, int p,
+                                        const PrepArgs& pa) {
+  if (pa.w == 0 && !pa.snv) return X[r * ldx + col];
+  float m = 0.f, sc = 1.f;
+  if (pa.snv) {
+    m = pa.rowstat[2 * r];
+    sc = pa.rowstat[2 * r + 1];
+  }
+  return ocm::prep_elem(X + r * ldx, p, col, pa, m, sc);
+}
+
+
 constexpr int MAXSEG = 32;
 
 struct SegTable {
@@ -464,7 +478,7 @@ __global__ __launch_bounds__(256) void k_gram_reduce(const float* __restrict__ p
 
 // Column mean over n rows: per (column, row-split) f64 partial sums.
 __global__ void k_colsum_part(const float* __restrict__ X, int64_t ldx, const int64_t* __restrict__ rows, int64_t n,
-                              int p, int64_t rows_per_split, double* __restrict__ part) {
+                              int p, int64_t rows_per_split, double* __restrict__ part, PrepArgs pa = PrepArgs{}) {
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
   const int sp = blockIdx.y;
   if (col >= p) return;
@@ -473,7 +487,7 @@ __global__ void k_colsum_part(const float* __restrict__ X, int64_t ldx, const in
   double v = 0.0;
   for (int64_t r = a; r < e; ++r) {
     const int64_t sr = rows ? rows[r] : r;
-    v += (double)X[sr * ldx + col];
+    v += (double)load_y(X, ldx, sr, col, p, pa);
   }
   part[(size_t)sp * p + col] = v;
 }
@@ -690,11 +704,12 @@ __device__ __forceinline__ int q8_qslot(int P) { return P ^ ((P >> 3) & 7); }
 constexpr int Q8QC = 32;                   // columns per quantiser workgroup
 constexpr int Q8QS = Q8BLK / 16;           // 16-row slices per block (96)
 constexpr int Q8QT = Q8QS * (Q8QC / 4);    // threads (768)
-template <bool GATHER, int CG = 1>
-__global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ X, int64_t ldx,
-                                                      const int64_t* __restrict__ rows, int p,
-                                                      const float* __restrict__ shift, SegTable st, Q8Plan q,
-                                                      double* __restrict__ colblk, int cb0) {
+// The quantiser after the load: v = this thread's 16 rows × 4 columns of
+// y − shift.  Column sums, the outlier screen, the block scale, the digits
+// and their LDS-staged stores (shared by k_q8_quant and k_q8_quant_prep).
+__device__ __forceinline__ void q8_tail(f32x4 (&v)[16], int tid, int cq, int rs, int cg0, int c0, int64_t rb,
+                                        const Q8Plan& q, int chunk, int b, const SegTable& st,
+                                        double* __restrict__ colblk) {
   constexpr int QC = Q8QC;
   __shared__ __attribute__((aligned(16))) char stage[Q8SPB * QC * 32];  // one digit plane: 24 KiB
   __shared__ __attribute__((aligned(16))) float wmax[Q8QS][QC];
@@ -702,63 +717,6 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ 
   __shared__ float pmax[8][QC];
   __shared__ double psum[8][QC];
   __shared__ __attribute__((aligned(16))) float fmax_[QC];
-  // CG > 1 (A/B): CG neighbouring 32-column groups of one row block on
-  // consecutive workgroups (they run at the same time on other CUs), so each
-  // row's CG·128 bytes are read close in time
-  const int gbk = (int)(blockIdx.x / CG) + cb0;  // (chunk, block) of the call's chunk range
-  const int chunk = gbk / q.nblk, b = gbk - chunk * q.nblk;
-  const int tid = threadIdx.x;
-  const int cq = tid & 7, rs = tid >> 3;
-  int s = 0;
-  while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
-  const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
-  const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
-  // blocks past the chunk's rows are written too (zero digits, scale 1): the
-  // Gram kernels read whole blocks
-  const int64_t rb = r0 + (int64_t)b * Q8BLK + 16 * rs;
-  const int cg0 = (int)(blockIdx.y * CG + blockIdx.x % CG) * QC;  // first column of the workgroup
-  const int c0 = cg0 + 4 * cq;                                    // first of this thread's 4 columns
-  const bool vec = (ldx % 4 == 0) && (c0 + 3 < p) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
-  f32x4 sh;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) sh[e] = c0 + e < p ? shift[c0 + e] : 0.f;
-  f32x4 v[16];
-  const int64_t rblk = r0 + (int64_t)b * Q8BLK;  // first row of the block
-  if (!GATHER && vec && (int64_t)Q8BLK * ldx * 4 < (1LL << 31)) {
-    // contiguous rows: one buffer descriptor over the block's valid rows (one
-    // address VGPR instead of 16 64-bit row pointers).  The whole byte offset,
-    // row step included, goes in the VECTOR offset: only voffset is checked
-    // against the descriptor's size (the scalar offset is not), so rows past
-    // r1 — a block whose valid row count is not a multiple of 16 — read as 0
-    // instead of touching memory past the end of X.
-    const int64_t nvalid = max((int64_t)0, min(r1 - rblk, (int64_t)Q8BLK));
-    const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(X + rblk * ldx), 0, (uint32_t)(nvalid * ldx * 4), 0x00020000);
-    const int voff = (int)((16 * rs * ldx + c0) * 4);
-    const int rstep = (int)(ldx * 4);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_x, voff + j * rstep, 0, 0));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[j][e] = (rb + j < r1) ? x[e] - sh[e] : 0.f;
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int64_t g = rb + j;
-      const int64_t gc = g < r1 ? g : r1 - 1;  // clamped: always a valid row
-      const float* xr = X + (GATHER ? rows[gc] : gc) * ldx;
-      f32x4 x;
-      if (vec) {
-        x = *reinterpret_cast<const f32x4*>(xr + c0);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) x[e] = xr[min(c0 + e, p - 1)];
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[j][e] = (g < r1 && c0 + e < p) ? x[e] - sh[e] : 0.f;
-    }
-  }
   // column sums over every row (the fix-up does not touch them)
   double cs[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -882,6 +840,211 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ 
   }
 }
 
+template <bool GATHER, int CG = 1>
+__global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ X, int64_t ldx,
+                                                      const int64_t* __restrict__ rows, int p,
+                                                      const float* __restrict__ shift, SegTable st, Q8Plan q,
+                                                      double* __restrict__ colblk, int cb0) {
+  constexpr int QC = Q8QC;
+  // CG > 1 (A/B): CG neighbouring 32-column groups of one row block on
+  // consecutive workgroups (they run at the same time on other CUs), so each
+  // row's CG·128 bytes are read close in time
+  const int gbk = (int)(blockIdx.x / CG) + cb0;  // (chunk, block) of the call's chunk range
+  const int chunk = gbk / q.nblk, b = gbk - chunk * q.nblk;
+  const int tid = threadIdx.x;
+  const int cq = tid & 7, rs = tid >> 3;
+  int s = 0;
+  while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
+  const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
+  const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
+  // blocks past the chunk's rows are written too (zero digits, scale 1): the
+  // Gram kernels read whole blocks
+  const int64_t rb = r0 + (int64_t)b * Q8BLK + 16 * rs;
+  const int cg0 = (int)(blockIdx.y * CG + blockIdx.x % CG) * QC;  // first column of the workgroup
+  const int c0 = cg0 + 4 * cq;                                    // first of this thread's 4 columns
+  const bool vec = (ldx % 4 == 0) && (c0 + 3 < p) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+  f32x4 sh;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sh[e] = c0 + e < p ? shift[c0 + e] : 0.f;
+  f32x4 v[16];
+  const int64_t rblk = r0 + (int64_t)b * Q8BLK;  // first row of the block
+  if (!GATHER && vec && (int64_t)Q8BLK * ldx * 4 < (1LL << 31)) {
+    // contiguous rows: one buffer descriptor over the block's valid rows (one
+    // address VGPR instead of 16 64-bit row pointers).  The whole byte offset,
+    // row step included, goes in the VECTOR offset: only voffset is checked
+    // against the descriptor's size (the scalar offset is not), so rows past
+    // r1 — a block whose valid row count is not a multiple of 16 — read as 0
+    // instead of touching memory past the end of X.
+    const int64_t nvalid = max((int64_t)0, min(r1 - rblk, (int64_t)Q8BLK));
+    const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(X + rblk * ldx), 0, (uint32_t)(nvalid * ldx * 4), 0x00020000);
+    const int voff = (int)((16 * rs * ldx + c0) * 4);
+    const int rstep = (int)(ldx * 4);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_x, voff + j * rstep, 0, 0));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = (rb + j < r1) ? x[e] - sh[e] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int64_t g = rb + j;
+      const int64_t gc = g < r1 ? g : r1 - 1;  // clamped: always a valid row
+      const float* xr = X + (GATHER ? rows[gc] : gc) * ldx;
+      f32x4 x;
+      if (vec) {
+        x = *reinterpret_cast<const f32x4*>(xr + c0);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = xr[min(c0 + e, p - 1)];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = (g < r1 && c0 + e < p) ? x[e] - sh[e] : 0.f;
+    }
+  }
+  q8_tail(v, tid, cq, rs, cg0, c0, rb, q, chunk, b, st, colblk);
+}
+
+// k_q8_quant with the preprocessing of a lazy view applied in the load path
+// (include/ocm.h ocm_prep; HH = window / 2 ∈ {0, 2, 7}).  Each thread loads
+// its raw quad of 16 rows as k_q8_quant does; lanes cq < HQ and cq ≥ 8 − HQ
+// also load the HQ = ⌈HH/4⌉ halo quads left / right of the workgroup's 32
+// columns.  Per row, the eight lanes of a row slice put their quads in a
+// wave-private LDS row image (columns cg0 − 8 .. cg0 + 39) and read back the
+// (4 + 2·HH)-sample window of their four outputs: the stencil runs on the
+// VALU under the HBM stream, the rows are read from HBM once.  Rows in
+// groups of four (raw quads and halos in flight per group) keep the VGPRs of
+// the 16 output quads plus one group's loads.
+constexpr int PQ_ROW = 48;  // floats per row image: 8 halo + 32 + 8 halo
+template <bool GATHER, int HH>
+__global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restrict__ X, int64_t ldx,
+                                                           const int64_t* __restrict__ rows, int p,
+                                                           const float* __restrict__ shift, SegTable st, Q8Plan q,
+                                                           double* __restrict__ colblk, int cb0, PrepArgs pa) {
+  constexpr int HQ = (HH + 3) / 4;
+  __shared__ __attribute__((aligned(16))) float img[Q8QT / 8][PQ_ROW];  // one row image per row slice
+  const int gbk = (int)blockIdx.x + cb0;
+  const int chunk = gbk / q.nblk, b = gbk - chunk * q.nblk;
+  const int tid = threadIdx.x;
+  const int cq = tid & 7, rs = tid >> 3;
+  int s = 0;
+  while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
+  const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
+  const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
+  const int64_t rb = r0 + (int64_t)b * Q8BLK + 16 * rs;
+  const int cg0 = (int)blockIdx.y * Q8QC;
+  const int c0 = cg0 + 4 * cq;
+  f32x4 sh;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sh[e] = c0 + e < p ? shift[c0 + e] : 0.f;
+  // this lane's halo quad (lanes cq < HQ: left, cq >= 8 - HQ: right)
+  const bool hl = cq < HQ, hr = cq >= 8 - HQ;
+  const int hcol = hl ? cg0 - 4 * HQ + 4 * cq : cg0 + Q8QC + 4 * (cq - (8 - HQ));
+  const bool hvalid = (hl || hr) && hcol >= 0 && hcol < p;
+  const int hslot = hl ? 8 - 4 * HQ + 4 * cq : 8 + Q8QC + 4 * (cq - (8 - HQ));
+  float* row_img = img[rs];
+  const float* c = pa.taps + HH;  // interior taps, offset -HH..HH
+  float ct[HH + 1];
+#pragma unroll
+  for (int t = 0; t <= HH; ++t) ct[t] = HH > 0 ? c[t] : 0.f;
+  const bool sub = pa.snv && pa.deriv == 0;
+  f32x4 v[16];
+  constexpr int GR = HH >= 7 ? 2 : 4;  // rows per load group (VGPRs: the 16 output quads stay live)
+#pragma unroll
+  for (int g4 = 0; g4 < 16 / GR; ++g4) {
+    f32x4 xq[GR], hq[GR];
+    float mr[GR], sr[GR];
+    int64_t xrow[GR];
+#pragma unroll
+    for (int u = 0; u < GR; ++u) {
+      const int64_t g = rb + GR * g4 + u;
+      const int64_t gc = g < r1 ? g : r1 - 1;  // clamped: always a valid row
+      xrow[u] = GATHER ? rows[gc] : gc;
+      const float* xr = X + xrow[u] * ldx;
+      xq[u] = c0 < p ? *reinterpret_cast<const f32x4*>(xr + c0) : f32x4{0.f, 0.f, 0.f, 0.f};
+      hq[u] = hvalid ? *reinterpret_cast<const f32x4*>(xr + hcol) : f32x4{0.f, 0.f, 0.f, 0.f};
+      mr[u] = 0.f;
+      sr[u] = 1.f;
+      if (pa.snv) {
+        mr[u] = pa.rowstat[2 * xrow[u]];
+        sr[u] = pa.rowstat[2 * xrow[u] + 1];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < GR; ++u) {
+      const int j = GR * g4 + u;
+      const int64_t g = rb + j;
+      f32x4 xs = xq[u], hs = hq[u];
+      if (sub)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xs[e] = __fsub_rn(xs[e], mr[u]);
+          hs[e] = __fsub_rn(hs[e], mr[u]);
+        }
+      // the lanes of one row slice exchange their quads through the row image
+      // (wave-private: LDS instructions of a wave execute in order)
+      *reinterpret_cast<f32x4*>(row_img + 8 + 4 * cq) = xs;
+      if (hl || hr) *reinterpret_cast<f32x4*>(row_img + hslot) = hs;
+      __builtin_amdgcn_wave_barrier();
+      float win[4 + 2 * 4 * HQ];  // columns c0 - 4HQ .. c0 + 3 + 4HQ
+#pragma unroll
+      for (int k = 0; k < 1 + 2 * HQ; ++k) {
+        const f32x4 t4 = *reinterpret_cast<const f32x4*>(row_img + 8 - 4 * HQ + 4 * cq + 4 * k);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) win[4 * k + e] = t4[e];
+      }
+      f32x4 y;  // interior formula (the first / last HH columns are redone below)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int o = 4 * HQ + e;  // window index of column c0 + e
+        float a;
+        if constexpr (HH == 0) {
+          a = win[o];
+        } else {
+          if (pa.deriv & 1) {
+            a = 0.f;
+#pragma unroll
+            for (int t = 1; t <= HH; ++t) a = fmaf(ct[t], __fsub_rn(win[o + t], win[o - t]), a);
+          } else if (pa.deriv == 0) {
+            a = __fmul_rn(ct[0], win[o]);
+#pragma unroll
+            for (int t = 1; t <= HH; ++t) a = fmaf(ct[t], __fadd_rn(win[o + t], win[o - t]), a);
+          } else {
+            const float uj = win[o];
+            a = 0.f;
+#pragma unroll
+            for (int t = 1; t <= HH; ++t)
+              a = fmaf(ct[t], __fadd_rn(__fsub_rn(win[o + t], uj), __fsub_rn(win[o - t], uj)), a);
+          }
+        }
+        y[e] = pa.snv ? __fmul_rn(a, sr[u]) : a;
+      }
+      __builtin_amdgcn_wave_barrier();  // the image is rewritten by the next row
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = (g < r1 && c0 + e < p) ? __fsub_rn(y[e], sh[e]) : 0.f;
+    }
+  }
+  if (HH > 0 && (c0 < HH || c0 + 3 >= p - HH)) {
+    // the least-squares edge rows of the first / last HH columns (two column
+    // groups of the grid): the scalar formula, the raw rows again from cache
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int64_t g = rb + j;
+      if (g >= r1) continue;
+      const int64_t xr = GATHER ? rows[g] : g;
+      const float m = pa.snv ? pa.rowstat[2 * xr] : 0.f, sc = pa.snv ? pa.rowstat[2 * xr + 1] : 1.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int jc = c0 + e;
+        if (jc < p && (jc < HH || jc >= p - HH))
+          v[j][e] = __fsub_rn(ocm::prep_elem(X + xr * ldx, p, jc, pa, m, sc), sh[e]);
+      }
+    }
+  }
+  q8_tail(v, tid, cq, rs, cg0, c0, rb, q, chunk, b, st, colblk);
+}
+
 // Column sums of the quantiser's per-block partials: rows [c0, c1) of colblk
 // (P8 wide) → colsum (p).  16 fixed row slices per column, combined in order.
 __global__ __launch_bounds__(256) void k_colblk_sum(const double* __restrict__ colblk, int64_t c0, int64_t c1,
@@ -917,7 +1080,7 @@ constexpr int QX_BINS = 128, QX_EMIN = -62;  // bin = clamp(e, −62, 65) + 62; 
 __global__ __launch_bounds__(256) void k_colexp_hist(const float* __restrict__ X, int64_t ldx,
                                                      const int64_t* __restrict__ rows, int64_t n, int p,
                                                      const float* __restrict__ shift, int64_t rows_per_split,
-                                                     uint32_t* __restrict__ hist) {
+                                                     uint32_t* __restrict__ hist, PrepArgs pa) {
   __shared__ uint32_t h[64][QX_BINS];
   for (int e = threadIdx.x; e < 64 * QX_BINS; e += 256) (&h[0][0])[e] = 0u;
   __syncthreads();
@@ -928,7 +1091,7 @@ __global__ __launch_bounds__(256) void k_colexp_hist(const float* __restrict__ X
   if (col < p) {
     const float sh = shift[col];
     for (int64_t r = a + w; r < e; r += 4) {
-      const float y = fabsf(X[(rows ? rows[r] : r) * ldx + col] - sh);
+      const float y = fabsf(load_y(X, ldx, rows ? rows[r] : r, col, p, pa) - sh);
       int ex = 0;
       (void)frexpf(y, &ex);
       const int bin = y > 0.f ? min(max(ex, QX_EMIN), QX_EMIN + QX_BINS - 1) - QX_EMIN : 0;
@@ -1040,7 +1203,7 @@ __global__ __launch_bounds__(256) void k_gram_fixup(const float* __restrict__ X,
                                                     const int64_t* __restrict__ list,
                                                     const uint32_t* __restrict__ nlist,
                                                     const uint32_t* __restrict__ flags, int fw, int nt,
-                                                    double* __restrict__ G) {
+                                                    double* __restrict__ G, PrepArgs pa) {
   __shared__ double yi[FX_R][FX_T], yj[FX_R][FX_T];
   __shared__ uint32_t mk[FX_R];  // bit 0/1: groups of the I columns, bit 2/3: of the J columns
   const int seg = blockIdx.y;
@@ -1070,9 +1233,9 @@ __global__ __launch_bounds__(256) void k_gram_fixup(const float* __restrict__ X,
       double a = 0.0, b = 0.0;
       if (r < nr) {
         const int64_t pos = list[f0 + r];
-        const float* xr = X + (rows ? rows[pos] : pos) * ldx;
-        if (I + c < p) a = (double)xr[I + c] - (double)shift[I + c];
-        if (J + c < p) b = (double)xr[J + c] - (double)shift[J + c];
+        const int64_t xrow = rows ? rows[pos] : pos;
+        if (I + c < p) a = (double)load_y(X, ldx, xrow, I + c, p, pa) - (double)shift[I + c];
+        if (J + c < p) b = (double)load_y(X, ldx, xrow, J + c, p, pa) - (double)shift[J + c];
       }
       yi[r][c] = a;
       yj[r][c] = b;
@@ -2140,7 +2303,8 @@ int gram_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, in
 // caller then recomputes the Gram on the bf16×3 path.
 int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
                const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
-               hipStream_t st, int64_t chunk_rows, bool k32) {
+               hipStream_t st, int64_t chunk_rows, bool k32, const PrepArgs& pa = PrepArgs{}) {
+  const bool prep = pa.w > 0 || pa.snv;
   const int P8 = (int)ocm::align_up((size_t)p, Q8T);
   const int nt = P8 / Q8T;
   const int ntiles = nt * (nt + 1) / 2;
@@ -2191,7 +2355,7 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   OCM_HIP(hipMemsetAsync(counters, 0, 16, st));
   OCM_HIP(hipMemsetAsync(xhist, 0, (size_t)p * QX_BINS * 4, st));
   hipLaunchKernelGGL(k_colexp_hist, dim3((p + 63) / 64, nsplit), dim3(256), 0, st, X, ldx, rows, nsamp, p, shift, rps,
-                     xhist);
+                     xhist, pa);
   hipLaunchKernelGGL(k_q8_thresholds, dim3(1), dim3(1024), 0, st, xhist, nsamp, p, P8, thr);
   OCM_CHECK_LAUNCH("k_q8_thresholds");
 
@@ -2289,7 +2453,20 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     const int cgw = qcg;  // column groups per quantiser workgroup (P8 / 32 is a multiple of 4)
     dim3 gq((unsigned)((c1 - c0) * nblk * cgw), (unsigned)(P8 / Q8QC / cgw));
     ocm::TimedRegion tq(ctx, OCM_KERNEL_QUANT, qs);
-    if (rows)
+    if (prep) {
+      const dim3 gp((unsigned)((c1 - c0) * nblk), (unsigned)(P8 / Q8QC));
+#define Q8P_LAUNCH(G_, H_)                                                                                        \
+  hipLaunchKernelGGL((k_q8_quant_prep<G_, H_>), gp, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g, \
+                     (int)(c0 * nblk), pa)
+      if (pa.h == 0) {
+        if (rows) Q8P_LAUNCH(true, 0); else Q8P_LAUNCH(false, 0);
+      } else if (pa.h == 2) {
+        if (rows) Q8P_LAUNCH(true, 2); else Q8P_LAUNCH(false, 2);
+      } else {
+        if (rows) Q8P_LAUNCH(true, 7); else Q8P_LAUNCH(false, 7);
+      }
+#undef Q8P_LAUNCH
+    } else if (rows)
       hipLaunchKernelGGL(k_q8_quant<true>, gq, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g,
                          (int)(c0 * nblk));
 #ifdef OCM_EXP_SELECTORS
@@ -2414,10 +2591,36 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     fs.nseg = s1 - s0;
     for (int s = s0; s <= s1; ++s) fs.begin[s - s0] = seg_offsets[s];
     hipLaunchKernelGGL(k_gram_fixup, dim3(nt64 * (nt64 + 1) / 2, s1 - s0), dim3(256), 0, st, X, ldx, rows, p, shift,
-                       fs, flist, counters + 1, flags, fw, nt64, G_out + (size_t)s0 * p * p);
+                       fs, flist, counters + 1, flags, fw, nt64, G_out + (size_t)s0 * p * p, pa);
   }
   OCM_CHECK_LAUNCH("k_gram_fixup");
   return OCM_OK;
+}
+
+// The Gram of a lazy view (ocm_prep) on the paths without a fused load:
+// the preprocessed rows go to a temporary device buffer (processed-row
+// order, so the gather list is consumed here) and the plain dispatch runs on it.
+int gram_dispatch(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                  const float* shift, const int64_t* seg_offsets, int32_t nseg, int32_t mode, int64_t chunk_rows,
+                  double* G_out, double* colsum_out, hipStream_t st);
+
+int gram_materialised(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                      const float* shift, const int64_t* seg_offsets, int32_t nseg, int32_t mode, int64_t chunk_rows,
+                      const PrepArgs& pa, double* G_out, double* colsum_out, hipStream_t st) {
+  float* Y = nullptr;
+  OCM_HIP(hipMallocAsync(reinterpret_cast<void**>(&Y), (size_t)n * p * sizeof(float), st));
+  ++ctx->prep_materialised;
+  int rc = ocm::prep_apply(ctx, X, ldx, rows, n, p, pa, Y, p, st);
+  if (rc == OCM_OK)
+    rc = gram_dispatch(ctx, Y, p, nullptr, n, p, shift, seg_offsets, nseg, mode, chunk_rows, G_out, colsum_out, st);
+  const hipError_t e = hipFreeAsync(Y, st);
+  if (rc == OCM_OK && e != hipSuccess) return ocm::fail(OCM_ERR_HIP, std::string("hipFreeAsync: ") + hipGetErrorString(e));
+  return rc;
+}
+
+bool prep_fused_gram(const float* X, int64_t ldx, int32_t p, int32_t mode, const PrepArgs& pa) {
+  return (mode == OCM_GRAM_I8X3) && p > SMALL_P && p % 4 == 0 && ldx % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(X) & 15) == 0 && (pa.h == 0 || pa.h == 2 || pa.h == 7) && p >= pa.w + 8;
 }
 
 int gram_dispatch(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
@@ -2457,7 +2660,7 @@ int ocm_colmean_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* ro
   auto* part = static_cast<double*>(ocm::workspace(ctx, (size_t)nsplit * p * sizeof(double), st));
   if (!part) return OCM_ERR_NOMEM;
   dim3 g1((p + 255) / 256, nsplit);
-  hipLaunchKernelGGL(k_colsum_part, g1, dim3(256), 0, st, X, ldx, rows, n, p, rps, part);
+  hipLaunchKernelGGL(k_colsum_part, g1, dim3(256), 0, st, X, ldx, rows, n, p, rps, part, PrepArgs{});
   OCM_CHECK_LAUNCH("k_colsum_part");
   hipLaunchKernelGGL(k_colsum_final, dim3((p + 255) / 256), dim3(256), 0, st, part, nsplit, p, 1.0 / (double)n,
                      mean_out);
@@ -2477,6 +2680,49 @@ int ocm_gram_f32_ex(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* ro
     OCM_REQUIRE(seg_offsets[s + 1] >= seg_offsets[s], "ocm_gram_f32: seg_offsets not ascending");
   return gram_dispatch(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, mode, chunk_rows, G_out, colsum_out,
                        (hipStream_t)stream);
+}
+
+int ocm_gram_f32_prep(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                      const float* shift, const int64_t* seg_offsets, int32_t nseg, int32_t mode,
+                      int64_t chunk_rows, const ocm_prep* prep, double* G_out, double* colsum_out, void* stream) {
+  OCM_REQUIRE(ctx && X && shift && seg_offsets && G_out && colsum_out, "ocm_gram_f32_prep: NULL argument");
+  OCM_REQUIRE(n > 0 && p > 0 && ldx >= p && nseg > 0, "ocm_gram_f32_prep: bad shape");
+  OCM_REQUIRE(seg_offsets[0] == 0 && seg_offsets[nseg] == n, "ocm_gram_f32_prep: seg_offsets must span [0, n]");
+  OCM_REQUIRE(mode == OCM_GRAM_I8X3 || mode == OCM_GRAM_F32 || mode == OCM_GRAM_BF16X3 || mode == OCM_GRAM_I8X3_K32,
+              "ocm_gram_f32_prep: bad mode");
+  for (int s = 0; s < nseg; ++s)
+    OCM_REQUIRE(seg_offsets[s + 1] >= seg_offsets[s], "ocm_gram_f32_prep: seg_offsets not ascending");
+  if (int rc = ocm::check_prep(prep, p, "ocm_gram_f32_prep")) return rc;
+  const PrepArgs pa = ocm::prep_args(prep);
+  hipStream_t st = (hipStream_t)stream;
+  if (prep_fused_gram(X, ldx, p, mode, pa)) {
+    const int rc = gram_impl8(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows,
+                              false, pa);
+    if (rc != 1) return rc;
+    mode = OCM_GRAM_BF16X3;  // too many screened rows: the exact split on the materialised rows
+  }
+  return gram_materialised(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, mode, chunk_rows, pa, G_out,
+                           colsum_out, st);
+}
+
+int ocm_colmean_f32_prep(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
+                         const ocm_prep* prep, double* mean_out, void* stream) {
+  OCM_REQUIRE(ctx && X && mean_out, "ocm_colmean_f32_prep: NULL argument");
+  OCM_REQUIRE(n > 0 && p > 0 && ldx >= p, "ocm_colmean_f32_prep: bad shape");
+  if (int rc = ocm::check_prep(prep, p, "ocm_colmean_f32_prep")) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t per = 32;
+  const int nsplit = (int)std::min<int64_t>((n + per - 1) / per, 4096);
+  const int64_t rps = (n + nsplit - 1) / nsplit;
+  auto* part = static_cast<double*>(ocm::workspace(ctx, (size_t)nsplit * p * sizeof(double), st));
+  if (!part) return OCM_ERR_NOMEM;
+  hipLaunchKernelGGL(k_colsum_part, dim3((p + 255) / 256, nsplit), dim3(256), 0, st, X, ldx, rows, n, p, rps, part,
+                     ocm::prep_args(prep));
+  OCM_CHECK_LAUNCH("k_colsum_part");
+  hipLaunchKernelGGL(k_colsum_final, dim3((p + 255) / 256), dim3(256), 0, st, part, nsplit, p, 1.0 / (double)n,
+                     mean_out);
+  OCM_CHECK_LAUNCH("k_colsum_final");
+  return OCM_OK;
 }
 
 int ocm_gram_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,

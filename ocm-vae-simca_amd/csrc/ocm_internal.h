@@ -19,6 +19,7 @@ struct ocm_ctx {
   size_t host_bytes = 0;
   int num_cus = 256;
   uint32_t last_gram_marks = 0;  // outlier-guard marks of the last i8×3 Gram (ocm_gram_last_marks)
+  int64_t prep_materialised = 0;  // lazy views written out by a fallback path (ocm_prep_materialised)
   // live kernel timing (ocm_ctx_set_timing): event pairs per timed kernel
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[OCM_TIMED_KERNELS];
@@ -124,3 +125,69 @@ __device__ __forceinline__ float wave_sum_f32(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+
+// ---- preprocessing in the load path (include/ocm.h ocm_prep) --------------
+// Kernel-side copy of an ocm_prep (by value), plus the one scalar definition
+// of the transform every fused kernel reproduces bit for bit.
+struct PrepArgs {
+  int w = 0;      // window (0: SNV only)
+  int h = 0;      // w / 2
+  int deriv = 0;  // 0, odd, even >= 2 select the interior form
+  int snv = 0;
+  const float* taps = nullptr;     // [w] interior ++ [h][w] left ++ [h][w] right
+  const float* rowstat = nullptr;  // (m_r, s_r) per row of X
+};
+
+namespace ocm {
+
+// PrepArgs from a host ocm_prep (validated by the caller)
+inline PrepArgs prep_args(const ocm_prep* p) {
+  PrepArgs a;
+  a.w = p->window;
+  a.h = p->window / 2;
+  a.deriv = p->window > 0 ? p->deriv : 0;
+  a.snv = p->snv;
+  a.taps = p->taps;
+  a.rowstat = p->rowstat;
+  return a;
+}
+
+int check_prep(const ocm_prep* prep, int p, const char* who);
+int prep_apply(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int p, const PrepArgs& pa,
+               float* out, int64_t ldo, hipStream_t st);
+
+// y_j of row `xr` (raw X row): the formula of include/ocm.h, scalar loads.
+// m, s: the row's (m_r, s_r) (ignored unless snv).
+__device__ __forceinline__ float prep_elem(const float* __restrict__ xr, int p, int j, const PrepArgs& pa, float m,
+                                           float s) {
+  const bool sub = pa.snv && pa.deriv == 0;
+  auto u = [&](int c) { return sub ? __fsub_rn(xr[c], m) : xr[c]; };
+  const int H = pa.h;
+  float a;
+  if (pa.w == 0) {
+    a = u(j);
+  } else if (j < H || j >= p - H) {
+    const bool left = j < H;
+    const float* e = pa.taps + pa.w + (left ? j : H + j - (p - H)) * pa.w;
+    const int s0 = left ? 0 : p - pa.w;
+    const float ref = pa.deriv >= 1 ? u(j) : 0.f;
+    a = 0.f;
+    for (int t = 0; t < pa.w; ++t) a = fmaf(e[t], __fsub_rn(u(s0 + t), ref), a);
+  } else {
+    const float* c = pa.taps + H;  // c[t] = tap at offset t, t in [-H, H]
+    if (pa.deriv & 1) {
+      a = 0.f;
+      for (int t = 1; t <= H; ++t) a = fmaf(c[t], __fsub_rn(u(j + t), u(j - t)), a);
+    } else if (pa.deriv == 0) {
+      a = __fmul_rn(c[0], u(j));
+      for (int t = 1; t <= H; ++t) a = fmaf(c[t], __fadd_rn(u(j + t), u(j - t)), a);
+    } else {
+      const float uj = u(j);
+      a = 0.f;
+      for (int t = 1; t <= H; ++t) a = fmaf(c[t], __fadd_rn(__fsub_rn(u(j + t), uj), __fsub_rn(u(j - t), uj)), a);
+    }
+  }
+  return pa.snv ? __fmul_rn(a, s) : a;
+}
+
+}  // namespace ocm

@@ -203,6 +203,108 @@ __global__ __launch_bounds__(256) void k_snv_sg4(const float* __restrict__ X, in
   }
 }
 
+
+// ---- lazy-view support (include/ocm.h ocm_prep) ---------------------------
+// Row statistics of the SNV, the one read-only pre-pass of the fused path:
+// (m_r, s_r) = (mean_r, 1/(std_r + 1e-8)), fp64 moments rounded to float32 as
+// k_snv_sg4 forms them.  One wave per row, four rows per workgroup; p ≤ 4096
+// keeps the row in registers (two-pass moments without a second read).
+template <int MAXSEG>
+__global__ __launch_bounds__(256) void k_prep_rowstats(const float* __restrict__ X, int64_t ldx, int64_t m, int p,
+                                                       float* __restrict__ out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  if (r >= m) return;
+  const float* xr = X + r * ldx;
+  double mean, ss = 0.0;
+  if constexpr (MAXSEG > 0) {
+    const int nseg = (p + 255) / 256;
+    f32x4 x[MAXSEG];
+#pragma unroll
+    for (int k = 0; k < MAXSEG; ++k) {
+      const int c0 = 256 * k + 4 * lane;
+      x[k] = (k < nseg && c0 < p) ? *reinterpret_cast<const f32x4*>(xr + c0) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < MAXSEG; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += (double)x[k][e];
+    mean = wave_sum_f64(s) / p;
+#pragma unroll
+    for (int k = 0; k < MAXSEG; ++k) {
+      const int c0 = 256 * k + 4 * lane;
+      if (k < nseg && c0 < p)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const double d = (double)x[k][e] - mean;
+          ss += d * d;
+        }
+    }
+  } else {  // any p: two passes over the row (the second from cache)
+    double s = 0.0;
+    for (int c = lane; c < p; c += 64) s += (double)xr[c];
+    mean = wave_sum_f64(s) / p;
+    for (int c = lane; c < p; c += 64) {
+      const double d = (double)xr[c] - mean;
+      ss += d * d;
+    }
+  }
+  const float sdf = (float)sqrt(wave_sum_f64(ss) / p);
+  if (lane == 0) {
+    out[2 * r] = (float)mean;
+    out[2 * r + 1] = 1.f / (sdf + 1e-8f);
+  }
+}
+
+// The materialised view (fallback shapes, tests): one thread per output
+// element, the scalar formula (its window loads hit the L1).
+__global__ __launch_bounds__(256) void k_prep_apply(const float* __restrict__ X, int64_t ldx,
+                                                    const int64_t* __restrict__ rows, int p, PrepArgs pa,
+                                                    float* __restrict__ out, int64_t ldo, int64_t i0) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = i0 + blockIdx.y;
+  if (j >= p) return;
+  const int64_t r = rows ? rows[i] : i;
+  float mr = 0.f, sr = 1.f;
+  if (pa.snv) {
+    mr = pa.rowstat[2 * r];
+    sr = pa.rowstat[2 * r + 1];
+  }
+  out[i * ldo + j] = ocm::prep_elem(X + r * ldx, p, j, pa, mr, sr);
+}
+
+}  // namespace
+
+namespace ocm {
+
+// Checks shared by every *_prep entry point.
+int check_prep(const ocm_prep* prep, int p, const char* who) {
+  OCM_REQUIRE(prep, std::string(who) + ": NULL prep");
+  const int w = prep->window;
+  OCM_REQUIRE(w == 0 || (w % 2 == 1 && w >= 3 && w <= 31 && w <= p), std::string(who) +
+              ": prep window must be 0 or odd in [3, 31] and <= p");
+  OCM_REQUIRE(w == 0 || prep->taps, std::string(who) + ": prep taps required");
+  OCM_REQUIRE(!prep->snv || prep->rowstat, std::string(who) + ": SNV needs rowstat");
+  OCM_REQUIRE(prep->deriv >= 0 && (w > 0 || prep->deriv == 0), std::string(who) + ": bad deriv");
+  OCM_REQUIRE(w > 0 || prep->snv, std::string(who) + ": empty prep (no SNV, no filter)");
+  return OCM_OK;
+}
+
+int prep_apply(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int p, const PrepArgs& pa,
+               float* out, int64_t ldo, hipStream_t st) {
+  for (int64_t i0 = 0; i0 < m; i0 += 65535) {  // grid y ≤ 65535 rows per launch
+    const unsigned cnt = (unsigned)std::min<int64_t>(65535, m - i0);
+    hipLaunchKernelGGL(k_prep_apply, dim3((unsigned)((p + 255) / 256), cnt), dim3(256), 0, st, X, ldx, rows, p, pa,
+                       out, ldo, i0);
+  }
+  OCM_CHECK_LAUNCH("k_prep_apply");
+  return OCM_OK;
+}
+
+}  // namespace ocm
+
+namespace {
 }  // namespace
 
 extern "C" {
@@ -260,6 +362,40 @@ int ocm_snv_savgol_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, int
                      window, dtaps, out, ldo);
   OCM_CHECK_LAUNCH("k_snv_savgol");
   return OCM_OK;
+}
+
+int ocm_prep_rowstats_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, int32_t p, float* rowstat_out,
+                          void* stream) {
+  OCM_REQUIRE(ctx && X && rowstat_out, "ocm_prep_rowstats_f32: NULL argument");
+  OCM_REQUIRE(m >= 0 && p >= 1 && ldx >= p, "ocm_prep_rowstats_f32: bad shape");
+  if (m == 0) return OCM_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g((unsigned)((m + 3) / 4));
+  const bool vec = p % 4 == 0 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+  if (vec && p <= 1024)
+    hipLaunchKernelGGL(k_prep_rowstats<4>, g, dim3(256), 0, st, X, ldx, m, p, rowstat_out);
+  else if (vec && p <= 2048)
+    hipLaunchKernelGGL(k_prep_rowstats<8>, g, dim3(256), 0, st, X, ldx, m, p, rowstat_out);
+  else if (vec && p <= 4096)
+    hipLaunchKernelGGL(k_prep_rowstats<16>, g, dim3(256), 0, st, X, ldx, m, p, rowstat_out);
+  else
+    hipLaunchKernelGGL(k_prep_rowstats<0>, g, dim3(256), 0, st, X, ldx, m, p, rowstat_out);
+  OCM_CHECK_LAUNCH("k_prep_rowstats");
+  return OCM_OK;
+}
+
+int ocm_prep_materialised(ocm_ctx* ctx, int64_t* count_out) {
+  OCM_REQUIRE(ctx && count_out, "ocm_prep_materialised: NULL argument");
+  *count_out = ctx->prep_materialised;
+  return OCM_OK;
+}
+
+int ocm_prep_apply_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
+                       const ocm_prep* prep, float* out, int64_t ldo, void* stream) {
+  OCM_REQUIRE(ctx && X && out, "ocm_prep_apply_f32: NULL argument");
+  OCM_REQUIRE(m >= 0 && p >= 1 && ldx >= p && ldo >= p, "ocm_prep_apply_f32: bad shape");
+  if (int rc = ocm::check_prep(prep, p, "ocm_prep_apply_f32")) return rc;
+  return ocm::prep_apply(ctx, X, ldx, rows, m, p, ocm::prep_args(prep), out, ldo, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -365,6 +365,18 @@ template <int N>
 __device__ __forceinline__ void wait_vm(f32x4& a) {
   asm volatile("s_waitcnt vmcnt(%1)" : "+a"(a) : "n"(N));
 }
+// the halo quad of a lazy view's row tile: a VGPR, loaded and waited the same way
+__device__ __forceinline__ void load_v(f32x4& h, const float* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(h) : "v"(p) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vv(f32x4& h) {
+  asm volatile("s_waitcnt vmcnt(%1)" : "+v"(h) : "n"(N));
+}
+// lane `src` (a byte address: 4·lane) of v
+__device__ __forceinline__ float xlane(int src, float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, v)));
+}
 
 // Sweep-1 block: acc[A..D] += a[e] · x[e] (comps 0..15), and for EX acc[E,F]
 // += b[e] ⊗ x[e] on 4x4x1 blocks (comps 16..19 of this lane's row over its
@@ -425,6 +437,22 @@ __device__ __forceinline__ void s2_pair(f32x4& x0, f32x4& x1, const float (&a0)[
         : [u0] "v"(a0[0]), [u1] "v"(a0[1]), [u2] "v"(a0[2]), [u3] "v"(a0[3]), [w0] "v"(a1[0]), [w1] "v"(a1[1]), [w2] "v"(a1[2]), [w3] "v"(a1[3]), [m0] "v"(m0), [m1] "v"(m1), [t0] "v"(tB[0]), [t1] "v"(tB[1]), [t2] "v"(tB[2]), [t3] "v"(tB[3]), [on] "v"(one));
   (void)s, (void)p0, (void)p1, (void)q;
 }
+// s1_block with the B operands in VGPRs (a lazy view's tile, transformed in registers)
+template <bool EX>
+__device__ __forceinline__ void s1_block_v(f32x4& acA, f32x4& acB, f32x4& acC, f32x4& acD, f32x4& acE, f32x4& acF,
+                                           const f32x4& a, const float (&b)[4], const f32x4& x) {
+  if constexpr (EX)
+    asm("s_nop 1\n\t" OCM_M4(cE, b0, x0) OCM_MF(cA, a0, x0) OCM_M4(cF, b1, x1) OCM_MF(cB, a1, x1)
+            OCM_M4(cE, b2, x2) OCM_MF(cC, a2, x2) OCM_M4(cF, b3, x3) OCM_MF(cD, a3, x3)
+        : [cA] "+v"(acA), [cB] "+v"(acB), [cC] "+v"(acC), [cD] "+v"(acD), [cE] "+v"(acE), [cF] "+v"(acF)
+        : [a0] "v"(a[0]), [a1] "v"(a[1]), [a2] "v"(a[2]), [a3] "v"(a[3]), [b0] "v"(b[0]), [b1] "v"(b[1]),
+          [b2] "v"(b[2]), [b3] "v"(b[3]), [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]));
+  else
+    asm("s_nop 1\n\t" OCM_MF(cA, a0, x0) OCM_MF(cB, a1, x1) OCM_MF(cC, a2, x2) OCM_MF(cD, a3, x3)
+        : [cA] "+v"(acA), [cB] "+v"(acB), [cC] "+v"(acC), [cD] "+v"(acD)
+        : [a0] "v"(a[0]), [a1] "v"(a[1]), [a2] "v"(a[2]), [a3] "v"(a[3]), [x0] "v"(x[0]), [x1] "v"(x[1]),
+          [x2] "v"(x[2]), [x3] "v"(x[3]));
+}
 #undef OCM_MF
 #undef OCM_M4
 #undef OCM_M2
@@ -432,7 +460,17 @@ __device__ __forceinline__ void s2_pair(f32x4& x0, f32x4& x1, const float (&a0)[
 #undef OCM_FM
 }  // namespace s1p
 
-template <int NJ, bool EX>
+// HH ≥ 0: a lazy view (include/ocm.h ocm_prep, window 2·HH + 1, or SNV only
+// at HH = 0).  Each raw tile is transformed in registers inside sweep 1, block
+// by block one block behind its loads: the quads of the neighbouring lanes of
+// a row (and of the block before / after) arrive by ds_bpermute, each tile
+// brings one more quad per lane — the HH columns beyond the wave's slice on
+// either side (lanes lq ≥ 2: virtual block −1, lq ≤ 1: virtual block NJ) —
+// and loads it first, the rows' (m_r, s_r) come through the scalar cache.
+// y replaces x in the AGPR tile, so sweep 2 and the epilogue are unchanged;
+// sweep 1 takes y from VGPRs.  The first / last HH columns of the row (wave 0
+// block 0, wave 3 block NJ − 1) use the least-squares edge rows.
+template <int NJ, bool EX, int HH = -1>
 __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X, int64_t ldx,
                                                      const int64_t* __restrict__ rows, int64_t m,
                                                      const double* __restrict__ P, const double* __restrict__ mu,
@@ -440,8 +478,12 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
                                                      float* __restrict__ T_out, double* __restrict__ T2_out,
                                                      float* __restrict__ Q_out, DecArgs dec,
                                                      double* __restrict__ acc_out, int64_t acc_stride,
-                                                     double* __restrict__ stat_part, int64_t ntiles) {
+                                                     double* __restrict__ stat_part, int64_t ntiles,
+                                                     PrepArgs pa, const float* __restrict__ ptaps,
+                                                     const float* __restrict__ prow) {
   using namespace s1p;
+  constexpr bool PREP = HH >= 0;
+  constexpr int GL = NJ + (HH > 0 ? 1 : 0);  // loads per tile group (the halo quad first)
   constexpr int PW = 16 * NJ;  // columns per wave
   constexpr int PP = W * PW;   // p
   constexpr int NCH = PP / 4;  // 16-B chunks per component row
@@ -480,13 +522,17 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
   // as the source, lanes 16c + col and 16(c + 2) + col met on one bank: a 2-way
   // conflict on every bpermute, 256 extra LDS cycles per wave and tile, the
   // whole SQ_LDS_BANK_CONFLICT count of round 2 (profiles/r02n_pmc_score.json)
-  float p1b[EX ? NJ : 1];
+  // (the widest lazy-view variant, HH = 7 at NJ = 32, has no VGPRs to spare for
+  // p1b: its sweep 1 reads p1a at the equivalent lane, 16c + 4lq + e, and takes
+  // the 2-way conflicts back — round 3 measured them at no cost in time)
+  constexpr bool NOP1B = EX && NJ == 32 && HH > 4;
+  float p1b[EX && !NOP1B ? NJ : 1];
   if constexpr (EX)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int64_t rowp = (int64_t)(16 + lq) * PP + w * PW + 16 * j;
       p1a[j] = 16 + lq < k ? (float)P[rowp + ln] : 0.f;
-      p1b[j] = 16 + lq < k ? (float)P[rowp + (ln ^ (8 * (lq >> 1)))] : 0.f;
+      if constexpr (!NOP1B) p1b[j] = 16 + lq < k ? (float)P[rowp + (ln ^ (8 * (lq >> 1)))] : 0.f;
     }
   double ad[5];
 #pragma unroll
@@ -511,6 +557,7 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
   // p1b[j] holds on lane 16c + ((4lq) ^ 8(c >> 1)) + e, c = ln&3 (ds_bpermute
   // address, bytes)
   const int bperm = 4 * (16 * (ln & 3) + ((4 * lq) ^ (8 * ((ln & 3) >> 1))));
+  const int bpermA = 4 * (16 * (ln & 3) + 4 * lq);  // the same operands from p1a (NOP1B)
   const float one = 1.f;  // B of the −μ step
   __syncthreads();
 
@@ -542,15 +589,133 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
   double T2 = 0.0, T2prev = 0.0;
 
   // ---- sweep 1 on tile Y: partial t (uncentred) → tpart[buf] ----------------
-  auto sweep1 = [&](f32x4 (&Y)[NJ], int buf) {
+  // ---- lazy view: (m_r, s_r) of lane row ln of tile tt (scalar loads, selects)
+  const bool psub = PREP && pa.snv && pa.deriv == 0;
+  auto rowstat_of = [&](int64_t tt, float& mr, float& sr) {
+    mr = 0.f;
+    sr = 1.f;
+    if (!PREP || !pa.snv) return;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int64_t r = tt * R + i;
+      const int64_t rr = r < m ? r : m - 1;
+      const int64_t xi = rows ? rows[rr] : rr;
+      const float mi = prow[2 * xi], si = prow[2 * xi + 1];
+      mr = ln == i ? mi : mr;
+      sr = ln == i ? si : sr;
+    }
+  };
+  // y of this lane's four columns of block j from the window u[c0 − HH .. c0 + 3 + HH]
+  auto stencil = [&](const float* win, float sr) __attribute__((always_inline)) -> f32x4 {
+    f32x4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int o = (HH > 0 ? HH : 0) + e;
+      float a;
+      if constexpr (HH <= 0) {
+        a = win[o];
+      } else {
+        if (pa.deriv & 1) {
+          a = 0.f;
+#pragma unroll
+          for (int t = 1; t <= HH; ++t) a = fmaf(ptaps[HH + t], __fsub_rn(win[o + t], win[o - t]), a);
+        } else if (pa.deriv == 0) {
+          a = __fmul_rn(ptaps[HH], win[o]);
+#pragma unroll
+          for (int t = 1; t <= HH; ++t) a = fmaf(ptaps[HH + t], __fadd_rn(win[o + t], win[o - t]), a);
+        } else {
+          const float uj = win[o];
+          a = 0.f;
+#pragma unroll
+          for (int t = 1; t <= HH; ++t)
+            a = fmaf(ptaps[HH + t], __fadd_rn(__fsub_rn(win[o + t], uj), __fsub_rn(win[o - t], uj)), a);
+        }
+      }
+      y[e] = pa.snv ? __fmul_rn(a, sr) : a;
+    }
+    return y;
+  };
+  // the first (LEFT) / last HH columns of the row: block 0 of wave 0 or block
+  // NJ − 1 of wave 3; the 16 u values of the block's row gathered from its
+  // four lanes, the edge rows from the scalar cache
+  auto edge_fix = [&](f32x4& y, const f32x4& ucur, float sr, bool left) __attribute__((always_inline)) {  // y: this lane's edge outputs
+    if constexpr (HH > 0) {
+      f32x4 q1, q2, q3;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        q1[e] = xlane(4 * (lane ^ 16), ucur[e]);
+        q2[e] = xlane(4 * (lane ^ 32), ucur[e]);
+        q3[e] = xlane(4 * (lane ^ 48), ucur[e]);
+      }
+      float row16[16];
+#pragma unroll
+      for (int sq = 0; sq < 4; ++sq)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int kk = lq ^ sq;  // the round that brought quad sq
+          row16[4 * sq + e] = kk == 0 ? ucur[e] : kk == 1 ? q1[e] : kk == 2 ? q2[e] : q3[e];
+        }
+      const int Wn = 2 * HH + 1;
+#pragma unroll
+      for (int i = 0; i < HH; ++i) {
+        const float* et = ptaps + Wn + (left ? i : HH + i) * Wn;
+        const int s0 = left ? 0 : 16 - Wn;           // window start within the block
+        const int cl = left ? i : 16 - HH + i;       // the output's column within the block
+        const float ref = pa.deriv >= 1 ? row16[cl] : 0.f;
+        float a = 0.f;
+#pragma unroll
+        for (int t = 0; t < Wn; ++t) a = fmaf(et[t], __fsub_rn(row16[s0 + t], ref), a);
+        const float yv = pa.snv ? __fmul_rn(a, sr) : a;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (4 * lq + e == cl) y[e] = yv;
+      }
+    }
+  };
+
+  auto sweep1 = [&](f32x4 (&Y)[NJ], f32x4& hy, int buf, int64_t tile) __attribute__((always_inline)) {
     f32x4 acA = {0.f, 0.f, 0.f, 0.f}, acB = acA, acC = acA, acD = acA, acE = acA, acF = acA;
+    f32x4 yE = acA;  // lazy view: this lane's outputs among the row's first / last HH columns
+    float mr = 0.f, sr = 1.f;
+    f32x4 uprev = acA, ucur = acA, unext = acA;
+    if constexpr (PREP) {
+      rowstat_of(tile, mr, sr);
+      // hy, Y[0], Y[1] (the oldest loads of the tile's group) have landed: the
+      // rest of this group and the other tile's whole group may be in flight
+      constexpr int W0 = NJ - 2 + GL < 63 ? NJ - 2 + GL : 63;
+      wait_vm<W0>(Y[1]);
+      wait_vm<W0>(Y[0]);
+      wait_vv<W0>(hy);
+      ucur = Y[0];
+      uprev = hy;
+      if (psub)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ucur[e] = __fsub_rn(ucur[e], mr);
+          uprev[e] = __fsub_rn(uprev[e], mr);
+        }
+      // the row ends first (wave 0: block 0, wave 3: block NJ − 1), before the
+      // block loop's registers are live
+      if constexpr (HH > 0) {
+        if (w == 0) edge_fix(yE, ucur, sr, true);
+        if (w == W - 1) {
+          wait_vm<GL>(Y[NJ - 1]);
+          f32x4 ul = Y[NJ - 1];
+          if (psub)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ul[e] = __fsub_rn(ul[e], mr);
+          edge_fix(yE, ul, sr, false);
+        }
+      }
+    }
     double t64[4] = {0.0, 0.0, 0.0, 0.0}, x164[4] = {0.0, 0.0, 0.0, 0.0};
     f32x4 aN = P0s[b1[0]];  // LDS / crossbar operands one block ahead
     float bN[4] = {0.f, 0.f, 0.f, 0.f};
     if constexpr (EX)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        bN[e] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(bperm + 4 * e, __builtin_bit_cast(int, p1b[0])));
+        bN[e] = NOP1B ? xlane(bpermA + 4 * e, p1a[0])
+                      : __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(bperm + 4 * e, __builtin_bit_cast(int, p1b[0])));
     static_for<NJ>([&](auto J) {
       constexpr int j = decltype(J)::value;
       const f32x4 a = aN;
@@ -563,13 +728,60 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             bN[e] = __builtin_bit_cast(float,
-                                       __builtin_amdgcn_ds_bpermute(bperm + 4 * e, __builtin_bit_cast(int, p1b[j + 1])));
+                                       __builtin_amdgcn_ds_bpermute(NOP1B ? bpermA + 4 * e : bperm + 4 * e,
+                                                                    __builtin_bit_cast(int, NOP1B ? p1a[j + 1] : p1b[NOP1B ? 0 : j + 1])));
       }
-      // Y[j] was issued before the rest of its tile (NJ − 1 − j loads) and
-      // the NJ refills of the other tile (stores issued since only make the
-      // wait earlier)
-      wait_vm<2 * NJ - 1 - j>(Y[j]);
-      s1_block<EX>(acA, acB, acC, acD, acE, acF, a, b, Y[j]);
+      if constexpr (!PREP) {
+        // Y[j] was issued before the rest of its tile (NJ − 1 − j loads) and
+        // the NJ refills of the other tile (stores issued since only make the
+        // wait earlier)
+        wait_vm<2 * NJ - 1 - j>(Y[j]);
+        s1_block<EX>(acA, acB, acC, acD, acE, acF, a, b, Y[j]);
+      } else {
+        // one block ahead: Y[j + 1] (the next block's raw quad) has landed
+        if constexpr (j + 1 < NJ) {
+          if constexpr (j > 0) wait_vm<NJ - 2 - j + GL>(Y[j + 1]);
+          unext = Y[j + 1];
+        } else {
+          unext = hy;  // lanes lq <= 1: virtual block NJ
+        }
+        if (psub)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) unext[e] = __fsub_rn(unext[e], mr);
+        float win[4 + 2 * (HH > 0 ? HH : 0)];
+        constexpr int H_ = HH > 0 ? HH : 0;
+        constexpr int NL1 = H_ < 4 ? H_ : 4;
+#pragma unroll
+        for (int e = 4 - NL1; e < 4; ++e) {  // quad lq − 1 (block j − 1 for lq = 0)
+          win[H_ - 4 + e] = xlane(4 * ((lane + 48) & 63), lq == 3 ? uprev[e] : ucur[e]);
+          win[H_ + 4 + (e - (4 - NL1))] = xlane(4 * ((lane + 16) & 63), lq == 0 ? unext[e - (4 - NL1)] : ucur[e - (4 - NL1)]);
+        }
+        if constexpr (H_ > 4) {
+#pragma unroll
+          for (int e = 8 - H_; e < 4; ++e)  // quad lq − 2
+            win[H_ - 8 + e] = xlane(4 * (lane ^ 32), lq >= 2 ? uprev[e] : ucur[e]);
+#pragma unroll
+          for (int e = 0; e < H_ - 4; ++e)  // quad lq + 2
+            win[H_ + 8 + e] = xlane(4 * (lane ^ 32), lq <= 1 ? unext[e] : ucur[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) win[H_ + e] = ucur[e];
+        f32x4 y = stencil(win, sr);
+        if constexpr (HH > 0) {
+          if ((j == 0 && w == 0) || (j == NJ - 1 && w == W - 1))
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int cl = 4 * lq + e;  // column within the block
+              if (j == 0 ? cl < HH : cl >= 16 - HH) y[e] = yE[e];
+            }
+        }
+        // y into the AGPR tile now (sweep 2 reads it there); a plain assignment
+        // would leave y in VGPRs until the next sweep 2 asks for the AGPRs
+        asm volatile("" : "=a"(Y[j]) : "0"(y));
+        uprev = ucur;
+        ucur = unext;
+        s1_block_v<EX>(acA, acB, acC, acD, acE, acF, a, b, y);
+      }
       __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting every block's reads
       if constexpr ((j & 15) == 15 || j == NJ - 1) {  // f32 partials over ≤ 64 columns per chain
         asm volatile("s_nop 11" ::: "memory");        // MFMA result → VALU read
@@ -623,7 +835,15 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
   };
   // ---- sweep 2 on tile Z (raw x of the tile being scored): Q partials →
   // qpart[buf]; each consumed block pair of Z is refilled from `pre`
-  auto sweep2 = [&](f32x4 (&Z)[NJ], const float* pre, int buf) {
+  // a lazy view's halo quad of the tile whose row pointer is `pre`: lanes
+  // lq ≥ 2 the quad of virtual block −1, lanes lq ≤ 1 of virtual block NJ (an
+  // in-row address at the row's ends, where the edge rows replace the stencil)
+  auto halo_ptr = [&](const float* pre) -> const float* {
+    const bool left = lq >= 2;
+    return left ? (w > 0 ? pre - 16 : pre) : (w < W - 1 ? pre + 16 * NJ : pre);
+  };
+  auto sweep2 = [&](f32x4 (&Z)[NJ], f32x4& hz, const float* pre, int buf) __attribute__((always_inline)) {
+    if constexpr (HH > 0) load_v(hz, halo_ptr(pre));  // first load of the refilled tile's group
     float q[4] = {0.f, 0.f, 0.f, 0.f};
     double q64 = 0.0;
     float aN[2][5], mN[2];  // A operands of the next block pair (one pair ahead)
@@ -716,13 +936,16 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
   // re-read a valid tile.
   int64_t t = blockIdx.x;
   auto clamp_tile = [&](int64_t tt) { return tt < ntiles ? tt : t; };
+  f32x4 hA = {0.f, 0.f, 0.f, 0.f}, hB = hA;  // lazy view: the tiles' halo quads
   {
     const float* p0 = col_base(index_of(t));
     const float* p1 = col_base(index_of(clamp_tile(t + G)));
+    if constexpr (HH > 0) load_v(hA, halo_ptr(p0));
     static_for<NJ>([&](auto J) { load_a<64 * decltype(J)::value>(XA[decltype(J)::value], p0); });
+    if constexpr (HH > 0) load_v(hB, halo_ptr(p1));
     static_for<NJ>([&](auto J) { load_a<64 * decltype(J)::value>(XB[decltype(J)::value], p1); });
   }
-  sweep1(XA, 0);
+  sweep1(XA, hA, 0, t);
   lds_barrier();
   compute_t(t, 0);
   int buf = 0;
@@ -738,13 +961,13 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
 #else
 #define OCM_STAMP(I)
 #endif
-  auto step = [&](f32x4 (&Xc)[NJ], f32x4 (&Yn)[NJ]) -> bool {
+  auto step = [&](f32x4 (&Xc)[NJ], f32x4& hc, f32x4 (&Yn)[NJ], f32x4& hn) __attribute__((always_inline)) -> bool {
     const int64_t tn = t + G;
     const bool more = tn < ntiles;
     OCM_STAMP(3)
-    sweep2(Xc, col_base(index_of(clamp_tile(tn + G))), buf);
+    sweep2(Xc, hc, col_base(index_of(clamp_tile(tn + G))), buf);
     OCM_STAMP(0)
-    if (more) sweep1(Yn, buf ^ 1);
+    if (more || PREP) sweep1(Yn, hn, buf ^ 1, tn);  // lazy view: unconditional (a tile past the end is a clamped valid one), so Yn never merges raw and transformed values
     OCM_STAMP(1)
     lds_barrier();
     OCM_STAMP(2)
@@ -758,14 +981,18 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
   };
 #undef OCM_STAMP
   for (;;) {
-    if (!step(XA, XB)) break;
-    if (!step(XB, XA)) break;
+    if (!step(XA, hA, XB, hB)) break;
+    if (!step(XB, hB, XA, hA)) break;
   }
   // drain the refills past the last tile before the wave ends
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     wait_vm<0>(XA[j]);
     wait_vm<0>(XB[j]);
+  }
+  if constexpr (HH > 0) {
+    wait_vv<0>(hA);
+    wait_vv<0>(hB);
   }
 #ifdef OCM_S1P_STAMPS
 #pragma unroll
@@ -974,18 +1201,35 @@ int ocm_score_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
                       accept_stride, stats_out, (hipStream_t)stream);
 }
 
-int ocm_score_f32_diag(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
-                       const double* P, const double* mu, const double* a_diag, int32_t k, float* T_out,
-                       double* T2_out, float* Q_out, const ocm_decision* dec, double* accept_out,
-                       int64_t accept_stride, double* stats_out, void* stream) {
-  OCM_REQUIRE(ctx && X && P && mu && a_diag, "ocm_score_f32_diag: NULL argument");
-  OCM_REQUIRE(m >= 0 && p > 0 && ldx >= p, "ocm_score_f32_diag: bad shape");
-  OCM_REQUIRE(k >= 1 && k <= p, "ocm_score_f32_diag: 1 <= k <= p");
-  OCM_REQUIRE(!dec || accept_out, "ocm_score_f32_diag: decision requires accept_out");
-  hipStream_t st = (hipStream_t)stream;
+}  // extern "C"
+
+namespace {
+
+int score_diag_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
+                    const PrepArgs* pp, const double* P, const double* mu, const double* a_diag, int32_t k,
+                    float* T_out, double* T2_out, float* Q_out, const ocm_decision* dec, double* accept_out,
+                    int64_t accept_stride, double* stats_out, hipStream_t st) {
   const int nj = p / 64;
   const bool vec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
-  const bool one_pass = vec && p % 64 == 0 && (nj == 4 || nj == 8 || nj == 16 || nj == 32) && k <= 20;
+  bool one_pass = vec && p % 64 == 0 && (nj == 4 || nj == 8 || nj == 16 || nj == 32) && k <= 20;
+  const PrepArgs pa = pp ? *pp : PrepArgs{};
+  if (pp && !(pa.h == 0 || pa.h == 2 || pa.h == 7)) one_pass = false;
+  if (!one_pass && pp) {  // a lazy view on the other shapes: materialise the rows, then score them
+    if (m == 0) {
+      if (stats_out) OCM_HIP(hipMemsetAsync(stats_out, 0, 4 * sizeof(double), st));
+      return OCM_OK;
+    }
+    float* Y = nullptr;
+    OCM_HIP(hipMallocAsync(reinterpret_cast<void**>(&Y), (size_t)m * p * sizeof(float), st));
+    ++ctx->prep_materialised;
+    int rc = ocm::prep_apply(ctx, X, ldx, rows, m, p, pa, Y, p, st);
+    if (rc == OCM_OK)
+      rc = score_diag_impl(ctx, Y, p, nullptr, m, p, nullptr, P, mu, a_diag, k, T_out, T2_out, Q_out, dec,
+                           accept_out, accept_stride, stats_out, st);
+    const hipError_t e = hipFreeAsync(Y, st);
+    if (rc == OCM_OK && e != hipSuccess) return ocm::fail(OCM_ERR_HIP, std::string("hipFreeAsync: ") + hipGetErrorString(e));
+    return rc;
+  }
   if (!one_pass)  // other shapes: the two-sweep kernel
     return score_direct(ctx, X, ldx, rows, m, p, P, mu, a_diag, 1, k, T_out, T2_out, Q_out, dec, accept_out,
                         accept_stride, stats_out, st);
@@ -1011,14 +1255,24 @@ int ocm_score_f32_diag(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t*
   }
   {
     ocm::TimedRegion tr(ctx, OCM_KERNEL_SCORE, st);
-#define OCM_S1P(NJ_, EX_)                                                                                    \
-  hipLaunchKernelGGL((k_score_1p<NJ_, EX_>), dim3(grid), dim3(256), 0, st, X, ldx, rows, m, P, mu, a_diag, k, \
-                     T_out, T2_out, Q_out, d, accept_out, accept_stride, part, ntiles)
+#define OCM_S1P_H(NJ_, EX_, H_)                                                                                 \
+  hipLaunchKernelGGL((k_score_1p<NJ_, EX_, H_>), dim3(grid), dim3(256), 0, st, X, ldx, rows, m, P, mu, a_diag, k, \
+                     T_out, T2_out, Q_out, d, accept_out, accept_stride, part, ntiles, pa, pa.taps, pa.rowstat)
+#define OCM_S1P(NJ_, EX_)                                  \
+  if (!pp)                                                 \
+    OCM_S1P_H(NJ_, EX_, -1);                               \
+  else if (pa.h == 0)                                      \
+    OCM_S1P_H(NJ_, EX_, 0);                                \
+  else if (pa.h == 2)                                      \
+    OCM_S1P_H(NJ_, EX_, 2);                                \
+  else                                                     \
+    OCM_S1P_H(NJ_, EX_, 7);
 #define OCM_S1P_K(NJ_) \
-  if (k > 16)          \
-    OCM_S1P(NJ_, true); \
-  else                 \
-    OCM_S1P(NJ_, false);
+  if (k > 16) {        \
+    OCM_S1P(NJ_, true) \
+  } else {             \
+    OCM_S1P(NJ_, false) \
+  }
     if (nj == 32) {
       OCM_S1P_K(32)
     } else if (nj == 16) {
@@ -1030,6 +1284,7 @@ int ocm_score_f32_diag(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t*
     }
 #undef OCM_S1P_K
 #undef OCM_S1P
+#undef OCM_S1P_H
   }
   OCM_CHECK_LAUNCH("k_score_1p");
   if (stats_out) {
@@ -1037,6 +1292,36 @@ int ocm_score_f32_diag(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t*
     OCM_CHECK_LAUNCH("k_stats_reduce");
   }
   return OCM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ocm_score_f32_diag(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
+                       const double* P, const double* mu, const double* a_diag, int32_t k, float* T_out,
+                       double* T2_out, float* Q_out, const ocm_decision* dec, double* accept_out,
+                       int64_t accept_stride, double* stats_out, void* stream) {
+  OCM_REQUIRE(ctx && X && P && mu && a_diag, "ocm_score_f32_diag: NULL argument");
+  OCM_REQUIRE(m >= 0 && p > 0 && ldx >= p, "ocm_score_f32_diag: bad shape");
+  OCM_REQUIRE(k >= 1 && k <= p, "ocm_score_f32_diag: 1 <= k <= p");
+  OCM_REQUIRE(!dec || accept_out, "ocm_score_f32_diag: decision requires accept_out");
+  return score_diag_impl(ctx, X, ldx, rows, m, p, nullptr, P, mu, a_diag, k, T_out, T2_out, Q_out, dec, accept_out,
+                         accept_stride, stats_out, (hipStream_t)stream);
+}
+
+int ocm_score_f32_diag_prep(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
+                            const ocm_prep* prep, const double* P, const double* mu, const double* a_diag, int32_t k,
+                            float* T_out, double* T2_out, float* Q_out, const ocm_decision* dec,
+                            double* accept_out, int64_t accept_stride, double* stats_out, void* stream) {
+  OCM_REQUIRE(ctx && X && P && mu && a_diag, "ocm_score_f32_diag_prep: NULL argument");
+  OCM_REQUIRE(m >= 0 && p > 0 && ldx >= p, "ocm_score_f32_diag_prep: bad shape");
+  OCM_REQUIRE(k >= 1 && k <= p, "ocm_score_f32_diag_prep: 1 <= k <= p");
+  OCM_REQUIRE(!dec || accept_out, "ocm_score_f32_diag_prep: decision requires accept_out");
+  if (int rc = ocm::check_prep(prep, p, "ocm_score_f32_diag_prep")) return rc;
+  const PrepArgs pa = ocm::prep_args(prep);
+  return score_diag_impl(ctx, X, ldx, rows, m, p, &pa, P, mu, a_diag, k, T_out, T2_out, Q_out, dec, accept_out,
+                         accept_stride, stats_out, (hipStream_t)stream);
 }
 
 int ocm_decide(ocm_ctx* ctx, const double* T2, const float* Q, int64_t m, const ocm_decision* dec, double* t2red_out,

@@ -126,9 +126,21 @@ SIGNATURES = {
     "ocm_conv1d_wgrad": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_i32, c_i32, c_i32,
                                  c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ocm_chan_sum": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
+    "ocm_prep_materialised": (c_i32, [c_void_p, ctypes.POINTER(c_i64)]),
+    "ocm_prep_rowstats_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p]),
+    "ocm_prep_apply_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_i64,
+                                   c_void_p]),
+    "ocm_colmean_f32_prep": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p,
+                                     c_void_p]),
+    "ocm_gram_f32_prep": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p,
+                                  ctypes.POINTER(c_i64), c_i32, c_i32, c_i64, c_void_p, c_void_p, c_void_p,
+                                  c_void_p]),
+    "ocm_score_f32_diag_prep": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p,
+                                        ctypes.POINTER(OcmDecision), c_void_p, c_i64, c_void_p, c_void_p]),
 }
 
-ABI_VERSION = 6  # include/ocm.h OCM_ABI_VERSION
+ABI_VERSION = 7  # include/ocm.h OCM_ABI_VERSION
 
 _lib = None
 _lib_lock = threading.Lock()

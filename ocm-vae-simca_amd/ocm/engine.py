@@ -26,6 +26,7 @@ import torch
 
 from . import _lib
 from ._lib import Context, OcmDecision, TYPE_CODES, check, ptr, stream_handle
+from .prepview import PrepView
 
 SHIFT_SAMPLE = 4096
 EIG_TOL = 1e-10
@@ -38,8 +39,11 @@ def require_device():
 
 
 def as_device_f32(X, device=None) -> torch.Tensor:
-    """Host NumPy / torch input -> contiguous float32 tensor in HBM."""
+    """Host NumPy / torch input -> contiguous float32 tensor in HBM (a lazy
+    ``PrepView`` passes through: the kernels read it in place)."""
     require_device()
+    if isinstance(X, PrepView):
+        return X
     if isinstance(X, torch.Tensor):
         t = X
         if device is None and t.is_cuda:
@@ -58,6 +62,8 @@ def as_device_x(X, device=None) -> torch.Tensor:
     """Spectra in HBM in the arithmetic the reference would use: float64 input
     stays float64 (sklearn's PCA follows the input dtype, utils/SIMCA.py:64-66),
     anything else becomes float32."""
+    if isinstance(X, PrepView):
+        return X
     f64 = (X.dtype == torch.float64) if isinstance(X, torch.Tensor) else (np.asarray(X).dtype == np.float64)
     if not f64:
         return as_device_f32(X, device)
@@ -116,6 +122,11 @@ def _stream(dev):
 def colmean(X: torch.Tensor, rows: torch.Tensor | None, n: int) -> torch.Tensor:
     ctx = Context.get(X.device.index)
     out = torch.empty(X.shape[1], dtype=torch.float64, device=X.device)
+    if isinstance(X, PrepView):
+        st = X.struct()
+        check(_lib.load().ocm_colmean_f32_prep(ctx.handle, ptr(X.X), X.X.stride(0), ptr(rows), n, X.shape[1],
+                                               ctypes.byref(st), ptr(out), _stream(X.device)), "ocm_colmean_f32_prep")
+        return out
     fn = "ocm_colmean_f64" if X.dtype == torch.float64 else "ocm_colmean_f32"
     check(getattr(_lib.load(), fn)(ctx.handle, ptr(X), X.stride(0), ptr(rows), n, X.shape[1], ptr(out),
                                    _stream(X.device)), fn)
@@ -157,6 +168,12 @@ def gram(X: torch.Tensor, rows: torch.Tensor | None, seg_offsets, shift32: torch
     cs = torch.empty((nseg, p), dtype=torch.float64, device=X.device)
     arr = (ctypes.c_int64 * len(seg))(*seg)
     ctx = Context.get(X.device.index)
+    if isinstance(X, PrepView):  # the preprocessing runs in the quantiser's load path
+        st = X.struct()
+        check(_lib.load().ocm_gram_f32_prep(ctx.handle, ptr(X.X), X.X.stride(0), ptr(rows), n, p, ptr(shift32), arr,
+                                            nseg, GRAM_MODES[mode or _gram_mode], int(chunk_rows), ctypes.byref(st),
+                                            ptr(G), ptr(cs), _stream(X.device)), "ocm_gram_f32_prep")
+        return G, cs
     if X.dtype == torch.float64:
         check(_lib.load().ocm_gram_f64(ctx.handle, ptr(X), X.stride(0), ptr(rows), n, p, ptr(shift32), arr, nseg,
                                        ptr(G), ptr(cs), _stream(X.device)), "ocm_gram_f64")
@@ -238,6 +255,8 @@ def score(X: torch.Tensor, rows: torch.Tensor | None, m: int, P64: torch.Tensor,
     k, p = P64.shape
     dev = X.device
     out = {}
+    if isinstance(X, PrepView) and A.dim() != 1:  # a general quadratic form: score the materialised rows
+        X, rows = X.materialize(rows), None
     f64 = X.dtype == torch.float64
     if f64 and A.dim() != 1:
         raise ValueError("float64 spectra are scored with a diagonal quadratic form (ocm_score_f64_diag)")
@@ -248,6 +267,14 @@ def score(X: torch.Tensor, rows: torch.Tensor | None, m: int, P64: torch.Tensor,
     st = torch.empty(4, dtype=torch.float64, device=dev) if want_stats else None
     ctx = Context.get(dev.index)
     dec_p = ctypes.byref(decision) if decision is not None else None
+    if isinstance(X, PrepView):  # the preprocessing runs on each row tile in registers
+        prep = X.struct()
+        check(_lib.load().ocm_score_f32_diag_prep(ctx.handle, ptr(X.X), X.X.stride(0), ptr(rows), m, p,
+                                                  ctypes.byref(prep), ptr(P64), ptr(mean64), ptr(A), k, ptr(T),
+                                                  ptr(T2), ptr(Q), dec_p, ptr(accept_out), accept_stride, ptr(st),
+                                                  _stream(dev)), "ocm_score_f32_diag_prep")
+        out["T"], out["T2"], out["Q"], out["stats"] = T, T2, Q, st
+        return out
     fn = "ocm_score_f64_diag" if f64 else ("ocm_score_f32_diag" if A.dim() == 1 else "ocm_score_f32")
     check(getattr(_lib.load(), fn)(ctx.handle, ptr(X), X.stride(0), ptr(rows), m, p, ptr(P64), ptr(mean64),
                                    ptr(A), k, ptr(T), ptr(T2), ptr(Q), dec_p, ptr(accept_out), accept_stride,

@@ -26,8 +26,9 @@ from scipy.signal import savgol_coeffs
 
 from . import _lib, engine
 from ._lib import Context, check, ptr
+from .prepview import PrepView
 
-__all__ = ["savgol_taps", "snv_savgol", "snv", "savgol_filter", "mahalanobis_outlier_mask"]
+__all__ = ["savgol_taps", "snv_savgol", "snv", "savgol_filter", "mahalanobis_outlier_mask", "PrepView"]
 
 
 @functools.lru_cache(maxsize=64)
@@ -54,13 +55,25 @@ def savgol_taps(window_length: int, polyorder: int, deriv: int = 0, delta: float
 
 
 def snv_savgol(X, window_length: int | None = None, polyorder: int = 2, deriv: int = 0, delta: float = 1.0,
-               snv: bool = True, out: torch.Tensor | None = None) -> torch.Tensor:
+               snv: bool = True, out: torch.Tensor | None = None, lazy: bool = False):
     """SNV (optional) then Savitzky–Golay (optional: ``window_length=None``)
-    along the wavelength axis of a (m, p) float32 matrix in HBM."""
+    along the wavelength axis of a (m, p) float32 matrix in HBM.
+
+    ``lazy=True`` returns a ``PrepView``: nothing is computed here (SNV row
+    statistics on first use), and ``utils.SIMCA`` fit / predict / transform,
+    the CV engine and the engine entry points apply the transform in their
+    load paths, so the preprocessed matrix is never written to HBM."""
     Xd = engine.as_device_f32(X)
+    if isinstance(Xd, PrepView):
+        Xd = Xd.materialize()
     m, p = Xd.shape
     if window_length is not None and int(window_length) > p:
         raise ValueError("If mode is 'interp', window_length must be less than or equal to the size of x.")
+    if lazy:
+        if out is not None:
+            raise ValueError("snv_savgol: `out` and lazy=True exclude each other")
+        tp = savgol_taps(int(window_length), int(polyorder), int(deriv), float(delta)) if window_length else None
+        return PrepView(Xd, window_length, polyorder, deriv, delta, snv, tp)
     if out is None:
         out = torch.empty((m, p), dtype=torch.float32, device=Xd.device)
     w = 0

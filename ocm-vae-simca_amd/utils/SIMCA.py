@@ -11,8 +11,11 @@ single-pass projection/Q/T² scoring); only the scalar limits are evaluated
 on the host.
 
 Inputs may be NumPy arrays (copied to HBM; results come back as NumPy, like
-the reference) or CUDA torch tensors (device-resident; ``predict`` then
-returns a device tensor and ``_model`` arrays are materialised lazily).
+the reference), CUDA torch tensors (device-resident; ``predict`` then
+returns a device tensor and ``_model`` arrays are materialised lazily), or a
+lazy preprocessed view (``ocm.preprocess.snv_savgol(X, ..., lazy=True)``:
+the drivers' SNV / Savitzky–Golay step, applied inside the Gram quantiser and
+the scoring kernel instead of as a pass of its own; results as for tensors).
 
 Documented deviations:
 * predict/transform use the exact top-k loadings of the covariance; the
@@ -41,6 +44,7 @@ import torch
 from sklearn.base import BaseEstimator, ClassifierMixin
 
 from ocm import engine, limits
+from ocm.prepview import PrepView
 
 __all__ = ["SIMCA"]
 
@@ -103,7 +107,7 @@ class EnginePCA:
         out = engine.score(Xd, None, Xd.shape[0], self._fit.P64, self._fit.mean64, self._fit.inv_diag,
                            want_T=True, want_T2=False, want_Q=False)
         T = out["T"]
-        return T if isinstance(X, torch.Tensor) else T.cpu().numpy().astype(self._dt)
+        return T if _is_dev(X) else T.cpu().numpy().astype(self._dt)
 
     def inverse_transform(self, T):
         # T·P + μ (sklearn/decomposition/_base.py:197); facade utility, not on the hot path
@@ -238,7 +242,7 @@ class SIMCA(BaseEstimator, ClassifierMixin):
         out = engine.score(Xd, None, Xd.shape[0], fit.P64, fit.mean64, fit.inv_diag)
         dec = self._decision(m["T2_limit"], m["Q_limit"], m["D_limit"])
         t2r, qr, _ = engine.decide(out["T2"], out["Q"], dec)
-        if isinstance(X, torch.Tensor):
+        if _is_dev(X):
             return out["T2"], t2r, out["Q"], qr
         return _np(out["T2"]), _np(t2r), _np(out["Q"], self._out_dtype), _np(qr)
 
@@ -256,7 +260,7 @@ class SIMCA(BaseEstimator, ClassifierMixin):
             acc = pred[:, i:] if C > 1 else pred
             engine.score(Xd, None, m, fit.P64, fit.mean64, fit.inv_diag, want_T2=False, want_Q=False,
                          decision=dec, accept_out=acc, accept_stride=C)
-        out = pred if isinstance(X, torch.Tensor) else pred.cpu().numpy()
+        out = pred if _is_dev(X) else pred.cpu().numpy()
         if y_true is not None:
             yt = _host_labels(y_true)
             for i, cls in enumerate(self.model_class):
@@ -362,8 +366,13 @@ def _boundary(type_name, dlim, npts=1201):
     return t, np.sqrt(np.maximum(dlim * dlim - t * t, 0.0))
 
 
+def _is_dev(X):
+    """Device-resident input (tensor or lazy view): results stay on the device."""
+    return isinstance(X, (torch.Tensor, PrepView))
+
+
 def _out_dtype(X):
-    if isinstance(X, torch.Tensor):
+    if isinstance(X, (torch.Tensor, PrepView)):
         return np.float64 if X.dtype == torch.float64 else np.float32
     return np.float64 if np.asarray(X).dtype == np.float64 else np.float32
 

@@ -665,3 +665,74 @@ def synth_spectra(n: int, p: int, k: int, rank: int = 40, seed: int = 1234, nois
         band /= np.linalg.norm(band)
         X[n - n_out:] += 3.0 * band[None, :] * rng.uniform(0.8, 1.2, size=(n_out, 1))
     return X.astype(dtype)
+
+
+# ---------------------------------------------------------------------------
+# Spectral preprocessing
+# ---------------------------------------------------------------------------
+
+
+def preprocess_reference(X: np.ndarray, window: int | None, polyorder: int = 2, deriv: int = 0,
+                         delta: float = 1.0, snv: bool = True) -> np.ndarray:
+    """The drivers' preprocessing as they run it: NumPy SNV in the array dtype
+    (simca_nuts.py:47-49, utils/data_utils.py:57) then
+    scipy.signal.savgol_filter(..., axis=1, mode='interp') (simca_nuts.py:51,
+    simca_new_cheese.py:37-38)."""
+    from scipy.signal import savgol_filter
+
+    Y = X
+    if snv:
+        Y = (Y - np.mean(Y, axis=1, keepdims=True)) / (np.std(Y, axis=1, keepdims=True) + 1e-8)
+    if window:
+        Y = savgol_filter(Y, window, polyorder, deriv=deriv, delta=delta, axis=1)
+    return Y
+
+
+def _fma32(c, d, a):
+    # fmaf: the product of two float32 is exact in float64
+    return (c.astype(np.float64) * d.astype(np.float64) + a.astype(np.float64)).astype(np.float32)
+
+
+def prep_fused_f32(X: np.ndarray, window: int, taps: np.ndarray, deriv: int, snv: bool) -> np.ndarray:
+    """NumPy restatement of the lazy view's float32 formula (include/ocm.h,
+    ``ocm_prep``): differences of neighbouring raw samples with antisymmetric
+    taps (odd deriv), symmetric pair sums (deriv 0), edge rows about u_j
+    (deriv >= 1), times 1/(std + 1e-8).  Used by the CPU tests to check that
+    the formula the kernels share is SG(SNV(x)) to float32 rounding."""
+    X = np.asarray(X, dtype=np.float32)
+    m, p = X.shape
+    w = int(window or 0)
+    h = w // 2
+    t32 = np.asarray(taps, dtype=np.float32) if w else None
+    mean = X.astype(np.float64).mean(1)
+    sd = np.sqrt(((X.astype(np.float64) - mean[:, None]) ** 2).mean(1)).astype(np.float32)
+    s = (np.float32(1.0) / (sd + np.float32(1e-8))).astype(np.float32)
+    mr = mean.astype(np.float32)
+    U = (X - mr[:, None]).astype(np.float32) if (snv and (not w or deriv == 0)) else X
+    if not w:
+        A = U
+    else:
+        A = np.zeros((m, p), dtype=np.float32)
+        c = t32[:w]
+        J = np.arange(h, p - h)
+        if deriv % 2 == 1:
+            for t in range(1, h + 1):
+                A[:, J] = _fma32(c[h + t], (U[:, J + t] - U[:, J - t]).astype(np.float32), A[:, J])
+        elif deriv == 0:
+            A[:, J] = (c[h] * U[:, J]).astype(np.float32)
+            for t in range(1, h + 1):
+                A[:, J] = _fma32(c[h + t], (U[:, J + t] + U[:, J - t]).astype(np.float32), A[:, J])
+        else:
+            for t in range(1, h + 1):
+                d = ((U[:, J + t] - U[:, J]).astype(np.float32) + (U[:, J - t] - U[:, J]).astype(np.float32))
+                A[:, J] = _fma32(c[h + t], d.astype(np.float32), A[:, J])
+        L = t32[w:w + h * w].reshape(h, w)
+        R = t32[w + h * w:].reshape(h, w)
+        for i in range(h):
+            for j, row, s0 in ((i, L[i], 0), (p - h + i, R[i], p - w)):
+                ref = U[:, j] if deriv >= 1 else np.zeros(m, np.float32)
+                a = np.zeros(m, np.float32)
+                for t in range(w):
+                    a = _fma32(row[t], (U[:, s0 + t] - ref).astype(np.float32), a)
+                A[:, j] = a
+    return (A * s[:, None]).astype(np.float32) if snv else A

@@ -100,3 +100,27 @@ def test_mahalanobis_outlier_mask_device():
     band = np.abs(md - ref_thr) > 1e-5 * ref_thr
     np.testing.assert_array_equal(mask.cpu().numpy()[band], (md <= ref_thr)[band])
     assert abs(int(mask.sum()) - int(0.95 * len(X))) <= 2
+
+
+@pytest.mark.parametrize("snv,setting", [(True, (5, 2, 1, 1.0)), (False, (15, 2, 1, 1.0)), (True, (15, 2, 1, 1.0)),
+                                         (True, (9, 2, 0, 1.0)), (False, (7, 3, 2, 0.5)), (True, None)])
+def test_lazy_view_formula_matches_scipy(snv, setting):
+    """The float32 formula every fused kernel applies (include/ocm.h ocm_prep,
+    restated in oracle.prep_fused_f32) is the drivers' SNV + savgol_filter to
+    float32 rounding: 2e-6 of the output scale, on spectra with a large
+    baseline (the raw differences keep it from costing precision)."""
+    from oracle.simca_oracle import prep_fused_f32, preprocess_reference
+
+    rng = np.random.default_rng(11)
+    p = 300
+    wl = np.linspace(0, 1, p)
+    x = (50.0 + 4 * wl + 0.3 * np.sin(9 * wl) + 0.02 * rng.standard_normal((64, p))).astype(np.float32)
+    if setting is None:
+        w, po, d, delta = 0, 0, 0, 1.0
+        tp = None
+    else:
+        w, po, d, delta = setting
+        tp = savgol_taps(w, po, d, delta)
+    ref = preprocess_reference(x.astype(np.float64), w, po, d, delta, snv)
+    got = prep_fused_f32(x, w, tp, d, snv)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=2e-6 * np.abs(ref).max())
