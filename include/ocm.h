@@ -312,6 +312,16 @@ int ocm_confusion_counts(ocm_ctx* ctx, const double* accept, int64_t m, int64_t 
 int ocm_snv_savgol_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, int32_t p, int32_t snv,
                        int32_t window, const double* taps, float* out, int64_t ldo, void* stream);
 
+/* ---- dense symmetric eigensolver (fp64) ----
+ * evals_out [dev] all p eigenvalues of C (p×p fp64, symmetric) in descending order; when k > 0,
+ * evecs_out [dev] k×p the leading k eigenvectors as rows (svd_flip sign: largest |entry| positive).
+ * Householder tridiagonalisation on the GPU, QL eigenvalues and inverse-iteration vectors of the
+ * tridiagonal on the host, back-transformation on the GPU.  Replaces the full spectrum of the
+ * reference's SVD (utils/SIMCA.py:64-66,88 `eigs_all`; sklearn _pca.py:584-598) and is the fallback of
+ * ocm_eig_topk when its subspace iteration does not converge.  Synchronises the stream. */
+int ocm_eigh_f64(ocm_ctx* ctx, const double* C, int32_t p, double* evals_out, int32_t k, double* evecs_out,
+                 void* stream);
+
 /* ---- preprocessing in the load path (lazy view) ----
  * The drivers run SNV then Savitzky–Golay right before SIMCA
  * (simca_nuts.py:47-52, simca_new_cheese.py:37-38, utils/data_utils.py:57-61).

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstddef>
+#include <cstdint>
 #include <limits>
 #include <vector>
 
@@ -150,6 +151,135 @@ inline void host_sym_eig(const double* A, int n, double* ev, double* Z) {
   for (int j = 0; j < n; ++j) {
     ev[j] = d[ord[j]];
     for (int i = 0; i < n; ++i) Z[(size_t)i * n + j] = z[(size_t)i * n + ord[j]];
+  }
+}
+
+// Eigenvalues of the symmetric tridiagonal matrix (d[0..n-1] diagonal,
+// e[0..n-2] off-diagonal) by implicit QL without vectors; descending into ev.
+inline void host_tridiag_eigvals(const double* d_in, const double* e_in, int n, double* ev) {
+  std::vector<double> d(d_in, d_in + n), e(n, 0.0);
+  for (int i = 0; i + 1 < n; ++i) e[i] = e_in[i];
+  const double eps = std::numeric_limits<double>::epsilon();
+  for (int l = 0; l < n; ++l) {
+    for (int iter = 0; iter < 60; ++iter) {
+      int m = l;
+      for (; m + 1 < n; ++m) {
+        const double dd = std::fabs(d[m]) + std::fabs(d[m + 1]);
+        if (std::fabs(e[m]) <= eps * dd) break;
+      }
+      if (m == l) break;
+      double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
+      double r = std::hypot(g, 1.0);
+      g = d[m] - d[l] + e[l] / (g + (g >= 0 ? r : -r));
+      double s = 1.0, c = 1.0, p = 0.0;
+      int i = m - 1;
+      bool underflow = false;
+      for (; i >= l; --i) {
+        double f = s * e[i], bb = c * e[i];
+        r = std::hypot(f, g);
+        e[i + 1] = r;
+        if (r == 0.0) {
+          d[i + 1] -= p;
+          e[m] = 0.0;
+          underflow = true;
+          break;
+        }
+        s = f / r;
+        c = g / r;
+        g = d[i + 1] - p;
+        r = (d[i] - g) * s + 2.0 * c * bb;
+        p = s * r;
+        d[i + 1] = g + p;
+        g = c * r - bb;
+      }
+      if (underflow) continue;
+      d[l] -= p;
+      e[l] = g;
+      e[m] = 0.0;
+    }
+  }
+  std::sort(d.begin(), d.end(), [](double a, double b) { return a > b; });
+  for (int i = 0; i < n; ++i) ev[i] = d[i];
+}
+
+// Eigenvectors of the tridiagonal matrix for the k eigenvalues lam[0..k-1]
+// (descending) by inverse iteration (LAPACK dstein's scheme: LU with partial
+// pivoting of T − λI, perturbed when λ repeats, and modified Gram–Schmidt
+// against the vectors of the same cluster, |λ_i − λ_j| ≤ 1e-3·‖T‖₁).
+// X[i·k + j] = component i of vector j (unit norm).
+inline void host_tridiag_invit(const double* d, const double* e, int n, const double* lam, int k, double* X) {
+  const double eps = std::numeric_limits<double>::epsilon();
+  double tnorm = 0.0;
+  for (int i = 0; i < n; ++i)
+    tnorm = std::max(tnorm, std::fabs(d[i]) + (i > 0 ? std::fabs(e[i - 1]) : 0.0) + (i + 1 < n ? std::fabs(e[i]) : 0.0));
+  if (!(tnorm > 0.0)) tnorm = 1.0;
+  const double ortol = 1e-3 * tnorm, pert = 10.0 * eps * tnorm;
+  std::vector<double> dl(n), dd(n), du(n), du2(n), b(n), x(n);
+  std::vector<int> piv(n);
+  double xprev = 0.0;
+  int cluster0 = 0;
+  uint64_t seed = 0x9E3779B97F4A7C15ull;
+  for (int j = 0; j < k; ++j) {
+    double xj = lam[j];
+    if (j > 0 && lam[j - 1] - lam[j] > ortol) cluster0 = j;
+    if (j > 0 && xj >= xprev - pert) xj = xprev - pert;  // separate repeated eigenvalues
+    xprev = xj;
+    // T − xj·I = L·U (partial pivoting)
+    for (int i = 0; i < n; ++i) {
+      dd[i] = d[i] - xj;
+      dl[i] = i + 1 < n ? e[i] : 0.0;
+      du[i] = i + 1 < n ? e[i] : 0.0;
+      du2[i] = 0.0;
+      piv[i] = i;
+    }
+    for (int i = 0; i + 1 < n; ++i) {
+      if (std::fabs(dd[i]) >= std::fabs(dl[i])) {
+        if (dd[i] == 0.0) dd[i] = pert;
+        const double f = dl[i] / dd[i];
+        dl[i] = f;
+        dd[i + 1] -= f * du[i];
+      } else {
+        const double f = dd[i] / dl[i];
+        dd[i] = dl[i];
+        dl[i] = f;
+        const double t = du[i];
+        du[i] = dd[i + 1];
+        dd[i + 1] = t - f * dd[i + 1];
+        if (i + 2 < n) {
+          du2[i] = du[i + 1];
+          du[i + 1] = -f * du[i + 1];
+        }
+        piv[i] = i + 1;
+      }
+    }
+    for (int i = 0; i < n; ++i)
+      if (dd[i] == 0.0) dd[i] = pert;
+    for (int i = 0; i < n; ++i) {  // a deterministic pseudo-random start
+      seed = seed * 6364136223846793005ull + 1442695040888963407ull;
+      b[i] = (double)((seed >> 11) & ((1ull << 52) - 1)) / (double)(1ull << 52) - 0.5;
+    }
+    for (int it = 0; it < 5; ++it) {
+      // solve L U x = b
+      for (int i = 0; i + 1 < n; ++i) {
+        if (piv[i] != i) std::swap(b[i], b[i + 1]);
+        b[i + 1] -= dl[i] * b[i];
+      }
+      x[n - 1] = b[n - 1] / dd[n - 1];
+      if (n > 1) x[n - 2] = (b[n - 2] - du[n - 2] * x[n - 1]) / dd[n - 2];
+      for (int i = n - 3; i >= 0; --i) x[i] = (b[i] - du[i] * x[i + 1] - du2[i] * x[i + 2]) / dd[i];
+      // against the earlier vectors of this cluster
+      for (int q = cluster0; q < j; ++q) {
+        double s = 0.0;
+        for (int i = 0; i < n; ++i) s += X[(size_t)i * k + q] * x[i];
+        for (int i = 0; i < n; ++i) x[i] -= s * X[(size_t)i * k + q];
+      }
+      double nrm = 0.0;
+      for (int i = 0; i < n; ++i) nrm += x[i] * x[i];
+      nrm = std::sqrt(nrm);
+      if (!(nrm > 0.0)) nrm = 1.0;
+      for (int i = 0; i < n; ++i) b[i] = x[i] / nrm;
+    }
+    for (int i = 0; i < n; ++i) X[(size_t)i * k + j] = b[i];
   }
 }
 

@@ -126,6 +126,7 @@ SIGNATURES = {
     "ocm_conv1d_wgrad": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_i32, c_i32, c_i32,
                                  c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ocm_chan_sum": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
+    "ocm_eigh_f64": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_i32, c_void_p, c_void_p]),
     "ocm_prep_materialised": (c_i32, [c_void_p, ctypes.POINTER(c_i64)]),
     "ocm_prep_rowstats_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p]),
     "ocm_prep_apply_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_i64,

@@ -94,6 +94,10 @@ def _applicable(base_est, X, y, cv, lv_values, param_grid):
             return None
     if max(lv_values) > 64 or min(lv_values) < 1:
         return None
+    from .prepview import PrepView
+
+    if isinstance(X, PrepView):
+        return cls_idx, labels[0], combos, base
     if (X.dtype == torch.float64) if isinstance(X, torch.Tensor) else (np.asarray(X).dtype == np.float64):
         return None  # float64 spectra: the refit loop runs the fp64 fits (utils/SIMCA.py:64-66 dtype rule)
     return cls_idx, tl, combos, base

@@ -208,12 +208,30 @@ def cov_from_gram(terms, shift32: torch.Tensor, n: int):
     return C, mean
 
 
-def eig_topk(C: torch.Tensor, k: int, theta_mode: int, tol=EIG_TOL, max_iter=EIG_MAX_ITER, theta3_slice=(0, 1)):
-    """Top-k eigenpairs + tail moments of C (ocm_eig_topk_ex).  Raises
-    ``OcmNotConverged`` when the Ritz residuals miss ``tol`` within ``max_iter``
-    iterations (loadings and limits from an unconverged subspace are never
-    handed on).  ``theta3_slice = (s, S)``: this call's share of the θ3 trace
-    work (the ranks of a sharded fit sum the partials)."""
+def eigh_dense(C: torch.Tensor, k: int = 0):
+    """Every eigenvalue of the symmetric fp64 C (descending) and, for k > 0,
+    the leading k eigenvectors as rows with the svd_flip sign
+    (ocm_eigh_f64: Householder tridiagonalisation on the GPU)."""
+    p = C.shape[0]
+    dev = C.device
+    evals = torch.empty(p, dtype=torch.float64, device=dev)
+    evecs = torch.empty((k, p), dtype=torch.float64, device=dev) if k > 0 else None
+    check(_lib.load().ocm_eigh_f64(Context.get(dev.index).handle, ptr(C.contiguous()), p, ptr(evals), int(k),
+                                   ptr(evecs), _stream(dev)), "ocm_eigh_f64")
+    return evals, evecs
+
+
+def eig_topk(C: torch.Tensor, k: int, theta_mode: int, tol=EIG_TOL, max_iter=EIG_MAX_ITER, theta3_slice=(0, 1),
+             dense_fallback=True):
+    """Top-k eigenpairs + tail moments of C (ocm_eig_topk_ex).  When the Ritz
+    residuals miss ``tol`` within ``max_iter`` iterations (no usable spectral
+    gap after component k: a flat noise floor), the loadings of the
+    unconverged subspace are never handed on: the dense solver
+    (``eigh_dense``) gives the exact top-k and θ_m = Σ_{i>k} λ_iᵐ, as the
+    reference's full SVD would (utils/SIMCA.py:64-66, 189-191), with a
+    warning; ``dense_fallback=False`` raises ``OcmNotConverged`` instead.
+    ``theta3_slice = (s, S)``: this call's share of the θ3 trace work (the
+    ranks of a sharded fit sum the partials)."""
     p = C.shape[0]
     dev = C.device
     evals = torch.empty(k, dtype=torch.float64, device=dev)
@@ -225,10 +243,22 @@ def eig_topk(C: torch.Tensor, k: int, theta_mode: int, tol=EIG_TOL, max_iter=EIG
                                      int(theta3_slice[1]), ptr(evals), ptr(evecs), ptr(theta), ctypes.byref(iters),
                                      _stream(dev))
     if rc == _lib.OCM_ERR_NOCONV:
-        raise _lib.OcmNotConverged(
-            f"ocm_eig_topk: the leading {k} eigenpairs of the {p}x{p} covariance did not converge to tol={tol} in "
-            f"{max_iter} iterations (no usable spectral gap after component {k}); pick n_components at a gap in "
-            "the spectrum")
+        msg = (f"ocm_eig_topk: the leading {k} eigenpairs of the {p}x{p} covariance did not converge to tol={tol} "
+               f"in {max_iter} iterations (no usable spectral gap after component {k})")
+        if not dense_fallback:
+            raise _lib.OcmNotConverged(msg + "; pick n_components at a gap in the spectrum")
+        import warnings
+
+        warnings.warn(msg + "; using the dense eigensolver (ocm_eigh_f64)", RuntimeWarning, stacklevel=2)
+        lam, vec = eigh_dense(C, k)
+        tail = lam[k:]
+        th = torch.zeros(3, dtype=torch.float64, device=dev)
+        if theta_mode >= 1:
+            th[0] = tail.sum()
+            th[1] = (tail * tail).sum()
+        if theta_mode >= 2 and theta3_slice[0] == 0:  # the whole θ3 on slice 0 (the ranks sum the slices)
+            th[2] = (tail * tail * tail).sum()
+        return lam[:k].clone(), vec, th, int(max_iter)
     check(rc, "ocm_eig_topk_ex")
     return evals, evecs, theta, int(iters.value)
 

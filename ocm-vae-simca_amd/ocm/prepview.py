@@ -130,6 +130,35 @@ class PrepView:
                                              stream_handle(self.X.device)), "ocm_prep_apply_f32")
         return out
 
+    def __getitem__(self, idx):
+        """Row selection (``X[rows]``, ``X[rows, :]``, as the CV refit loop
+        does): a view of the selected raw rows (the reference's X[rows] is a
+        copy too); anything else indexes the materialised matrix."""
+        if isinstance(idx, tuple):
+            if len(idx) == 2 and isinstance(idx[1], slice) and idx[1] == slice(None):
+                idx = idx[0]
+            else:
+                return self.materialize()[idx]
+        if isinstance(idx, slice):
+            sel = idx
+        else:
+            sel = torch.as_tensor(idx, device=self.X.device)
+            if sel.dtype == torch.bool:
+                sel = torch.nonzero(sel).flatten()
+            sel = sel.to(torch.int64)
+        sub = PrepView.__new__(PrepView)
+        sub.__dict__.update(self.__dict__)
+        sub.X = self.X[sel]
+        if sub.X.dim() != 2:
+            raise IndexError("PrepView: select rows (a 2-D view)")
+        sub.X = sub.X.contiguous()
+        sub._rowstat = self._rowstat[sel].contiguous() if self._rowstat is not None else None
+        return sub
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.numpy()
+        return a if dtype is None else a.astype(dtype)
+
     def cpu(self):
         return self.materialize().cpu()
 

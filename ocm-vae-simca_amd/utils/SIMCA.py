@@ -25,8 +25,9 @@ Documented deviations:
   PCA attributes drivers read (``components_``, ``mean_``, ``transform``,
   ``inverse_transform``);
 * ``eigs_all`` holds the leading k eigenvalues from the HIP eigensolver and,
-  on first access only, the rest of the spectrum (a diagnostic no limit uses;
-  the θ moments come from device traces);
+  on first access only, the rest of the spectrum from libocm's dense
+  eigensolver (a diagnostic no limit uses; the θ moments come from device
+  traces);
 * float64 inputs are computed in float64 as the reference's PCA then is
   (fp64-MFMA Gram, fp64 scoring; T, Q and ``_model`` arrays float64);
 * ``n_components`` may be any k ≤ p as in the reference; beyond 64 the
@@ -34,8 +35,9 @@ Documented deviations:
   launch per 64 components, and a CV sweep with ``LV_max`` > 64 runs the
   generic refit loop instead of the fold engine;
 * a fit whose leading k eigenpairs do not converge (no spectral gap after
-  component k within the iteration budget) raises ``ocm.OcmNotConverged``
-  instead of returning loadings of an unconverged subspace.
+  component k within the iteration budget) takes the dense eigensolver
+  (``ocm_eigh_f64``) with a RuntimeWarning instead of returning loadings of
+  an unconverged subspace.
 """
 from __future__ import annotations
 
@@ -390,12 +392,14 @@ def _device_labels(y, device):
 
 
 def _all_eigs(fit: engine.ClassFit, n: int):
-    """Full explained-variance spectrum (min(n, p) values, descending): the
-    leading k from the HIP eigensolver, the rest from the HBM-resident
-    covariance on first access (diagnostic only)."""
+    """Full explained-variance spectrum (min(n, p) values, descending,
+    utils/SIMCA.py:88): the leading k from the fit's eigensolver, the rest from
+    the dense libocm eigensolver on the HBM-resident covariance on first
+    access (``ocm_eigh_f64``; diagnostic only, no limit uses it)."""
     r = min(n, fit.p)
     if fit.C is None:
         return fit.evals_host.copy()
-    full = torch.linalg.eigvalsh(fit.C).flip(0)[:r].cpu().numpy()
+    lam, _ = engine.eigh_dense(fit.C, 0)
+    full = lam[:r].cpu().numpy()
     full[: fit.k] = fit.evals_host
     return full

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--k", default="16,20")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--kernels", default="diag,full")
+    ap.add_argument("--prep", default="none", help="comma list of none, snv (SNV only), snv5 (SNV + w 5 d 1), "
+                    "sg15 (w 15 d 1): score lazy views (diag kernel)")
     ap.add_argument("--tag", default=os.path.basename(os.environ.get("OCM_LIB", "libocm.so")))
     args = ap.parse_args()
     import torch
@@ -35,6 +37,31 @@ def main():
     n, p = args.rows, args.p
     X = synth_device(n, p, 20, 7, dev)
     mean = X[:4096].double().mean(0)
+    from ocm import preprocess
+
+    views = {"none": X, "snv": preprocess.snv_savgol(X, None, lazy=True),
+             "snv5": preprocess.snv_savgol(X, 5, 2, 1, lazy=True),
+             "sg15": preprocess.snv_savgol(X, 15, 2, 1, snv=False, lazy=True)}
+    for pv in args.prep.split(","):
+        if pv == "none":
+            continue
+        Xv = views[pv]
+        Xv.rowstat()
+        for k in [int(v) for v in args.k.split(",")]:
+            P, _ = torch.linalg.qr(torch.randn(p, k, dtype=torch.float64, device=dev))
+            P = P.T.contiguous()
+            inv = torch.linspace(1.0, 0.1, k, dtype=torch.float64, device=dev)
+            engine.score(Xv, None, n, P, mean, inv, want_stats=True)
+            st = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(args.reps):
+                engine.score(Xv, None, n, P, mean, inv, want_stats=True)
+            e1.record(st)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / args.reps
+            print(json.dumps({"lib": args.tag, "kernel": "diag", "prep": pv, "k": k, "p": p, "rows": n,
+                              "ms": round(ms, 4), "GBs_alg": round(4 * p * n / ms / 1e6, 1)}), flush=True)
     for k in [int(v) for v in args.k.split(",")]:
         P, _ = torch.linalg.qr(torch.randn(p, k, dtype=torch.float64, device=dev))
         P = P.T.contiguous()

@@ -215,8 +215,8 @@ def test_k96_wide_block_vs_fp64_oracle():
 
 
 def test_eig_not_converged_raises():
-    """a covariance with no gap at k (a nearly flat spectrum)
-    cannot converge in a short iteration budget; the engine raises
+    """A covariance with no gap at k (a nearly flat spectrum) cannot converge in
+    a short iteration budget: with ``dense_fallback=False`` the engine raises
     OcmNotConverged instead of handing on an unconverged subspace."""
     import torch
 
@@ -228,9 +228,83 @@ def test_eig_not_converged_raises():
     lam = np.linspace(1.0, 0.995, p)
     C = torch.from_numpy((Qm * lam) @ Qm.T).cuda()
     with pytest.raises(OcmNotConverged):
-        engine.eig_topk(C, k, 2, max_iter=30)
+        engine.eig_topk(C, k, 2, max_iter=30, dense_fallback=False)
     # the same call with a gap converges
     lam[:k] *= 10
     C = torch.from_numpy((Qm * lam) @ Qm.T).cuda()
     ev, _, _, it = engine.eig_topk(C, k, 2, max_iter=30)
     np.testing.assert_allclose(ev.cpu().numpy(), np.sort(lam)[::-1][:k], rtol=1e-10)
+
+
+def test_eig_not_converged_dense_fallback():
+    """on a flat tail the default path does not abort (the
+    reference's full SVD always returns): the dense eigensolver gives the
+    top-k, θ1..θ3 from the eigenvalue tail, with a RuntimeWarning — and a
+    SIMCA fit on spectra whose noise floor is flat at k completes and matches
+    the fp64 oracle's limits."""
+    import torch
+
+    from ocm import engine
+
+    p, k = 256, 20
+    rng = np.random.default_rng(9)
+    Qm, _ = np.linalg.qr(rng.standard_normal((p, p)))
+    lam = np.linspace(1.0, 0.995, p)
+    C = (Qm * lam) @ Qm.T
+    with pytest.warns(RuntimeWarning, match="dense eigensolver"):
+        ev, vec, th, _ = engine.eig_topk(torch.from_numpy(C).cuda(), k, 2, max_iter=30)
+    w = np.sort(np.linalg.eigvalsh(C))[::-1]
+    np.testing.assert_allclose(ev.cpu().numpy(), w[:k], rtol=1e-12)
+    tail = w[k:]
+    np.testing.assert_allclose(th.cpu().numpy(), [tail.sum(), (tail ** 2).sum(), (tail ** 3).sum()], rtol=1e-12)
+    V = vec.cpu().numpy()
+    np.testing.assert_allclose(V @ V.T, np.eye(k), atol=1e-10)
+    np.testing.assert_allclose(V @ C, ev.cpu().numpy()[:, None] * V, atol=1e-10)
+
+
+@pytest.mark.parametrize("p,k", [(2048, 20), (300, 7), (3, 2), (1, 1), (64, 64)])
+def test_eigh_dense_vs_numpy(p, k):
+    """ocm_eigh_f64 (Householder tridiagonalisation on the GPU, QL + inverse
+    iteration on the host): all eigenvalues vs numpy.linalg.eigvalsh, the top-k
+    vectors orthonormal with residuals at fp64 level and the svd_flip sign;
+    a covariance with repeated eigenvalues included."""
+    import torch
+
+    from ocm import engine
+
+    rng = np.random.default_rng(p)
+    if p >= 64:
+        Qm, _ = np.linalg.qr(rng.standard_normal((p, p)))
+        lam = np.concatenate([np.linspace(50, 10, min(k, p)), np.full(max(p - k, 0), 0.5)])[:p]
+        lam[k // 2: k // 2 + 3] = lam[k // 2]  # a repeated eigenvalue inside the top k
+        C = (Qm * lam) @ Qm.T
+    else:
+        A = rng.standard_normal((p, p))
+        C = A @ A.T
+    ev, vec = engine.eigh_dense(torch.from_numpy(C).cuda(), k)
+    ev = ev.cpu().numpy()
+    w = np.sort(np.linalg.eigvalsh(C))[::-1]
+    np.testing.assert_allclose(ev, w, rtol=0, atol=1e-12 * np.abs(w).max() * max(1, p // 64))
+    V = vec.cpu().numpy()
+    np.testing.assert_allclose(V @ V.T, np.eye(k), atol=1e-9)
+    np.testing.assert_allclose(V @ C, ev[:k, None] * V, atol=1e-9 * np.abs(w).max())
+    idx = np.argmax(np.abs(V), axis=1)
+    assert np.all(V[np.arange(k), idx] > 0)
+
+
+def test_eigs_all_from_libocm(golden_dir):
+    """`_model[cls]['eigs_all']` (utils/SIMCA.py:88): the whole spectrum from
+    ocm_eigh_f64, against the reference's values at the north-star shape."""
+    from utils import SIMCA
+
+    g = _load(golden_dir, "simca_ns.npz")
+    X_fit, _, k = _regen(g)
+    est = SIMCA(n_components=k, model_class=0, verbose=False)
+    with contextlib.redirect_stdout(io.StringIO()):
+        est.fit(X_fit, np.zeros(len(X_fit), dtype=np.int64))
+    got = est._model[0]["eigs_all"]
+    ref = g["eigs_all"]
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got[:k], ref[:k], rtol=1e-5)
+    # the float32 SVD's tail is noise-level: compare to its scale
+    np.testing.assert_allclose(got, ref, rtol=0, atol=2e-5 * ref[0])

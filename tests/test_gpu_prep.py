@@ -211,3 +211,36 @@ def test_c2_view_vs_fp64_oracle(snv, w, po, d):
     c0 = materialised_count(0)
     _c2_vs_oracle(snv, w, po, d)
     assert materialised_count(0) == c0  # fit and predict ran on the fused paths
+
+
+@pytest.mark.parametrize("fast", [True, False])
+def test_cv_grid_on_view(fast):
+    """cross_validate_simca_grid on a lazy view (fold engine, and the generic
+    refit loop slicing X[rows, :]) = the same on the materialised rows."""
+    import torch
+
+    from utils import SIMCA, ClasswiseKFoldWithExternalVal, cross_validate_simca_grid
+    import utils.CVSIMCA as CVmod
+
+    n, p = 6000, 512
+    X = _spectra(n, p, seed=21)
+    y = np.zeros(n, dtype=np.int64)
+    y[::7] = 1
+    v = _view(torch.from_numpy(X).cuda(), True, 5, 2, 1)
+    outs = []
+    for data in (v, v.materialize()):
+        saved = CVmod._fast_grid
+        if not fast:
+            CVmod._fast_grid = lambda *a, **k: (None, None)
+        try:
+            with contextlib.redirect_stdout(io.StringIO()):
+                outs.append(cross_validate_simca_grid(
+                    SIMCA(verbose=False), data, y, ClasswiseKFoldWithExternalVal(n_splits=4, cls_label=0),
+                    LV_min=3, LV_max=6, param_grid={"type": ["alt", "sim"]}, print_summary=False,
+                    store_predictions=True))
+        finally:
+            CVmod._fast_grid = saved
+    a, b = outs
+    assert [(r["LV"], r["spec"], r["sens"]) for r in a["results"]] == \
+        [(r["LV"], r["spec"], r["sens"]) for r in b["results"]]
+    assert a["best_LV"] == b["best_LV"]

@@ -29,8 +29,18 @@ int main(int argc, char** argv) {
   std::vector<double> A((size_t)n * n), out((size_t)n * n + n);
   if (std::fread(A.data(), 8, A.size(), f) != A.size()) return 2;
   std::fclose(f);
-  if (mode[0] == 'e') ocm::host_sym_eig(A.data(), n, out.data() + (size_t)n * n, out.data());
-  else ocm::host_chol_inv_t(A.data(), n, out.data());
+  if (mode[0] == 'e') {
+    ocm::host_sym_eig(A.data(), n, out.data() + (size_t)n * n, out.data());
+  } else if (mode[0] == 't') {  // tridiagonal: eigenvalues by QL, the top k vectors by inverse iteration
+    std::vector<double> d(n), e(n > 1 ? n - 1 : 1);
+    for (int i = 0; i < n; ++i) d[i] = A[(size_t)i * n + i];
+    for (int i = 0; i + 1 < n; ++i) e[i] = A[(size_t)(i + 1) * n + i];
+    ocm::host_tridiag_eigvals(d.data(), e.data(), n, out.data() + (size_t)n * n);
+    const int k = n < 12 ? n : 12;
+    ocm::host_tridiag_invit(d.data(), e.data(), n, out.data() + (size_t)n * n, k, out.data());
+  } else {
+    ocm::host_chol_inv_t(A.data(), n, out.data());
+  }
   FILE* g = std::fopen(argv[3], "wb");
   std::fwrite(out.data(), 8, out.size(), g);
   std::fclose(g);
@@ -115,3 +125,37 @@ def test_chol_inverse_transpose(driver, n, cond):
     # CholQR identity: (W M)ᵀ (W M) = I for S = WᵀW
     W = np.linalg.cholesky(S).T  # any W with WᵀW = S
     np.testing.assert_allclose((W @ M).T @ (W @ M), np.eye(n), atol=1e-5 if cond > 1e8 else 1e-10)
+
+
+def _tridiag(d, e):
+    return np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
+
+
+@pytest.mark.parametrize("case", ["random", "graded", "clustered", "split"])
+def test_tridiag_eigvals_and_inverse_iteration(driver, case):
+    """The dense fallback / eigs_all path (ocm_eigh_f64): QL eigenvalues of the
+    Householder tridiagonal and inverse-iteration vectors for the top 12,
+    including exactly repeated eigenvalues (a split tridiagonal)."""
+    rng = np.random.default_rng(3)
+    n = 300
+    if case == "random":
+        d, e = rng.standard_normal(n), rng.standard_normal(n - 1)
+    elif case == "graded":
+        d, e = np.logspace(2, -6, n), 1e-3 * rng.standard_normal(n - 1)
+    elif case == "clustered":
+        d, e = 1.0 + 1e-9 * rng.standard_normal(n), 1e-10 * rng.standard_normal(n - 1)
+        d[:5] += 3.0
+    else:  # three equal blocks: every eigenvalue three times
+        b = 100
+        db, eb = rng.standard_normal(b), rng.standard_normal(b - 1)
+        d = np.tile(db, 3)
+        e = np.concatenate([eb, [0.0], eb, [0.0], eb])
+    T = _tridiag(d, e)
+    X, ev = _run(driver, "t", T)
+    ref = np.sort(np.linalg.eigvalsh(T))[::-1]
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(ev, ref, rtol=0, atol=1e-13 * scale * n)
+    k = 12
+    V = X.reshape(-1)[: n * k].reshape(n, k)
+    np.testing.assert_allclose(V.T @ V, np.eye(k), atol=1e-9)
+    np.testing.assert_allclose(T @ V, V * ev[:k], atol=1e-10 * scale)
