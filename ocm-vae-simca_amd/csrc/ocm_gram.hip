@@ -2646,6 +2646,14 @@ int gram_dispatch(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
 
 }  // namespace
 
+namespace ocm {
+int gram_rows_i8(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t n, int p, const float* shift, double* G,
+                 double* colsum, hipStream_t st) {
+  const int64_t seg[2] = {0, n};
+  return gram_dispatch(ctx, X, ldx, nullptr, n, p, shift, seg, 1, OCM_GRAM_I8X3, 0, G, colsum, st);
+}
+}  // namespace ocm
+
 extern "C" {
 
 int ocm_colmean_f32(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,

@@ -153,6 +153,11 @@ inline PrepArgs prep_args(const ocm_prep* p) {
 }
 
 int check_prep(const ocm_prep* prep, int p, const char* who);
+// G = Σ_rows (x − shift)(x − shift)ᵀ of n float32 rows on the default i8×3 path
+// (ocm_gram.hip); uses the context workspace from offset 0 (callers must not
+// hold workspace carve-outs across it).
+int gram_rows_i8(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t n, int p, const float* shift, double* G,
+                 double* colsum, hipStream_t st);
 int prep_apply(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int p, const PrepArgs& pa,
                float* out, int64_t ldo, hipStream_t st);
 

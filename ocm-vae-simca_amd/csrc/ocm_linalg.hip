@@ -1194,6 +1194,60 @@ int dgemm_ta(const double* A, const double* B, int p, int b, double* S, double* 
   return OCM_OK;
 }
 
+// θ3 = trace(D³) of the deflated covariance D = Δ + O (Δ its diagonal, O the
+// off-diagonal part), expanded so that only O goes through a Gram:
+//   trace(D³) = Σ_i Δ_i³ + 3 Σ_i Δ_i Σ_j O_ij² + Σ_ij O_ij (O²)_ij
+// (the terms with one O vanish: O_ii = 0).  The first two are exact fp64 sums
+// over rows [r0, r1) (this slice's rows); O² is the i8×3 Gram of O's rows
+// [r0, r1) (a Gram over a row subset is a partial of O², and the trace is
+// linear in it), and the last term pairs it with all of O.  O has no
+// dominant diagonal, so the Gram's outlier guard stays quiet.
+__global__ __launch_bounds__(256) void k_theta3_diag(const double* __restrict__ D, int p, int r0, int r1,
+                                                      float* __restrict__ O32, double* __restrict__ part) {
+  __shared__ double red[4];
+  const int i = r0 + blockIdx.x;
+  double acc = 0.0;
+  if (i < r1) {
+    const double* row = D + (int64_t)i * p;
+    const double di = row[i];
+    double s = 0.0;
+    for (int j = threadIdx.x; j < p; j += 256) {
+      const double o = j == i ? 0.0 : row[j];
+      s += o * o;
+    }
+    acc = 3.0 * di * s;
+    if (threadIdx.x == 0) acc += di * di * di;
+  }
+  acc = wave_sum_f64(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void k_offdiag_f32(const double* __restrict__ D, int p, float* __restrict__ O32) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)p * p) return;
+  const int i = (int)(e / p), j = (int)(e % p);
+  O32[e] = i == j ? 0.f : (float)D[e];
+}
+
+// partial Σ_ij O_ij G_ij, one row per workgroup (rows in order: deterministic)
+__global__ __launch_bounds__(256) void k_trace_og(const float* __restrict__ O32, const double* __restrict__ G, int p,
+                                                   double* __restrict__ part) {
+  __shared__ double red[4];
+  const int64_t base = (int64_t)blockIdx.x * p;
+  double s = 0.0;
+  for (int j = threadIdx.x; j < p; j += 256) s += (double)O32[base + j] * G[base + j];
+  s = wave_sum_f64(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void k_add3(const double* __restrict__ a, const double* __restrict__ b, double* __restrict__ out) {
+  if (threadIdx.x == 0) *out = *a + *b;
+}
+
 int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
                   int32_t theta_mode, int32_t slice, int32_t nslices, double* evals_out, double* evecs_out,
                   double* theta_out, int32_t* iters_out, hipStream_t st) {
@@ -1228,22 +1282,12 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   const size_t pb = (size_t)p * b, bb = (size_t)b * b;
   const int nblk = (p + 63) / 64;
   const size_t def_blocks = (size_t)((p + DT - 1) / DT) * ((p + DT - 1) / DT);  // deflate GEMM tiles
-  // the trace GEMM's K split (the trace is linear in the K segments; the
-  // split fixes the fp64 summation order, so the product library never
-  // changes it — `make exp` builds read OCM_TRACE_KSPLIT for A/B)
-#ifdef OCM_EXP_SELECTORS
-  static const int trace_ks_env = getenv("OCM_TRACE_KSPLIT") ? atoi(getenv("OCM_TRACE_KSPLIT")) : 0;
-  const int TRACE_KSPLIT = trace_ks_env >= 1 && trace_ks_env <= 16 ? trace_ks_env : 4;
-#else
-  constexpr int TRACE_KSPLIT = 4;
-#endif
-  const size_t trace_wgs = (size_t)TRACE_KSPLIT * ((p + DT - 1) / DT) * ((p + DT - 1) / DT);
   const size_t plane_cap = std::max((size_t)ksplit * pb, wide ? 16 * bb : 0);
   size_t need = (6 * pb + 6 * bb + plane_cap + (wide ? 0 : (size_t)nblk * bb) + 4 * b + 64) * sizeof(double);
   need += ((size_t)CQ_G * 768 + 2048 + 64) * sizeof(double) + 3 * 256;  // CholQR partials, M1/M2, ticket
   const int cv_rb = (p + 15) / 16;  // k_cv32 row blocks
   need += ((size_t)cv_rb * 2 * 512) * sizeof(double) + (size_t)cv_rb * sizeof(unsigned) + 2 * 256;
-  if (theta_mode) need += ((size_t)p * p + 4 * (size_t)k * p + 2 * def_blocks + trace_wgs + 8) * sizeof(double);
+  if (theta_mode) need += ((size_t)p * p + 4 * (size_t)k * p + 2 * def_blocks + 8) * sizeof(double);
   void* w = ocm::workspace(ctx, need + 16 * 256, st);
   if (!w) return OCM_ERR_NOMEM;
   ocm::Carve cv{static_cast<char*>(w)};
@@ -1433,7 +1477,6 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     if (rc) return rc;
     double* Ct = cv.take<double>((size_t)p * p);
     double* dpart = cv.take<double>(2 * def_blocks);
-    double* tpart = cv.take<double>(trace_wgs);
     double* tr2 = cv.take<double>(2);
     double* U = cv.take<double>((size_t)2 * k * p);
     double* Wt = cv.take<double>((size_t)2 * k * p);
@@ -1447,23 +1490,39 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     hipLaunchKernelGGL(k_sum_pairs, dim3(1), dim3(256), 0, st, dpart, (int)(gd.x * gd.y), tr2);
     OCM_CHECK_LAUNCH("k_sum_pairs");
     OCM_HIP(hipMemcpyAsync(theta_out, tr2, 2 * sizeof(double), hipMemcpyDeviceToDevice, st));
-    // this slice's share of the upper-triangle tiles of the trace GEMM
-    const int nt = (p + DT - 1) / DT;
-    const int ntri = nt * (nt + 1) / 2;
-    const int t0 = (int)((int64_t)ntri * slice / nslices), t1 = (int)((int64_t)ntri * (slice + 1) / nslices);
-    if (theta_mode >= 2 && t1 > t0) {
-      // split-K: 4× the workgroups of the upper-triangle tile grid (528 tiles at p = 2048 fill the
-      // chip only once), partial traces summed in a fixed order.  (A 128×128-tile variant at one wave
-      // per SIMD measured 393 vs 234 µs at p = 2048: this one keeps four waves per SIMD.)
-      int kper = (p + TRACE_KSPLIT - 1) / TRACE_KSPLIT;
-      kper = (kper + DBK - 1) / DBK * DBK;
-      const int nz = (p + kper - 1) / kper;
-      dim3 g((unsigned)(t1 - t0), 1, (unsigned)nz);
-      hipLaunchKernelGGL(k_dgemm<1>, g, dim3(256), 0, st, Ct, (int64_t)p, Ct, (int64_t)p, nullptr, 0, p, p, p, kper, Ct,
-                         (int64_t)p, tpart, t0);
-      OCM_CHECK_LAUNCH("k_dgemm trace");
-      hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, tpart, (int)(g.x * g.z), theta_out + 2);
-      OCM_CHECK_LAUNCH("k_sum_partials");
+    // θ3: this slice's rows of the Δ / O expansion (k_theta3_diag), then the
+    // i8×3 Gram of those rows of O.  The Gram takes the context workspace, so
+    // O (f32), its Gram and the partials live in stream-ordered allocations and
+    // everything the eigensolver's carve-outs feed is already in the outputs.
+    const int r0 = (int)((int64_t)p * slice / nslices), r1 = (int)((int64_t)p * (slice + 1) / nslices);
+    if (theta_mode >= 2 && r1 > r0) {
+      const int nr = r1 - r0;
+      float* O32 = nullptr;
+      double* Gp = nullptr;
+      const size_t pp = (size_t)p * p;
+      OCM_HIP(hipMallocAsync(reinterpret_cast<void**>(&O32), pp * sizeof(float), st));
+      OCM_HIP(hipMallocAsync(reinterpret_cast<void**>(&Gp), (pp + 3 * (size_t)p + 8) * sizeof(double), st));
+      double* csum = Gp + pp;
+      double* dpart3 = csum + p;  // p row partials of the Δ terms
+      double* opart = dpart3 + p;  // p row partials of the O·O² term
+      double* t3 = opart + p;
+      hipLaunchKernelGGL(k_theta3_diag, dim3(nr), dim3(256), 0, st, Ct, p, r0, r1, O32, dpart3);
+      hipLaunchKernelGGL(k_offdiag_f32, dim3((unsigned)((pp + 255) / 256)), dim3(256), 0, st, Ct, p, O32);
+      hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, dpart3, nr, t3);
+      OCM_CHECK_LAUNCH("k_theta3_diag");
+      // the shift of the Gram is zero: a p-vector of zeros (taken from the partials' tail)
+      float* zshift = reinterpret_cast<float*>(opart);
+      OCM_HIP(hipMemsetAsync(zshift, 0, (size_t)p * sizeof(float), st));
+      rc = ocm::gram_rows_i8(ctx, O32 + (size_t)r0 * p, p, nr, p, zshift, Gp, csum, st);
+      if (rc == OCM_OK) {
+        hipLaunchKernelGGL(k_trace_og, dim3(p), dim3(256), 0, st, O32, Gp, p, opart);
+        hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, opart, p, t3 + 1);
+        hipLaunchKernelGGL(k_add3, dim3(1), dim3(64), 0, st, t3, t3 + 1, theta_out + 2);
+        OCM_CHECK_LAUNCH("k_trace_og");
+      }
+      const hipError_t e1 = hipFreeAsync(O32, st), e2 = hipFreeAsync(Gp, st);
+      if (rc) return rc;
+      if (e1 != hipSuccess || e2 != hipSuccess) return ocm::fail(OCM_ERR_HIP, "hipFreeAsync (theta3)");
     } else {
       OCM_HIP(hipMemsetAsync(theta_out + 2, 0, sizeof(double), st));
     }

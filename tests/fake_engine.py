@@ -84,19 +84,18 @@ def cov_from_packed(packed, p):
 
 
 def _theta3_slice(D, slice_):
-    """Σ over this slice's 64×64 upper-triangle tiles (off-diagonal ×2) of
-    (D²)∘D — the tile split of the ocm_eig_topk_ex trace GEMM."""
+    """This slice's share of θ3 = trace(D³) as ocm_eig_topk_ex splits it: rows
+    [p·s/S, p·(s+1)/S) of the Δ / O expansion (Δ the diagonal, O the rest),
+    Σ_i Δ_i³ + 3 Σ_i Δ_i Σ_j O_ij² + Σ_ij O_ij (O_rowsᵀ O_rows)_ij."""
     p = D.shape[0]
-    nt = (p + 63) // 64
-    tiles = [(i, j) for i in range(nt) for j in range(i, nt)]
     s, S = slice_
-    t0, t1 = len(tiles) * s // S, len(tiles) * (s + 1) // S
-    D2 = D @ D
-    tot = 0.0
-    for i, j in tiles[t0:t1]:
-        blk = (D2[i * 64:(i + 1) * 64, j * 64:(j + 1) * 64] * D[i * 64:(i + 1) * 64, j * 64:(j + 1) * 64]).sum()
-        tot += blk if i == j else 2.0 * blk
-    return tot
+    r0, r1 = p * s // S, p * (s + 1) // S
+    dg = np.diag(D)
+    O = D - np.diag(dg)
+    rows = slice(r0, r1)
+    t = (dg[rows] ** 3).sum() + 3.0 * (dg[rows] * (O[rows] ** 2).sum(1)).sum()
+    G = O[rows].T @ O[rows]
+    return t + (O * G).sum()
 
 
 def eig_topk(C, k, theta_mode, tol=None, max_iter=None, theta3_slice=(0, 1)):
