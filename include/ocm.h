@@ -466,6 +466,49 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
 int ocm_chan_sum(ocm_ctx* ctx, int32_t dtype, const void* v, int32_t B, int32_t C, int32_t L, float* out,
                  void* scratch, void* stream);
 
+/* ---- the VAE training step's small tensors, fused (vae_model.py:136-158, vae_bce_nut.py:178-203,
+ * utils/final_vaesimca.py:198-224): the graphed step is bound by its kernel count, so the
+ * reparameterisation + KL, the de-standardisation + reconstruction term + total, their backward
+ * passes and Adam each take one launch.  Activations in dtype (OCM_DTYPE_*), sums fp64 with
+ * fixed-order partials, losses float32; graph-capturable (scratch caller-owned,
+ * ocm_vae_scratch_bytes(B) bytes, zeroed once before first use).
+ *
+ * ocm_vae_bottleneck_fwd: z = μ + ε·exp(½·logσ²); kl_out = −½·mean_B Σ_d (1 + logσ² − μ² − exp(logσ²))
+ *   (vae_model.py:150-152, reparameterize :124-126).  μ, logσ², ε, z [dev] B×d.
+ * ocm_vae_bottleneck_bwd: dμ = dz + dkl·μ/B, dlogσ² = dz·ε·½exp(½logσ²) − ½·dkl·(1 − exp(logσ²))/B
+ *   (dz or dkl may be NULL: no gradient from that output).
+ * ocm_vae_recon_fwd: x̂ = xs·std + mean (forward's de-standardisation, vae_model.py:130-134); kind
+ *   OCM_VAE_LOSS_BCE: mean BCE-with-logits(x̂, clamp((x − min_x)/(max_x − min_x + eps), 0, 1)) per
+ *   sample min / max (vae_model.py:153-156); OCM_VAE_LOSS_MSE: mean (x̂ − x)² (final_vaesimca.py:208);
+ *   out2 [dev] {recon + β·kl, recon} (kl [dev] nullable: 0); gxs_out [dev] B×L f32 = d recon / d xs.
+ * ocm_vae_recon_bwd: dxs = dtotal·gxs (n values, written in dtype), dkl_out = β·dtotal (nullable).
+ * ocm_adam_step: torch.optim.Adam (L2 weight_decay, no amsgrad) over `ntensors` tensors of
+ *   `table` [dev] (offsets: prefix of numel, total = Σ numel); step [dev] f32 counter, advanced by
+ *   one per call (bias corrections 1 − βᵗ). */
+#define OCM_VAE_LOSS_BCE 0
+#define OCM_VAE_LOSS_MSE 1
+typedef struct ocm_adam_tensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t offset;
+  int64_t numel;
+} ocm_adam_tensor;
+size_t ocm_vae_scratch_bytes(int32_t B);
+int ocm_vae_bottleneck_fwd(ocm_ctx* ctx, int32_t dtype, const void* mu, const void* logvar, const void* eps, int32_t B,
+                           int32_t d, void* z_out, float* kl_out, void* stream);
+int ocm_vae_bottleneck_bwd(ocm_ctx* ctx, int32_t dtype, const void* dz, const float* dkl, const void* mu,
+                           const void* logvar, const void* eps, int32_t B, int32_t d, void* dmu_out, void* dlogvar_out,
+                           void* stream);
+int ocm_vae_recon_fwd(ocm_ctx* ctx, int32_t kind, const float* x, int32_t dtype, const void* xs, int32_t B, int32_t L,
+                      const float* mean, const float* std, float eps, const float* kl, float beta, float* gxs_out,
+                      float* out2, void* scratch, void* stream);
+int ocm_vae_recon_bwd(ocm_ctx* ctx, const float* dtotal, const float* gxs, int64_t n, int32_t dtype, void* dxs_out,
+                      float beta, float* dkl_out, void* stream);
+int ocm_adam_step(ocm_ctx* ctx, const ocm_adam_tensor* table, int32_t ntensors, int64_t total, float* step, float lr,
+                  float beta1, float beta2, float eps, float weight_decay, void* scratch, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

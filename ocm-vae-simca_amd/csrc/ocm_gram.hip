@@ -2303,7 +2303,11 @@ int gram_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, in
 // caller then recomputes the Gram on the bf16×3 path.
 int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
                const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
-               hipStream_t st, int64_t chunk_rows, bool k32, const PrepArgs& pa = PrepArgs{}) {
+               hipStream_t st, int64_t chunk_rows, bool k32, const PrepArgs& pa = PrepArgs{},
+               bool unguarded = false) {
+  // unguarded: an internal Gram (the eigensolver's θ3 of the off-diagonal
+  // deflated covariance) — no outlier screen (thresholds +inf, nothing marked,
+  // no read-back), not timed, ctx->last_gram_marks left alone
   const bool prep = pa.w > 0 || pa.snv;
   const int P8 = (int)ocm::align_up((size_t)p, Q8T);
   const int nt = P8 / Q8T;
@@ -2353,11 +2357,15 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
 
   OCM_HIP(hipMemsetAsync(flags, 0, (size_t)n * fw * 4, st));
   OCM_HIP(hipMemsetAsync(counters, 0, 16, st));
-  OCM_HIP(hipMemsetAsync(xhist, 0, (size_t)p * QX_BINS * 4, st));
-  hipLaunchKernelGGL(k_colexp_hist, dim3((p + 63) / 64, nsplit), dim3(256), 0, st, X, ldx, rows, nsamp, p, shift, rps,
-                     xhist, pa);
-  hipLaunchKernelGGL(k_q8_thresholds, dim3(1), dim3(1024), 0, st, xhist, nsamp, p, P8, thr);
-  OCM_CHECK_LAUNCH("k_q8_thresholds");
+  if (unguarded) {
+    OCM_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(thr), 0x7f800000, (size_t)P8, st));  // +inf
+  } else {
+    OCM_HIP(hipMemsetAsync(xhist, 0, (size_t)p * QX_BINS * 4, st));
+    hipLaunchKernelGGL(k_colexp_hist, dim3((p + 63) / 64, nsplit), dim3(256), 0, st, X, ldx, rows, nsamp, p, shift,
+                       rps, xhist, pa);
+    hipLaunchKernelGGL(k_q8_thresholds, dim3(1), dim3(1024), 0, st, xhist, nsamp, p, P8, thr);
+    OCM_CHECK_LAUNCH("k_q8_thresholds");
+  }
 
   // all quantiser launches first, then the mark count is read back while the
   // Gram runs
@@ -2424,7 +2432,7 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   if (const char* pv = getenv("OCM_GRAM8_PIECES")) pieces = std::max(1, atoi(pv));
   if (const char* qv = getenv("OCM_Q8_CG")) qcg = atoi(qv);
 #endif
-  if (capturing || k32 || tabs.size() != 1) pieces = 1;
+  if (capturing || k32 || unguarded || tabs.size() != 1) pieces = 1;
   if (pieces > 1) {
     const int64_t gch = cprefix[tab_s0[0] + tabs[0].nseg] - cprefix[tab_s0[0]];
     pieces = (int)std::min<int64_t>(pieces, gch / 2);
@@ -2452,7 +2460,7 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     double* col_g = colpart + (size_t)cprefix[s0] * nblk * P8;
     const int cgw = qcg;  // column groups per quantiser workgroup (P8 / 32 is a multiple of 4)
     dim3 gq((unsigned)((c1 - c0) * nblk * cgw), (unsigned)(P8 / Q8QC / cgw));
-    ocm::TimedRegion tq(ctx, OCM_KERNEL_QUANT, qs);
+    ocm::TimedRegion tq(ctx, OCM_KERNEL_QUANT, qs, !unguarded);
     if (prep) {
       const dim3 gp((unsigned)((c1 - c0) * nblk), (unsigned)(P8 / Q8QC));
 #define Q8P_LAUNCH(G_, H_)                                                                                        \
@@ -2486,7 +2494,7 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     const int64_t total = (c1 - c0) * nwg;
     const Q8Plan q = plan_for(s0);
     float* pg = part + (size_t)cprefix[s0] * ntiles * Q8T * Q8T;
-    ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st);
+    ocm::TimedRegion tr(ctx, OCM_KERNEL_GRAM, st, !unguarded);
 #define G8E_LAUNCH(A_, S_)                                                                                   \
   hipLaunchKernelGGL((k_gram8e<A_, S_>), dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles, (int)total, \
                      nwg, nblocks, pg, (no_remap && c0 == 0) ? -1 : (int)c0)
@@ -2522,11 +2530,12 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   // all quantiser launches first (or, with pieces, range by range on the side
   // stream), then the mark count is read back while the Gram runs
   hipEvent_t ev = nullptr;
-  if (!capturing) OCM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  const bool readback = !capturing && !unguarded;
+  if (readback) OCM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   if (pieces == 1) {
     for (size_t t = 0; t < tabs.size(); ++t) quantise(t, 0, cprefix[tab_s0[t] + tabs[t].nseg] - cprefix[tab_s0[t]]);
     OCM_CHECK_LAUNCH("k_q8_quant");
-    if (!capturing) {
+    if (readback) {
       OCM_HIP(hipMemcpyAsync(host, counters, 4, hipMemcpyDeviceToHost, st));
       OCM_HIP(hipEventRecord(ev, st));
     }
@@ -2567,6 +2576,7 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     OCM_CHECK_LAUNCH("k_colblk_sum");
     OCM_CHECK_LAUNCH("k_gram_reduce");
   }
+  if (unguarded) return OCM_OK;  // thresholds +inf: nothing was marked
   if (!capturing) {  // capturing: the fix-up runs on device-side counts
     const hipError_t e = hipEventSynchronize(ev);
     (void)hipEventDestroy(ev);
@@ -2650,7 +2660,8 @@ namespace ocm {
 int gram_rows_i8(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t n, int p, const float* shift, double* G,
                  double* colsum, hipStream_t st) {
   const int64_t seg[2] = {0, n};
-  return gram_dispatch(ctx, X, ldx, nullptr, n, p, shift, seg, 1, OCM_GRAM_I8X3, 0, G, colsum, st);
+  if (p <= SMALL_P) return gram_small(ctx, X, ldx, nullptr, p, shift, seg, 1, G, colsum, st);
+  return gram_impl8(ctx, X, ldx, nullptr, n, p, shift, seg, 1, G, colsum, st, 0, false, PrepArgs{}, true);
 }
 }  // namespace ocm
 

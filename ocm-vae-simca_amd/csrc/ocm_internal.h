@@ -37,8 +37,8 @@ struct TimedRegion {
   int id;
   hipStream_t st;
   std::pair<hipEvent_t, hipEvent_t> pr{nullptr, nullptr};
-  TimedRegion(ocm_ctx* c, int i, hipStream_t s) : ctx(c), id(i), st(s) {
-    if (!ctx->timing) return;
+  TimedRegion(ocm_ctx* c, int i, hipStream_t s, bool on = true) : ctx(c), id(i), st(s) {
+    if (!ctx->timing || !on) return;
     if (!ctx->ev_pool.empty()) {
       pr = ctx->ev_pool.back();
       ctx->ev_pool.pop_back();

@@ -673,9 +673,35 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
     }
   };
 
+  // the window u[c0 − HH .. c0 + 3 + HH] of this lane's quad in one block:
+  // the neighbouring quads of the row by ds_bpermute (lanes ±16, ±32; the
+  // quad before / after the block from the providing lanes' prev / next)
+  auto exchange = [&](const f32x4& uprev, const f32x4& ucur, const f32x4& unext, float* win)
+      __attribute__((always_inline)) {
+    constexpr int H_ = HH > 0 ? HH : 0;
+    constexpr int NL1 = H_ < 4 ? H_ : 4;
+#pragma unroll
+    for (int e = 4 - NL1; e < 4; ++e) {  // quad lq − 1 (block j − 1 for lq = 0)
+      win[H_ - 4 + e] = xlane(4 * ((lane + 48) & 63), lq == 3 ? uprev[e] : ucur[e]);
+      win[H_ + 4 + (e - (4 - NL1))] =
+          xlane(4 * ((lane + 16) & 63), lq == 0 ? unext[e - (4 - NL1)] : ucur[e - (4 - NL1)]);
+    }
+    if constexpr (H_ > 4) {
+#pragma unroll
+      for (int e = 8 - H_; e < 4; ++e)  // quad lq − 2
+        win[H_ - 8 + e] = xlane(4 * (lane ^ 32), lq >= 2 ? uprev[e] : ucur[e]);
+#pragma unroll
+      for (int e = 0; e < H_ - 4; ++e)  // quad lq + 2
+        win[H_ + 8 + e] = xlane(4 * (lane ^ 32), lq <= 1 ? unext[e] : ucur[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) win[H_ + e] = ucur[e];
+  };
+
   auto sweep1 = [&](f32x4 (&Y)[NJ], f32x4& hy, int buf, int64_t tile) __attribute__((always_inline)) {
     f32x4 acA = {0.f, 0.f, 0.f, 0.f}, acB = acA, acC = acA, acD = acA, acE = acA, acF = acA;
     f32x4 yE = acA;  // lazy view: this lane's outputs among the row's first / last HH columns
+    float win[4 + 2 * (HH > 0 ? HH : 0)];  // lazy view: the window of the next block to transform
     float mr = 0.f, sr = 1.f;
     f32x4 uprev = acA, ucur = acA, unext = acA;
     if constexpr (PREP) {
@@ -707,6 +733,14 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
           edge_fix(yE, ul, sr, false);
         }
       }
+      // block 0's window (uprev = the halo, ucur = Y[0], unext = Y[1])
+      unext = Y[1];
+      if (psub)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) unext[e] = __fsub_rn(unext[e], mr);
+      exchange(uprev, ucur, unext, win);
+      uprev = ucur;
+      ucur = unext;
     }
     double t64[4] = {0.0, 0.0, 0.0, 0.0}, x164[4] = {0.0, 0.0, 0.0, 0.0};
     f32x4 aN = P0s[b1[0]];  // LDS / crossbar operands one block ahead
@@ -738,34 +772,8 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
         wait_vm<2 * NJ - 1 - j>(Y[j]);
         s1_block<EX>(acA, acB, acC, acD, acE, acF, a, b, Y[j]);
       } else {
-        // one block ahead: Y[j + 1] (the next block's raw quad) has landed
-        if constexpr (j + 1 < NJ) {
-          if constexpr (j > 0) wait_vm<NJ - 2 - j + GL>(Y[j + 1]);
-          unext = Y[j + 1];
-        } else {
-          unext = hy;  // lanes lq <= 1: virtual block NJ
-        }
-        if (psub)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) unext[e] = __fsub_rn(unext[e], mr);
-        float win[4 + 2 * (HH > 0 ? HH : 0)];
-        constexpr int H_ = HH > 0 ? HH : 0;
-        constexpr int NL1 = H_ < 4 ? H_ : 4;
-#pragma unroll
-        for (int e = 4 - NL1; e < 4; ++e) {  // quad lq − 1 (block j − 1 for lq = 0)
-          win[H_ - 4 + e] = xlane(4 * ((lane + 48) & 63), lq == 3 ? uprev[e] : ucur[e]);
-          win[H_ + 4 + (e - (4 - NL1))] = xlane(4 * ((lane + 16) & 63), lq == 0 ? unext[e - (4 - NL1)] : ucur[e - (4 - NL1)]);
-        }
-        if constexpr (H_ > 4) {
-#pragma unroll
-          for (int e = 8 - H_; e < 4; ++e)  // quad lq − 2
-            win[H_ - 8 + e] = xlane(4 * (lane ^ 32), lq >= 2 ? uprev[e] : ucur[e]);
-#pragma unroll
-          for (int e = 0; e < H_ - 4; ++e)  // quad lq + 2
-            win[H_ + 8 + e] = xlane(4 * (lane ^ 32), lq <= 1 ? unext[e] : ucur[e]);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) win[H_ + e] = ucur[e];
+        // y of block j from the window exchanged during block j − 1 (its
+        // ds_bpermutes had the previous block's MFMAs to land)
         f32x4 y = stencil(win, sr);
         if constexpr (HH > 0) {
           if ((j == 0 && w == 0) || (j == NJ - 1 && w == W - 1))
@@ -778,8 +786,20 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
         // y into the AGPR tile now (sweep 2 reads it there); a plain assignment
         // would leave y in VGPRs until the next sweep 2 asks for the AGPRs
         asm volatile("" : "=a"(Y[j]) : "0"(y));
-        uprev = ucur;
-        ucur = unext;
+        if constexpr (j + 1 < NJ) {  // the window of block j + 1: Y[j + 2] (or the halo) has landed
+          if constexpr (j + 2 < NJ) {
+            wait_vm<NJ - 3 - j + GL>(Y[j + 2]);
+            unext = Y[j + 2];
+          } else {
+            unext = hy;  // lanes lq <= 1: virtual block NJ
+          }
+          if (psub)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) unext[e] = __fsub_rn(unext[e], mr);
+          exchange(uprev, ucur, unext, win);
+          uprev = ucur;
+          ucur = unext;
+        }
         s1_block_v<EX>(acA, acB, acC, acD, acE, acF, a, b, y);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting every block's reads

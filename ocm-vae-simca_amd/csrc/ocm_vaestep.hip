@@ -1,0 +1,262 @@
+// The small tensors of the VAE training step (vae_model.py:136-158,
+// vae_bce_nut.py:178-203; utils/final_vaesimca.py:198-224, 362-375) fused
+// into a few launches: the graphed C4 step is bound by its kernel count (each
+// torch elementwise kernel costs ≈ 4.5 µs of the replay however small its
+// tensor, profiles/r03n_vae_step_trace_by_grid.md), not by its bytes.
+//
+//   ocm_vae_bottleneck_fwd   z = μ + ε·exp(½ logσ²)  and  kl = −½ mean_B Σ_d (1 + logσ² − μ² − σ²)
+//   ocm_vae_bottleneck_bwd   dμ = dz + dkl·μ/B,  dlogσ² = dz·ε·½exp(½logσ²) − ½dkl·(1 − σ²)/B
+//   ocm_vae_recon_fwd        x̂ = xs·std + mean (the de-standardisation), the reconstruction term
+//                            (BCE-with-logits vs the per-sample min–max scaled x, or MSE), total =
+//                            recon + β·kl, and d total/d xs kept for the backward
+//   ocm_vae_recon_bwd        dxs = dtotal·(d total/d xs), dkl = β·dtotal
+//   ocm_adam_step            torch.optim.Adam (L2 weight decay, no amsgrad) over a table of tensors
+//
+// Sums are fp64 with per-workgroup partials combined in a fixed order by the
+// last workgroup (a ticket counter): deterministic, graph-capturable (all
+// scratch is caller-owned).
+#include "ocm_internal.h"
+
+namespace {
+
+constexpr int VT = 256;
+
+__device__ __forceinline__ float ld_act(const void* p, int dt, int64_t i) {
+  if (dt == OCM_DTYPE_BF16) {
+    const uint16_t h = static_cast<const uint16_t*>(p)[i];
+    return __uint_as_float((uint32_t)h << 16);
+  }
+  return static_cast<const float*>(p)[i];
+}
+
+__device__ __forceinline__ void st_act(void* p, int dt, int64_t i, float v) {
+  if (dt == OCM_DTYPE_BF16) {  // round to nearest even
+    uint32_t u = __float_as_uint(v);
+    if ((u & 0x7f800000u) != 0x7f800000u) u += 0x7fffu + ((u >> 16) & 1u);
+    static_cast<uint16_t*>(p)[i] = (uint16_t)(u >> 16);
+  } else {
+    static_cast<float*>(p)[i] = v;
+  }
+}
+
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  v = wave_sum_f64(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+  return s;
+}
+
+__device__ __forceinline__ float block_minmax(float v, bool is_max, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float u = __shfl_xor(v, o, 64);
+    v = is_max ? fmaxf(v, u) : fminf(v, u);
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = red[0];
+  for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r = is_max ? fmaxf(r, red[w]) : fminf(r, red[w]);
+  return r;
+}
+
+// one workgroup: z and the KL (B·d ≤ a few 10⁴ values)
+__global__ __launch_bounds__(1024) void k_bottleneck_fwd(const void* mu, const void* lv, const void* eps, int dt,
+                                                          int64_t n, int B, void* z, float* kl) {
+  __shared__ double red[16];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const float m = ld_act(mu, dt, i), l = ld_act(lv, dt, i), e = ld_act(eps, dt, i);
+    st_act(z, dt, i, m + e * expf(0.5f * l));
+    s += 1.0 + (double)l - (double)m * m - exp((double)l);
+  }
+  const double t = block_sum_d(s, red);
+  if (threadIdx.x == 0) *kl = (float)(-0.5 * t / B);
+}
+
+__global__ __launch_bounds__(VT) void k_bottleneck_bwd(const void* dz, const float* dkl, const void* mu,
+                                                        const void* lv, const void* eps, int dt, int64_t n, int B,
+                                                        void* dmu, void* dlv) {
+  const int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x;
+  if (i >= n) return;
+  const float g = dz ? ld_act(dz, dt, i) : 0.f;
+  const float k = dkl ? *dkl : 0.f;
+  const float m = ld_act(mu, dt, i), l = ld_act(lv, dt, i), e = ld_act(eps, dt, i);
+  st_act(dmu, dt, i, g + k * m / B);
+  st_act(dlv, dt, i, g * e * 0.5f * expf(0.5f * l) - 0.5f * k * (1.f - expf(l)) / B);
+}
+
+// one workgroup per row: x̂ = xs·std + mean; BCE-with-logits against t =
+// clamp((x − lo)/(hi − lo + eps), 0, 1) (torch's stable form) or MSE; the
+// gradient (d recon/d xs) into gxs; row partials → the last workgroup sums
+// them in order and writes {total, recon}.
+__global__ __launch_bounds__(VT) void k_recon_fwd(int kind, const float* __restrict__ x, const void* xs, int dt,
+                                                   int B, int L, const float* __restrict__ mean,
+                                                   const float* __restrict__ sd, float eps, const float* kl,
+                                                   float beta, float* __restrict__ gxs, double* __restrict__ part,
+                                                   unsigned* __restrict__ ticket, float* __restrict__ out) {
+  __shared__ float redf[VT / 64];
+  __shared__ double red[VT / 64];
+  __shared__ bool last;
+  const int b = blockIdx.x;
+  const float* xr = x + (int64_t)b * L;
+  const double inv = 1.0 / ((double)B * L);
+  float lo = 0.f, den = 1.f;
+  if (kind == OCM_VAE_LOSS_BCE) {
+    float mn = __builtin_inff(), mx = -__builtin_inff();
+    for (int j = threadIdx.x; j < L; j += VT) {
+      mn = fminf(mn, xr[j]);
+      mx = fmaxf(mx, xr[j]);
+    }
+    lo = block_minmax(mn, false, redf);
+    const float hi = block_minmax(mx, true, redf);
+    den = hi - lo + eps;
+  }
+  double s = 0.0;
+  for (int j = threadIdx.x; j < L; j += VT) {
+    const int64_t e = (int64_t)b * L + j;
+    const float z = ld_act(xs, dt, e) * sd[j] + mean[j];
+    float g;
+    if (kind == OCM_VAE_LOSS_BCE) {
+      const float t = fminf(fmaxf((xr[j] - lo) / den, 0.f), 1.f);
+      s += (double)(fmaxf(z, 0.f) - z * t + log1pf(expf(-fabsf(z))));
+      const float sg = 1.f / (1.f + expf(-z));
+      g = (float)((double)(sg - t) * inv);
+    } else {  // MSE
+      const float d = z - xr[j];
+      s += (double)d * d;
+      g = (float)(2.0 * d * inv);
+    }
+    gxs[e] = g * sd[j];
+  }
+  const double ps = block_sum_d(s, red);
+  if (threadIdx.x == 0) {
+    part[b] = ps;
+    __threadfence();
+    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  double t = 0.0;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += VT) t += part[i];
+  const double tot = block_sum_d(t, red);
+  if (threadIdx.x == 0) {
+    const float recon = (float)(tot * inv);
+    out[1] = recon;
+    out[0] = recon + beta * (kl ? *kl : 0.f);
+    *ticket = 0u;
+  }
+}
+
+__global__ __launch_bounds__(VT) void k_recon_bwd(const float* __restrict__ dtotal, const float* __restrict__ gxs,
+                                                   int64_t n, int dt, void* dxs, float beta, float* dkl) {
+  const int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x;
+  const float g = *dtotal;
+  if (i < n) st_act(dxs, dt, i, g * gxs[i]);
+  if (i == 0 && dkl) *dkl = beta * g;
+}
+
+// Adam over a table of tensors: grid-stride over the concatenation (the
+// prefix of element counts in the table); the step counter (f32, on the
+// device) is read as t − 1 and advanced by the last workgroup.
+__global__ __launch_bounds__(VT) void k_adam(const ocm_adam_tensor* __restrict__ tab, int nt, int64_t total,
+                                              float* __restrict__ step, float lr, float b1, float b2, float eps,
+                                              float wd, unsigned* __restrict__ ticket) {
+  __shared__ bool last;
+  const float t = *step + 1.f;
+  const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
+  const float step_size = lr / bc1, bc2s = sqrtf(bc2);
+  int cur = 0;
+  for (int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x; i < total; i += (int64_t)gridDim.x * VT) {
+    while (cur + 1 < nt && i >= tab[cur + 1].offset) ++cur;
+    while (cur > 0 && i < tab[cur].offset) --cur;
+    const ocm_adam_tensor& T = tab[cur];
+    const int64_t j = i - T.offset;
+    float g = T.grad[j];
+    const float pv = T.param[j];
+    if (wd != 0.f) g += wd * pv;
+    const float m = b1 * T.exp_avg[j] + (1.f - b1) * g;
+    const float v = b2 * T.exp_avg_sq[j] + (1.f - b2) * g * g;
+    T.exp_avg[j] = m;
+    T.exp_avg_sq[j] = v;
+    T.param[j] = pv - step_size * m / (sqrtf(v) / bc2s + eps);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    *step = t;
+    *ticket = 0u;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t ocm_vae_scratch_bytes(int32_t B) { return (size_t)(B + 64) * sizeof(double) + 256; }
+
+int ocm_vae_bottleneck_fwd(ocm_ctx* ctx, int32_t dtype, const void* mu, const void* logvar, const void* eps, int32_t B,
+                           int32_t d, void* z_out, float* kl_out, void* stream) {
+  OCM_REQUIRE(ctx && mu && logvar && eps && z_out && kl_out, "ocm_vae_bottleneck_fwd: NULL argument");
+  OCM_REQUIRE(B > 0 && d > 0 && (dtype == OCM_DTYPE_F32 || dtype == OCM_DTYPE_BF16), "ocm_vae_bottleneck_fwd: bad args");
+  hipLaunchKernelGGL(k_bottleneck_fwd, dim3(1), dim3(1024), 0, (hipStream_t)stream, mu, logvar, eps, dtype,
+                     (int64_t)B * d, B, z_out, kl_out);
+  OCM_CHECK_LAUNCH("k_bottleneck_fwd");
+  return OCM_OK;
+}
+
+int ocm_vae_bottleneck_bwd(ocm_ctx* ctx, int32_t dtype, const void* dz, const float* dkl, const void* mu,
+                           const void* logvar, const void* eps, int32_t B, int32_t d, void* dmu_out, void* dlogvar_out,
+                           void* stream) {
+  OCM_REQUIRE(ctx && mu && logvar && eps && dmu_out && dlogvar_out, "ocm_vae_bottleneck_bwd: NULL argument");
+  OCM_REQUIRE(B > 0 && d > 0 && (dtype == OCM_DTYPE_F32 || dtype == OCM_DTYPE_BF16), "ocm_vae_bottleneck_bwd: bad args");
+  const int64_t n = (int64_t)B * d;
+  hipLaunchKernelGGL(k_bottleneck_bwd, dim3((unsigned)((n + VT - 1) / VT)), dim3(VT), 0, (hipStream_t)stream, dz, dkl,
+                     mu, logvar, eps, dtype, n, B, dmu_out, dlogvar_out);
+  OCM_CHECK_LAUNCH("k_bottleneck_bwd");
+  return OCM_OK;
+}
+
+int ocm_vae_recon_fwd(ocm_ctx* ctx, int32_t kind, const float* x, int32_t dtype, const void* xs, int32_t B, int32_t L,
+                      const float* mean, const float* std, float eps, const float* kl, float beta, float* gxs_out,
+                      float* out2, void* scratch, void* stream) {
+  OCM_REQUIRE(ctx && x && xs && mean && std && gxs_out && out2 && scratch, "ocm_vae_recon_fwd: NULL argument");
+  OCM_REQUIRE(kind == OCM_VAE_LOSS_BCE || kind == OCM_VAE_LOSS_MSE, "ocm_vae_recon_fwd: kind BCE or MSE");
+  OCM_REQUIRE(B > 0 && L > 0 && (dtype == OCM_DTYPE_F32 || dtype == OCM_DTYPE_BF16), "ocm_vae_recon_fwd: bad args");
+  auto* part = static_cast<double*>(scratch);
+  auto* ticket = reinterpret_cast<unsigned*>(part + B + 32);
+  hipLaunchKernelGGL(k_recon_fwd, dim3(B), dim3(VT), 0, (hipStream_t)stream, kind, x, xs, dtype, B, L, mean, std, eps,
+                     kl, beta, gxs_out, part, ticket, out2);
+  OCM_CHECK_LAUNCH("k_recon_fwd");
+  return OCM_OK;
+}
+
+int ocm_vae_recon_bwd(ocm_ctx* ctx, const float* dtotal, const float* gxs, int64_t n, int32_t dtype, void* dxs_out,
+                      float beta, float* dkl_out, void* stream) {
+  OCM_REQUIRE(ctx && dtotal && gxs && dxs_out, "ocm_vae_recon_bwd: NULL argument");
+  OCM_REQUIRE(n > 0 && (dtype == OCM_DTYPE_F32 || dtype == OCM_DTYPE_BF16), "ocm_vae_recon_bwd: bad args");
+  hipLaunchKernelGGL(k_recon_bwd, dim3((unsigned)((n + VT - 1) / VT)), dim3(VT), 0, (hipStream_t)stream, dtotal, gxs, n,
+                     dtype, dxs_out, beta, dkl_out);
+  OCM_CHECK_LAUNCH("k_recon_bwd");
+  return OCM_OK;
+}
+
+int ocm_adam_step(ocm_ctx* ctx, const ocm_adam_tensor* table, int32_t ntensors, int64_t total, float* step, float lr,
+                  float beta1, float beta2, float eps, float weight_decay, void* scratch, void* stream) {
+  OCM_REQUIRE(ctx && table && step && scratch && ntensors > 0 && total > 0, "ocm_adam_step: bad arguments");
+  const int grid = (int)std::min<int64_t>((total + VT - 1) / VT, 1024);
+  hipLaunchKernelGGL(k_adam, dim3(grid), dim3(VT), 0, (hipStream_t)stream, table, ntensors, total, step, lr, beta1,
+                     beta2, eps, weight_decay, static_cast<unsigned*>(scratch));
+  OCM_CHECK_LAUNCH("k_adam");
+  return OCM_OK;
+}
+
+}  // extern "C"

@@ -126,6 +126,17 @@ SIGNATURES = {
     "ocm_conv1d_wgrad": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_i32, c_i32, c_i32,
                                  c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ocm_chan_sum": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
+    "ocm_vae_scratch_bytes": (ctypes.c_size_t, [c_i32]),
+    "ocm_vae_bottleneck_fwd": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_i32, c_i32, c_void_p,
+                                       c_void_p, c_void_p]),
+    "ocm_vae_bottleneck_bwd": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i32,
+                                       c_i32, c_void_p, c_void_p, c_void_p]),
+    "ocm_vae_recon_fwd": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_void_p, c_i32, c_i32, c_void_p, c_void_p,
+                                  ctypes.c_float, c_void_p, ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ocm_vae_recon_bwd": (c_i32, [c_void_p, c_void_p, c_void_p, c_i64, c_i32, c_void_p, ctypes.c_float, c_void_p,
+                                  c_void_p]),
+    "ocm_adam_step": (c_i32, [c_void_p, c_void_p, c_i32, c_i64, c_void_p, ctypes.c_float, ctypes.c_float,
+                              ctypes.c_float, ctypes.c_float, ctypes.c_float, c_void_p, c_void_p]),
     "ocm_eigh_f64": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_i32, c_void_p, c_void_p]),
     "ocm_prep_materialised": (c_i32, [c_void_p, ctypes.POINTER(c_i64)]),
     "ocm_prep_rowstats_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p]),

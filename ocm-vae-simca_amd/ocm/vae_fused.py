@@ -1,0 +1,202 @@
+"""The VAE training step's small tensors on libocm (csrc/ocm_vaestep.hip).
+
+The graphed C4 step (ocm/vae_train.py) is bound by its kernel count: every
+torch elementwise / reduction kernel costs ≈ 4.5 µs of the replay however
+small its tensor (profiles/r03n_vae_step_trace_by_grid.md: 192 kernels, ≈ 80
+of them torch's).  The reference's step (vae_bce_nut.py:178-203 with
+vae_model.py:124-158) is restated here as three autograd functions and one
+optimizer kernel:
+
+* ``bottleneck(mu, logvar, eps)`` → (z, kl): z = μ + ε·exp(½logσ²)
+  (reparameterize, vae_model.py:124-126) and the KL term (vae_model.py:150-152)
+  in one launch, their backward in one launch;
+* ``recon_total(x, xs, kl, ...)`` → (total, recon): the de-standardisation
+  x̂ = xs·std + mean (forward, vae_model.py:130-134), the reconstruction term
+  (BCE-with-logits against the per-sample min–max scaled input,
+  vae_model.py:153-156, or the MSE of utils/final_vaesimca.py:208-209) and
+  total = recon + β·kl in one launch; the backward is one launch;
+* ``FusedAdam``: torch.optim.Adam (L2 weight decay) over every parameter in
+  one launch (ocm_adam_step), with its moments and step counter on the device.
+
+ε is drawn with torch.randn_like on the graph-safe generator, exactly as the
+model's reparameterize draws it.  Sums are fp64 with fixed-order partials.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import Context, check, ptr, stream_handle
+
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+LOSS_KINDS = {"bce": 0, "euclidean": 1}  # include/ocm.h OCM_VAE_LOSS_*
+
+
+def _h(dev):
+    return Context.get(dev.index).handle
+
+
+class _Bottleneck(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mu, logvar, eps):
+        mu, logvar, eps = mu.contiguous(), logvar.contiguous(), eps.contiguous()
+        B, d = mu.shape
+        z = torch.empty_like(mu)
+        kl = torch.empty((), dtype=torch.float32, device=mu.device)
+        check(_lib.load().ocm_vae_bottleneck_fwd(_h(mu.device), _DT[mu.dtype], ptr(mu), ptr(logvar), ptr(eps), B, d,
+                                                 ptr(z), ptr(kl), stream_handle(mu.device)), "ocm_vae_bottleneck_fwd")
+        ctx.save_for_backward(mu, logvar, eps)
+        ctx.set_materialize_grads(False)
+        return z, kl
+
+    @staticmethod
+    def backward(ctx, dz, dkl):
+        mu, logvar, eps = ctx.saved_tensors
+        B, d = mu.shape
+        dmu, dlv = torch.empty_like(mu), torch.empty_like(logvar)
+        if dz is not None:
+            dz = dz.to(mu.dtype).contiguous()
+        if dkl is not None:
+            dkl = dkl.to(torch.float32).contiguous()
+        check(_lib.load().ocm_vae_bottleneck_bwd(_h(mu.device), _DT[mu.dtype], ptr(dz), ptr(dkl), ptr(mu),
+                                                 ptr(logvar), ptr(eps), B, d, ptr(dmu), ptr(dlv),
+                                                 stream_handle(mu.device)), "ocm_vae_bottleneck_bwd")
+        return dmu, dlv, None
+
+
+class _ReconTotal(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, xs, kl, bufs, kind, beta, eps):
+        xs = xs.contiguous()
+        B, L = xs.shape
+        gxs, out2, scratch, mean, std = bufs.get(B, L, x.device)
+        check(_lib.load().ocm_vae_recon_fwd(_h(x.device), kind, ptr(x), _DT[xs.dtype], ptr(xs), B, L, ptr(mean),
+                                            ptr(std), float(eps), ptr(kl), float(beta), ptr(gxs), ptr(out2),
+                                            ptr(scratch), stream_handle(x.device)), "ocm_vae_recon_fwd")
+        ctx.xs_dtype = xs.dtype
+        ctx.beta = float(beta)
+        ctx.gxs = gxs
+        ctx.has_kl = kl is not None
+        ctx.set_materialize_grads(False)
+        return out2[0]  # total; recon stays in bufs (out2[1])
+
+    @staticmethod
+    def backward(ctx, dtotal):
+        gxs = ctx.gxs
+        B, L = gxs.shape
+        if dtotal is None:
+            return None, None, None, None, None, None, None
+        dtotal = dtotal.to(torch.float32).contiguous()
+        dxs = torch.empty((B, L), dtype=ctx.xs_dtype, device=gxs.device)
+        dkl = torch.empty((), dtype=torch.float32, device=gxs.device) if ctx.has_kl else None
+        check(_lib.load().ocm_vae_recon_bwd(_h(gxs.device), ptr(dtotal), ptr(gxs), B * L, _DT[ctx.xs_dtype], ptr(dxs),
+                                            ctx.beta, ptr(dkl), stream_handle(gxs.device)), "ocm_vae_recon_bwd")
+        return None, dxs, dkl, None, None, None, None
+
+
+class ReconBuffers:
+    """Persistent device buffers of the fused reconstruction term (graph
+    replays reuse them): the gradient d recon / d xs, {total, recon}, the
+    ticket scratch (zeroed once), and the model's mean / std."""
+
+    def __init__(self, spec_mean: torch.Tensor, spec_std: torch.Tensor):
+        self.mean = spec_mean.detach().to(torch.float32).contiguous()
+        self.std = spec_std.detach().to(torch.float32).contiguous()
+        self._b = {}
+
+    def get(self, B, L, dev):
+        key = (B, L)
+        if key not in self._b:
+            nb = int(_lib.load().ocm_vae_scratch_bytes(B))
+            self._b[key] = (torch.empty((B, L), dtype=torch.float32, device=dev),
+                            torch.empty(2, dtype=torch.float32, device=dev),
+                            torch.zeros((nb + 7) // 8, dtype=torch.float64, device=dev))
+        gxs, out2, scratch = self._b[key]
+        return gxs, out2, scratch, self.mean, self.std
+
+
+def bottleneck(mu, logvar, eps):
+    return _Bottleneck.apply(mu, logvar, eps)
+
+
+def recon_total(x, xs, kl, bufs: ReconBuffers, loss: str, beta: float, eps: float = 1e-8):
+    """(total, recon): total carries the gradient; recon is the term's value."""
+    total = _ReconTotal.apply(x, xs, kl, bufs, LOSS_KINDS[loss], float(beta), float(eps))
+    return total, bufs.get(xs.shape[0], xs.shape[1], xs.device)[1][1]
+
+
+class FusedAdam:
+    """torch.optim.Adam (L2 weight decay, no amsgrad) over ``params`` in one
+    launch per step (ocm_adam_step).  The table of (param, grad, moments)
+    pointers is written when the gradients' addresses change (eager steps);
+    a step captured into a HIP graph keeps the table of its capture."""
+
+    _FIELDS = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+               ("exp_avg_sq", ctypes.c_void_p), ("offset", ctypes.c_int64), ("numel", ctypes.c_int64)]
+
+    class _Entry(ctypes.Structure):
+        pass
+
+    _Entry._fields_ = _FIELDS
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        self.params = [p for p in params if p.requires_grad]
+        dev = self.params[0].device
+        self.lr, self.b1, self.b2, self.eps, self.wd = float(lr), float(betas[0]), float(betas[1]), float(eps), \
+            float(weight_decay)
+        self.exp_avg = [torch.zeros_like(p, memory_format=torch.contiguous_format) for p in self.params]
+        self.exp_avg_sq = [torch.zeros_like(p, memory_format=torch.contiguous_format) for p in self.params]
+        self.step_t = torch.zeros((), dtype=torch.float32, device=dev)
+        self.total = sum(p.numel() for p in self.params)
+        n = len(self.params)
+        self.table = torch.empty(n * ctypes.sizeof(self._Entry), dtype=torch.uint8, device=dev)
+        self.scratch = torch.zeros(64, dtype=torch.int32, device=dev)
+        self._key = None
+
+    def zero_grad(self, set_to_none=True):
+        for p in self.params:
+            if set_to_none:
+                p.grad = None
+            elif p.grad is not None:
+                p.grad.zero_()
+
+    def _write_table(self, capturing: bool):
+        key = tuple(p.grad.data_ptr() for p in self.params)
+        if key == self._key:
+            return
+        arr = (self._Entry * len(self.params))()
+        o = 0
+        for i, p in enumerate(self.params):
+            if not (p.is_contiguous() and p.grad.is_contiguous() and p.grad.dtype == torch.float32):
+                raise RuntimeError("FusedAdam: contiguous float32 parameters and gradients only")
+            arr[i] = self._Entry(p.data_ptr(), p.grad.data_ptr(), self.exp_avg[i].data_ptr(),
+                                 self.exp_avg_sq[i].data_ptr(), o, p.numel())
+            o += p.numel()
+        raw = torch.frombuffer(bytearray(arr), dtype=torch.uint8)
+        if capturing:  # written once after the capture (the graph replays the capture's addresses)
+            self._pending = raw.clone()
+        else:  # eager steps: a synchronous copy (the host staging is reused next step)
+            self.table.copy_(raw.to(self.table.device))
+        self._key = key
+
+    def flush_pending(self):
+        """After a graph capture: the table of the captured step's gradients."""
+        if getattr(self, "_pending", None) is not None:
+            self.table.copy_(self._pending.to(self.table.device))
+            torch.cuda.synchronize(self.table.device)
+            self._pending = None
+
+    def step(self):
+        capturing = torch.cuda.is_current_stream_capturing()
+        self._write_table(capturing)
+        dev = self.table.device
+        check(_lib.load().ocm_adam_step(_h(dev), ptr(self.table), len(self.params), self.total, ptr(self.step_t),
+                                        self.lr, self.b1, self.b2, self.eps, self.wd, ptr(self.scratch),
+                                        stream_handle(dev)), "ocm_adam_step")
+
+    def reset_state(self):
+        for t in self.exp_avg + self.exp_avg_sq:
+            t.zero_()
+        self.step_t.zero_()

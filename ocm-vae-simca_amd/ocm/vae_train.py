@@ -50,7 +50,8 @@ class GraphedVAETrainer:
     LOSSES = ("bce", "cosine", "bce_prob", "euclidean")
 
     def __init__(self, model, batch: int, lr=1e-3, weight_decay=0.0, beta=1.0, loss="bce",
-                 dtype=torch.bfloat16, graph=True, warmup=3, restore=True, group=None, grad_allreduce=None):
+                 dtype=torch.bfloat16, graph=True, warmup=3, restore=True, group=None, grad_allreduce=None,
+                 fused=True):
         self.model = model
         self.module = getattr(model, "module", model)
         dev = next(self.module.parameters()).device
@@ -71,9 +72,24 @@ class GraphedVAETrainer:
         # steps/s for the foreach form on MI355X (C4 net, B = 512), losses equal to
         # 1e-4; OCM_VAE_ADAM=foreach for A/B.  Eager CPU steps keep the reference's
         # Adam arithmetic exactly (tests/test_vae_train.py)
-        fused = dev.type == "cuda" and os.environ.get("OCM_VAE_ADAM", "fused") == "fused"
-        self.opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay, capturable=graph,
-                                    **({"fused": True} if fused else {"foreach": True}))
+        # On the GPU the small tensors of the step run on libocm (ocm/vae_fused.py):
+        # the reparameterisation + KL, the de-standardisation + reconstruction
+        # term + total and their backward passes in four launches, Adam in one —
+        # the graphed step is bound by its kernel count.  Eager CPU steps keep
+        # the reference's torch arithmetic exactly (tests/test_vae_train.py);
+        # fused=False keeps torch on the GPU too (A/B, tests).
+        self.fused = (dev.type == "cuda" and fused and loss in ("bce", "euclidean")
+                      and hasattr(self.module, "encode") and hasattr(self.module, "decode"))
+        if self.fused:
+            from . import vae_fused
+
+            self._vf = vae_fused
+            self.opt = vae_fused.FusedAdam(model.parameters(), lr=lr, weight_decay=weight_decay)
+            self._rbufs = vae_fused.ReconBuffers(self.module.spec_mean, self.module.spec_std)
+        else:
+            gpu_fused = dev.type == "cuda"
+            self.opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay, capturable=graph,
+                                        **({"fused": True} if gpu_fused else {"foreach": True}))
         self.x = torch.zeros((batch, self.module.input_length), dtype=torch.float32, device=dev)
         self.graph = None
         self.restore = restore
@@ -117,7 +133,12 @@ class GraphedVAETrainer:
         # its freshly computed gradient (no per-parameter memset + accumulate
         # kernel: 43 adds and 11 fills per step in the r03g trace); with the
         # flat all-reduce buffer the .grad views must persist
-        self.opt.zero_grad(set_to_none=not self.allreduce)
+        if self.fused and self.allreduce:
+            self.flat_grad.zero_()  # one fill for every gradient view
+        else:
+            self.opt.zero_grad(set_to_none=not self.allreduce)
+        if self.fused:
+            return self._body_fused()
         with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32):
             x_rec, mu, logvar = self.model(self.x)
         x_rec, mu, logvar = x_rec.float(), mu.float(), logvar.float()
@@ -137,6 +158,25 @@ class GraphedVAETrainer:
             self.flat_grad.div_(self.world)
         self.opt.step()
         return total.detach(), recon.detach(), kl.detach()
+
+    def _body_fused(self):
+        """The same step as _body with the loss terms and Adam on libocm: the
+        network (encode / decode, vae_model.py:116-134) under autocast, then
+        z = μ + ε·exp(½logσ²) and the KL (one launch), the de-standardised
+        reconstruction term and the total (one launch)."""
+        m = self.module
+        with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32):
+            mu, logvar = m.encode((self.x - m.spec_mean) / m.spec_std)
+            eps = torch.randn_like(mu)
+            z, kl = self._vf.bottleneck(mu, logvar, eps)
+            xs = m.decode(z)
+        total, recon = self._vf.recon_total(self.x, xs, kl, self._rbufs, self.loss, self.beta)
+        total.backward()
+        if self.allreduce:  # DDP averaging: one RCCL all-reduce of the flat gradient
+            dist.all_reduce(self.flat_grad, group=self.group)
+            self.flat_grad.div_(self.world)
+        self.opt.step()
+        return total.detach(), recon, kl.detach()
 
     def _capture(self, warmup):
         self.model.train()
@@ -163,15 +203,20 @@ class GraphedVAETrainer:
             mode = "thread_local"
         with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.out = self._body()
+        if self.fused:
+            self.opt.flush_pending()
         if not self.restore:
             return
         with torch.no_grad():
             for k, v in self.module.state_dict().items():
                 v.copy_(saved[k])
-            for st in self.opt.state.values():  # fresh Adam moments and step counters
-                for t in st.values():
-                    if torch.is_tensor(t):
-                        t.zero_()
+            if self.fused:
+                self.opt.reset_state()
+            else:
+                for st in self.opt.state.values():  # fresh Adam moments and step counters
+                    for t in st.values():
+                        if torch.is_tensor(t):
+                            t.zero_()
 
     def step(self, x: torch.Tensor | None = None):
         """Run one training step on ``x`` (copied into the static batch buffer);

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--k", default="16,20")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--kernels", default="diag,full")
+    ap.add_argument("--gram", action="store_true", help="also time the i8x3 Gram (quantiser + Gram) per view")
     ap.add_argument("--prep", default="none", help="comma list of none, snv (SNV only), snv5 (SNV + w 5 d 1), "
                     "sg15 (w 15 d 1): score lazy views (diag kernel)")
     ap.add_argument("--tag", default=os.path.basename(os.environ.get("OCM_LIB", "libocm.so")))
@@ -62,6 +63,29 @@ def main():
             ms = e0.elapsed_time(e1) / args.reps
             print(json.dumps({"lib": args.tag, "kernel": "diag", "prep": pv, "k": k, "p": p, "rows": n,
                               "ms": round(ms, 4), "GBs_alg": round(4 * p * n / ms / 1e6, 1)}), flush=True)
+    if args.gram:
+        from ocm import _lib
+
+        ctx = _lib.Context.get(0)
+        for pv in args.prep.split(","):
+            Xv = views[pv]
+            if pv != "none":
+                Xv.rowstat()
+            shift = engine.cast_f32(engine.colmean(Xv, None, 4096))
+            engine.gram(Xv, None, [0, n], shift)
+            torch.cuda.synchronize()
+            for kid in range(3):
+                ctx.read_timing(kid)
+            ctx.set_timing(True)
+            for _ in range(3):
+                engine.gram(Xv, None, [0, n], shift)
+            torch.cuda.synchronize()
+            ctx.set_timing(False)
+            t = {nm: ctx.read_timing(kid) for kid, nm in enumerate(("gram", "score", "quant"))}
+            print(json.dumps({"kernel": "gram_i8x3", "prep": pv, "rows": n, "p": p,
+                              "quant_ms": round(t["quant"][0] / max(1, t["quant"][1]), 4),
+                              "gram_ms": round(t["gram"][0] / max(1, t["gram"][1]), 4),
+                              "marks": engine.last_gram_marks(0)}), flush=True)
     for k in [int(v) for v in args.k.split(",")]:
         P, _ = torch.linalg.qr(torch.randn(p, k, dtype=torch.float64, device=dev))
         P = P.T.contiguous()
