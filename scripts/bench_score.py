@@ -52,7 +52,7 @@ def main():
             P, _ = torch.linalg.qr(torch.randn(p, k, dtype=torch.float64, device=dev))
             P = P.T.contiguous()
             inv = torch.linspace(1.0, 0.1, k, dtype=torch.float64, device=dev)
-            engine.score(Xv, None, n, P, mean, inv, want_stats=True)
+            outv = engine.score(Xv, None, n, P, mean, inv, want_stats=True)
             st = torch.cuda.current_stream()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
@@ -61,7 +61,11 @@ def main():
             e1.record(st)
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.reps
-            print(json.dumps({"lib": args.tag, "kernel": "diag", "prep": pv, "k": k, "p": p, "rows": n,
+            extra = {}
+            if os.environ.get("OCM_STAMPS"):
+                tiles = (n + 15) // 16
+                extra["cycles_per_tile"] = [round(v / tiles, 1) for v in outv["stats"].cpu().tolist()]
+            print(json.dumps({**extra, "lib": args.tag, "kernel": "diag", "prep": pv, "k": k, "p": p, "rows": n,
                               "ms": round(ms, 4), "GBs_alg": round(4 * p * n / ms / 1e6, 1)}), flush=True)
     if args.gram:
         from ocm import _lib

@@ -249,16 +249,19 @@ def test_c5_shape_rank_share_and_latent_simca(tmp_path):
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
 @pytest.mark.parametrize("loss", ["bce", "euclidean"])
 def test_fused_step_matches_torch_step(loss):
-    """The libocm step (ocm/vae_fused.py: reparameterisation + KL, the
-    de-standardised reconstruction term + total, their backward passes and
-    Adam, five launches) against the torch step on the GPU, eager float32 with
-    the same ε draws: losses to 1e-5, parameters after 5 steps to 1e-5."""
+    """The libocm loss path (ocm/vae_fused.py: reparameterisation + KL, the
+    de-standardised reconstruction term + total and their backward passes)
+    against the torch step on the GPU, eager float32, identical ε draws:
+    losses to 1e-5 over 3 steps and every parameter gradient to 1e-4 of its
+    norm.  (Parameter values are not compared after several Adam steps: the
+    biases a BatchNorm cancels have rounding-level gradients, which Adam
+    turns into ±lr steps in either implementation.)"""
     from ocm.vae_train import GraphedVAETrainer
 
     dev = torch.device("cuda", 0)
     L, d, B = 256, 8, 64
     g = torch.Generator(device="cpu").manual_seed(3)
-    X = (1.0 + 0.3 * torch.randn(B * 5, L, generator=g)).to(dev)
+    X = (1.0 + 0.3 * torch.randn(B * 3, L, generator=g)).to(dev)
     mean, std = X.mean(0).cpu().numpy(), X.std(0).cpu().numpy()
     torch.manual_seed(0)
     m1 = V.ConvVAE1D(L, d, mean, std, conv_blocks=2, n_filters=3, kernel_size=5, hidden_fc=32).to(dev)
@@ -267,12 +270,43 @@ def test_fused_step_matches_torch_step(loss):
     tt = GraphedVAETrainer(m2, B, lr=1e-3, weight_decay=1e-4, beta=0.7, loss=loss, dtype=torch.float32, graph=False,
                            fused=False)
     assert tf.fused and not tt.fused
-    for i in range(5):
+    for i in range(3):
         xb = X[i * B:(i + 1) * B]
         torch.manual_seed(50 + i)
         a = [float(v) for v in tf.step(xb)]
         torch.manual_seed(50 + i)
         b = [float(v) for v in tt.step(xb)]
         np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-7)
-    for (n1, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
-        torch.testing.assert_close(p1, p2, rtol=1e-5, atol=1e-6, msg=n1)
+        if i == 0:  # identical weights before the first update: the gradients must agree
+            gmax = max(float(p.grad.norm()) for p in m2.parameters())
+            for (n1, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+                scale = float(p2.grad.norm())
+                # BN-cancelled biases: rounding-level gradients, compared at the global scale
+                tol = 1e-4 * scale if scale > 1e-5 * gmax else 1e-6 * gmax
+                assert float((p1.grad - p2.grad).norm()) <= tol, n1
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+def test_fused_adam_matches_torch_adam():
+    """ocm_adam_step (one launch over a table of tensors) = torch.optim.Adam
+    with L2 weight decay, 10 steps on the same gradients."""
+    from ocm.vae_fused import FusedAdam
+
+    dev = torch.device("cuda", 0)
+    rng = torch.Generator(device="cpu").manual_seed(5)
+    shapes = [(3, 1, 7), (3,), (64, 32), (1000,), (5, 5)]
+    p1 = [torch.randn(s, generator=rng).to(dev).requires_grad_() for s in shapes]
+    p2 = [p.detach().clone().requires_grad_() for p in p1]
+    fa = FusedAdam(p1, lr=2e-3, weight_decay=1e-3)
+    ta = torch.optim.Adam(p2, lr=2e-3, weight_decay=1e-3)
+    for _ in range(10):
+        grads = [torch.randn(s, generator=rng).to(dev) for s in shapes]
+        for p, gr in zip(p1, grads):
+            p.grad = gr.clone()
+        for p, gr in zip(p2, grads):
+            p.grad = gr.clone()
+        fa.step()
+        ta.step()
+    for a, b in zip(p1, p2):
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-5, atol=1e-6)
