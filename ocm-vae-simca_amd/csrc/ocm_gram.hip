@@ -938,92 +938,118 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restri
   f32x4 sh;
 #pragma unroll
   for (int e = 0; e < 4; ++e) sh[e] = c0 + e < p ? shift[c0 + e] : 0.f;
-  // this lane's halo quad (lanes cq < HQ: left, cq >= 8 - HQ: right)
-  const bool hl = cq < HQ, hr = cq >= 8 - HQ;
-  const int hcol = hl ? cg0 - 4 * HQ + 4 * cq : cg0 + Q8QC + 4 * (cq - (8 - HQ));
-  const bool hvalid = (hl || hr) && hcol >= 0 && hcol < p;
-  const int hslot = hl ? 8 - 4 * HQ + 4 * cq : 8 + Q8QC + 4 * (cq - (8 - HQ));
-  float* row_img = img[rs];
-  const float* c = pa.taps + HH;  // interior taps, offset -HH..HH
+  const float* c = pa.taps + HH;  // interior taps, offset -HH..HH (scalar loads)
   float ct[HH + 1];
 #pragma unroll
   for (int t = 0; t <= HH; ++t) ct[t] = HH > 0 ? c[t] : 0.f;
+  // Loads, issued before any compute (the plain quantiser's memory-level
+  // parallelism): this lane's raw quad of each of its 16 rows, the rows' SNV
+  // scales, and one row's halo — the HQ quads left and right of the 32 columns
+  // of row cq of the slice's first 8 rows; lane j reloads its halo registers
+  // with row 8 + j's once row j is through, 8 rows ahead of use.  Halo columns
+  // outside the row read as 0 (the edge columns are recomputed below).
+  float* row_img = img[rs];
   const bool sub = pa.snv && pa.deriv == 0;
   f32x4 v[16];
-  constexpr int GR = HH >= 7 ? 2 : 4;  // rows per load group (VGPRs: the 16 output quads stay live)
+  float srl[2];  // the SNV scales of rows 2cq, 2cq + 1 (row j's comes from lane j / 2 of the slice)
+  f32x4 hq[2][HQ > 0 ? HQ : 1];  // [left / right][quad]
+  auto load_halo = [&](int jr) {
+    const int64_t g = rb + jr;
+    const int64_t gc = g < r1 ? g : r1 - 1;
+    const float* xr = X + (GATHER ? rows[gc] : gc) * ldx;
 #pragma unroll
-  for (int g4 = 0; g4 < 16 / GR; ++g4) {
-    f32x4 xq[GR], hq[GR];
-    float mr[GR], sr[GR];
-    int64_t xrow[GR];
+    for (int side = 0; side < 2; ++side)
 #pragma unroll
-    for (int u = 0; u < GR; ++u) {
-      const int64_t g = rb + GR * g4 + u;
-      const int64_t gc = g < r1 ? g : r1 - 1;  // clamped: always a valid row
-      xrow[u] = GATHER ? rows[gc] : gc;
-      const float* xr = X + xrow[u] * ldx;
-      xq[u] = c0 < p ? *reinterpret_cast<const f32x4*>(xr + c0) : f32x4{0.f, 0.f, 0.f, 0.f};
-      hq[u] = hvalid ? *reinterpret_cast<const f32x4*>(xr + hcol) : f32x4{0.f, 0.f, 0.f, 0.f};
-      mr[u] = 0.f;
-      sr[u] = 1.f;
-      if (pa.snv) {
-        mr[u] = pa.rowstat[2 * xrow[u]];
-        sr[u] = pa.rowstat[2 * xrow[u] + 1];
+      for (int i = 0; i < HQ; ++i) {
+        const int col = side == 0 ? cg0 - 4 * HQ + 4 * i : cg0 + Q8QC + 4 * i;
+        hq[side][i] = col >= 0 && col < p ? *reinterpret_cast<const f32x4*>(xr + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+  };
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int64_t g = rb + j;
+    const int64_t gc = g < r1 ? g : r1 - 1;  // clamped: always a valid row
+    const int64_t xi = GATHER ? rows[gc] : gc;
+    const float* xr = X + xi * ldx;
+    v[j] = c0 < p ? *reinterpret_cast<const f32x4*>(xr + c0) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t g = rb + 2 * cq + u;
+    const int64_t gc = g < r1 ? g : r1 - 1;
+    srl[u] = pa.snv ? pa.rowstat[2 * (GATHER ? rows[gc] : gc) + 1] : 1.f;
+  }
+  if constexpr (HQ > 0) load_halo(cq);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int64_t g = rb + j;
+    f32x4 xs = v[j];
+    float mrj = 0.f;  // the row mean: only SNV with a deriv-0 filter subtracts it (rare: read here)
+    if (sub) {
+      const int64_t gc = g < r1 ? g : r1 - 1;
+      mrj = pa.rowstat[2 * (GATHER ? rows[gc] : gc)];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xs[e] = __fsub_rn(xs[e], mrj);
+    }
+    // the lanes of one row slice exchange their quads through the row image
+    // (wave-private: LDS instructions of a wave execute in order); lane j % 8
+    // holds the row's halo
+    *reinterpret_cast<f32x4*>(row_img + 8 + 4 * cq) = xs;
+    if constexpr (HQ > 0) {
+      if (cq == (j & 7)) {
+#pragma unroll
+        for (int i = 0; i < HQ; ++i) {
+          f32x4 lh = hq[0][i], rh = hq[1][i];
+          if (sub)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              lh[e] = __fsub_rn(lh[e], mrj);
+              rh[e] = __fsub_rn(rh[e], mrj);
+            }
+          *reinterpret_cast<f32x4*>(row_img + 8 - 4 * HQ + 4 * i) = lh;
+          *reinterpret_cast<f32x4*>(row_img + 8 + Q8QC + 4 * i) = rh;
+        }
+        if (j < 8) load_halo(j + 8);
       }
     }
+    __builtin_amdgcn_wave_barrier();
+    const float srj = __shfl(srl[j & 1], j >> 1, 8);
+    float win[4 + 2 * 4 * HQ];  // columns c0 - 4HQ .. c0 + 3 + 4HQ
 #pragma unroll
-    for (int u = 0; u < GR; ++u) {
-      const int j = GR * g4 + u;
-      const int64_t g = rb + j;
-      f32x4 xs = xq[u], hs = hq[u];
-      if (sub)
+    for (int k = 0; k < 1 + 2 * HQ; ++k) {
+      const f32x4 t4 = *reinterpret_cast<const f32x4*>(row_img + 8 - 4 * HQ + 4 * cq + 4 * k);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          xs[e] = __fsub_rn(xs[e], mr[u]);
-          hs[e] = __fsub_rn(hs[e], mr[u]);
-        }
-      // the lanes of one row slice exchange their quads through the row image
-      // (wave-private: LDS instructions of a wave execute in order)
-      *reinterpret_cast<f32x4*>(row_img + 8 + 4 * cq) = xs;
-      if (hl || hr) *reinterpret_cast<f32x4*>(row_img + hslot) = hs;
-      __builtin_amdgcn_wave_barrier();
-      float win[4 + 2 * 4 * HQ];  // columns c0 - 4HQ .. c0 + 3 + 4HQ
+      for (int e = 0; e < 4; ++e) win[4 * k + e] = t4[e];
+    }
+    f32x4 y;  // interior formula (the first / last HH columns are redone below)
 #pragma unroll
-      for (int k = 0; k < 1 + 2 * HQ; ++k) {
-        const f32x4 t4 = *reinterpret_cast<const f32x4*>(row_img + 8 - 4 * HQ + 4 * cq + 4 * k);
+    for (int e = 0; e < 4; ++e) {
+      const int o = 4 * HQ + e;  // window index of column c0 + e
+      float a;
+      if constexpr (HH == 0) {
+        a = win[o];
+      } else {
+        if (pa.deriv & 1) {
+          a = 0.f;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) win[4 * k + e] = t4[e];
-      }
-      f32x4 y;  // interior formula (the first / last HH columns are redone below)
+          for (int t = 1; t <= HH; ++t) a = fmaf(ct[t], __fsub_rn(win[o + t], win[o - t]), a);
+        } else if (pa.deriv == 0) {
+          a = __fmul_rn(ct[0], win[o]);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int o = 4 * HQ + e;  // window index of column c0 + e
-        float a;
-        if constexpr (HH == 0) {
-          a = win[o];
+          for (int t = 1; t <= HH; ++t) a = fmaf(ct[t], __fadd_rn(win[o + t], win[o - t]), a);
         } else {
-          if (pa.deriv & 1) {
-            a = 0.f;
+          const float uj = win[o];
+          a = 0.f;
 #pragma unroll
-            for (int t = 1; t <= HH; ++t) a = fmaf(ct[t], __fsub_rn(win[o + t], win[o - t]), a);
-          } else if (pa.deriv == 0) {
-            a = __fmul_rn(ct[0], win[o]);
-#pragma unroll
-            for (int t = 1; t <= HH; ++t) a = fmaf(ct[t], __fadd_rn(win[o + t], win[o - t]), a);
-          } else {
-            const float uj = win[o];
-            a = 0.f;
-#pragma unroll
-            for (int t = 1; t <= HH; ++t)
-              a = fmaf(ct[t], __fadd_rn(__fsub_rn(win[o + t], uj), __fsub_rn(win[o - t], uj)), a);
-          }
+          for (int t = 1; t <= HH; ++t)
+            a = fmaf(ct[t], __fadd_rn(__fsub_rn(win[o + t], uj), __fsub_rn(win[o - t], uj)), a);
         }
-        y[e] = pa.snv ? __fmul_rn(a, sr[u]) : a;
       }
-      __builtin_amdgcn_wave_barrier();  // the image is rewritten by the next row
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[j][e] = (g < r1 && c0 + e < p) ? __fsub_rn(y[e], sh[e]) : 0.f;
+      y[e] = pa.snv ? __fmul_rn(a, srj) : a;
     }
+    __builtin_amdgcn_wave_barrier();  // the image is rewritten by the next row
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[j][e] = (g < r1 && c0 + e < p) ? __fsub_rn(y[e], sh[e]) : 0.f;
   }
   if (HH > 0 && (c0 < HH || c0 + 3 >= p - HH)) {
     // the least-squares edge rows of the first / last HH columns (two column
