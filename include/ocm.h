@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCM_ABI_VERSION 7
+#define OCM_ABI_VERSION 8
 
 #define OCM_OK 0
 #define OCM_ERR_ARG (-1)         /* invalid argument (maps to ValueError) */
@@ -414,11 +414,15 @@ int ocm_decide_f64(ocm_ctx* ctx, const double* T2, const double* Q, int64_t m, c
  * biased variance normalises, unbiased variance feeds running_var with
  * `momentum`).  Replaces the MIOpen spatial BN the reference's nn.BatchNorm1d
  * lowers to (vae_model.py:45-47, 75-77).  running_mean / running_var may both
- * be NULL (no update); gamma / beta may be NULL (affine=False).  scratch [dev,
- * nullable] ocm_bn_scratch_bytes(C) bytes: caller-owned memory that stays
- * put while a captured hipGraph replays the launches (NULL = the context
- * arena, which a later, larger libocm call may re-allocate — do not capture
- * with NULL).  All work is stream-ordered (graph-capturable). */
+ * be NULL (no update); gamma / beta may be NULL (affine=False); num_batches_tracked
+ * [nullable] is incremented by one (nn.BatchNorm1d's counter).  scratch [dev]
+ * ocm_bn_scratch_bytes(C) bytes of caller-owned memory that stays put while a
+ * captured hipGraph replays the launches, ZERO-FILLED BEFORE ITS FIRST USE and
+ * then reused by every call of that layer (forward and backward): it ends in
+ * per-channel completion counters — the last of a channel's reduction
+ * workgroups forms the statistics, one launch per direction fewer — which
+ * every call leaves zero.  Calls sharing one scratch must be stream-ordered.
+ * All work is stream-ordered (graph-capturable). */
 #define OCM_DTYPE_F32 0
 #define OCM_DTYPE_BF16 1
 /* act: OCM_ACT_ELU fuses the ELU (α = 1) that follows every batch norm of the
@@ -429,8 +433,8 @@ int ocm_decide_f64(ocm_ctx* ctx, const double* T2, const double* Q, int64_t m, c
 size_t ocm_bn_scratch_bytes(int32_t C);
 int ocm_bn_fwd_train(ocm_ctx* ctx, int32_t dtype, const void* x, int32_t N, int32_t C, int32_t L,
                      const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
-                     float* running_var, int32_t act, void* y, float* save_mean, float* save_invstd, void* scratch,
-                     void* stream);
+                     float* running_var, int64_t* num_batches_tracked, int32_t act, void* y, float* save_mean,
+                     float* save_invstd, void* scratch, void* stream);
 /* dx = γ·invstd·(dz − mean(dz) − x̂·mean(dz·x̂)), dz = dy (act NONE) or the ELU's input gradient;
  * dgamma = Σ dz·x̂, dbeta = Σ dz (either may be NULL); y [act ELU] the forward's output. */
 int ocm_bn_bwd(ocm_ctx* ctx, int32_t dtype, const void* x, const void* dy, int32_t N, int32_t C, int32_t L,
@@ -452,8 +456,11 @@ int ocm_bn_bwd(ocm_ctx* ctx, int32_t dtype, const void* x, const void* dy, int32
  * ocm_conv1d_wgrad: G[o][i][t] = Σ_b Σ_l P[b][o][l]·Q[b][i][l·s + t − pad], written [O][I][K]
  *   (Conv1d: P = dy, Q = x → its [O][I][K] weight gradient; ConvTranspose1d: P = x, Q = dy → its
  *   [I][O][K] weight gradient); psum_out [nullable] = Σ_b Σ_l P[b][o][l] (Conv1d's bias gradient).
- *   scratch ≥ ocm_conv1d_scratch_bytes(O, I, K); fixed-order two-stage sums (deterministic).
- * ocm_chan_sum: out[c] = Σ_b Σ_l v[b][c][l] (the bias gradient); scratch as above with O·I·K ≥ C. */
+ *   scratch ≥ ocm_conv1d_scratch_bytes(O, I, K), zero-filled before its first use and reused (it
+ *   starts with completion counters that every call leaves zero: the last partial workgroup of
+ *   an output group sums the partials — one launch); fixed-order two-stage sums (deterministic).
+ * ocm_chan_sum: out[c] = Σ_b Σ_l v[b][c][l] (the bias gradient), C ≤ 284; scratch as above with
+ *   O·I·K ≥ C (the same zero-filled, reused memory as the layer's wgrad may serve both). */
 #define OCM_CONV_DOWN 0
 #define OCM_CONV_UP 1
 size_t ocm_conv1d_scratch_bytes(int32_t O, int32_t I, int32_t K);

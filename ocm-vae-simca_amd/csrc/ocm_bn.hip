@@ -16,7 +16,7 @@
 namespace {
 
 constexpr int BN_SPLIT = 64;       // workgroups per channel for the reductions, at least
-constexpr int BN_SPLIT_MAX = 512;  // and at most
+constexpr int BN_SPLIT_MAX = 256;  // and at most
 constexpr int BN_U = 4;            // elements per thread per pass of the reduction kernels
 constexpr int BN_T = 256;
 
@@ -62,10 +62,39 @@ __device__ __forceinline__ float bn_ld_or0(const T* p, int C, int L, int c, int 
   return ok ? v : 0.f;
 }
 
-// grid (split, C): partial Σx, Σx² of channel c over its share of the N·L elements
+// the split partials of channel c summed by one wave (lane-strided, then the
+// fixed butterfly: deterministic)
+__device__ __forceinline__ void bn_part_sum(const double* part, int c, int split, double& s1, double& s2) {
+  const int lane = threadIdx.x & 63;
+  double a1 = 0.0, a2 = 0.0;
+  for (int i = lane; i < split; i += 64) {  // other workgroups' partials: write-through loads
+    a1 += ld_agent(part + ((size_t)c * split + i) * 2 + 0);
+    a2 += ld_agent(part + ((size_t)c * split + i) * 2 + 1);
+  }
+  s1 = wave_sum_f64(a1);
+  s2 = wave_sum_f64(a2);
+}
+
+// The workgroup's partials → part (write-through); true in the last of channel
+// c's split workgroups to arrive (ocm_internal.h last_arrival)
+__device__ __forceinline__ bool bn_ticket(double s1, double s2, double* part, unsigned* ticket, int c, int sp,
+                                          int split) {
+  if (threadIdx.x == 0) {
+    st_agent(part + ((size_t)c * split + sp) * 2 + 0, s1);
+    st_agent(part + ((size_t)c * split + sp) * 2 + 1, s2);
+  }
+  return last_arrival2(ticket, c, (unsigned)split, (unsigned)sp);
+}
+
+// grid (split, C): partial Σx, Σx² of channel c over its share of the N·L
+// elements; the channel's last workgroup forms mean / invstd and the running
+// statistics (and counts the batch in num_batches_tracked, channel 0)
 template <typename T>
 __global__ __launch_bounds__(BN_T) void k_bn_stats(const T* __restrict__ x, int N, int C, int L,
-                                                   double* __restrict__ part) {
+                                                   double* __restrict__ part, unsigned* __restrict__ ticket,
+                                                   float eps, float momentum, float* __restrict__ save_mean,
+                                                   float* __restrict__ save_invstd, float* __restrict__ running_mean,
+                                                   float* __restrict__ running_var, int64_t* __restrict__ nbt) {
   __shared__ double red[BN_T / 64];
   const int c = blockIdx.y, sp = blockIdx.x, split = gridDim.x;
   const int total = N * L, step = split * BN_T;
@@ -82,37 +111,13 @@ __global__ __launch_bounds__(BN_T) void k_bn_stats(const T* __restrict__ x, int 
   }
   const double s1 = block_sum_f64(a1, red);
   const double s2 = block_sum_f64(a2, red);
-  if (threadIdx.x == 0) {
-    part[((size_t)c * split + sp) * 2 + 0] = s1;
-    part[((size_t)c * split + sp) * 2 + 1] = s2;
-  }
-}
-
-// the split partials of channel c summed by one wave (lane-strided, then the
-// fixed butterfly: deterministic)
-__device__ __forceinline__ void bn_part_sum(const double* part, int c, int split, double& s1, double& s2) {
-  const int lane = threadIdx.x;
-  double a1 = 0.0, a2 = 0.0;
-  for (int i = lane; i < split; i += 64) {
-    a1 += part[((size_t)c * split + i) * 2 + 0];
-    a2 += part[((size_t)c * split + i) * 2 + 1];
-  }
-  s1 = wave_sum_f64(a1);
-  s2 = wave_sum_f64(a2);
-}
-
-// grid C × one wave: mean / invstd and the running-stat update
-__global__ __launch_bounds__(64) void k_bn_finalize(const double* __restrict__ part, int C, int split, int64_t M,
-                                                    float eps, float momentum, float* __restrict__ save_mean,
-                                                    float* __restrict__ save_invstd,
-                                                    float* __restrict__ running_mean,
-                                                    float* __restrict__ running_var) {
-  const int c = blockIdx.x;
-  double s1, s2;
-  bn_part_sum(part, c, split, s1, s2);
+  if (!bn_ticket(s1, s2, part, ticket, c, sp, split) || threadIdx.x >= 64) return;
+  double t1, t2;
+  bn_part_sum(part, c, split, t1, t2);
   if (threadIdx.x != 0) return;
-  const double mean = s1 / (double)M;
-  const double var = fmax(s2 / (double)M - mean * mean, 0.0);
+  const int64_t M = (int64_t)N * L;
+  const double mean = t1 / (double)M;
+  const double var = fmax(t2 / (double)M - mean * mean, 0.0);
   save_mean[c] = (float)mean;
   save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
   if (running_mean) {
@@ -120,6 +125,7 @@ __global__ __launch_bounds__(64) void k_bn_finalize(const double* __restrict__ p
     running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
     running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
   }
+  if (nbt && c == 0) *nbt += 1;
 }
 
 // grid (ceil(L / BN_T), N·C): y = (x − μ)·invstd·γ + β, then ELU (α = 1) when
@@ -149,12 +155,15 @@ __device__ __forceinline__ float bn_grad(const T* dy, const T* ya, int64_t i) {
   return v > 0.f ? g : g * (v + 1.f);
 }
 
-// grid (split, C): partial Σdz, Σdz·x̂
+// grid (split, C): partial Σdz, Σdz·x̂; the channel's last workgroup forms
+// the sums (and dβ, dγ)
 template <typename T, bool ELU>
 __global__ __launch_bounds__(BN_T) void k_bn_bwd_stats(const T* __restrict__ x, const T* __restrict__ dy,
                                                        const T* __restrict__ ya, int N,
                                                        int C, int L, const float* __restrict__ mean,
-                                                       const float* __restrict__ invstd, double* __restrict__ part) {
+                                                       const float* __restrict__ invstd, double* __restrict__ part,
+                                                       unsigned* __restrict__ ticket, double* __restrict__ sums,
+                                                       float* __restrict__ dgamma, float* __restrict__ dbeta) {
   __shared__ double red[BN_T / 64];
   const int c = blockIdx.y, sp = blockIdx.x, split = gridDim.x;
   const float mu = mean[c], is = invstd[c];
@@ -180,23 +189,14 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_stats(const T* __restrict__ x, 
   }
   const double s1 = block_sum_f64(a1, red);
   const double s2 = block_sum_f64(a2, red);
-  if (threadIdx.x == 0) {
-    part[((size_t)c * split + sp) * 2 + 0] = s1;
-    part[((size_t)c * split + sp) * 2 + 1] = s2;
-  }
-}
-
-__global__ __launch_bounds__(64) void k_bn_bwd_finalize(const double* __restrict__ part, int C, int split,
-                                                        double* __restrict__ sums, float* __restrict__ dgamma,
-                                                        float* __restrict__ dbeta) {
-  const int c = blockIdx.x;
-  double s1, s2;
-  bn_part_sum(part, c, split, s1, s2);
+  if (!bn_ticket(s1, s2, part, ticket, c, sp, split) || threadIdx.x >= 64) return;
+  double t1, t2;
+  bn_part_sum(part, c, split, t1, t2);
   if (threadIdx.x != 0) return;
-  sums[2 * c] = s1;
-  sums[2 * c + 1] = s2;
-  if (dbeta) dbeta[c] = (float)s1;
-  if (dgamma) dgamma[c] = (float)s2;
+  sums[2 * c] = t1;
+  sums[2 * c + 1] = t2;
+  if (dbeta) dbeta[c] = (float)t1;
+  if (dgamma) dgamma[c] = (float)t2;
 }
 
 // dx = γ·invstd·(dz − Σdz/M − x̂·Σ(dz·x̂)/M)
@@ -218,20 +218,23 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_apply(const T* __restrict__ x, 
   bn_st(dx, i, k * (bn_grad<ELU>(dy, ya, i) - m1 - xh * m2));
 }
 
-// scratch of one forward / backward call: per-(channel, split) partials + the
-// backward's channel sums
-size_t bn_scratch(int C) { return ((size_t)C * bn_split(C) * 2 + 2 * (size_t)C) * sizeof(double); }
+// scratch of the forward / backward calls: per-(channel, split) partials, the
+// backward's channel sums, then one completion counter per channel (zero
+// before the first call; every call leaves them zero)
+size_t bn_part_doubles(int C) { return (size_t)C * bn_split(C) * 2 + 2 * (size_t)C; }
+size_t bn_scratch(int C) {
+  return bn_part_doubles(C) * sizeof(double) + (size_t)C * tickets_per_slot(bn_split(C)) * TICKET_STRIDE * sizeof(unsigned);
+}
 
 template <typename T>
 int bn_fwd(ocm_ctx* ctx, const void* x, int N, int C, int L, const float* gamma, const float* beta, float eps,
-           float momentum, float* rmean, float* rvar, void* y, float* smean, float* sinv, void* scratch, int act,
-           hipStream_t st) {
-  auto* part = static_cast<double*>(scratch ? scratch : ocm::workspace(ctx, bn_scratch(C), st));
-  if (!part) return OCM_ERR_NOMEM;
+           float momentum, float* rmean, float* rvar, int64_t* nbt, void* y, float* smean, float* sinv,
+           void* scratch, int act, hipStream_t st) {
+  auto* part = static_cast<double*>(scratch);
+  auto* ticket = reinterpret_cast<unsigned*>(part + bn_part_doubles(C));
   const int split = bn_split(C);
-  hipLaunchKernelGGL(k_bn_stats<T>, dim3(split, C), dim3(BN_T), 0, st, static_cast<const T*>(x), N, C, L, part);
-  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(64), 0, st, part, C, split, (int64_t)N * L, eps,
-                     momentum, smean, sinv, rmean, rvar);
+  hipLaunchKernelGGL(k_bn_stats<T>, dim3(split, C), dim3(BN_T), 0, st, static_cast<const T*>(x), N, C, L, part,
+                     ticket, eps, momentum, smean, sinv, rmean, rvar, nbt);
   const dim3 ga((L + BN_T - 1) / BN_T, N * C);
   if (act == OCM_ACT_ELU)
     hipLaunchKernelGGL((k_bn_apply<T, true>), ga, dim3(BN_T), 0, st, static_cast<const T*>(x), C, L, smean, sinv,
@@ -247,13 +250,13 @@ template <typename T, bool ELU>
 int bn_bwd(ocm_ctx* ctx, const void* x, const void* dy, const void* ya, int N, int C, int L, const float* gamma,
            const float* smean, const float* sinv, void* dx, float* dgamma, float* dbeta, void* scratch,
            hipStream_t st) {
-  auto* part = static_cast<double*>(scratch ? scratch : ocm::workspace(ctx, bn_scratch(C), st));
-  if (!part) return OCM_ERR_NOMEM;
+  auto* part = static_cast<double*>(scratch);
+  auto* ticket = reinterpret_cast<unsigned*>(part + bn_part_doubles(C));
   const int split = bn_split(C);
   double* sums = part + (size_t)C * split * 2;
   hipLaunchKernelGGL((k_bn_bwd_stats<T, ELU>), dim3(split, C), dim3(BN_T), 0, st, static_cast<const T*>(x),
-                     static_cast<const T*>(dy), static_cast<const T*>(ya), N, C, L, smean, sinv, part);
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(C), dim3(64), 0, st, part, C, split, sums, dgamma, dbeta);
+                     static_cast<const T*>(dy), static_cast<const T*>(ya), N, C, L, smean, sinv, part, ticket, sums,
+                     dgamma, dbeta);
   hipLaunchKernelGGL((k_bn_bwd_apply<T, ELU>), dim3((L + BN_T - 1) / BN_T, N * C), dim3(BN_T), 0, st,
                      static_cast<const T*>(x), static_cast<const T*>(dy), static_cast<const T*>(ya), C, L,
                      (int64_t)N * L, smean, sinv, gamma, sums, static_cast<T*>(dx));
@@ -269,26 +272,26 @@ size_t ocm_bn_scratch_bytes(int32_t C) { return C > 0 ? bn_scratch(C) : 0; }
 
 int ocm_bn_fwd_train(ocm_ctx* ctx, int32_t dtype, const void* x, int32_t N, int32_t C, int32_t L,
                      const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
-                     float* running_var, int32_t act, void* y, float* save_mean, float* save_invstd, void* scratch,
-                     void* stream) {
-  OCM_REQUIRE(ctx && x && y && save_mean && save_invstd, "ocm_bn_fwd_train: NULL argument");
+                     float* running_var, int64_t* num_batches_tracked, int32_t act, void* y, float* save_mean,
+                     float* save_invstd, void* scratch, void* stream) {
+  OCM_REQUIRE(ctx && x && y && save_mean && save_invstd && scratch, "ocm_bn_fwd_train: NULL argument");
   OCM_REQUIRE(N > 0 && C > 0 && L > 0 && (int64_t)N * L < INT32_MAX, "ocm_bn_fwd_train: bad shape");
   OCM_REQUIRE(!running_mean == !running_var, "ocm_bn_fwd_train: running_mean and running_var go together");
   OCM_REQUIRE(act == OCM_ACT_NONE || act == OCM_ACT_ELU, "ocm_bn_fwd_train: act must be OCM_ACT_NONE or OCM_ACT_ELU");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == OCM_DTYPE_F32)
-    return bn_fwd<float>(ctx, x, N, C, L, gamma, beta, eps, momentum, running_mean, running_var, y, save_mean,
-                         save_invstd, scratch, act, st);
+    return bn_fwd<float>(ctx, x, N, C, L, gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked,
+                         y, save_mean, save_invstd, scratch, act, st);
   if (dtype == OCM_DTYPE_BF16)
-    return bn_fwd<bf16_t>(ctx, x, N, C, L, gamma, beta, eps, momentum, running_mean, running_var, y, save_mean,
-                          save_invstd, scratch, act, st);
+    return bn_fwd<bf16_t>(ctx, x, N, C, L, gamma, beta, eps, momentum, running_mean, running_var,
+                          num_batches_tracked, y, save_mean, save_invstd, scratch, act, st);
   return ocm::fail(OCM_ERR_ARG, "ocm_bn_fwd_train: dtype must be OCM_DTYPE_F32 or OCM_DTYPE_BF16");
 }
 
 int ocm_bn_bwd(ocm_ctx* ctx, int32_t dtype, const void* x, const void* dy, int32_t N, int32_t C, int32_t L,
                const float* gamma, const float* save_mean, const float* save_invstd, int32_t act, const void* y,
                void* dx, float* dgamma, float* dbeta, void* scratch, void* stream) {
-  OCM_REQUIRE(ctx && x && dy && dx && save_mean && save_invstd, "ocm_bn_bwd: NULL argument");
+  OCM_REQUIRE(ctx && x && dy && dx && save_mean && save_invstd && scratch, "ocm_bn_bwd: NULL argument");
   OCM_REQUIRE(N > 0 && C > 0 && L > 0 && (int64_t)N * L < INT32_MAX, "ocm_bn_bwd: bad shape");
   OCM_REQUIRE(act == OCM_ACT_NONE || (act == OCM_ACT_ELU && y), "ocm_bn_bwd: the fused ELU needs its output y");
   hipStream_t st = (hipStream_t)stream;

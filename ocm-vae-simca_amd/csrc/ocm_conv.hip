@@ -52,6 +52,16 @@ __device__ __forceinline__ float cv_ld_or0(const T* p, int i, int n, bool ok) {
 }
 constexpr int WG_SPLIT = 128;   // csum partial workgroups per channel
 constexpr int WG_MAXSPLIT = 1024;  // wgrad partial workgroups per (o, i) pair, at most
+// scratch layout: CV_TICKETS completion counter words (zero before the first
+// call; every call leaves them zero), then the partials.  wgrad: groups ·
+// tickets_per_slot(split) counters, ≤ 2·1024 + 4096/16; chan_sum: C·9
+constexpr int CV_TICKETS = 2560 * TICKET_STRIDE;
+
+// true in the last of the gridDim.x workgroups of slot `slot` to arrive
+// (ocm_internal.h last_arrival; partials stored with st_agent)
+__device__ __forceinline__ bool cv_last(unsigned* ticket, int slot) {
+  return last_arrival2(ticket, slot, gridDim.x, blockIdx.x);
+}
 
 // down / up: grid (ceil(Lout / CV_T), ceil(O / 4), B).  KT ≥ K is the
 // compile-time tap count, so the taps of one input channel unroll and their
@@ -140,7 +150,8 @@ __global__ __launch_bounds__(CV_T) void k_conv(const TI* __restrict__ x, int I, 
 template <int KT, bool WB, typename TP, typename TQ>
 __global__ __launch_bounds__(CV_T) void k_conv_wgrad(const TP* __restrict__ P, int O, int Lp, const TQ* __restrict__ Q,
                                                     int I, int Lq, int B, int K, int s, int pad,
-                                                    float* __restrict__ part) {
+                                                    float* __restrict__ part, unsigned* __restrict__ ticket,
+                                                    float* __restrict__ G, float* __restrict__ db) {
   constexpr int NA = KT + (WB ? 1 : 0);
   __shared__ float red[CV_T / 64][CV_OG][NA];
   const int i = blockIdx.y % I, o0 = (blockIdx.y / I) * CV_OG;
@@ -188,33 +199,33 @@ __global__ __launch_bounds__(CV_T) void k_conv_wgrad(const TP* __restrict__ P, i
     const int u = e / KS, t = e % KS, o = o0 + u;
     const int ts = (WB && t == K) ? NA - 1 : t;
     if (o < O)
-      part[(((int64_t)o * I + i) * gridDim.x + blockIdx.x) * KS + t] =
-          (red[0][u][ts] + red[1][u][ts]) + (red[2][u][ts] + red[3][u][ts]);
+      st_agent(part + (((int64_t)o * I + i) * gridDim.x + blockIdx.x) * KS + t,
+               (red[0][u][ts] + red[1][u][ts]) + (red[2][u][ts] + red[3][u][ts]));
+  }
+  // the group's last workgroup: G[(o·I + i)·K + t] = Σ_x part[((o·I + i)·split + x)·KS + t],
+  // one wave per output (lane-strided partials, then the wave sum: a fixed
+  // order); with WB the i = 0 slot t = K of each o is its bias gradient, db[o]
+  if (!cv_last(ticket, blockIdx.y)) return;
+  const int split = gridDim.x;
+  for (int e = wv; e < CV_OG * KS; e += CV_T / 64) {
+    const int u = e / KS, t = e % KS, o = o0 + u;
+    if (o >= O) continue;
+    const int64_t pair = (int64_t)o * I + i;
+    float v = 0.f;
+    for (int xb = lane; xb < split; xb += 64) v += ld_agent(part + (pair * split + xb) * KS + t);
+    v = wave_sum_f32(v);
+    if (lane) continue;
+    if (t < K) G[pair * K + t] = v;
+    else if (i == 0) db[o] = v;
   }
 }
 
-// G[(o·I + i)·K + t] = Σ_x part[((o·I + i)·split + x)·KS + t], one wave per
-// output (lane-strided partials, then the wave sum: a fixed order); with WB
-// the i = 0 slot t = K of each o is its bias gradient, db[o].
-__global__ __launch_bounds__(CV_T) void k_conv_wgrad_reduce(const float* __restrict__ part, int O, int I, int K,
-                                                           int KS, int split, float* __restrict__ G,
-                                                           float* __restrict__ db) {
-  const int wv = (blockIdx.x * CV_T + threadIdx.x) >> 6, lane = threadIdx.x & 63;
-  const int nout = O * I * KS;
-  if (wv >= nout) return;
-  const int pair = wv / KS, t = wv % KS;
-  float v = 0.f;
-  for (int xb = lane; xb < split; xb += 64) v += part[((int64_t)pair * split + xb) * KS + t];
-  v = wave_sum_f32(v);
-  if (lane) return;
-  if (t < K) G[(int64_t)pair * K + t] = v;
-  else if (pair % I == 0) db[pair / I] = v;
-}
-
-// per-channel sums of (B, C, L): grid (WG_SPLIT, C) partials, then one reduce
+// per-channel sums of (B, C, L): grid (WG_SPLIT, C) partials; the channel's
+// last workgroup sums them in order (fp64)
 template <typename T>
 __global__ __launch_bounds__(CV_T) void k_chan_sum(const T* __restrict__ v, int B, int C, int L,
-                                                  float* __restrict__ part) {
+                                                  float* __restrict__ part, unsigned* __restrict__ ticket,
+                                                  float* __restrict__ out) {
   __shared__ float red[CV_T / 64];
   const int c = blockIdx.y;
   const int total = B * L;  // < 2³¹ (checked by the host)
@@ -226,15 +237,11 @@ __global__ __launch_bounds__(CV_T) void k_chan_sum(const T* __restrict__ v, int 
   a = wave_sum_f32(a);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
   __syncthreads();
-  if (threadIdx.x == 0) part[(int64_t)c * WG_SPLIT + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
-}
-
-__global__ void k_chan_sum_reduce(const float* __restrict__ part, int C, float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double v = 0.0;
-  for (int xb = 0; xb < WG_SPLIT; ++xb) v += part[(int64_t)c * WG_SPLIT + xb];
-  out[c] = (float)v;
+  if (threadIdx.x == 0) st_agent(part + (int64_t)c * WG_SPLIT + blockIdx.x, (red[0] + red[1]) + (red[2] + red[3]));
+  if (!cv_last(ticket, c) || threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int xb = 0; xb < WG_SPLIT; ++xb) s += ld_agent(part + (int64_t)c * WG_SPLIT + xb);
+  out[c] = (float)s;
 }
 
 template <bool UP, int KT>
@@ -269,7 +276,8 @@ int launch_conv(int dti, int dto, const void* x, int B, int I, int Lin, const fl
 extern "C" {
 
 size_t ocm_conv1d_scratch_bytes(int32_t O, int32_t I, int32_t K) {
-  return (size_t)((int64_t)O * I * (K + 1) + (int64_t)(O > I ? O : I)) * WG_MAXSPLIT * sizeof(float) + 256;
+  return CV_TICKETS * sizeof(unsigned) +
+         (size_t)((int64_t)O * I * (K + 1) + (int64_t)(O > I ? O : I)) * WG_MAXSPLIT * sizeof(float) + 256;
 }
 
 int ocm_conv1d(ocm_ctx* ctx, int32_t mode, int32_t dtype_in, const void* x, int32_t B, int32_t I, int32_t Lin,
@@ -292,14 +300,15 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
                      const void* Q, int32_t I, int32_t Lq, int32_t B, int32_t K, int32_t stride, int32_t pad,
                      float* G_out, float* psum_out, void* scratch, void* stream) {
   OCM_REQUIRE(ctx && P && Q && G_out && scratch, "ocm_conv1d_wgrad: NULL argument");
-  OCM_REQUIRE(B > 0 && O > 0 && I > 0 && Lp > 0 && Lq > 0 && (int64_t)I * ((O + CV_OG - 1) / CV_OG) <= 65535,
+  OCM_REQUIRE(B > 0 && O > 0 && I > 0 && Lp > 0 && Lq > 0 && (int64_t)I * ((O + CV_OG - 1) / CV_OG) <= 1024,
               "ocm_conv1d_wgrad: bad shape");
   OCM_REQUIRE(K >= 1 && K <= CV_KMAX && stride >= 1 && pad >= 0, "ocm_conv1d_wgrad: kernel ≤ 15, stride ≥ 1");
   OCM_REQUIRE((dtype_p == OCM_DTYPE_F32 || dtype_p == OCM_DTYPE_BF16) &&
                   (dtype_q == OCM_DTYPE_F32 || dtype_q == OCM_DTYPE_BF16),
               "ocm_conv1d_wgrad: float32 / bfloat16 activations");
   hipStream_t st = (hipStream_t)stream;
-  float* part = static_cast<float*>(scratch);
+  auto* ticket = static_cast<unsigned*>(scratch);
+  float* part = reinterpret_cast<float*>(ticket + CV_TICKETS);
   OCM_REQUIRE((int64_t)B * Lp < (1LL << 31), "ocm_conv1d_wgrad: B·Lp must be < 2^31");
   const int groups = I * ((O + CV_OG - 1) / CV_OG);
   // ≈ 4096 workgroups in all, so a layer with few channels still fills the chip,
@@ -310,7 +319,7 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
   dim3 g((unsigned)split, (unsigned)groups);
 #define OCM_WG_K(KT, WB, TP, TQ)                                                                            \
   hipLaunchKernelGGL((k_conv_wgrad<KT, WB, TP, TQ>), g, dim3(CV_T), 0, st, static_cast<const TP*>(P), O, Lp,   \
-                     static_cast<const TQ*>(Q), I, Lq, B, K, stride, pad, part)
+                     static_cast<const TQ*>(Q), I, Lq, B, K, stride, pad, part, ticket, G_out, psum_out)
 #define OCM_WG_L(TP, TQ)                                  \
   do {                                                    \
     if (K <= 7 && wb) OCM_WG_K(7, true, TP, TQ);          \
@@ -325,29 +334,27 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
 #undef OCM_WG_L
 #undef OCM_WG_K
   OCM_CHECK_LAUNCH("k_conv_wgrad");
-  const int KS = K + (wb ? 1 : 0);
-  const int64_t waves = (int64_t)O * I * KS;
-  hipLaunchKernelGGL(k_conv_wgrad_reduce, dim3((unsigned)((waves * 64 + CV_T - 1) / CV_T)), dim3(CV_T), 0, st, part,
-                     O, I, K, KS, split, G_out, psum_out);
-  OCM_CHECK_LAUNCH("k_conv_wgrad_reduce");
   return OCM_OK;
 }
 
 int ocm_chan_sum(ocm_ctx* ctx, int32_t dtype, const void* v, int32_t B, int32_t C, int32_t L, float* out,
                  void* scratch, void* stream) {
   OCM_REQUIRE(ctx && v && out && scratch, "ocm_chan_sum: NULL argument");
-  OCM_REQUIRE(B > 0 && C > 0 && L > 0 && C <= 65535 && (int64_t)B * L < (1LL << 31), "ocm_chan_sum: bad shape");
+  OCM_REQUIRE(B > 0 && C > 0 && L > 0 && C * tickets_per_slot(WG_SPLIT) * TICKET_STRIDE <= CV_TICKETS &&
+                  (int64_t)B * L < (1LL << 31),
+              "ocm_chan_sum: bad shape (C ≤ 284)");
   OCM_REQUIRE(dtype == OCM_DTYPE_F32 || dtype == OCM_DTYPE_BF16, "ocm_chan_sum: float32 / bfloat16");
   hipStream_t st = (hipStream_t)stream;
-  float* part = static_cast<float*>(scratch);
+  auto* ticket = static_cast<unsigned*>(scratch);
+  float* part = reinterpret_cast<float*>(ticket + CV_TICKETS);
   dim3 g(WG_SPLIT, (unsigned)C);
   if (dtype == OCM_DTYPE_F32)
-    hipLaunchKernelGGL(k_chan_sum<float>, g, dim3(CV_T), 0, st, static_cast<const float*>(v), B, C, L, part);
+    hipLaunchKernelGGL(k_chan_sum<float>, g, dim3(CV_T), 0, st, static_cast<const float*>(v), B, C, L, part, ticket,
+                       out);
   else
-    hipLaunchKernelGGL(k_chan_sum<bf16_t>, g, dim3(CV_T), 0, st, static_cast<const bf16_t*>(v), B, C, L, part);
+    hipLaunchKernelGGL(k_chan_sum<bf16_t>, g, dim3(CV_T), 0, st, static_cast<const bf16_t*>(v), B, C, L, part,
+                       ticket, out);
   OCM_CHECK_LAUNCH("k_chan_sum");
-  hipLaunchKernelGGL(k_chan_sum_reduce, dim3((unsigned)((C + 63) / 64)), dim3(64), 0, st, part, C, out);
-  OCM_CHECK_LAUNCH("k_chan_sum_reduce");
   return OCM_OK;
 }
 

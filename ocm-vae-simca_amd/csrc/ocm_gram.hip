@@ -707,16 +707,26 @@ constexpr int Q8QT = Q8QS * (Q8QC / 4);    // threads (768)
 // The quantiser after the load: v = this thread's 16 rows × 4 columns of
 // y − shift.  Column sums, the outlier screen, the block scale, the digits
 // and their LDS-staged stores (shared by k_q8_quant and k_q8_quant_prep).
+// q8_tail's LDS (the caller declares it: k_q8_quant_prep overlays its own
+// load-phase buffers on it)
+struct Q8TailLds {
+  __attribute__((aligned(16))) char stage[Q8SPB * Q8QC * 32];  // one digit plane: 24 KiB
+  __attribute__((aligned(16))) float wmax[Q8QS][Q8QC];
+  __attribute__((aligned(16))) double wsum[Q8QS][Q8QC];
+  float pmax[8][Q8QC];
+  double psum[8][Q8QC];
+  __attribute__((aligned(16))) float fmax_[Q8QC];
+};
 __device__ __forceinline__ void q8_tail(f32x4 (&v)[16], int tid, int cq, int rs, int cg0, int c0, int64_t rb,
                                         const Q8Plan& q, int chunk, int b, const SegTable& st,
-                                        double* __restrict__ colblk) {
+                                        double* __restrict__ colblk, Q8TailLds& L) {
   constexpr int QC = Q8QC;
-  __shared__ __attribute__((aligned(16))) char stage[Q8SPB * QC * 32];  // one digit plane: 24 KiB
-  __shared__ __attribute__((aligned(16))) float wmax[Q8QS][QC];
-  __shared__ __attribute__((aligned(16))) double wsum[Q8QS][QC];
-  __shared__ float pmax[8][QC];
-  __shared__ double psum[8][QC];
-  __shared__ __attribute__((aligned(16))) float fmax_[QC];
+  char* stage = L.stage;
+  auto& wmax = L.wmax;
+  auto& wsum = L.wsum;
+  auto& pmax = L.pmax;
+  auto& psum = L.psum;
+  float* fmax_ = L.fmax_;
   // column sums over every row (the fix-up does not touch them)
   double cs[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -903,28 +913,50 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ 
       for (int e = 0; e < 4; ++e) v[j][e] = (g < r1 && c0 + e < p) ? x[e] - sh[e] : 0.f;
     }
   }
-  q8_tail(v, tid, cq, rs, cg0, c0, rb, q, chunk, b, st, colblk);
+  __shared__ Q8TailLds lds;
+  q8_tail(v, tid, cq, rs, cg0, c0, rb, q, chunk, b, st, colblk, lds);
 }
 
 // k_q8_quant with the preprocessing of a lazy view applied in the load path
-// (include/ocm.h ocm_prep; HH = window / 2 ∈ {0, 2, 7}).  Each thread loads
-// its raw quad of 16 rows as k_q8_quant does; lanes cq < HQ and cq ≥ 8 − HQ
-// also load the HQ = ⌈HH/4⌉ halo quads left / right of the workgroup's 32
-// columns.  Per row, the eight lanes of a row slice put their quads in a
-// wave-private LDS row image (columns cg0 − 8 .. cg0 + 39) and read back the
-// (4 + 2·HH)-sample window of their four outputs: the stencil runs on the
-// VALU under the HBM stream, the rows are read from HBM once.  Rows in
-// groups of four (raw quads and halos in flight per group) keep the VGPRs of
-// the 16 output quads plus one group's loads.
-constexpr int PQ_ROW = 48;  // floats per row image: 8 halo + 32 + 8 halo
+// (include/ocm.h ocm_prep; the fused forms of PrepArgs::fused_form, HH =
+// window / 2 ∈ {0, 2, 7}).  Load phase, before any compute (k_q8_quant's
+// memory-level parallelism): each lane's raw quad of its 16 rows, the rows'
+// SNV (s_r, m_r) and — HH > 0 — the halo of two of its slice's rows (lane cq:
+// rows cq and cq + 8, the HQ = ⌈HH/4⌉ quads left and right of the workgroup's
+// 32 columns), which go to an LDS halo table as soon as they land: the row
+// loop holds only the 16 output quads.  Per row, the eight lanes of a row
+// slice put their quads in a wave-private LDS row image and read their
+// (4 + 2·4HQ)-column window back from the image or the halo table; the row
+// ends use the least-squares edge rows.  The load phase's LDS overlays
+// q8_tail's.
+template <int HH>
+struct Q8PrepLds {
+  static constexpr int HQ = (HH + 3) / 4, WN = 2 * HH + 1;
+  __attribute__((aligned(16))) float img[Q8QS][Q8QC];                 // one row image per row slice
+  __attribute__((aligned(16))) f32x4 halo[HQ > 0 ? Q8QS * 16 * 2 * HQ : 1];  // [slice][row][side][quad]
+  float etap[HH > 0 ? 2 * HH * WN : 1];                                // the edge rows
+};
+template <int HH>
+union Q8PrepUnion {
+  Q8TailLds tail;
+  Q8PrepLds<HH> ld;
+};
 template <bool GATHER, int HH>
 __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restrict__ X, int64_t ldx,
                                                            const int64_t* __restrict__ rows, int p,
                                                            const float* __restrict__ shift, SegTable st, Q8Plan q,
-                                                           double* __restrict__ colblk, int cb0, PrepArgs pa) {
+                                                           double* __restrict__ colblk, int cb0, int ncg,
+                                                           PrepArgs pa) {
   constexpr int HQ = (HH + 3) / 4;
-  __shared__ __attribute__((aligned(16))) float img[Q8QT / 8][PQ_ROW];  // one row image per row slice
-  const int gbk = (int)blockIdx.x + cb0;
+  constexpr int WN = 2 * HH + 1;
+  __shared__ Q8PrepUnion<HH> lds;
+  auto& L = lds.ld;
+  // workgroup → (row block, column group): row blocks fastest, as k_q8_quant
+  // (an XCD-aware order that runs a row block's neighbouring column groups
+  // back to back on one XCD measured 2× slower at HH = 7, r04h)
+  const int nbk = (int)gridDim.x / ncg;
+  const int bki = (int)blockIdx.x % nbk, cgi = (int)blockIdx.x / nbk;
+  const int gbk = bki + cb0;
   const int chunk = gbk / q.nblk, b = gbk - chunk * q.nblk;
   const int tid = threadIdx.x;
   const int cq = tid & 7, rs = tid >> 3;
@@ -933,7 +965,7 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restri
   const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
   const int64_t r1 = min(r0 + (int64_t)st.chunk_rows, st.begin[s + 1]);
   const int64_t rb = r0 + (int64_t)b * Q8BLK + 16 * rs;
-  const int cg0 = (int)blockIdx.y * Q8QC;
+  const int cg0 = cgi * Q8QC;
   const int c0 = cg0 + 4 * cq;
   f32x4 sh;
 #pragma unroll
@@ -942,133 +974,132 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restri
   float ct[HH + 1];
 #pragma unroll
   for (int t = 0; t <= HH; ++t) ct[t] = HH > 0 ? c[t] : 0.f;
-  // Loads, issued before any compute (the plain quantiser's memory-level
-  // parallelism): this lane's raw quad of each of its 16 rows, the rows' SNV
-  // scales, and one row's halo — the HQ quads left and right of the 32 columns
-  // of row cq of the slice's first 8 rows; lane j reloads its halo registers
-  // with row 8 + j's once row j is through, 8 rows ahead of use.  Halo columns
-  // outside the row read as 0 (the edge columns are recomputed below).
-  float* row_img = img[rs];
-  const bool sub = pa.snv && pa.deriv == 0;
+  const bool edge_wg = HH > 0 && (cg0 < HH || cg0 + Q8QC > p - HH);
+  if (edge_wg)
+    for (int i = tid; i < 2 * HH * WN; i += Q8QT) L.etap[i] = pa.taps[WN + i];
+  // ---- load phase.  Addresses are clamped into the row (p % 4 = 0 here):
+  // quads past p are never read back, halo quads outside the row are zeroed.
+  constexpr bool sub = HH == 0;  // SNV alone subtracts the row mean
   f32x4 v[16];
-  float srl[2];  // the SNV scales of rows 2cq, 2cq + 1 (row j's comes from lane j / 2 of the slice)
-  f32x4 hq[2][HQ > 0 ? HQ : 1];  // [left / right][quad]
-  auto load_halo = [&](int jr) {
-    const int64_t g = rb + jr;
-    const int64_t gc = g < r1 ? g : r1 - 1;
-    const float* xr = X + (GATHER ? rows[gc] : gc) * ldx;
-#pragma unroll
-    for (int side = 0; side < 2; ++side)
-#pragma unroll
-      for (int i = 0; i < HQ; ++i) {
-        const int col = side == 0 ? cg0 - 4 * HQ + 4 * i : cg0 + Q8QC + 4 * i;
-        hq[side][i] = col >= 0 && col < p ? *reinterpret_cast<const f32x4*>(xr + col) : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-  };
+  float srl[2], mrl[2];  // the SNV (s_r, m_r) of rows 2cq, 2cq + 1 (row j's come from lane j / 2 of the slice)
+  const int cl0 = min(c0, p - 4);
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int64_t g = rb + j;
     const int64_t gc = g < r1 ? g : r1 - 1;  // clamped: always a valid row
     const int64_t xi = GATHER ? rows[gc] : gc;
-    const float* xr = X + xi * ldx;
-    v[j] = c0 < p ? *reinterpret_cast<const f32x4*>(xr + c0) : f32x4{0.f, 0.f, 0.f, 0.f};
+    v[j] = *reinterpret_cast<const f32x4*>(X + xi * ldx + cl0);
   }
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int64_t g = rb + 2 * cq + u;
     const int64_t gc = g < r1 ? g : r1 - 1;
-    srl[u] = pa.snv ? pa.rowstat[2 * (GATHER ? rows[gc] : gc) + 1] : 1.f;
+    const int64_t xi = GATHER ? rows[gc] : gc;
+    srl[u] = pa.snv ? pa.rowstat[2 * xi + 1] : 1.f;
+    mrl[u] = sub ? pa.rowstat[2 * xi] : 0.f;
   }
-  if constexpr (HQ > 0) load_halo(cq);
+  if constexpr (HQ > 0) {
+    f32x4 hq[2][2][HQ];  // [row cq, cq + 8][left / right][quad]
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t g = rb + cq + 8 * u;
+      const int64_t gc = g < r1 ? g : r1 - 1;
+      const float* xr = X + (GATHER ? rows[gc] : gc) * ldx;
+#pragma unroll
+      for (int side = 0; side < 2; ++side)
+#pragma unroll
+        for (int i = 0; i < HQ; ++i) {
+          const int col = side == 0 ? cg0 - 4 * HQ + 4 * i : cg0 + Q8QC + 4 * i;
+          const f32x4 t4 = *reinterpret_cast<const f32x4*>(xr + min(max(col, 0), p - 4));
+          hq[u][side][i] = col >= 0 && col < p ? t4 : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int side = 0; side < 2; ++side)
+#pragma unroll
+        for (int i = 0; i < HQ; ++i) L.halo[((rs * 16 + cq + 8 * u) * 2 + side) * HQ + i] = hq[u][side][i];
+  }
+  if (edge_wg) __syncthreads();  // etap (the halo table and the row images are wave-private)
+  float* row_img = L.img[rs];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int64_t g = rb + j;
     f32x4 xs = v[j];
-    float mrj = 0.f;  // the row mean: only SNV with a deriv-0 filter subtracts it (rare: read here)
-    if (sub) {
-      const int64_t gc = g < r1 ? g : r1 - 1;
-      mrj = pa.rowstat[2 * (GATHER ? rows[gc] : gc)];
+    if constexpr (sub) {
+      const float mrj = __shfl(mrl[j & 1], j >> 1, 8);
 #pragma unroll
       for (int e = 0; e < 4; ++e) xs[e] = __fsub_rn(xs[e], mrj);
     }
     // the lanes of one row slice exchange their quads through the row image
-    // (wave-private: LDS instructions of a wave execute in order); lane j % 8
-    // holds the row's halo
-    *reinterpret_cast<f32x4*>(row_img + 8 + 4 * cq) = xs;
-    if constexpr (HQ > 0) {
-      if (cq == (j & 7)) {
-#pragma unroll
-        for (int i = 0; i < HQ; ++i) {
-          f32x4 lh = hq[0][i], rh = hq[1][i];
-          if (sub)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              lh[e] = __fsub_rn(lh[e], mrj);
-              rh[e] = __fsub_rn(rh[e], mrj);
-            }
-          *reinterpret_cast<f32x4*>(row_img + 8 - 4 * HQ + 4 * i) = lh;
-          *reinterpret_cast<f32x4*>(row_img + 8 + Q8QC + 4 * i) = rh;
-        }
-        if (j < 8) load_halo(j + 8);
-      }
-    }
+    // (wave-private: LDS instructions of a wave execute in order)
+    *reinterpret_cast<f32x4*>(row_img + 4 * cq) = xs;
     __builtin_amdgcn_wave_barrier();
     const float srj = __shfl(srl[j & 1], j >> 1, 8);
-    float win[4 + 2 * 4 * HQ];  // columns c0 - 4HQ .. c0 + 3 + 4HQ
+    const f32x4* hrow = L.halo + (rs * 16 + j) * 2 * HQ;  // this row's halo: [side][quad]
+    float win[4 + 2 * 4 * HQ];  // columns c0 − 4HQ .. c0 + 3 + 4HQ
 #pragma unroll
     for (int k = 0; k < 1 + 2 * HQ; ++k) {
-      const f32x4 t4 = *reinterpret_cast<const f32x4*>(row_img + 8 - 4 * HQ + 4 * cq + 4 * k);
+      const int qp = cq - HQ + k;  // quad of the row image (−HQ .. 8 + HQ − 1)
+      const f32x4* src = qp < 0 ? hrow + (HQ + qp)
+                       : qp >= Q8QC / 4 ? hrow + HQ + (qp - Q8QC / 4)
+                                        : reinterpret_cast<const f32x4*>(row_img) + qp;
+      const f32x4 t4 = *src;
 #pragma unroll
       for (int e = 0; e < 4; ++e) win[4 * k + e] = t4[e];
     }
-    f32x4 y;  // interior formula (the first / last HH columns are redone below)
+    f32x4 y;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int o = 4 * HQ + e;  // window index of column c0 + e
       float a;
       if constexpr (HH == 0) {
         a = win[o];
-      } else {
-        if (pa.deriv & 1) {
-          a = 0.f;
+      } else {  // odd derivative
+        a = 0.f;
 #pragma unroll
-          for (int t = 1; t <= HH; ++t) a = fmaf(ct[t], __fsub_rn(win[o + t], win[o - t]), a);
-        } else if (pa.deriv == 0) {
-          a = __fmul_rn(ct[0], win[o]);
+        for (int t = 1; t <= HH; ++t) a = fmaf(ct[t], __fsub_rn(win[o + t], win[o - t]), a);
+      }
+      y[e] = ocm::mul_nc(a, srj);  // s_r = 1 without SNV (exact)
+    }
+    if constexpr (HH > 0) {
+      // the row's first / last HH columns: the edge rows over the row's first /
+      // last WN samples (prep_fused_gram keeps them inside this workgroup's
+      // image and halo); deriv ≥ 1 subtracts the output column's own sample
+      if (edge_wg) {
+        auto at = [&](int col) -> float {
+          const int d = col - cg0;
+          const float* hf = reinterpret_cast<const float*>(hrow);
+          return *(d < 0 ? hf + 4 * HQ + d : d >= Q8QC ? hf + 4 * HQ + (d - Q8QC) : row_img + d);
+        };
+        // (rolled loops: two workgroup columns of the grid run this, and
+        // unrolled it would keep 4·WN addresses live across the row loop)
+#pragma unroll 1
+        for (int e = 0; e < 4; ++e) {
+          const int jc = c0 + e;
+          const bool left = jc < HH;
+          float a = 0.f;
+          if (left || (jc >= p - HH && jc < p)) {
+            const int i = left ? jc : HH + jc - (p - HH);
+            const int s0 = left ? 0 : p - WN;
+            const float ref = at(jc);
+#pragma unroll 1
+            for (int t = 0; t < WN; ++t) a = fmaf(L.etap[i * WN + t], __fsub_rn(at(s0 + t), ref), a);
+            a = ocm::mul_nc(a, srj);
+          }
 #pragma unroll
-          for (int t = 1; t <= HH; ++t) a = fmaf(ct[t], __fadd_rn(win[o + t], win[o - t]), a);
-        } else {
-          const float uj = win[o];
-          a = 0.f;
-#pragma unroll
-          for (int t = 1; t <= HH; ++t)
-            a = fmaf(ct[t], __fadd_rn(__fsub_rn(win[o + t], uj), __fsub_rn(win[o - t], uj)), a);
+          for (int u = 0; u < 4; ++u)
+            if (u == e && (left || (jc >= p - HH && jc < p))) y[u] = a;
         }
       }
-      y[e] = pa.snv ? __fmul_rn(a, srj) : a;
     }
     __builtin_amdgcn_wave_barrier();  // the image is rewritten by the next row
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[j][e] = (g < r1 && c0 + e < p) ? __fsub_rn(y[e], sh[e]) : 0.f;
   }
-  if (HH > 0 && (c0 < HH || c0 + 3 >= p - HH)) {
-    // the least-squares edge rows of the first / last HH columns (two column
-    // groups of the grid): the scalar formula, the raw rows again from cache
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int64_t g = rb + j;
-      if (g >= r1) continue;
-      const int64_t xr = GATHER ? rows[g] : g;
-      const float m = pa.snv ? pa.rowstat[2 * xr] : 0.f, sc = pa.snv ? pa.rowstat[2 * xr + 1] : 1.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int jc = c0 + e;
-        if (jc < p && (jc < HH || jc >= p - HH))
-          v[j][e] = __fsub_rn(ocm::prep_elem(X + xr * ldx, p, jc, pa, m, sc), sh[e]);
-      }
-    }
-  }
-  q8_tail(v, tid, cq, rs, cg0, c0, rb, q, chunk, b, st, colblk);
+  __syncthreads();  // q8_tail's LDS overlays the load phase's
+  q8_tail(v, tid, cq, rs, cg0, c0, rb, q, chunk, b, st, colblk, lds.tail);
 }
 
 // Column sums of the quantiser's per-block partials: rows [c0, c1) of colblk
@@ -2488,10 +2519,11 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     dim3 gq((unsigned)((c1 - c0) * nblk * cgw), (unsigned)(P8 / Q8QC / cgw));
     ocm::TimedRegion tq(ctx, OCM_KERNEL_QUANT, qs, !unguarded);
     if (prep) {
-      const dim3 gp((unsigned)((c1 - c0) * nblk), (unsigned)(P8 / Q8QC));
+      const int ncg = P8 / Q8QC;
+      const dim3 gp((unsigned)((c1 - c0) * nblk * ncg));
 #define Q8P_LAUNCH(G_, H_)                                                                                        \
   hipLaunchKernelGGL((k_q8_quant_prep<G_, H_>), gp, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g, \
-                     (int)(c0 * nblk), pa)
+                     (int)(c0 * nblk), ncg, pa)
       if (pa.h == 0) {
         if (rows) Q8P_LAUNCH(true, 0); else Q8P_LAUNCH(false, 0);
       } else if (pa.h == 2) {
@@ -2656,7 +2688,9 @@ int gram_materialised(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* 
 
 bool prep_fused_gram(const float* X, int64_t ldx, int32_t p, int32_t mode, const PrepArgs& pa) {
   return (mode == OCM_GRAM_I8X3) && p > SMALL_P && p % 4 == 0 && ldx % 4 == 0 &&
-         (reinterpret_cast<uintptr_t>(X) & 15) == 0 && (pa.h == 0 || pa.h == 2 || pa.h == 7) && p >= pa.w + 8;
+         (reinterpret_cast<uintptr_t>(X) & 15) == 0 && pa.fused_form() && p >= pa.w + 8 &&
+         // the right edge rows' samples inside the last column group's row image
+         (pa.h < 7 || p % Q8QC != 4);
 }
 
 int gram_dispatch(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,

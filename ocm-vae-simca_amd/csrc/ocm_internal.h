@@ -126,6 +126,75 @@ __device__ __forceinline__ float wave_sum_f32(float v) {
   return v;
 }
 
+// ---- last-workgroup reductions without fences -----------------------------
+// A grid's partial results meet in its last workgroup to finish.  MI355X's
+// eight XCDs keep private L2s and a CU's L1 is never refreshed by other CUs'
+// stores, so the hand-off is write-through (MI355X_MICROARCH.md, inter-
+// workgroup visibility, valid forms, table row 1): every partial is stored
+// sc1 (an agent-scope relaxed atomic store), each storing wave drains its
+// stores (s_waitcnt vmcnt(0)) and then ONE lane per workgroup adds to an
+// agent-scope counter; the workgroup whose add returns n − 1 is last and
+// reads the partials with sc1 loads (which bypass its L1).  No
+// __threadfence(): its L2 write-back + L1 invalidate cost ≈ 3.5 µs per
+// workgroup (round 4: a 512-workgroup batch-norm reduction went 6 → 46 µs).
+__device__ __forceinline__ void st_agent(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Called by every thread of the workgroup after its st_agent stores: true in
+// the last of the n workgroups that share `*counter`, which it resets to 0 (so
+// a counter zeroed once stays reusable across launches and graph replays).
+__device__ __forceinline__ bool last_arrival(unsigned* counter, unsigned n) {
+  __shared__ bool last_;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have left
+  __syncthreads();                                   // ... and every other wave's
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_ = old == n - 1;
+    if (last_) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return last_;
+}
+// Two-level form for wide grids: n arrivals at one counter queue up at the
+// memory-side atomic unit (≈ 50 ns apart: 256 workgroups of one batch-norm
+// channel took ≈ 13 µs to count), so workgroup `idx` of the n counts in
+// sub-counter idx / 16 and the last of each sixteen counts in the main
+// counter: ≤ 16 + ⌈n/16⌉ adds in a row.  Counters of `slot` start at word
+// slot · tickets_per_slot(n) · TICKET_STRIDE, one per 128-B line.
+constexpr int TICKET_STRIDE = 32;
+__host__ __device__ constexpr int tickets_per_slot(int n) { return 1 + (n + 15) / 16; }
+__device__ __forceinline__ bool last_arrival2(unsigned* tickets, int slot, unsigned n, unsigned idx) {
+  __shared__ bool last_;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have left
+  __syncthreads();                                   // ... and every other wave's
+  if (threadIdx.x == 0) {
+    const unsigned nsub = (n + 15) / 16, g = idx / 16;
+    const unsigned gsize = n - 16 * g < 16u ? n - 16 * g : 16u;
+    unsigned* base = tickets + (size_t)slot * tickets_per_slot((int)n) * TICKET_STRIDE;
+    unsigned* sub = base + (1 + g) * TICKET_STRIDE;
+    bool l = false;
+    if (__hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+      __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(base, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsub - 1) {
+        __hip_atomic_store(base, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        l = true;
+      }
+    }
+    last_ = l;
+  }
+  __syncthreads();
+  return last_;
+}
+
 // ---- preprocessing in the load path (include/ocm.h ocm_prep) --------------
 // Kernel-side copy of an ocm_prep (by value), plus the one scalar definition
 // of the transform every fused kernel reproduces bit for bit.
@@ -136,6 +205,10 @@ struct PrepArgs {
   int snv = 0;
   const float* taps = nullptr;     // [w] interior ++ [h][w] left ++ [h][w] right
   const float* rowstat = nullptr;  // (m_r, s_r) per row of X
+  // the forms the fused load paths implement (k_score_1p, the i8×3 quantiser):
+  // SNV alone, or an odd-derivative filter (every reference driver: deriv 1)
+  // of half-width 2 or 7, SNV optional; the rest is materialised first
+  bool fused_form() const { return w == 0 ? snv != 0 : (h == 2 || h == 7) && (deriv & 1); }
 };
 
 namespace ocm {
@@ -161,6 +234,16 @@ int gram_rows_i8(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t n, int p, co
 int prep_apply(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int p, const PrepArgs& pa,
                float* out, int64_t ldo, hipStream_t st);
 
+// a·b rounded to float32 and never fused into a consumer's add (HIP compiles
+// with -ffp-contract=fast-honor-pragmas: a product written as a * b, or
+// __fmul_rn, may become an FMA with the caller's y − shift; this one carries
+// no contract flag).  Every kernel that forms a lazy view's values uses it, so
+// they all round the same way.
+__device__ __forceinline__ float mul_nc(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+
 // y_j of row `xr` (raw X row): the formula of include/ocm.h, scalar loads.
 // m, s: the row's (m_r, s_r) (ignored unless snv).
 __device__ __forceinline__ float prep_elem(const float* __restrict__ xr, int p, int j, const PrepArgs& pa, float m,
@@ -184,7 +267,7 @@ __device__ __forceinline__ float prep_elem(const float* __restrict__ xr, int p, 
       a = 0.f;
       for (int t = 1; t <= H; ++t) a = fmaf(c[t], __fsub_rn(u(j + t), u(j - t)), a);
     } else if (pa.deriv == 0) {
-      a = __fmul_rn(c[0], u(j));
+      a = mul_nc(c[0], u(j));
       for (int t = 1; t <= H; ++t) a = fmaf(c[t], __fadd_rn(u(j + t), u(j - t)), a);
     } else {
       const float uj = u(j);
@@ -192,7 +275,7 @@ __device__ __forceinline__ float prep_elem(const float* __restrict__ xr, int p, 
       for (int t = 1; t <= H; ++t) a = fmaf(c[t], __fadd_rn(__fsub_rn(u(j + t), uj), __fsub_rn(u(j - t), uj)), a);
     }
   }
-  return pa.snv ? __fmul_rn(a, s) : a;
+  return pa.snv ? mul_nc(a, s) : a;
 }
 
 }  // namespace ocm

@@ -589,8 +589,15 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
   double T2 = 0.0, T2prev = 0.0;
 
   // ---- sweep 1 on tile Y: partial t (uncentred) → tpart[buf] ----------------
-  // ---- lazy view: (m_r, s_r) of lane row ln of tile tt (scalar loads, selects)
-  const bool psub = PREP && pa.snv && pa.deriv == 0;
+  // ---- lazy view.  The fused forms (score_diag_impl routes the rest through a
+  // materialised copy): SNV alone (HH = 0), y = (x − m_r)·s_r, and an
+  // odd-derivative filter (HH > 0), y = s_r·Σ_t c_t (x_{j+t} − x_{j−t}), s_r = 1
+  // without SNV (a·1 = a exactly: one formula, no per-element selects).
+  float ctap[HH > 0 ? HH + 1 : 1];  // interior taps c_1 .. c_HH (wave-uniform)
+  if constexpr (HH > 0)
+#pragma unroll
+    for (int t = 1; t <= HH; ++t) ctap[t] = ptaps[HH + t];
+  // (m_r, s_r) of lane row ln of tile tt (scalar loads, selects)
   auto rowstat_of = [&](int64_t tt, float& mr, float& sr) {
     mr = 0.f;
     sr = 1.f;
@@ -606,33 +613,22 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
     }
   };
   // y of this lane's four columns of block j from the window u[c0 − HH .. c0 + 3 + HH]
+  auto stencil_e = [&](const float* win, float sr, int e) __attribute__((always_inline)) -> float {
+    const int o = (HH > 0 ? HH : 0) + e;
+    float a;
+    if constexpr (HH <= 0) {
+      a = win[o];  // x − m_r (the window is mean-subtracted at HH = 0)
+    } else {
+      a = 0.f;
+#pragma unroll
+      for (int t = 1; t <= HH; ++t) a = fmaf(ctap[t], __fsub_rn(win[o + t], win[o - t]), a);
+    }
+    return ocm::mul_nc(a, sr);
+  };
   auto stencil = [&](const float* win, float sr) __attribute__((always_inline)) -> f32x4 {
     f32x4 y;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int o = (HH > 0 ? HH : 0) + e;
-      float a;
-      if constexpr (HH <= 0) {
-        a = win[o];
-      } else {
-        if (pa.deriv & 1) {
-          a = 0.f;
-#pragma unroll
-          for (int t = 1; t <= HH; ++t) a = fmaf(ptaps[HH + t], __fsub_rn(win[o + t], win[o - t]), a);
-        } else if (pa.deriv == 0) {
-          a = __fmul_rn(ptaps[HH], win[o]);
-#pragma unroll
-          for (int t = 1; t <= HH; ++t) a = fmaf(ptaps[HH + t], __fadd_rn(win[o + t], win[o - t]), a);
-        } else {
-          const float uj = win[o];
-          a = 0.f;
-#pragma unroll
-          for (int t = 1; t <= HH; ++t)
-            a = fmaf(ptaps[HH + t], __fadd_rn(__fsub_rn(win[o + t], uj), __fsub_rn(win[o - t], uj)), a);
-        }
-      }
-      y[e] = pa.snv ? __fmul_rn(a, sr) : a;
-    }
+    for (int e = 0; e < 4; ++e) y[e] = stencil_e(win, sr, e);
     return y;
   };
   // the first (LEFT) / last HH columns of the row: block 0 of wave 0 or block
@@ -661,11 +657,11 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
         const float* et = ptaps + Wn + (left ? i : HH + i) * Wn;
         const int s0 = left ? 0 : 16 - Wn;           // window start within the block
         const int cl = left ? i : 16 - HH + i;       // the output's column within the block
-        const float ref = pa.deriv >= 1 ? row16[cl] : 0.f;
+        const float ref = row16[cl];  // deriv ≥ 1
         float a = 0.f;
 #pragma unroll
         for (int t = 0; t < Wn; ++t) a = fmaf(et[t], __fsub_rn(row16[s0 + t], ref), a);
-        const float yv = pa.snv ? __fmul_rn(a, sr) : a;
+        const float yv = ocm::mul_nc(a, sr);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (4 * lq + e == cl) y[e] = yv;
@@ -698,50 +694,14 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
     for (int e = 0; e < 4; ++e) win[H_ + e] = ucur[e];
   };
 
-  auto sweep1 = [&](f32x4 (&Y)[NJ], f32x4& hy, int buf, int64_t tile) __attribute__((always_inline)) {
+  // XG: vector-memory ops issued after Y's group (the other tile's group in
+  // the loop; none for the first tile, whose sweep runs before the second
+  // tile's loads are issued — two tiles' loads in flight around the first
+  // sweep made the compiler stage some through VGPRs, copying them before
+  // they landed: scripts/tile_hazard_check.py)
+  auto sweep1 = [&](f32x4 (&Y)[NJ], f32x4& hy, int buf, int64_t tile, auto XGc) __attribute__((always_inline)) {
+    constexpr int XG = decltype(XGc)::value;
     f32x4 acA = {0.f, 0.f, 0.f, 0.f}, acB = acA, acC = acA, acD = acA, acE = acA, acF = acA;
-    f32x4 yE = acA;  // lazy view: this lane's outputs among the row's first / last HH columns
-    float win[4 + 2 * (HH > 0 ? HH : 0)];  // lazy view: the window of the next block to transform
-    float mr = 0.f, sr = 1.f;
-    f32x4 uprev = acA, ucur = acA, unext = acA;
-    if constexpr (PREP) {
-      rowstat_of(tile, mr, sr);
-      // hy, Y[0], Y[1] (the oldest loads of the tile's group) have landed: the
-      // rest of this group and the other tile's whole group may be in flight
-      constexpr int W0 = NJ - 2 + GL < 63 ? NJ - 2 + GL : 63;
-      wait_vm<W0>(Y[1]);
-      wait_vm<W0>(Y[0]);
-      wait_vv<W0>(hy);
-      ucur = Y[0];
-      uprev = hy;
-      if (psub)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          ucur[e] = __fsub_rn(ucur[e], mr);
-          uprev[e] = __fsub_rn(uprev[e], mr);
-        }
-      // the row ends first (wave 0: block 0, wave 3: block NJ − 1), before the
-      // block loop's registers are live
-      if constexpr (HH > 0) {
-        if (w == 0) edge_fix(yE, ucur, sr, true);
-        if (w == W - 1) {
-          wait_vm<GL>(Y[NJ - 1]);
-          f32x4 ul = Y[NJ - 1];
-          if (psub)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) ul[e] = __fsub_rn(ul[e], mr);
-          edge_fix(yE, ul, sr, false);
-        }
-      }
-      // block 0's window (uprev = the halo, ucur = Y[0], unext = Y[1])
-      unext = Y[1];
-      if (psub)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) unext[e] = __fsub_rn(unext[e], mr);
-      exchange(uprev, ucur, unext, win);
-      uprev = ucur;
-      ucur = unext;
-    }
     double t64[4] = {0.0, 0.0, 0.0, 0.0}, x164[4] = {0.0, 0.0, 0.0, 0.0};
     f32x4 aN = P0s[b1[0]];  // LDS / crossbar operands one block ahead
     float bN[4] = {0.f, 0.f, 0.f, 0.f};
@@ -750,10 +710,10 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
       for (int e = 0; e < 4; ++e)
         bN[e] = NOP1B ? xlane(bpermA + 4 * e, p1a[0])
                       : __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(bperm + 4 * e, __builtin_bit_cast(int, p1b[0])));
-    static_for<NJ>([&](auto J) {
+    // the A / B operands of block j (taken from the prefetch) and block j + 1's prefetch
+    auto operands = [&](auto J, f32x4& a, float (&b)[4]) __attribute__((always_inline)) {
       constexpr int j = decltype(J)::value;
-      const f32x4 a = aN;
-      float b[4];
+      a = aN;
 #pragma unroll
       for (int e = 0; e < 4; ++e) b[e] = bN[e];
       if constexpr (j + 1 < NJ) {
@@ -765,54 +725,134 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
                                        __builtin_amdgcn_ds_bpermute(NOP1B ? bpermA + 4 * e : bperm + 4 * e,
                                                                     __builtin_bit_cast(int, NOP1B ? p1a[j + 1] : p1b[NOP1B ? 0 : j + 1])));
       }
-      if constexpr (!PREP) {
+    };
+    // f32 partials over ≤ 64 columns per chain, flushed to f64.  The MFMAs are
+    // asm (hipcc pads no hazard of theirs): the s_nop covers MFMA result →
+    // VALU read, and ties the accumulators so no read is scheduled above it
+    // (a "memory" clobber orders loads and stores only — with it, the reads of
+    // the last MFMA's first elements had moved up and read stale values)
+    auto flush = [&]() __attribute__((always_inline)) {
+      asm volatile("s_nop 11" : "+v"(acA), "+v"(acB), "+v"(acC), "+v"(acD), "+v"(acE), "+v"(acF));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        t64[i] += ((double)acA[i] + (double)acB[i]) + ((double)acC[i] + (double)acD[i]);
+        x164[i] += (double)acE[i] + (double)acF[i];
+        acA[i] = acB[i] = acC[i] = acD[i] = acE[i] = acF[i] = 0.f;
+      }
+    };
+    if constexpr (!PREP) {
+      static_for<NJ>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        f32x4 a;
+        float b[4];
+        operands(J, a, b);
         // Y[j] was issued before the rest of its tile (NJ − 1 − j loads) and
         // the NJ refills of the other tile (stores issued since only make the
         // wait earlier)
-        wait_vm<2 * NJ - 1 - j>(Y[j]);
+        wait_vm<NJ - 1 - j + XG>(Y[j]);
         s1_block<EX>(acA, acB, acC, acD, acE, acF, a, b, Y[j]);
-      } else {
-        // y of block j from the window exchanged during block j − 1 (its
-        // ds_bpermutes had the previous block's MFMAs to land)
-        f32x4 y = stencil(win, sr);
-        if constexpr (HH > 0) {
-          if ((j == 0 && w == 0) || (j == NJ - 1 && w == W - 1))
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int cl = 4 * lq + e;  // column within the block
-              if (j == 0 ? cl < HH : cl >= 16 - HH) y[e] = yE[e];
-            }
+        __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting every block's reads
+        if constexpr ((j & 15) == 15 || j == NJ - 1) {
+          flush();
         }
-        // y into the AGPR tile now (sweep 2 reads it there); a plain assignment
-        // would leave y in VGPRs until the next sweep 2 asks for the AGPRs
-        asm volatile("" : "=a"(Y[j]) : "0"(y));
-        if constexpr (j + 1 < NJ) {  // the window of block j + 1: Y[j + 2] (or the halo) has landed
-          if constexpr (j + 2 < NJ) {
-            wait_vm<NJ - 3 - j + GL>(Y[j + 2]);
-            unext = Y[j + 2];
-          } else {
-            unext = hy;  // lanes lq <= 1: virtual block NJ
+      });
+    } else {
+      // Lazy view, two blocks in flight: block j's MFMAs (compiler builtins,
+      // so the scheduler can fill their issue gaps) run beside the stencil of
+      // block j + 1 (its window was exchanged during block j − 1) and the
+      // ds_bpermute exchange of block j + 2's window.  y_j replaces x_j in the
+      // AGPR tile once its MFMAs are issued (sweep 2 and the epilogue read it
+      // there).
+      constexpr int H_ = HH > 0 ? HH : 0;
+      float win[4 + 2 * H_];
+      float mr, sr;
+      rowstat_of(tile, mr, sr);
+      // hy, Y[0..2] (the oldest loads of the tile's group) have landed: the
+      // rest of this group and the other tile's whole group may be in flight
+      constexpr int W0 = NJ - 3 + XG < 63 ? NJ - 3 + XG : 63;
+      wait_vm<W0>(Y[2]);
+      wait_vm<W0>(Y[1]);
+      wait_vm<W0>(Y[0]);
+      wait_vv<W0>(hy);
+      auto raw = [&](const f32x4& v) __attribute__((always_inline)) {
+        f32x4 u = v;
+        if constexpr (HH == 0)  // SNV alone subtracts the row mean first
+#pragma unroll
+          for (int e = 0; e < 4; ++e) u[e] = __fsub_rn(u[e], mr);
+        return u;
+      };
+      f32x4 uprev = raw(hy), ucur = raw(Y[0]), unext = raw(Y[1]);
+      // the row ends first (wave 0: block 0, wave 3: block NJ − 1)
+      f32x4 yE = {0.f, 0.f, 0.f, 0.f};  // this lane's outputs among the row's first / last HH columns
+      if constexpr (HH > 0) {
+        // every wave waits (the tile's group landed during the last sweep 2):
+        // a tied wait inside the branch would make the compiler merge two
+        // versions of Y[NJ − 1] with register copies, and copying a tile
+        // register whose load is in flight reads garbage
+        wait_vm<XG>(Y[NJ - 1]);
+        if (w == 0) edge_fix(yE, ucur, sr, true);
+        if (w == W - 1) edge_fix(yE, raw(Y[NJ - 1]), sr, false);
+      }
+      auto patch = [&](f32x4& y, bool right) __attribute__((always_inline)) {
+        if constexpr (HH > 0)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int cl = 4 * lq + e;  // column within the block
+            const bool ed = right ? (w == W - 1) & (cl >= 16 - HH) : (w == 0) & (cl < HH);
+            y[e] = ed ? yE[e] : y[e];
           }
-          if (psub)
+      };
+      auto advance = [&](const f32x4& nx) __attribute__((always_inline)) {
+        unext = raw(nx);
+        exchange(uprev, ucur, unext, win);
+        uprev = ucur;
+        ucur = unext;
+      };
+      exchange(uprev, ucur, unext, win);  // block 0's window
+      uprev = ucur;
+      ucur = unext;
+      f32x4 y = stencil(win, sr);
+      patch(y, false);
+      if constexpr (NJ == 1) patch(y, true);
+      advance(Y[2]);  // block 1's window
+      static_for<NJ>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        f32x4 a;
+        float b[4];
+        operands(J, a, b);
+        // block j's MFMAs as compiler builtins (it pads their hazards — an asm
+        // MFMA's sources were rewritten by the next VALU while it still read
+        // them — and fills their issue gaps with block j + 1's stencil; the
+        // accumulators stay in VGPRs, -amdgpu-mfma-vgpr-form, Makefile: the
+        // AGPRs are the tiles, whose in-flight loads must never be copied)
+        f32x4 yn = y;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) unext[e] = __fsub_rn(unext[e], mr);
-          exchange(uprev, ucur, unext, win);
-          uprev = ucur;
-          ucur = unext;
+        for (int e = 0; e < 4; ++e) {
+          if constexpr (EX)
+            (e & 1 ? acF : acE) = __builtin_amdgcn_mfma_f32_4x4x1f32(b[e], y[e], e & 1 ? acF : acE, 0, 0, 0);
+          f32x4& c = e == 0 ? acA : e == 1 ? acB : e == 2 ? acC : acD;
+          c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], y[e], c, 0, 0, 0);
+          if constexpr (j + 1 < NJ) yn[e] = stencil_e(win, sr, e);
         }
-        s1_block_v<EX>(acA, acB, acC, acD, acE, acF, a, b, y);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting every block's reads
-      if constexpr ((j & 15) == 15 || j == NJ - 1) {  // f32 partials over ≤ 64 columns per chain
-        asm volatile("s_nop 11" ::: "memory");        // MFMA result → VALU read
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          t64[i] += ((double)acA[i] + (double)acB[i]) + ((double)acC[i] + (double)acD[i]);
-          x164[i] += (double)acE[i] + (double)acF[i];
-          acA[i] = acB[i] = acC[i] = acD[i] = acE[i] = acF[i] = 0.f;
+        asm volatile("" : "=a"(Y[j]) : "0"(y));  // y into the AGPR tile
+        if constexpr (j + 1 < NJ) {
+          y = yn;
+          if constexpr (j + 1 == NJ - 1) patch(y, true);
+          if constexpr (j + 2 < NJ) {  // block j + 2's window: Y[j + 3] (or the halo) has landed
+            if constexpr (j + 3 < NJ) {
+              wait_vm<NJ - 4 - j + XG>(Y[j + 3]);
+              advance(Y[j + 3]);
+            } else {
+              advance(hy);  // lanes lq <= 1: virtual block NJ
+            }
+          }
         }
-      }
-    });
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr ((j & 15) == 15 || j == NJ - 1) {
+          flush();
+        }
+      });
+    }
     double* tp = tpart[buf];
 #pragma unroll
     for (int i = 0; i < 4; ++i) tp[(w * 20 + 4 * lq + i) * R + ln] = t64[i];
@@ -959,13 +999,15 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
   f32x4 hA = {0.f, 0.f, 0.f, 0.f}, hB = hA;  // lazy view: the tiles' halo quads
   {
     const float* p0 = col_base(index_of(t));
-    const float* p1 = col_base(index_of(clamp_tile(t + G)));
     if constexpr (HH > 0) load_v(hA, halo_ptr(p0));
     static_for<NJ>([&](auto J) { load_a<64 * decltype(J)::value>(XA[decltype(J)::value], p0); });
+  }
+  sweep1(XA, hA, 0, t, std::integral_constant<int, 0>{});
+  {
+    const float* p1 = col_base(index_of(clamp_tile(t + G)));
     if constexpr (HH > 0) load_v(hB, halo_ptr(p1));
     static_for<NJ>([&](auto J) { load_a<64 * decltype(J)::value>(XB[decltype(J)::value], p1); });
   }
-  sweep1(XA, hA, 0, t);
   lds_barrier();
   compute_t(t, 0);
   int buf = 0;
@@ -987,7 +1029,7 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
     OCM_STAMP(3)
     sweep2(Xc, hc, col_base(index_of(clamp_tile(tn + G))), buf);
     OCM_STAMP(0)
-    if (more || PREP) sweep1(Yn, hn, buf ^ 1, tn);  // lazy view: unconditional (a tile past the end is a clamped valid one), so Yn never merges raw and transformed values
+    if (more || PREP) sweep1(Yn, hn, buf ^ 1, tn, std::integral_constant<int, GL>{});  // lazy view: unconditional (a tile past the end is a clamped valid one), so Yn never merges raw and transformed values
     OCM_STAMP(1)
     lds_barrier();
     OCM_STAMP(2)
@@ -1233,7 +1275,7 @@ int score_diag_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* ro
   const bool vec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
   bool one_pass = vec && p % 64 == 0 && (nj == 4 || nj == 8 || nj == 16 || nj == 32) && k <= 20;
   const PrepArgs pa = pp ? *pp : PrepArgs{};
-  if (pp && !(pa.h == 0 || pa.h == 2 || pa.h == 7)) one_pass = false;
+  if (pp && !pa.fused_form()) one_pass = false;
   if (!one_pass && pp) {  // a lazy view on the other shapes: materialise the rows, then score them
     if (m == 0) {
       if (stats_out) OCM_HIP(hipMemsetAsync(stats_out, 0, 4 * sizeof(double), st));

@@ -100,7 +100,6 @@ __global__ __launch_bounds__(VT) void k_recon_fwd(int kind, const float* __restr
                                                    unsigned* __restrict__ ticket, float* __restrict__ out) {
   __shared__ float redf[VT / 64];
   __shared__ double red[VT / 64];
-  __shared__ bool last;
   const int b = blockIdx.x;
   const float* xr = x + (int64_t)b * L;
   const double inv = 1.0 / ((double)B * L);
@@ -133,22 +132,15 @@ __global__ __launch_bounds__(VT) void k_recon_fwd(int kind, const float* __restr
     gxs[e] = g * sd[j];
   }
   const double ps = block_sum_d(s, red);
-  if (threadIdx.x == 0) {
-    part[b] = ps;
-    __threadfence();
-    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
+  if (threadIdx.x == 0) st_agent(part + b, ps);  // write-through (ocm_internal.h last_arrival)
+  if (!last_arrival(ticket, gridDim.x)) return;
   double t = 0.0;
-  for (int i = threadIdx.x; i < (int)gridDim.x; i += VT) t += part[i];
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += VT) t += ld_agent(part + i);
   const double tot = block_sum_d(t, red);
   if (threadIdx.x == 0) {
     const float recon = (float)(tot * inv);
     out[1] = recon;
     out[0] = recon + beta * (kl ? *kl : 0.f);
-    *ticket = 0u;
   }
 }
 
@@ -166,7 +158,6 @@ __global__ __launch_bounds__(VT) void k_recon_bwd(const float* __restrict__ dtot
 __global__ __launch_bounds__(VT) void k_adam(const ocm_adam_tensor* __restrict__ tab, int nt, int64_t total,
                                               float* __restrict__ step, float lr, float b1, float b2, float eps,
                                               float wd, unsigned* __restrict__ ticket) {
-  __shared__ bool last;
   const float t = *step + 1.f;
   const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
   const float step_size = lr / bc1, bc2s = sqrtf(bc2);
@@ -185,16 +176,9 @@ __global__ __launch_bounds__(VT) void k_adam(const ocm_adam_tensor* __restrict__
     T.exp_avg_sq[j] = v;
     T.param[j] = pv - step_size * m / (sqrtf(v) / bc2s + eps);
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (last && threadIdx.x == 0) {
-    *step = t;
-    *ticket = 0u;
-  }
+  // the last workgroup advances the counter: every workgroup read it before
+  // its own arrival (no data hand-off, so no fence)
+  if (last_arrival(ticket, gridDim.x) && threadIdx.x == 0) *step = t;
 }
 
 }  // namespace

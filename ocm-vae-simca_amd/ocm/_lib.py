@@ -116,8 +116,8 @@ SIGNATURES = {
                                c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
     "ocm_bn_scratch_bytes": (ctypes.c_size_t, [c_i32]),
     "ocm_bn_fwd_train": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, ctypes.c_float,
-                                 ctypes.c_float, c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_void_p,
-                                 c_void_p]),
+                                 ctypes.c_float, c_void_p, c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p]),
     "ocm_bn_bwd": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p,
                            c_i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ocm_conv1d_scratch_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
@@ -152,7 +152,7 @@ SIGNATURES = {
                                         ctypes.POINTER(OcmDecision), c_void_p, c_i64, c_void_p, c_void_p]),
 }
 
-ABI_VERSION = 7  # include/ocm.h OCM_ABI_VERSION
+ABI_VERSION = 8  # include/ocm.h OCM_ABI_VERSION
 
 _lib = None
 _lib_lock = threading.Lock()

@@ -7,7 +7,10 @@ of csrc/ocm_bn.hip instead of MIOpen's spatial BN, which handles the VAE's
 3-12-channel × 512-2048-position activations at a few GB/s.  Evaluation mode
 (running statistics) and host tensors use the stock module.  The kernels
 launch on the current stream, so the module is HIP-graph capturable
-(ocm/vae_train.py); their reduction scratch is caller-owned (``_scratch``).
+(ocm/vae_train.py); their reduction scratch is caller-owned: one zero-filled
+buffer per module (``_layer_scratch``), reused by every call — the kernels'
+per-channel completion counters live at its end and every call leaves them
+zero, so each direction is one reduction launch plus the elementwise pass.
 
 ``fuse_elu()`` folds the ELU that follows every batch norm of the VAE
 (vae_model.py:45-49, 75-79) into the same kernels: the normalisation pass
@@ -29,18 +32,23 @@ _DT = {torch.float32: 0, torch.bfloat16: 1}
 ACT_NONE, ACT_ELU = 0, 1  # include/ocm.h OCM_ACT_*
 
 
-def _scratch(C: int, dev) -> torch.Tensor:
-    """Per-call reduction scratch from torch's caching allocator.  Under
-    HIP-graph capture it comes from the graph's private pool, so a replay
-    never writes through a pointer that a later (larger) libocm call has
-    re-allocated — the context arena does move."""
+def _layer_scratch(mod, C: int, dev) -> torch.Tensor:
+    """The module's reduction scratch (include/ocm.h ocm_bn_scratch_bytes):
+    zero-filled once, then reused by its forward and backward calls, which
+    are stream-ordered.  A plain attribute, not a buffer: state_dict keys do
+    not move.  Allocated on the first (eager) call, before any graph capture,
+    so a captured replay writes through a pointer that stays put."""
     nbytes = int(_lib.load().ocm_bn_scratch_bytes(C))
-    return torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=dev)
+    buf = mod.__dict__.get("_ocm_scratch")
+    if buf is None or buf.device != dev or buf.numel() * 8 < nbytes:
+        buf = torch.zeros((nbytes + 7) // 8, dtype=torch.float64, device=dev)
+        mod.__dict__["_ocm_scratch"] = buf
+    return buf
 
 
 class _BNTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, act):
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, eps, momentum, act, scratch):
         x = x.contiguous()
         N, C, L = x.shape
         dev = x.device
@@ -50,12 +58,12 @@ class _BNTrain(torch.autograd.Function):
         w = weight.detach().float().contiguous() if weight is not None else None
         b = bias.detach().float().contiguous() if bias is not None else None
         h = Context.get(dev.index).handle
-        scratch = _scratch(C, dev)
         check(_lib.load().ocm_bn_fwd_train(h, _DT[x.dtype], ptr(x), N, C, L, ptr(w), ptr(b), float(eps),
-                                           float(momentum), ptr(running_mean), ptr(running_var), act, ptr(y),
-                                           ptr(smean), ptr(sinv), ptr(scratch), stream_handle(dev)),
+                                           float(momentum), ptr(running_mean), ptr(running_var), ptr(nbt), act,
+                                           ptr(y), ptr(smean), ptr(sinv), ptr(scratch), stream_handle(dev)),
               "ocm_bn_fwd_train")
         ctx.act = act
+        ctx.scratch = scratch
         ctx.save_for_backward(x, w, smean, sinv, y if act else None)
         ctx.has_w, ctx.has_b = weight is not None, bias is not None
         return y
@@ -70,11 +78,11 @@ class _BNTrain(torch.autograd.Function):
         dw = torch.empty(C, dtype=torch.float32, device=dev) if ctx.has_w else None
         db = torch.empty(C, dtype=torch.float32, device=dev) if ctx.has_b else None
         h = Context.get(dev.index).handle
-        scratch = _scratch(C, dev)
         check(_lib.load().ocm_bn_bwd(h, _DT[x.dtype], ptr(x), ptr(dy), N, C, L, ptr(w), ptr(smean), ptr(sinv),
-                                     ctx.act, ptr(y), ptr(dx), ptr(dw), ptr(db), ptr(scratch), stream_handle(dev)),
+                                     ctx.act, ptr(y), ptr(dx), ptr(dw), ptr(db), ptr(ctx.scratch),
+                                     stream_handle(dev)),
               "ocm_bn_bwd")
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
 class FastBatchNorm1d(nn.BatchNorm1d):
@@ -92,9 +100,13 @@ class FastBatchNorm1d(nn.BatchNorm1d):
             # eval (running statistics), host tensors, cumulative-average momentum: the stock module
             y = super().forward(x)
             return F.elu(y) if self.act == ACT_ELU else y
-        if self.track_running_stats and self.num_batches_tracked is not None:
+        # the batch count is incremented by the statistics kernel (one launch fewer)
+        nbt = (self.num_batches_tracked if self.track_running_stats and self.num_batches_tracked is not None
+               and self.num_batches_tracked.dtype == torch.int64 and self.num_batches_tracked.is_cuda else None)
+        if self.track_running_stats and self.num_batches_tracked is not None and nbt is None:
             self.num_batches_tracked.add_(1)
         momentum = self.momentum
         track = self.track_running_stats and self.running_mean is not None
+        scratch = _layer_scratch(self, x.shape[1], x.device)
         return _BNTrain.apply(x, self.weight, self.bias, self.running_mean if track else None,
-                              self.running_var if track else None, self.eps, momentum, self.act)
+                              self.running_var if track else None, nbt, self.eps, momentum, self.act, scratch)

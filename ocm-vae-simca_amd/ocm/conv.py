@@ -10,7 +10,9 @@ Under bf16 autocast the activations are bf16, as torch's autocast conv would
 make them; the weights stay float32 (torch would round them to bf16 first) and
 every sum is float32.  Other shapes, host tensors and bf16 weights take the
 stock module.  All launches are on the current stream with caller-owned
-scratch, so the modules are HIP-graph capturable (ocm/vae_train.py).
+scratch — one zero-filled buffer per module, reused by every backward call
+(the reductions' completion counters live in it and every call leaves them
+zero) — so the modules are HIP-graph capturable (ocm/vae_train.py).
 """
 from __future__ import annotations
 
@@ -24,9 +26,16 @@ _DT = {torch.float32: 0, torch.bfloat16: 1}
 DOWN, UP = 0, 1  # include/ocm.h OCM_CONV_DOWN / OCM_CONV_UP
 
 
-def _scratch(O: int, I: int, K: int, dev) -> torch.Tensor:
+def _layer_scratch(mod, O: int, I: int, K: int, dev) -> torch.Tensor:
+    """The module's wgrad / bias-sum scratch (include/ocm.h
+    ocm_conv1d_scratch_bytes): zero-filled once, reused by its stream-ordered
+    backward calls; a plain attribute (state_dict keys do not move)."""
     nbytes = int(_lib.load().ocm_conv1d_scratch_bytes(O, I, K))
-    return torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+    buf = mod.__dict__.get("_ocm_scratch")
+    if buf is None or buf.device != dev or buf.numel() * 4 < nbytes:
+        buf = torch.zeros((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+        mod.__dict__["_ocm_scratch"] = buf
+    return buf
 
 
 def _launch(mode, x, w, bias, O, Lout, K, stride, pad, out_dtype):
@@ -43,7 +52,7 @@ class _ConvFn(torch.autograd.Function):
     (transposed=True, weight [I][O][K]) of x (B, I, Lin)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, transposed, Lout, out_dtype):
+    def forward(ctx, x, weight, bias, stride, pad, transposed, Lout, out_dtype, scratch):
         x = x.contiguous()
         w = weight.detach().contiguous()
         b = bias.detach().contiguous() if bias is not None else None
@@ -52,6 +61,7 @@ class _ConvFn(torch.autograd.Function):
         y = _launch(UP if transposed else DOWN, x, w, b, O, Lout, K, stride, pad, out_dtype)
         ctx.save_for_backward(x, w)
         ctx.conf = (stride, pad, transposed, bias is not None)
+        ctx.scratch = scratch
         return y
 
     @staticmethod
@@ -74,7 +84,7 @@ class _ConvFn(torch.autograd.Function):
             dx = _launch(DOWN if transposed else UP, dy, w, None, I, Lin, K, stride, pad, x.dtype)
         want_db = has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or want_db:
-            scratch = _scratch(O, I, K, dev)
+            scratch = ctx.scratch
             db = torch.empty(O, dtype=torch.float32, device=dev) if want_db else None
             dw = torch.empty_like(w)
             if transposed:  # dW[i][o][t] = Σ x[b][i][l] · dy[b][o][l·s + t − pad]; db = Σ dy separately
@@ -89,7 +99,7 @@ class _ConvFn(torch.autograd.Function):
                       "ocm_chan_sum")
             if not ctx.needs_input_grad[1]:
                 dw = None
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
 def _fast_ok(mod, x) -> bool:
@@ -114,7 +124,8 @@ class FastConv1d(nn.Conv1d):
             return super().forward(x)
         K, s, pad = self.kernel_size[0], self.stride[0], self.padding[0]
         Lout = (x.shape[-1] + 2 * pad - K) // s + 1
-        return _ConvFn.apply(x, self.weight, self.bias, s, pad, False, Lout, _act_dtype(x))
+        scratch = _layer_scratch(self, self.out_channels, self.in_channels, K, x.device)
+        return _ConvFn.apply(x, self.weight, self.bias, s, pad, False, Lout, _act_dtype(x), scratch)
 
 
 class FastConvTranspose1d(nn.ConvTranspose1d):
@@ -125,4 +136,5 @@ class FastConvTranspose1d(nn.ConvTranspose1d):
             return super().forward(x, output_size)
         K, s, pad, op = self.kernel_size[0], self.stride[0], self.padding[0], self.output_padding[0]
         Lout = (x.shape[-1] - 1) * s - 2 * pad + K + op
-        return _ConvFn.apply(x, self.weight, self.bias, s, pad, True, Lout, _act_dtype(x))
+        scratch = _layer_scratch(self, self.in_channels, self.out_channels, K, x.device)
+        return _ConvFn.apply(x, self.weight, self.bias, s, pad, True, Lout, _act_dtype(x), scratch)

@@ -27,6 +27,8 @@ from __future__ import annotations
 
 import os
 
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -200,6 +202,10 @@ class GraphedVAETrainer:
         mode = "global"
         if self.allreduce:
             torch.cuda.synchronize()
+            # the watchdog drops a finished collective on its next poll (every
+            # 100 ms); one still listed is queried during the capture, which
+            # HIP refuses even in thread-local mode (seen once in round 4)
+            time.sleep(0.35)
             mode = "thread_local"
         with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.out = self._body()

@@ -13,8 +13,8 @@ transformed in registers), the shift / threshold samples and the fix-up.
   run on the materialised view (every fused kernel forms the same float32
   values), with gather lists, segments, outlier rows, the row ends and every
   fused window; the fused paths materialise nothing (ocm_prep_materialised);
-* the fallback shapes / windows (materialised inside libocm) give the same
-  results too;
+* the fallback shapes / windows / even-derivative filters (materialised
+  inside libocm) give the same results too;
 * the drop-in SIMCA on a view vs the fp64 oracle on SciPy-preprocessed X at
   C2 (100k × 2048, k = 20) for (w 5, p 2, d 1, SNV) and (w 15, p 2, d 1,
   no SNV): T², Q rtol 1e-4, limits 1e-5, decisions outside the 1e-4 band.
@@ -32,6 +32,13 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="n
 DRIVERS = [(True, 5, 2, 1), (False, 15, 2, 1)]
 OTHERS = [(True, 15, 2, 1), (True, None, 0, 0), (True, 5, 2, 0), (False, 5, 2, 2), (True, 9, 2, 1),
           (False, 7, 3, 0)]
+
+
+def _fused_form(snv, w, d):
+    """The forms the fused load paths implement (csrc PrepArgs::fused_form):
+    SNV alone, or an odd-derivative filter of window 5 or 15 (every driver's
+    deriv 1), SNV optional; the rest is materialised inside libocm."""
+    return (w is None and snv) or (w in (5, 15) and d % 2 == 1)
 
 
 def _spectra(n, p, seed=5, base=1.0):
@@ -96,7 +103,7 @@ def test_view_gram_bit_identical(snv, w, po, d, n, p):
 
     X = _spectra(n, p)
     v = _view(torch.from_numpy(X).cuda(), snv, w, po, d)
-    fused = p % 4 == 0 and (w in (None, 5, 15))
+    fused = p % 4 == 0 and _fused_form(snv, w, d)
     c0 = materialised_count(0)
     Ga, ca, Gb, cb = _gram_pair(v, None, [0, n])
     assert torch.equal(Ga, Gb) and torch.equal(ca, cb)
@@ -159,7 +166,7 @@ def test_view_score_bit_identical(snv, w, po, d, p, k):
     for key in ("T", "T2", "Q", "stats"):
         assert torch.equal(a[key], b[key]), key
     assert torch.equal(acc_a, acc_b)
-    fused = w in (None, 5, 15)
+    fused = _fused_form(snv, w, d)
     assert (materialised_count(0) == c0) == fused
     rows = torch.arange(n - 1, 0, -2, device="cuda")
     a, b, acc_a, acc_b = _score_pair(v, rows, rows.numel(), k)
