@@ -156,14 +156,15 @@ def cpu_baseline(rows, p, k, repeats=3):
                       f"NumPy scores, fit+predict on the same rows (median {dt:.2f} s)"}
 
 
-def vae_bench(device, steps, warmup, batch=512, length=2048, dtype=None):
+def vae_bench(device, steps, warmup, batch=512, length=2048, dtype=None, latent_rows=1_000_000):
     """Secondary metric (BASELINE.json): VAE-SIMCA train steps/s, C4 network
     (cb=3, nf=3, ks=7, hid=64, d=32) at B=512 × L=2048 in bf16,
     one HIP-graph replay per optimizer step (ocm/vae_train.py).  Every timed
     step takes a distinct batch of a (warmup + steps) × B synthetic set in
     HBM.  Then SIMCA-on-latents, timed on its own (utils/final_vaesimca.py:
-    406-442, 500-533): encode + decode the training rows (eval, no grad),
-    latent statistics and the f-distance decision on libocm."""
+    406-442, 500-533) at C4's scale (1M × 2048): encode +
+    decode ``latent_rows`` synthetic spectra of the same distribution (eval,
+    no grad), latent statistics and the f-distance decision on libocm."""
     import torch
 
     import vae_model as V
@@ -192,8 +193,12 @@ def vae_bench(device, steps, warmup, batch=512, length=2048, dtype=None):
     loss = float(tr.out[0].item())
     finite = all(bool(torch.isfinite(p).all()) for p in m.parameters())
 
-    # SIMCA-on-latents over every training row
+    # SIMCA-on-latents over C4's 1M rows (a fresh synthetic set of the
+    # training distribution; the 107k training rows are a tenth of it)
     m.eval()
+    if latent_rows:
+        del X
+        X = synth_device(latent_rows, length, 20, seed=7, device=device)
     n = X.shape[0]
     eb = 8192
     ac = torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16)

@@ -17,7 +17,7 @@ namespace {
 
 constexpr int BN_SPLIT = 64;       // workgroups per channel for the reductions, at least
 constexpr int BN_SPLIT_MAX = 256;  // and at most
-constexpr int BN_U = 4;            // elements per thread per pass of the reduction kernels
+constexpr int BN_U = 8;            // elements per thread per pass of the reduction kernels (loads issued together)
 constexpr int BN_T = 256;
 
 struct bf16_t {  // raw bfloat16 storage (torch.bfloat16 bit layout)
@@ -31,6 +31,40 @@ __device__ __forceinline__ void bn_st(bf16_t* p, int64_t i, float v) {
   const uint32_t u = __float_as_uint(v);
   const uint32_t r = (u & 0x7fffffffu) > 0x7f800000u ? (u | 0x00400000u) : u + 0x7fffu + ((u >> 16) & 1u);
   p[i].bits = (uint16_t)(r >> 16);
+}
+
+// eight consecutive elements (16-B aligned: the row length is a multiple of 8)
+__device__ __forceinline__ void bn_ld8(const float* p, int64_t i, float (&v)[8]) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p + i), b = *reinterpret_cast<const f32x4*>(p + i + 4);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = a[e];
+    v[4 + e] = b[e];
+  }
+}
+__device__ __forceinline__ void bn_ld8(const bf16_t* p, int64_t i, float (&v)[8]) {
+  const uint4 q = *reinterpret_cast<const uint4*>(p + i);
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = __uint_as_float(w[e] << 16);
+    v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void bn_st8(float* p, int64_t i, const float (&v)[8]) {
+  *reinterpret_cast<f32x4*>(p + i) = f32x4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(p + i + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+__device__ __forceinline__ void bn_st8(bf16_t* p, int64_t i, const float (&v)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    bf16_t lo, hi;
+    bn_st(&lo, 0, v[2 * e]);
+    bn_st(&hi, 0, v[2 * e + 1]);
+    w[e] = (uint32_t)lo.bits | ((uint32_t)hi.bits << 16);
+  }
+  *reinterpret_cast<uint4*>(p + i) = uint4{w[0], w[1], w[2], w[3]};
 }
 
 __device__ __forceinline__ double block_sum_f64(double v, double* red) {
@@ -66,13 +100,9 @@ __device__ __forceinline__ float bn_ld_or0(const T* p, int C, int L, int c, int 
 // fixed butterfly: deterministic)
 __device__ __forceinline__ void bn_part_sum(const double* part, int c, int split, double& s1, double& s2) {
   const int lane = threadIdx.x & 63;
-  double a1 = 0.0, a2 = 0.0;
-  for (int i = lane; i < split; i += 64) {  // other workgroups' partials: write-through loads
-    a1 += ld_agent(part + ((size_t)c * split + i) * 2 + 0);
-    a2 += ld_agent(part + ((size_t)c * split + i) * 2 + 1);
-  }
-  s1 = wave_sum_f64(a1);
-  s2 = wave_sum_f64(a2);
+  // other workgroups' partials: write-through loads, eight per lane in flight
+  s1 = wave_sum_f64(lane_sum_agent<double, double>(part + (size_t)c * split * 2, 2, split, lane));
+  s2 = wave_sum_f64(lane_sum_agent<double, double>(part + (size_t)c * split * 2 + 1, 2, split, lane));
 }
 
 // The workgroup's partials → part (write-through); true in the last of channel
@@ -145,6 +175,29 @@ __global__ __launch_bounds__(BN_T) void k_bn_apply(const T* __restrict__ x, int 
   bn_st(y, i, ELU ? (z > 0.f ? z : expf(z) - 1.f) : z);
 }
 
+// the same, eight consecutive positions per thread (L % 8 = 0): grid
+// (ceil(L / (8·BN_T)), N·C), 16-B loads and stores
+template <typename T, bool ELU>
+__global__ __launch_bounds__(BN_T) void k_bn_apply8(const T* __restrict__ x, int C, int L,
+                                                    const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    T* __restrict__ y) {
+  const int row = blockIdx.y, c = row % C;
+  const int l = (blockIdx.x * BN_T + threadIdx.x) * 8;
+  if (l >= L) return;
+  const float a = invstd[c] * (gamma ? gamma[c] : 1.f);
+  const float b = (beta ? beta[c] : 0.f) - mean[c] * a;
+  const int64_t i = (int64_t)row * L + l;
+  float v[8];
+  bn_ld8(x, i, v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float z = fmaf(v[e], a, b);
+    v[e] = ELU ? (z > 0.f ? z : expf(z) - 1.f) : z;
+  }
+  bn_st8(y, i, v);
+}
+
 // the gradient reaching the batch norm's output: with the fused ELU, dz = dy·(y > 0 ? 1 : y + 1)
 // from the ELU output y (torch's elu_backward on the result)
 template <bool ELU, typename T>
@@ -170,18 +223,16 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_stats(const T* __restrict__ x, 
   const int total = N * L, step = split * BN_T;
   float a1 = 0.f, a2 = 0.f;
   for (int e0 = sp * BN_T + threadIdx.x; e0 < total; e0 += BN_U * step) {
-    float g[BN_U], xv[BN_U];
+    float g[BN_U], xv[BN_U], yv[BN_U];
 #pragma unroll
-    for (int r = 0; r < BN_U; ++r) {
+    for (int r = 0; r < BN_U; ++r) {  // every load of the pass first
       g[r] = bn_ld_or0(dy, C, L, c, e0 + r * step, total);
       xv[r] = bn_ld_or0(x, C, L, c, e0 + r * step, total);
-      if (ELU) {
-        const float v = bn_ld_or0(ya, C, L, c, e0 + r * step, total);
-        g[r] = v > 0.f ? g[r] : g[r] * (v + 1.f);
-      }
+      if (ELU) yv[r] = bn_ld_or0(ya, C, L, c, e0 + r * step, total);
     }
 #pragma unroll
     for (int r = 0; r < BN_U; ++r) {
+      if (ELU) g[r] = yv[r] > 0.f ? g[r] : g[r] * (yv[r] + 1.f);
       a1 += g[r];
       // padded elements: g = 0, so the (0 − μ)·invstd term adds nothing
       a2 = fmaf(g[r], (xv[r] - mu) * is, a2);
@@ -218,6 +269,33 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_apply(const T* __restrict__ x, 
   bn_st(dx, i, k * (bn_grad<ELU>(dy, ya, i) - m1 - xh * m2));
 }
 
+template <typename T, bool ELU>
+__global__ __launch_bounds__(BN_T) void k_bn_bwd_apply8(const T* __restrict__ x, const T* __restrict__ dy,
+                                                        const T* __restrict__ ya, int C,
+                                                        int L, int64_t M, const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd,
+                                                        const float* __restrict__ gamma,
+                                                        const double* __restrict__ sums, T* __restrict__ dx) {
+  const int row = blockIdx.y, c = row % C;
+  const int l = (blockIdx.x * BN_T + threadIdx.x) * 8;
+  if (l >= L) return;
+  const float is = invstd[c], mu = mean[c];
+  const float k = is * (gamma ? gamma[c] : 1.f);
+  const float m1 = (float)(sums[2 * c] / (double)M), m2 = (float)(sums[2 * c + 1] / (double)M);
+  const int64_t i = (int64_t)row * L + l;
+  float xv[8], g[8], yv[8];
+  bn_ld8(x, i, xv);
+  bn_ld8(dy, i, g);
+  if (ELU) bn_ld8(ya, i, yv);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float gz = ELU ? (yv[e] > 0.f ? g[e] : g[e] * (yv[e] + 1.f)) : g[e];
+    const float xh = (xv[e] - mu) * is;
+    xv[e] = k * (gz - m1 - xh * m2);
+  }
+  bn_st8(dx, i, xv);
+}
+
 // scratch of the forward / backward calls: per-(channel, split) partials, the
 // backward's channel sums, then one completion counter per channel (zero
 // before the first call; every call leaves them zero)
@@ -235,13 +313,17 @@ int bn_fwd(ocm_ctx* ctx, const void* x, int N, int C, int L, const float* gamma,
   const int split = bn_split(C);
   hipLaunchKernelGGL(k_bn_stats<T>, dim3(split, C), dim3(BN_T), 0, st, static_cast<const T*>(x), N, C, L, part,
                      ticket, eps, momentum, smean, sinv, rmean, rvar, nbt);
-  const dim3 ga((L + BN_T - 1) / BN_T, N * C);
-  if (act == OCM_ACT_ELU)
-    hipLaunchKernelGGL((k_bn_apply<T, true>), ga, dim3(BN_T), 0, st, static_cast<const T*>(x), C, L, smean, sinv,
-                       gamma, beta, static_cast<T*>(y));
-  else
-    hipLaunchKernelGGL((k_bn_apply<T, false>), ga, dim3(BN_T), 0, st, static_cast<const T*>(x), C, L, smean, sinv,
-                       gamma, beta, static_cast<T*>(y));
+  const bool v8 = L % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+  const dim3 ga(v8 ? (L / 8 + BN_T - 1) / BN_T : (L + BN_T - 1) / BN_T, N * C);
+#define OCM_BN_APPLY(K_, E_) \
+  hipLaunchKernelGGL((K_<T, E_>), ga, dim3(BN_T), 0, st, static_cast<const T*>(x), C, L, smean, sinv, gamma, beta, \
+                     static_cast<T*>(y))
+  if (act == OCM_ACT_ELU) {
+    if (v8) OCM_BN_APPLY(k_bn_apply8, true); else OCM_BN_APPLY(k_bn_apply, true);
+  } else {
+    if (v8) OCM_BN_APPLY(k_bn_apply8, false); else OCM_BN_APPLY(k_bn_apply, false);
+  }
+#undef OCM_BN_APPLY
   OCM_CHECK_LAUNCH("k_bn_fwd");
   return OCM_OK;
 }
@@ -257,9 +339,15 @@ int bn_bwd(ocm_ctx* ctx, const void* x, const void* dy, const void* ya, int N, i
   hipLaunchKernelGGL((k_bn_bwd_stats<T, ELU>), dim3(split, C), dim3(BN_T), 0, st, static_cast<const T*>(x),
                      static_cast<const T*>(dy), static_cast<const T*>(ya), N, C, L, smean, sinv, part, ticket, sums,
                      dgamma, dbeta);
-  hipLaunchKernelGGL((k_bn_bwd_apply<T, ELU>), dim3((L + BN_T - 1) / BN_T, N * C), dim3(BN_T), 0, st,
-                     static_cast<const T*>(x), static_cast<const T*>(dy), static_cast<const T*>(ya), C, L,
-                     (int64_t)N * L, smean, sinv, gamma, sums, static_cast<T*>(dx));
+  const auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (L % 8 == 0 && al(x) && al(dy) && (!ELU || al(ya)) && al(dx))
+    hipLaunchKernelGGL((k_bn_bwd_apply8<T, ELU>), dim3((L / 8 + BN_T - 1) / BN_T, N * C), dim3(BN_T), 0, st,
+                       static_cast<const T*>(x), static_cast<const T*>(dy), static_cast<const T*>(ya), C, L,
+                       (int64_t)N * L, smean, sinv, gamma, sums, static_cast<T*>(dx));
+  else
+    hipLaunchKernelGGL((k_bn_bwd_apply<T, ELU>), dim3((L + BN_T - 1) / BN_T, N * C), dim3(BN_T), 0, st,
+                       static_cast<const T*>(x), static_cast<const T*>(dy), static_cast<const T*>(ya), C, L,
+                       (int64_t)N * L, smean, sinv, gamma, sums, static_cast<T*>(dx));
   OCM_CHECK_LAUNCH("k_bn_bwd");
   return OCM_OK;
 }

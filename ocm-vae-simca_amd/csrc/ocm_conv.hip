@@ -52,9 +52,10 @@ __device__ __forceinline__ float cv_ld_or0(const T* p, int i, int n, bool ok) {
 }
 constexpr int WG_SPLIT = 128;   // csum partial workgroups per channel
 constexpr int WG_MAXSPLIT = 1024;  // wgrad partial workgroups per (o, i) pair, at most
+constexpr int WG_PPT = 4;          // wgrad positions per thread and pass
 // scratch layout: CV_TICKETS completion counter words (zero before the first
 // call; every call leaves them zero), then the partials.  wgrad: groups ·
-// tickets_per_slot(split) counters, ≤ 2·1024 + 4096/16; chan_sum: C·9
+// tickets_per_slot(split) counters, ≤ 2·1024 + 8192/16; chan_sum: C·9
 constexpr int CV_TICKETS = 2560 * TICKET_STRIDE;
 
 // true in the last of the gridDim.x workgroups of slot `slot` to arrive
@@ -161,29 +162,41 @@ __global__ __launch_bounds__(CV_T) void k_conv_wgrad(const TP* __restrict__ P, i
   for (int u = 0; u < CV_OG; ++u)
 #pragma unroll
     for (int t = 0; t < NA; ++t) acc[u][t] = 0.f;
-  for (int e = blockIdx.x * CV_T + threadIdx.x; e < total; e += gridDim.x * CV_T) {
-    const int b = e / Lp, l = e - b * Lp;
-    const TQ* qr = Q + ((int64_t)b * I + i) * Lq;
-    const int j0 = l * s - pad;
-    float qv[KT], pv[CV_OG];
+  // WG_PPT positions per thread and pass, all their loads issued before any
+  // FMA (a position at a time waited out one memory latency per position:
+  // 16 in a row, ≈ 40 µs for a 5-MB layer, round 4)
+  const int stride = gridDim.x * CV_T;
+  for (int e0 = blockIdx.x * CV_T + threadIdx.x; e0 < total; e0 += WG_PPT * stride) {
+    float qv[WG_PPT][KT], pv[WG_PPT][CV_OG];
 #pragma unroll
-    for (int t = 0; t < KT; ++t) {
-      const int j = j0 + t;
-      qv[t] = cv_ld_or0(qr, j, Lq, t < K && j >= 0 && j < Lq);
+    for (int r = 0; r < WG_PPT; ++r) {
+      const int e = e0 + r * stride;
+      const bool in = e < total;
+      const int ec = in ? e : 0;  // clamped: a valid position, its products dropped
+      const int b = ec / Lp, l = ec - b * Lp;
+      const TQ* qr = Q + ((int64_t)b * I + i) * Lq;
+      const int j0 = l * s - pad;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const int j = j0 + t;
+        qv[r][t] = cv_ld_or0(qr, j, Lq, in && t < K && j >= 0 && j < Lq);
+      }
+      // channels past O read channel O − 1 (valid memory) and are dropped
+      const TP* pb = P + (int64_t)b * O * Lp + l;
+#pragma unroll
+      for (int u = 0; u < CV_OG; ++u) {
+        const float v = cv_ld(pb, (int64_t)min(o0 + u, O - 1) * Lp);
+        pv[r][u] = in && o0 + u < O ? v : 0.f;
+      }
     }
-    // channels past O read channel O − 1 (valid memory) and are dropped
-    const TP* pb = P + (int64_t)b * O * Lp + l;
 #pragma unroll
-    for (int u = 0; u < CV_OG; ++u) {
-      const float v = cv_ld(pb, (int64_t)min(o0 + u, O - 1) * Lp);
-      pv[u] = o0 + u < O ? v : 0.f;
-    }
+    for (int r = 0; r < WG_PPT; ++r)
 #pragma unroll
-    for (int u = 0; u < CV_OG; ++u) {
+      for (int u = 0; u < CV_OG; ++u) {
 #pragma unroll
-      for (int t = 0; t < KT; ++t) acc[u][t] = fmaf(pv[u], qv[t], acc[u][t]);
-      if (WB) acc[u][NA - 1] += pv[u];
-    }
+        for (int t = 0; t < KT; ++t) acc[u][t] = fmaf(pv[r][u], qv[r][t], acc[u][t]);
+        if (WB) acc[u][NA - 1] += pv[r][u];
+      }
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -211,8 +224,7 @@ __global__ __launch_bounds__(CV_T) void k_conv_wgrad(const TP* __restrict__ P, i
     const int u = e / KS, t = e % KS, o = o0 + u;
     if (o >= O) continue;
     const int64_t pair = (int64_t)o * I + i;
-    float v = 0.f;
-    for (int xb = lane; xb < split; xb += 64) v += ld_agent(part + (pair * split + xb) * KS + t);
+    float v = lane_sum_agent<float, float>(part + pair * split * KS + t, KS, split, lane);
     v = wave_sum_f32(v);
     if (lane) continue;
     if (t < K) G[pair * K + t] = v;
@@ -230,18 +242,28 @@ __global__ __launch_bounds__(CV_T) void k_chan_sum(const T* __restrict__ v, int 
   const int c = blockIdx.y;
   const int total = B * L;  // < 2³¹ (checked by the host)
   float a = 0.f;
-  for (int e = blockIdx.x * CV_T + threadIdx.x; e < total; e += WG_SPLIT * CV_T) {
-    const int b = e / L, l = e - b * L;
-    a += cv_ld(v, ((int64_t)b * C + c) * L + l);
+  // eight positions per thread and pass, their loads issued together
+  constexpr int U = 8;
+  for (int e0 = blockIdx.x * CV_T + threadIdx.x; e0 < total; e0 += U * WG_SPLIT * CV_T) {
+    float t[U];
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+      const int e = e0 + r * WG_SPLIT * CV_T;
+      const int ec = e < total ? e : 0;
+      const int b = ec / L, l = ec - b * L;
+      const float x = cv_ld(v, ((int64_t)b * C + c) * L + l);
+      t[r] = e < total ? x : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < U; ++r) a += t[r];
   }
   a = wave_sum_f32(a);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
   __syncthreads();
   if (threadIdx.x == 0) st_agent(part + (int64_t)c * WG_SPLIT + blockIdx.x, (red[0] + red[1]) + (red[2] + red[3]));
-  if (!cv_last(ticket, c) || threadIdx.x != 0) return;
-  double s = 0.0;
-  for (int xb = 0; xb < WG_SPLIT; ++xb) s += ld_agent(part + (int64_t)c * WG_SPLIT + xb);
-  out[c] = (float)s;
+  if (!cv_last(ticket, c) || threadIdx.x >= 64) return;
+  const double s = wave_sum_f64(lane_sum_agent<float, double>(part + (int64_t)c * WG_SPLIT, 1, WG_SPLIT, threadIdx.x));
+  if (threadIdx.x == 0) out[c] = (float)s;
 }
 
 template <bool UP, int KT>
@@ -311,10 +333,11 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
   float* part = reinterpret_cast<float*>(ticket + CV_TICKETS);
   OCM_REQUIRE((int64_t)B * Lp < (1LL << 31), "ocm_conv1d_wgrad: B·Lp must be < 2^31");
   const int groups = I * ((O + CV_OG - 1) / CV_OG);
-  // ≈ 4096 workgroups in all, so a layer with few channels still fills the chip,
-  // but ≥ 16 positions per thread (the block reductions are not free)
-  const int per16 = (int)(((int64_t)B * Lp + 16 * CV_T - 1) / (16 * CV_T));
-  const int split = std::max(1, std::min({WG_MAXSPLIT, std::max(1, 4096 / groups), per16}));
+  // four passes of WG_PPT positions per thread where the grid allows (≤ 8192
+  // workgroups in all, ≤ WG_MAXSPLIT per group: the completion counters fit
+  // CV_TICKETS), so a layer with few channels still fills the chip
+  const int pass = (int)(((int64_t)B * Lp + 4 * WG_PPT * CV_T - 1) / (4 * WG_PPT * CV_T));
+  const int split = std::max(1, std::min({WG_MAXSPLIT, std::max(1, 8192 / groups), pass}));
   const bool wb = psum_out != nullptr;
   dim3 g((unsigned)split, (unsigned)groups);
 #define OCM_WG_K(KT, WB, TP, TQ)                                                                            \

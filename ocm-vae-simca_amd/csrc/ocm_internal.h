@@ -149,6 +149,25 @@ __device__ __forceinline__ double ld_agent(const double* p) {
 __device__ __forceinline__ float ld_agent(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Σ_k p[k·stride] over k = lane, lane + 64, … < count in that order (one lane
+// of a wave-strided sum), eight write-through loads in flight at a time (a
+// runtime loop of atomic loads waits out each one: ≈ 1 µs apiece)
+template <typename T, typename A>
+__device__ __forceinline__ A lane_sum_agent(const T* p, int64_t stride, int count, int lane) {
+  A acc = A(0);
+  for (int k0 = lane; k0 < count; k0 += 64 * 8) {
+    T v[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int k = k0 + 64 * r;
+      const T x = ld_agent(p + (int64_t)(k < count ? k : lane) * stride);
+      v[r] = k < count ? x : T(0);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc += (A)v[r];
+  }
+  return acc;
+}
 // Called by every thread of the workgroup after its st_agent stores: true in
 // the last of the n workgroups that share `*counter`, which it resets to 0 (so
 // a counter zeroed once stays reusable across launches and graph replays).

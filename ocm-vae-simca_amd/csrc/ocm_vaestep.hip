@@ -134,8 +134,7 @@ __global__ __launch_bounds__(VT) void k_recon_fwd(int kind, const float* __restr
   const double ps = block_sum_d(s, red);
   if (threadIdx.x == 0) st_agent(part + b, ps);  // write-through (ocm_internal.h last_arrival)
   if (!last_arrival(ticket, gridDim.x)) return;
-  double t = 0.0;
-  for (int i = threadIdx.x; i < (int)gridDim.x; i += VT) t += ld_agent(part + i);
+  const double t = threadIdx.x < 64 ? lane_sum_agent<double, double>(part, 1, (int)gridDim.x, threadIdx.x) : 0.0;
   const double tot = block_sum_d(t, red);
   if (threadIdx.x == 0) {
     const float recon = (float)(tot * inv);
@@ -181,9 +180,77 @@ __global__ __launch_bounds__(VT) void k_adam(const ocm_adam_tensor* __restrict__
   if (last_arrival(ticket, gridDim.x) && threadIdx.x == 0) *step = t;
 }
 
+// up to CAST_MAX tensors converted in one launch (the arguments by value:
+// graph-capturable without a device table)
+constexpr int CAST_MAX = 32;
+struct CastArgs {
+  const void* src[CAST_MAX];
+  void* dst[CAST_MAX];
+  int64_t end[CAST_MAX];  // prefix sums of the element counts
+  int n;
+};
+__global__ __launch_bounds__(VT) void k_cast_multi(CastArgs a, int sdt, int ddt) {
+  const int64_t total = a.end[a.n - 1];
+  int cur = 0;
+  for (int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x; i < total; i += (int64_t)gridDim.x * VT) {
+    while (i >= a.end[cur]) ++cur;
+    const int64_t j = i - (cur ? a.end[cur - 1] : 0);
+    st_act(a.dst[cur], ddt, j, ld_act(a.src[cur], sdt, j));
+  }
+}
+
+// xs = (x − mean) / std, per column of a B×L float32 matrix, written in dtype
+__global__ __launch_bounds__(VT) void k_standardise(const float* __restrict__ x, const float* __restrict__ mean,
+                                                     const float* __restrict__ sd, int64_t n, int L, int dt,
+                                                     void* out) {
+  const int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x;
+  if (i >= n) return;
+  const int j = (int)(i % L);
+  st_act(out, dt, i, (x[i] - mean[j]) / sd[j]);
+}
+
 }  // namespace
 
 extern "C" {
+
+int ocm_cast_multi(ocm_ctx* ctx, int32_t n, const void* const* src, int32_t src_dtype, void* const* dst,
+                   int32_t dst_dtype, const int64_t* numel, void* stream) {
+  OCM_REQUIRE(ctx && src && dst && numel, "ocm_cast_multi: NULL argument");
+  OCM_REQUIRE(n >= 0 && n <= CAST_MAX, "ocm_cast_multi: at most 32 tensors");
+  OCM_REQUIRE((src_dtype == OCM_DTYPE_F32 || src_dtype == OCM_DTYPE_BF16) &&
+                  (dst_dtype == OCM_DTYPE_F32 || dst_dtype == OCM_DTYPE_BF16),
+              "ocm_cast_multi: float32 / bfloat16");
+  CastArgs a{};
+  int64_t t = 0;
+  int m = 0;
+  for (int k = 0; k < n; ++k) {
+    OCM_REQUIRE(numel[k] >= 0 && (numel[k] == 0 || (src[k] && dst[k])), "ocm_cast_multi: bad tensor");
+    if (numel[k] == 0) continue;
+    t += numel[k];
+    a.src[m] = src[k];
+    a.dst[m] = dst[k];
+    a.end[m] = t;
+    ++m;
+  }
+  a.n = m;
+  if (m == 0) return OCM_OK;
+  const int64_t blocks = std::min<int64_t>((t + VT - 1) / VT, 4 * (int64_t)ctx->num_cus);
+  hipLaunchKernelGGL(k_cast_multi, dim3((unsigned)blocks), dim3(VT), 0, (hipStream_t)stream, a, src_dtype,
+                     dst_dtype);
+  OCM_CHECK_LAUNCH("k_cast_multi");
+  return OCM_OK;
+}
+
+int ocm_vae_standardise(ocm_ctx* ctx, const float* x, int32_t B, int32_t L, const float* mean, const float* std_,
+                        int32_t dtype, void* out, void* stream) {
+  OCM_REQUIRE(ctx && x && mean && std_ && out, "ocm_vae_standardise: NULL argument");
+  OCM_REQUIRE(B > 0 && L > 0 && (dtype == OCM_DTYPE_F32 || dtype == OCM_DTYPE_BF16), "ocm_vae_standardise: bad args");
+  const int64_t n = (int64_t)B * L;
+  hipLaunchKernelGGL(k_standardise, dim3((unsigned)((n + VT - 1) / VT)), dim3(VT), 0, (hipStream_t)stream, x, mean,
+                     std_, n, L, dtype, out);
+  OCM_CHECK_LAUNCH("k_standardise");
+  return OCM_OK;
+}
 
 size_t ocm_vae_scratch_bytes(int32_t B) { return (size_t)(B + 64) * sizeof(double) + 256; }
 

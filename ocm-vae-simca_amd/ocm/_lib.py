@@ -137,6 +137,8 @@ SIGNATURES = {
                                   c_void_p]),
     "ocm_adam_step": (c_i32, [c_void_p, c_void_p, c_i32, c_i64, c_void_p, ctypes.c_float, ctypes.c_float,
                               ctypes.c_float, ctypes.c_float, ctypes.c_float, c_void_p, c_void_p]),
+    "ocm_cast_multi": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_void_p, c_i32, c_void_p, c_void_p]),
+    "ocm_vae_standardise": (c_i32, [c_void_p, c_void_p, c_i32, c_i32, c_void_p, c_void_p, c_i32, c_void_p, c_void_p]),
     "ocm_eigh_f64": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_i32, c_void_p, c_void_p]),
     "ocm_prep_materialised": (c_i32, [c_void_p, ctypes.POINTER(c_i64)]),
     "ocm_prep_rowstats_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p]),

@@ -18,6 +18,13 @@ optimizer kernel:
 * ``FusedAdam``: torch.optim.Adam (L2 weight decay) over every parameter in
   one launch (ocm_adam_step), with its moments and step counter on the device.
 
+* ``cast_bf16(*params)``: the Linear layers' float32 weights and biases to
+  bfloat16 in one launch per step (autocast would cast each one, and cast each
+  bfloat16 gradient back, in a kernel of its own: 20 launches per step), and
+  their bfloat16 gradients back to float32 in one launch (ocm_cast_multi);
+* ``standardise(x, mean, std)``: the encoder's input (x − mean)/std in bf16,
+  one launch (vae_model.py:128-129).
+
 ε is drawn with torch.randn_like on the graph-safe generator, exactly as the
 model's reparameterize draws it.  Sums are fp64 with fixed-order partials.
 """
@@ -200,3 +207,62 @@ class FusedAdam:
         for t in self.exp_avg + self.exp_avg_sq:
             t.zero_()
         self.step_t.zero_()
+
+
+def _cast_multi(srcs, dsts, sdt, ddt, dev):
+    n = len(srcs)
+    src = (ctypes.c_void_p * n)(*[t.data_ptr() for t in srcs])
+    dst = (ctypes.c_void_p * n)(*[t.data_ptr() for t in dsts])
+    numel = (ctypes.c_int64 * n)(*[t.numel() for t in srcs])
+    check(_lib.load().ocm_cast_multi(_h(dev), n, src, sdt, dst, ddt, numel, stream_handle(dev)), "ocm_cast_multi")
+
+
+class _CastBF16(torch.autograd.Function):
+    """float32 parameters → bfloat16 copies (one launch); the backward turns
+    their bfloat16 gradients into float32 ones (one launch), written straight
+    into the parameters' .grad views when every parameter has one (the flat
+    all-reduce buffer of the data-parallel step), else returned."""
+
+    @staticmethod
+    def forward(ctx, *params):
+        outs = [torch.empty_like(p, dtype=torch.bfloat16, memory_format=torch.contiguous_format) for p in params]
+        _cast_multi([p.detach().contiguous() for p in params], outs, _DT[torch.float32], _DT[torch.bfloat16],
+                    params[0].device)
+        ctx.params = params
+        ctx.set_materialize_grads(False)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        params = ctx.params
+        live = [(p, g) for p, g in zip(params, grads) if g is not None]
+        if not live:
+            return (None,) * len(params)
+        into_views = all(p.grad is not None and p.grad.is_contiguous() for p, _ in live)
+        outs = [p.grad if into_views else torch.empty_like(p, memory_format=torch.contiguous_format)
+                for p, _ in live]
+        _cast_multi([g.contiguous() for _, g in live], outs, _DT[torch.bfloat16], _DT[torch.float32],
+                    params[0].device)
+        if into_views:
+            return (None,) * len(params)
+        res, k = [], 0
+        for g in grads:
+            if g is None:
+                res.append(None)
+            else:
+                res.append(outs[k])
+                k += 1
+        return tuple(res)
+
+
+def cast_bf16(*params):
+    return _CastBF16.apply(*params)
+
+
+def standardise(x: torch.Tensor, mean: torch.Tensor, std: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    """(x − mean) / std per column of a B×L float32 batch, in ``dtype``."""
+    B, L = x.shape
+    out = torch.empty((B, L), dtype=dtype, device=x.device)
+    check(_lib.load().ocm_vae_standardise(_h(x.device), ptr(x), B, L, ptr(mean), ptr(std), _DT[dtype], ptr(out),
+                                          stream_handle(x.device)), "ocm_vae_standardise")
+    return out

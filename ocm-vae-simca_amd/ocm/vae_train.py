@@ -31,10 +31,28 @@ import time
 
 import torch
 import torch.distributed as dist
+from torch import nn
 
 import vae_model as V
 
 __all__ = ["GraphedVAETrainer"]
+
+
+class _FusedForward(nn.Module):
+    """encode → z = μ + ε·exp(½logσ²) and the KL (libocm) → decode, as one
+    module so torch.func.functional_call can run it on substituted (bf16)
+    Linear parameters (vae_model.py:116-134)."""
+
+    def __init__(self, m, vf):
+        super().__init__()
+        self.m = m
+        self._vf = vf
+
+    def forward(self, xin):
+        mu, logvar = self.m.encode(xin)
+        eps = torch.randn_like(mu)
+        z, kl = self._vf.bottleneck(mu, logvar, eps)
+        return self.m.decode(z), kl
 
 
 class GraphedVAETrainer:
@@ -88,6 +106,12 @@ class GraphedVAETrainer:
             self._vf = vae_fused
             self.opt = vae_fused.FusedAdam(model.parameters(), lr=lr, weight_decay=weight_decay)
             self._rbufs = vae_fused.ReconBuffers(self.module.spec_mean, self.module.spec_std)
+            # bf16 steps: the Linear layers run on bf16 copies of their
+            # parameters made in one launch per step (vae_fused.cast_bf16)
+            self._fwd = _FusedForward(self.module, vae_fused)
+            self._lin = [("m." + n, p) for n, p in self.module.named_parameters()
+                         if p.requires_grad and "." in n
+                         and isinstance(self.module.get_submodule(n.rsplit(".", 1)[0]), nn.Linear)]
         else:
             gpu_fused = dev.type == "cuda"
             self.opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay, capturable=graph,
@@ -167,11 +191,14 @@ class GraphedVAETrainer:
         z = μ + ε·exp(½logσ²) and the KL (one launch), the de-standardised
         reconstruction term and the total (one launch)."""
         m = self.module
-        with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32):
-            mu, logvar = m.encode((self.x - m.spec_mean) / m.spec_std)
-            eps = torch.randn_like(mu)
-            z, kl = self._vf.bottleneck(mu, logvar, eps)
-            xs = m.decode(z)
+        if self.dtype == torch.bfloat16 and self._lin:
+            casted = self._vf.cast_bf16(*[p for _, p in self._lin])
+            xin = self._vf.standardise(self.x, m.spec_mean, m.spec_std)
+            with torch.autocast("cuda", dtype=self.dtype):
+                xs, kl = torch.func.functional_call(self._fwd, dict(zip([n for n, _ in self._lin], casted)), (xin,))
+        else:
+            with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32):
+                xs, kl = self._fwd((self.x - m.spec_mean) / m.spec_std)
         total, recon = self._vf.recon_total(self.x, xs, kl, self._rbufs, self.loss, self.beta)
         total.backward()
         if self.allreduce:  # DDP averaging: one RCCL all-reduce of the flat gradient
