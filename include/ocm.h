@@ -481,7 +481,9 @@ int ocm_chan_sum(ocm_ctx* ctx, int32_t dtype, const void* v, int32_t B, int32_t 
  * ocm_vae_scratch_bytes(B) bytes, zeroed once before first use).
  *
  * ocm_vae_bottleneck_fwd: z = μ + ε·exp(½·logσ²); kl_out = −½·mean_B Σ_d (1 + logσ² − μ² − exp(logσ²))
- *   (vae_model.py:150-152, reparameterize :124-126).  μ, logσ², ε, z [dev] B×d.
+ *   (vae_model.py:150-152, reparameterize :124-126).  μ, logσ², ε, z [dev] B×d, B·d ≤ 2²⁰; scratch
+ *   [dev] ocm_vae_bottleneck_scratch_bytes(), zero-filled once before first use (its counters are
+ *   left zero).
  * ocm_vae_bottleneck_bwd: dμ = dz + dkl·μ/B, dlogσ² = dz·ε·½exp(½logσ²) − ½·dkl·(1 − exp(logσ²))/B
  *   (dz or dkl may be NULL: no gradient from that output).
  * ocm_vae_recon_fwd: x̂ = xs·std + mean (forward's de-standardisation, vae_model.py:130-134); kind
@@ -503,8 +505,9 @@ typedef struct ocm_adam_tensor {
   int64_t numel;
 } ocm_adam_tensor;
 size_t ocm_vae_scratch_bytes(int32_t B);
+size_t ocm_vae_bottleneck_scratch_bytes(void);
 int ocm_vae_bottleneck_fwd(ocm_ctx* ctx, int32_t dtype, const void* mu, const void* logvar, const void* eps, int32_t B,
-                           int32_t d, void* z_out, float* kl_out, void* stream);
+                           int32_t d, void* z_out, float* kl_out, void* scratch, void* stream);
 int ocm_vae_bottleneck_bwd(ocm_ctx* ctx, int32_t dtype, const void* dz, const float* dkl, const void* mu,
                            const void* logvar, const void* eps, int32_t B, int32_t d, void* dmu_out, void* dlogvar_out,
                            void* stream);
@@ -515,6 +518,16 @@ int ocm_vae_recon_bwd(ocm_ctx* ctx, const float* dtotal, const float* gxs, int64
                       float beta, float* dkl_out, void* stream);
 int ocm_adam_step(ocm_ctx* ctx, const ocm_adam_tensor* table, int32_t ntensors, int64_t total, float* step, float lr,
                   float beta1, float beta2, float eps, float weight_decay, void* scratch, void* stream);
+/* ocm_cast_multi: dst[k] = src[k] converted (float32 ↔ bfloat16, round to nearest even) for n ≤ 32
+ *   tensors of numel[k] elements in one launch (src / dst / numel: HOST arrays of device pointers;
+ *   the pointers travel as kernel arguments, so a captured graph replays them).  The VAE step casts
+ *   its Linear weights to bf16 once per step, and their bf16 gradients back, in one launch each.
+ * ocm_vae_standardise: out = (x − mean) / std per column of a B×L float32 batch, in dtype
+ *   (vae_model.py:128-129 standardises the spectra before the encoder). */
+int ocm_cast_multi(ocm_ctx* ctx, int32_t n, const void* const* src, int32_t src_dtype, void* const* dst,
+                   int32_t dst_dtype, const int64_t* numel, void* stream);
+int ocm_vae_standardise(ocm_ctx* ctx, const float* x, int32_t B, int32_t L, const float* mean, const float* std_,
+                        int32_t dtype, void* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -75,22 +75,7 @@ __global__ __launch_bounds__(CV_T) void k_conv(const TI* __restrict__ x, int I, 
   // ds_read_b128 serves the four FMAs of a tap (CV_KMAX slots, zero past K)
   __shared__ f32x4 sw[CV_CMAX * CV_KMAX];
   const int o0 = blockIdx.y * CV_OG, b = blockIdx.z;
-  for (int e = threadIdx.x; e < I * CV_KMAX; e += CV_T) {
-    const int i = e / CV_KMAX, t = e - i * CV_KMAX;
-    f32x4 wv;
-#pragma unroll
-    for (int u = 0; u < CV_OG; ++u) {
-      const int o = o0 + u;
-      wv[u] = (o < O && t < K) ? (UP ? w[((int64_t)i * O + o) * K + t] : w[((int64_t)o * I + i) * K + t]) : 0.f;
-    }
-    sw[e] = wv;
-  }
-  __syncthreads();
-  const int l = blockIdx.x * CV_T + threadIdx.x;
-  if (l >= Lout) return;
-  float acc[CV_OG];
-#pragma unroll
-  for (int u = 0; u < CV_OG; ++u) acc[u] = (bias && o0 + u < O) ? bias[o0 + u] : 0.f;
+  const int l = blockIdx.x * CV_T + threadIdx.x;  // this thread's output position (≥ Lout: none)
   const TI* xb = x + (int64_t)b * I * Lin;
   // up: the taps that reach output l are t ≡ (l + pad) mod s, input l' = (l + pad − t)/s;
   // the t-th of them is tap t0 + t·s at input jb − t (one division per thread)
@@ -115,8 +100,25 @@ __global__ __launch_bounds__(CV_T) void k_conv(const TI* __restrict__ x, int I, 
       v[t] = cv_ld_or0(xr, j, Lin, ok);
     }
   };
+  // the first channel's taps are issued before the weights are staged (their
+  // latencies overlap; the loads are clamped, so idle threads issue them too)
   float va[KT], vb[KT];
   taps(0, va);
+  for (int e = threadIdx.x; e < I * CV_KMAX; e += CV_T) {
+    const int i = e / CV_KMAX, t = e - i * CV_KMAX;
+    f32x4 wv;
+#pragma unroll
+    for (int u = 0; u < CV_OG; ++u) {
+      const int o = o0 + u;
+      wv[u] = (o < O && t < K) ? (UP ? w[((int64_t)i * O + o) * K + t] : w[((int64_t)o * I + i) * K + t]) : 0.f;
+    }
+    sw[e] = wv;
+  }
+  __syncthreads();
+  if (l >= Lout) return;
+  float acc[CV_OG];
+#pragma unroll
+  for (int u = 0; u < CV_OG; ++u) acc[u] = (bias && o0 + u < O) ? bias[o0 + u] : 0.f;
   for (int i = 0; i < I; i += 2) {
     if (i + 1 < I) taps(i + 1, vb);
 #pragma unroll
@@ -333,11 +335,14 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
   float* part = reinterpret_cast<float*>(ticket + CV_TICKETS);
   OCM_REQUIRE((int64_t)B * Lp < (1LL << 31), "ocm_conv1d_wgrad: B·Lp must be < 2^31");
   const int groups = I * ((O + CV_OG - 1) / CV_OG);
-  // four passes of WG_PPT positions per thread where the grid allows (≤ 8192
-  // workgroups in all, ≤ WG_MAXSPLIT per group: the completion counters fit
-  // CV_TICKETS), so a layer with few channels still fills the chip
-  const int pass = (int)(((int64_t)B * Lp + 4 * WG_PPT * CV_T - 1) / (4 * WG_PPT * CV_T));
-  const int split = std::max(1, std::min({WG_MAXSPLIT, std::max(1, 8192 / groups), pass}));
+  // ≈ 1024 workgroups in all (a one-group layer must fill the chip), between
+  // one and four passes of WG_PPT positions per thread; ≤ 8192 workgroups in
+  // all and ≤ WG_MAXSPLIT per group (the completion counters fit CV_TICKETS)
+  const int64_t pos = (int64_t)B * Lp;
+  const int one = (int)((pos + WG_PPT * CV_T - 1) / (WG_PPT * CV_T));
+  const int four = (int)((pos + 4 * WG_PPT * CV_T - 1) / (4 * WG_PPT * CV_T));
+  const int want = std::min(one, std::max(four, (1024 + groups - 1) / groups));
+  const int split = std::max(1, std::min({WG_MAXSPLIT, std::max(1, 8192 / groups), want}));
   const bool wb = psum_out != nullptr;
   dim3 g((unsigned)split, (unsigned)groups);
 #define OCM_WG_K(KT, WB, TP, TQ)                                                                            \

@@ -63,18 +63,25 @@ __device__ __forceinline__ float block_minmax(float v, bool is_max, float* red) 
   return r;
 }
 
-// one workgroup: z and the KL (B·d ≤ a few 10⁴ values)
-__global__ __launch_bounds__(1024) void k_bottleneck_fwd(const void* mu, const void* lv, const void* eps, int dt,
-                                                          int64_t n, int B, void* z, float* kl) {
-  __shared__ double red[16];
+// z and the KL: one element per thread, the workgroups' KL partials summed
+// by the last one (ocm_internal.h last_arrival2)
+__global__ __launch_bounds__(VT) void k_bottleneck_fwd(const void* mu, const void* lv, const void* eps, int dt,
+                                                        int64_t n, int B, void* z, float* kl, double* part,
+                                                        unsigned* ticket) {
+  __shared__ double red[VT / 64];
+  const int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x;
   double s = 0.0;
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+  if (i < n) {
     const float m = ld_act(mu, dt, i), l = ld_act(lv, dt, i), e = ld_act(eps, dt, i);
     st_act(z, dt, i, m + e * expf(0.5f * l));
-    s += 1.0 + (double)l - (double)m * m - exp((double)l);
+    s = 1.0 + (double)l - (double)m * m - exp((double)l);
   }
-  const double t = block_sum_d(s, red);
-  if (threadIdx.x == 0) *kl = (float)(-0.5 * t / B);
+  const double ps = block_sum_d(s, red);
+  if (threadIdx.x == 0) st_agent(part + blockIdx.x, ps);
+  if (!last_arrival2(ticket, 0, gridDim.x, blockIdx.x)) return;
+  const double t = threadIdx.x < 64 ? lane_sum_agent<double, double>(part, 1, (int)gridDim.x, threadIdx.x) : 0.0;
+  const double tot = block_sum_d(t, red);
+  if (threadIdx.x == 0) *kl = (float)(-0.5 * tot / B);
 }
 
 __global__ __launch_bounds__(VT) void k_bottleneck_bwd(const void* dz, const float* dkl, const void* mu,
@@ -151,29 +158,58 @@ __global__ __launch_bounds__(VT) void k_recon_bwd(const float* __restrict__ dtot
   if (i == 0 && dkl) *dkl = beta * g;
 }
 
-// Adam over a table of tensors: grid-stride over the concatenation (the
-// prefix of element counts in the table); the step counter (f32, on the
+// Adam over a table of tensors: each thread takes ADAM_U elements of the
+// concatenation (the prefix of element counts in the table), all their loads
+// before any arithmetic; the tensor of an element is found by binary search
+// in an LDS copy of the offsets (a linear walk through the table in global
+// memory cost one memory latency per step); the step counter (f32, on the
 // device) is read as t − 1 and advanced by the last workgroup.
+constexpr int ADAM_U = 4, ADAM_TMAX = 256;
 __global__ __launch_bounds__(VT) void k_adam(const ocm_adam_tensor* __restrict__ tab, int nt, int64_t total,
                                               float* __restrict__ step, float lr, float b1, float b2, float eps,
                                               float wd, unsigned* __restrict__ ticket) {
+  __shared__ int64_t offs[ADAM_TMAX];
+  for (int k = threadIdx.x; k < nt; k += VT) offs[k] = tab[k].offset;
+  __syncthreads();
   const float t = *step + 1.f;
   const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
   const float step_size = lr / bc1, bc2s = sqrtf(bc2);
-  int cur = 0;
-  for (int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x; i < total; i += (int64_t)gridDim.x * VT) {
-    while (cur + 1 < nt && i >= tab[cur + 1].offset) ++cur;
-    while (cur > 0 && i < tab[cur].offset) --cur;
-    const ocm_adam_tensor& T = tab[cur];
-    const int64_t j = i - T.offset;
-    float g = T.grad[j];
-    const float pv = T.param[j];
-    if (wd != 0.f) g += wd * pv;
-    const float m = b1 * T.exp_avg[j] + (1.f - b1) * g;
-    const float v = b2 * T.exp_avg_sq[j] + (1.f - b2) * g * g;
-    T.exp_avg[j] = m;
-    T.exp_avg_sq[j] = v;
-    T.param[j] = pv - step_size * m / (sqrtf(v) / bc2s + eps);
+  const int64_t stride = (int64_t)gridDim.x * VT;
+  for (int64_t i0 = (int64_t)blockIdx.x * VT + threadIdx.x; i0 < total; i0 += ADAM_U * stride) {
+    float* pp[ADAM_U];
+    float* mp[ADAM_U];
+    float* vp[ADAM_U];
+    float g[ADAM_U], pv[ADAM_U], m[ADAM_U], v[ADAM_U];
+#pragma unroll
+    for (int r = 0; r < ADAM_U; ++r) {
+      const int64_t i = i0 + r * stride;
+      const int64_t ic = i < total ? i : total - 1;
+      int lo = 0, hi = nt - 1;  // the last tensor whose offset ≤ ic
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (offs[mid] <= ic) lo = mid; else hi = mid - 1;
+      }
+      const ocm_adam_tensor& T = tab[lo];
+      const int64_t j = ic - offs[lo];
+      pp[r] = T.param + j;
+      mp[r] = T.exp_avg + j;
+      vp[r] = T.exp_avg_sq + j;
+      g[r] = T.grad[j];
+      pv[r] = *pp[r];
+      m[r] = *mp[r];
+      v[r] = *vp[r];
+    }
+#pragma unroll
+    for (int r = 0; r < ADAM_U; ++r) {
+      if (i0 + r * stride >= total) continue;
+      float gr = g[r];
+      if (wd != 0.f) gr += wd * pv[r];
+      const float mm = b1 * m[r] + (1.f - b1) * gr;
+      const float vv = b2 * v[r] + (1.f - b2) * gr * gr;
+      *mp[r] = mm;
+      *vp[r] = vv;
+      *pp[r] = pv[r] - step_size * mm / (sqrtf(vv) / bc2s + eps);
+    }
   }
   // the last workgroup advances the counter: every workgroup read it before
   // its own arrival (no data hand-off, so no fence)
@@ -253,13 +289,19 @@ int ocm_vae_standardise(ocm_ctx* ctx, const float* x, int32_t B, int32_t L, cons
 }
 
 size_t ocm_vae_scratch_bytes(int32_t B) { return (size_t)(B + 64) * sizeof(double) + 256; }
+size_t ocm_vae_bottleneck_scratch_bytes() { return 4096 * sizeof(double) + tickets_per_slot(4096) * TICKET_STRIDE * sizeof(unsigned); }
 
 int ocm_vae_bottleneck_fwd(ocm_ctx* ctx, int32_t dtype, const void* mu, const void* logvar, const void* eps, int32_t B,
-                           int32_t d, void* z_out, float* kl_out, void* stream) {
-  OCM_REQUIRE(ctx && mu && logvar && eps && z_out && kl_out, "ocm_vae_bottleneck_fwd: NULL argument");
+                           int32_t d, void* z_out, float* kl_out, void* scratch, void* stream) {
+  OCM_REQUIRE(ctx && mu && logvar && eps && z_out && kl_out && scratch, "ocm_vae_bottleneck_fwd: NULL argument");
   OCM_REQUIRE(B > 0 && d > 0 && (dtype == OCM_DTYPE_F32 || dtype == OCM_DTYPE_BF16), "ocm_vae_bottleneck_fwd: bad args");
-  hipLaunchKernelGGL(k_bottleneck_fwd, dim3(1), dim3(1024), 0, (hipStream_t)stream, mu, logvar, eps, dtype,
-                     (int64_t)B * d, B, z_out, kl_out);
+  const int64_t n = (int64_t)B * d;
+  const int64_t nb = (n + VT - 1) / VT;
+  OCM_REQUIRE(nb <= 4096, "ocm_vae_bottleneck_fwd: B·d ≤ 2²⁰");
+  auto* part = static_cast<double*>(scratch);
+  auto* ticket = reinterpret_cast<unsigned*>(part + 4096);
+  hipLaunchKernelGGL(k_bottleneck_fwd, dim3((unsigned)nb), dim3(VT), 0, (hipStream_t)stream, mu, logvar, eps, dtype,
+                     n, B, z_out, kl_out, part, ticket);
   OCM_CHECK_LAUNCH("k_bottleneck_fwd");
   return OCM_OK;
 }
@@ -302,8 +344,9 @@ int ocm_vae_recon_bwd(ocm_ctx* ctx, const float* dtotal, const float* gxs, int64
 
 int ocm_adam_step(ocm_ctx* ctx, const ocm_adam_tensor* table, int32_t ntensors, int64_t total, float* step, float lr,
                   float beta1, float beta2, float eps, float weight_decay, void* scratch, void* stream) {
-  OCM_REQUIRE(ctx && table && step && scratch && ntensors > 0 && total > 0, "ocm_adam_step: bad arguments");
-  const int grid = (int)std::min<int64_t>((total + VT - 1) / VT, 1024);
+  OCM_REQUIRE(ctx && table && step && scratch && ntensors > 0 && ntensors <= ADAM_TMAX && total > 0,
+              "ocm_adam_step: bad arguments (≤ 256 tensors)");
+  const int grid = (int)std::min<int64_t>((total + ADAM_U * VT - 1) / (ADAM_U * VT), 4096);
   hipLaunchKernelGGL(k_adam, dim3(grid), dim3(VT), 0, (hipStream_t)stream, table, ntensors, total, step, lr, beta1,
                      beta2, eps, weight_decay, static_cast<unsigned*>(scratch));
   OCM_CHECK_LAUNCH("k_adam");

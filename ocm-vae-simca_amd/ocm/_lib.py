@@ -127,8 +127,9 @@ SIGNATURES = {
                                  c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ocm_chan_sum": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
     "ocm_vae_scratch_bytes": (ctypes.c_size_t, [c_i32]),
+    "ocm_vae_bottleneck_scratch_bytes": (ctypes.c_size_t, []),
     "ocm_vae_bottleneck_fwd": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_i32, c_i32, c_void_p,
-                                       c_void_p, c_void_p]),
+                                       c_void_p, c_void_p, c_void_p]),
     "ocm_vae_bottleneck_bwd": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i32,
                                        c_i32, c_void_p, c_void_p, c_void_p]),
     "ocm_vae_recon_fwd": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_void_p, c_i32, c_i32, c_void_p, c_void_p,

@@ -45,6 +45,20 @@ def _h(dev):
     return Context.get(dev.index).handle
 
 
+_BSCRATCH = {}
+
+
+def _bottleneck_scratch(dev) -> torch.Tensor:
+    """The KL reduction's scratch (ocm_vae_bottleneck_scratch_bytes), one per
+    device, zero-filled once (its completion counters are left zero; the
+    step's launches are stream-ordered).  Allocated by the first, eager, call."""
+    key = dev.index
+    if key not in _BSCRATCH:
+        nb = int(_lib.load().ocm_vae_bottleneck_scratch_bytes())
+        _BSCRATCH[key] = torch.zeros((nb + 7) // 8, dtype=torch.float64, device=dev)
+    return _BSCRATCH[key]
+
+
 class _Bottleneck(torch.autograd.Function):
     @staticmethod
     def forward(ctx, mu, logvar, eps):
@@ -53,7 +67,8 @@ class _Bottleneck(torch.autograd.Function):
         z = torch.empty_like(mu)
         kl = torch.empty((), dtype=torch.float32, device=mu.device)
         check(_lib.load().ocm_vae_bottleneck_fwd(_h(mu.device), _DT[mu.dtype], ptr(mu), ptr(logvar), ptr(eps), B, d,
-                                                 ptr(z), ptr(kl), stream_handle(mu.device)), "ocm_vae_bottleneck_fwd")
+                                                 ptr(z), ptr(kl), ptr(_bottleneck_scratch(mu.device)),
+                                                 stream_handle(mu.device)), "ocm_vae_bottleneck_fwd")
         ctx.save_for_backward(mu, logvar, eps)
         ctx.set_materialize_grads(False)
         return z, kl
