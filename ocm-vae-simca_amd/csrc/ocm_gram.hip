@@ -951,11 +951,29 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restri
   constexpr int WN = 2 * HH + 1;
   __shared__ Q8PrepUnion<HH> lds;
   auto& L = lds.ld;
-  // workgroup → (row block, column group): row blocks fastest, as k_q8_quant
-  // (an XCD-aware order that runs a row block's neighbouring column groups
-  // back to back on one XCD measured 2× slower at HH = 7, r04h)
+  // workgroup → (row block, column group), XCD-aware: a group's halo columns
+  // belong to its neighbours, so the neighbours must read those lines close in
+  // time on one XCD (its L2).  Workgroup i runs on XCD i mod 8: XCD x takes
+  // the row blocks ≡ x (mod 8) and sweeps each one's column groups in order,
+  // ≈ 32 neighbours in flight.  In the plain order (row blocks fastest) every
+  // halo line came from HBM again: 25 GB fetched per launch for 8.2 GB of X
+  // (profiles/r04x_pmc.json)
   const int nbk = (int)gridDim.x / ncg;
-  const int bki = (int)blockIdx.x % nbk, cgi = (int)blockIdx.x / nbk;
+  int bki, cgi;
+  {
+    const int id = (int)blockIdx.x;
+    const int nb8 = nbk & ~7, head = nb8 * ncg;  // row blocks in whole groups of eight
+    if (id < head) {
+      const int x = id & 7, kk = id >> 3;
+      const int sweep = kk / ncg;  // this XCD's sweep-th row block
+      bki = 8 * sweep + x;
+      cgi = kk - sweep * ncg;
+    } else {  // the last nbk mod 8 row blocks: row blocks fastest
+      const int r = id - head, nt = nbk - nb8;
+      bki = nb8 + r % nt;
+      cgi = r / nt;
+    }
+  }
   const int gbk = bki + cb0;
   const int chunk = gbk / q.nblk, b = gbk - chunk * q.nblk;
   const int tid = threadIdx.x;
@@ -983,13 +1001,24 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restri
   f32x4 v[16];
   float srl[2], mrl[2];  // the SNV (s_r, m_r) of rows 2cq, 2cq + 1 (row j's come from lane j / 2 of the slice)
   const int cl0 = min(c0, p - 4);
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int64_t g = rb + j;
+  // contiguous rows: one buffer descriptor over the block's valid rows and
+  // 32-bit row offsets (16 row pointers of 64 bits spilled registers);
+  // rows past r1 read as 0 (their outputs are dropped below)
+  const int64_t rblk = r0 + (int64_t)b * Q8BLK;
+  constexpr bool bufd = !GATHER;  // prep_fused_gram: Q8BLK·ldx·4 < 2³¹
+  const int64_t nvalid = max((int64_t)0, min(r1 - rblk, (int64_t)Q8BLK));
+  const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(X + (bufd ? rblk * ldx : 0)), 0, bufd ? (uint32_t)(nvalid * ldx * 4) : 0u, 0x00020000);
+  auto load_q = [&](int jr, int col) -> f32x4 {  // the quad at column col of slice row jr
+    if constexpr (bufd)
+      return __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_x, (int)(((16 * rs + jr) * ldx + col) * 4), 0, 0));
+    const int64_t g = rb + jr;
     const int64_t gc = g < r1 ? g : r1 - 1;  // clamped: always a valid row
-    const int64_t xi = GATHER ? rows[gc] : gc;
-    v[j] = *reinterpret_cast<const f32x4*>(X + xi * ldx + cl0);
-  }
+    return *reinterpret_cast<const f32x4*>(X + (GATHER ? rows[gc] : gc) * ldx + col);
+  };
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = load_q(j, cl0);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int64_t g = rb + 2 * cq + u;
@@ -1001,19 +1030,15 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restri
   if constexpr (HQ > 0) {
     f32x4 hq[2][2][HQ];  // [row cq, cq + 8][left / right][quad]
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t g = rb + cq + 8 * u;
-      const int64_t gc = g < r1 ? g : r1 - 1;
-      const float* xr = X + (GATHER ? rows[gc] : gc) * ldx;
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int side = 0; side < 2; ++side)
 #pragma unroll
         for (int i = 0; i < HQ; ++i) {
           const int col = side == 0 ? cg0 - 4 * HQ + 4 * i : cg0 + Q8QC + 4 * i;
-          const f32x4 t4 = *reinterpret_cast<const f32x4*>(xr + min(max(col, 0), p - 4));
+          const f32x4 t4 = load_q(cq + 8 * u, min(max(col, 0), p - 4));
           hq[u][side][i] = col >= 0 && col < p ? t4 : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-    }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -2689,6 +2714,7 @@ int gram_materialised(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* 
 bool prep_fused_gram(const float* X, int64_t ldx, int32_t p, int32_t mode, const PrepArgs& pa) {
   return (mode == OCM_GRAM_I8X3) && p > SMALL_P && p % 4 == 0 && ldx % 4 == 0 &&
          (reinterpret_cast<uintptr_t>(X) & 15) == 0 && pa.fused_form() && p >= pa.w + 8 &&
+         (int64_t)Q8BLK * ldx * 4 < (1LL << 31) &&
          // the right edge rows' samples inside the last column group's row image
          (pa.h < 7 || p % Q8QC != 4);
 }
