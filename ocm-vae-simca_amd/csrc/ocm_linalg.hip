@@ -1402,16 +1402,24 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   int rc = orth(T1, V, 1, 1);  // a Gaussian block is well conditioned: one pass
   if (rc) return rc;
 
-  // The first iterations are plain orthogonal iterations V ← orth(C V): the
-  // subspace converges at the same rate without the Rayleigh–Ritz step, and a
-  // 32×32 Jacobi on an unconverged projection costs many sweeps (11, 5, 3 …
-  // on the bench data) plus a host read of the residuals.  Rayleigh–Ritz and
-  // the convergence test start at iteration PLAIN + 1.  The subspace after
-  // iteration i is span(Cⁱ V₀) whatever rotations happen in between, so the
-  // spectra that converge at iteration 5 (the bench data, p = 2048, k = 20)
-  // need one Rayleigh–Ritz step at PLAIN = 4 instead of two at 3.
+  // Iterations are plain orthogonal iterations V ← orth(C V) except at the
+  // Rayleigh–Ritz steps, which are the only ones that can test convergence:
+  // the subspace after iteration i is span(Cⁱ V₀) whatever rotations happen in
+  // between, so Rayleigh–Ritz only has to run where the test can pass.  A
+  // Rayleigh–Ritz step costs ~5 plain iterations (a 32×32 Jacobi on the
+  // projection, two rotations, the residuals and a host read of them), so the
+  // next one is scheduled where the residual is predicted to reach the
+  // tolerance: the max residual (that of Ritz pair k) shrinks by λ_{b+1}/λ_k
+  // per iteration, estimated by θ_b/θ_k (θ_b ≤ λ_b) and, from the second test
+  // on, by the measured decay since the last one, whichever is slower.  A
+  // short prediction costs one more test, a long one a few plain iterations
+  // past convergence; the stopping rule itself is unchanged.  The first test
+  // comes at iteration PLAIN + 1: the spectra of the bench data (p = 2048,
+  // k = 20) converge at iteration 5, the derivative spectra of the nuts
+  // preprocessing (simca_nuts.py:47-52) at ~33.
   constexpr int PLAIN = 4;
-  int it = 0;
+  int it = 0, next_rr = std::min(PLAIN + 1, max_iter), prev_it = 0;
+  double prev_rmax = 0.0;
   bool converged = false;
   for (it = 1; it <= max_iter; ++it) {
     if (!wide && b == 32) {  // W = C V
@@ -1421,11 +1429,12 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
       rc = dgemm(C, p, V, b, W, b, p, b, p, ksplit, planes, st);
       if (rc) return rc;
     }
-    if (it <= PLAIN && it < max_iter) {
+    if (it < next_rr) {
       // W is not needed again (recomputed next iteration).  One CholQR pass
-      // keeps span(W) exactly; the basis that feeds Rayleigh–Ritz (the last
-      // plain iteration) gets the second pass for orthonormality to rounding.
-      rc = orth(W, V, 500 + it, it == PLAIN ? 2 : 1);
+      // keeps span(W) exactly; the basis that feeds Rayleigh–Ritz (the
+      // iteration before a test) gets the second pass for orthonormality to
+      // rounding.
+      rc = orth(W, V, 500 + it, it == next_rr - 1 ? 2 : 1);
       if (rc) return rc;
       continue;
     }
@@ -1446,17 +1455,28 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     hipLaunchKernelGGL(k_ritz_residual, dim3(k), dim3(256), 0, st, W, V, theta, p, b, res);
     OCM_CHECK_LAUNCH("k_ritz_residual");
     OCM_HIP(hipMemcpyAsync(hres, res, k * sizeof(double), hipMemcpyDeviceToHost, st));
-    OCM_HIP(hipMemcpyAsync(hres + b, theta, sizeof(double), hipMemcpyDeviceToHost, st));
+    OCM_HIP(hipMemcpyAsync(hres + b, theta, b * sizeof(double), hipMemcpyDeviceToHost, st));
     OCM_HIP(hipStreamSynchronize(st));
     double rmax = 0.0;
     for (int i = 0; i < k; ++i) rmax = std::max(rmax, hres[i]);
     const double scale = std::fabs(hres[b]);
     if (!(rmax == rmax)) return ocm::fail(OCM_ERR_ARG, "ocm_eig_topk: NaN in covariance");
-    if (rmax <= tol * (scale > 0 ? scale : 1.0)) {
+    const double target = tol * (scale > 0 ? scale : 1.0);
+    if (rmax <= target) {
       converged = true;
       break;
     }
     if (it == max_iter) break;  // keep V, W, theta consistent for the outputs
+    // predicted iterations to the tolerance (at least one, at most 64 untested)
+    const double tk = std::fabs(hres[b + k - 1]);
+    double rate = tk > 0 ? std::fabs(hres[2 * b - 1]) / tk : 1.0;
+    if (prev_it > 0 && prev_rmax > 0) rate = std::max(rate, std::pow(rmax / prev_rmax, 1.0 / (it - prev_it)));
+    int ahead = 1;
+    if (rate < 0.999) ahead = (int)std::ceil(std::log(target / rmax) / std::log(std::max(rate, 1e-3)));
+    ahead = std::max(1, std::min(ahead, 64));
+    next_rr = std::min(it + ahead, max_iter);
+    prev_it = it;
+    prev_rmax = rmax;
     // next basis: orth(C · Ritz vectors)
     OCM_HIP(hipMemcpyAsync(T1, W, pb * sizeof(double), hipMemcpyDeviceToDevice, st));
     rc = orth(T1, V, 1000 + it, 2);
