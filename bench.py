@@ -503,7 +503,7 @@ def main():
         peak_basis = "FP32 MFMA dense peak; achieved counts algorithmic flops n*p*(p+1) (symmetric Gram)"
     # HBM bytes per launch from this round's PMC passes (scripts/pmc_passes.sh →
     # scripts/pmc_latest.py → profiles/pmc_gram_latest.json; FETCH_SIZE doubled)
-    traffic, traffic_src, score_traffic = None, None, None
+    traffic, traffic_src, score_traffic, score_src = None, None, None, None
     pmc = os.path.join(REPO, "profiles", "pmc_gram_latest.json")
     if os.path.exists(pmc) and n == 1_000_000:
         try:
@@ -511,6 +511,7 @@ def main():
             traffic = lat.get(gram_kernel, {}).get("hbm_bytes_per_launch")
             traffic_src = lat.get(gram_kernel, {}).get("source")
             score_traffic = lat.get("k_score_1p", {}).get("hbm_bytes_per_launch")
+            score_src = lat.get("k_score_1p", {}).get("source")
         except Exception:
             traffic = None
 
@@ -554,7 +555,8 @@ def main():
         "score_kernel": {"kernel": "k_score_1p (fused projection/Q/T2/decision, one HBM pass; row tile kept in registers)", "bound": "hbm",
                          "achieved_GBs": round(score_gbs, 1), "peak_GBs": HBM_PEAK_GBS,
                          "frac": round(score_gbs / HBM_PEAK_GBS, 4), "avg_launch_ms": round(score_avg_s * 1e3, 4),
-                         "launches": score_n, "bytes_per_launch": n * p * 4, "traffic": score_traffic},
+                         "launches": score_n, "bytes_per_launch": n * p * 4, "traffic": score_traffic,
+                         "traffic_source": score_src},
         "checks": {"accept_rate": round(head["accepted"] / max(n, 1), 4),
                    "eig_iters": head["eig_iters"], "T2_limit": head["T2_limit"], "Q_limit": head["Q_limit"],
                    "gram_guard_marks": head["marks"]},
