@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCM_ABI_VERSION 8
+#define OCM_ABI_VERSION 9
 
 #define OCM_OK 0
 #define OCM_ERR_ARG (-1)         /* invalid argument (maps to ValueError) */
@@ -183,6 +183,12 @@ int ocm_cov_from_packed(ocm_ctx* ctx, const double* packed, int32_t p, double* C
  * fp64 matrix, d ≤ 64 (np.linalg.pinv(np.cov(...)) at utils/SIMCA.py:69,
  * VAE_SIMCA.py:247-248, utils/final_vaesimca.py:430-434).  [dev] in/out. */
 int ocm_sym_pinv_f64(ocm_ctx* ctx, const double* A, int32_t d, double rcond, double* out, void* stream);
+
+/* diag(pinv(cov(T))) on the eigenbasis, cov(T) = diag(λ): out_i = 1/λ_i
+ * where |λ_i| > rcond·max|λ|, else 0 (np.linalg.pinv's cutoff, rcond 1e-15,
+ * utils/SIMCA.py:69).  One launch in place of the host-issued elementwise
+ * ops of the fit.  [dev] evals / out (k doubles, may alias).  ABI 9. */
+int ocm_inv_evals_f64(ocm_ctx* ctx, const double* evals, int32_t k, double rcond, double* out, void* stream);
 
 /* Fused scoring of float32 spectra (utils/SIMCA.py:65-71 fit, 104-107
  * transform, 127-130 predict):  y = x - mu; t = P·y (k); Q = ‖y − Pᵀt‖²;

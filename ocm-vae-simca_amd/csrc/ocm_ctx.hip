@@ -17,24 +17,30 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
-void* workspace(ocm_ctx* ctx, size_t bytes, hipStream_t stream) {
+static void* grow(void*& buf, size_t& have, size_t bytes, hipStream_t stream) {
   bytes = align_up(bytes, 1 << 20);
-  if (bytes <= ctx->ws_bytes) return ctx->ws;
-  if (ctx->ws) {
+  if (bytes <= have) return buf;
+  if (buf) {
     // Work queued on this stream may still read the old buffer.
     (void)hipStreamSynchronize(stream);
-    (void)hipFree(ctx->ws);
-    ctx->ws = nullptr;
-    ctx->ws_bytes = 0;
+    (void)hipFree(buf);
+    buf = nullptr;
+    have = 0;
   }
   void* p = nullptr;
   if (hipMalloc(&p, bytes) != hipSuccess) {
     set_error("workspace hipMalloc failed (" + std::to_string(bytes) + " bytes)");
     return nullptr;
   }
-  ctx->ws = p;
-  ctx->ws_bytes = bytes;
+  buf = p;
+  have = bytes;
   return p;
+}
+
+void* workspace(ocm_ctx* ctx, size_t bytes, hipStream_t stream) { return grow(ctx->ws, ctx->ws_bytes, bytes, stream); }
+
+void* workspace_aux(ocm_ctx* ctx, size_t bytes, hipStream_t stream) {
+  return grow(ctx->ws_aux, ctx->ws_aux_bytes, bytes, stream);
 }
 
 void* host_staging(ocm_ctx* ctx, size_t bytes) {
@@ -80,6 +86,7 @@ int ocm_ctx_create(int device, ocm_ctx** out) {
 int ocm_ctx_destroy(ocm_ctx* ctx) {
   if (!ctx) return OCM_OK;
   if (ctx->ws) (void)hipFree(ctx->ws);
+  if (ctx->ws_aux) (void)hipFree(ctx->ws_aux);
   if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   for (auto e : ctx->fork_ev) (void)hipEventDestroy(e);

@@ -485,10 +485,15 @@ __global__ void k_colsum_part(const float* __restrict__ X, int64_t ldx, const in
   const int64_t a = (int64_t)sp * rows_per_split;
   const int64_t e = min(n, a + rows_per_split);
   double v = 0.0;
-  for (int64_t r = a; r < e; ++r) {
-    const int64_t sr = rows ? rows[r] : r;
-    v += (double)load_y(X, ldx, sr, col, p, pa);
+  int64_t r = a;
+  for (; r + 8 <= e; r += 8) {  // eight loads in flight, summed in row order
+    float y[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) y[u] = load_y(X, ldx, rows ? rows[r + u] : r + u, col, p, pa);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += (double)y[u];
   }
+  for (; r < e; ++r) v += (double)load_y(X, ldx, rows ? rows[r] : r, col, p, pa);
   part[(size_t)sp * p + col] = v;
 }
 
@@ -497,7 +502,15 @@ __global__ void k_colsum_final(const double* __restrict__ part, int nsplit, int 
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
   if (col >= p) return;
   double v = 0.0;
-  for (int s = 0; s < nsplit; ++s) v += part[(size_t)s * p + col];
+  int s = 0;
+  for (; s + 8 <= nsplit; s += 8) {  // eight loads in flight, summed in split order
+    double y[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) y[u] = part[(size_t)(s + u) * p + col];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += y[u];
+  }
+  for (; s < nsplit; ++s) v += part[(size_t)s * p + col];
   mean[col] = v * inv_n;
 }
 
@@ -1190,23 +1203,37 @@ __global__ __launch_bounds__(256) void k_colexp_hist(const float* __restrict__ X
 
 // thr_j = τ·max(2^e_j, 2⁻⁸·max_k 2^e_k), e_j the median exponent bin of
 // column j (padded columns: +inf).  The floor keeps near-constant sample
-// columns from marking every later row.  One workgroup of 1024 threads.
-__global__ __launch_bounds__(1024) void k_q8_thresholds(const uint32_t* __restrict__ hist, int64_t nsamp, int p,
-                                                        int P8, float* __restrict__ thr) {
+// columns from marking every later row.  First the median bins, one wave per
+// column (lane L holds bins 2L, 2L + 1; a wave prefix sum finds the first bin
+// whose cumulative count reaches half the sample — a thread walking its
+// column's bins one dependent load at a time took 63 µs), then the floor and
+// the padding in one workgroup.
+__global__ __launch_bounds__(256) void k_q8_colmed(const uint32_t* __restrict__ hist, int64_t nsamp, int p,
+                                                   float* __restrict__ thr) {
+  static_assert(QX_BINS == 128, "two bins per lane");
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= p) return;  // whole waves
+  const uint32_t half = (uint32_t)((nsamp + 1) / 2);
+  const uint32_t h0 = hist[(size_t)c * QX_BINS + 2 * lane], h1 = hist[(size_t)c * QX_BINS + 2 * lane + 1];
+  uint32_t inc = h0 + h1;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  const uint32_t pre = inc - h0 - h1;
+  const uint64_t hit = __ballot(inc >= half);
+  const int L = hit ? __builtin_ctzll(hit) : 63;
+  const uint32_t preL = __shfl(pre, L, 64), h0L = __shfl(h0, L, 64);
+  const int bin = hit ? (preL + h0L >= half ? 2 * L : 2 * L + 1) : QX_BINS - 1;
+  if (lane == 0) thr[c] = bin == 0 ? 0.f : ldexpf(1.f, bin + QX_EMIN);  // provisional
+}
+
+__global__ __launch_bounds__(1024) void k_q8_thresholds(int p, int P8, float* __restrict__ thr) {
   __shared__ float red[16];
   float mx = 0.f;
-  const uint32_t half = (uint32_t)((nsamp + 1) / 2);
-  for (int c = threadIdx.x; c < p; c += 1024) {
-    uint32_t acc = 0;
-    int bin = 0;
-    for (; bin < QX_BINS - 1; ++bin) {
-      acc += hist[(size_t)c * QX_BINS + bin];
-      if (acc >= half) break;
-    }
-    const float sc = bin == 0 ? 0.f : ldexpf(1.f, bin + QX_EMIN);
-    thr[c] = sc;  // provisional
-    mx = fmaxf(mx, sc);
-  }
+  for (int c = threadIdx.x; c < p; c += 1024) mx = fmaxf(mx, thr[c]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
@@ -1215,7 +1242,6 @@ __global__ __launch_bounds__(1024) void k_q8_thresholds(const uint32_t* __restri
 #pragma unroll
   for (int w = 0; w < 16; ++w) gmax = fmaxf(gmax, red[w]);
   const float floor_ = gmax * (1.f / 256.f);
-  __syncthreads();
   for (int c = threadIdx.x; c < P8; c += 1024)
     thr[c] = c < p ? Q8TAU * fmaxf(thr[c], floor_) : __builtin_inff();
 }
@@ -2445,7 +2471,8 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     OCM_HIP(hipMemsetAsync(xhist, 0, (size_t)p * QX_BINS * 4, st));
     hipLaunchKernelGGL(k_colexp_hist, dim3((p + 63) / 64, nsplit), dim3(256), 0, st, X, ldx, rows, nsamp, p, shift,
                        rps, xhist, pa);
-    hipLaunchKernelGGL(k_q8_thresholds, dim3(1), dim3(1024), 0, st, xhist, nsamp, p, P8, thr);
+    hipLaunchKernelGGL(k_q8_colmed, dim3((p + 3) / 4), dim3(256), 0, st, xhist, nsamp, p, thr);
+    hipLaunchKernelGGL(k_q8_thresholds, dim3(1), dim3(1024), 0, st, p, P8, thr);
     OCM_CHECK_LAUNCH("k_q8_thresholds");
   }
 

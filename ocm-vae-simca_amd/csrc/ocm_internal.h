@@ -15,6 +15,8 @@ struct ocm_ctx {
   int device = 0;
   void* ws = nullptr;  // device workspace, grows on demand (ocm_ctx_reserve pre-sizes it)
   size_t ws_bytes = 0;
+  void* ws_aux = nullptr;  // second grow-only arena for buffers that live across a call that takes `ws`
+  size_t ws_aux_bytes = 0;
   void* host_pinned = nullptr;  // small pinned staging area for D2H scalars
   size_t host_bytes = 0;
   int num_cus = 256;
@@ -62,6 +64,7 @@ int fail(int code, const std::string& msg);
 // growing it to at least `bytes` (all outstanding work on `stream` is drained
 // before a re-allocation).
 void* workspace(ocm_ctx* ctx, size_t bytes, hipStream_t stream);
+void* workspace_aux(ocm_ctx* ctx, size_t bytes, hipStream_t stream);
 void* host_staging(ocm_ctx* ctx, size_t bytes);
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }

@@ -1248,6 +1248,25 @@ __global__ void k_add3(const double* __restrict__ a, const double* __restrict__ 
   if (threadIdx.x == 0) *out = *a + *b;
 }
 
+// 1/λ with np.linalg.pinv's cutoff (|λ| ≤ rcond·max|λ| → 0); one workgroup,
+// every thread reads all k values (k is the component count: ≤ p, small)
+__global__ __launch_bounds__(256) void k_inv_evals(const double* __restrict__ ev, int k, double rcond,
+                                                   double* __restrict__ out) {
+  __shared__ double red[4];
+  double mx = 0.0;
+  for (int i = threadIdx.x; i < k; i += 256) mx = fmax(mx, fabs(ev[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  const double cut = rcond * fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  __syncthreads();  // out may alias ev: every read of ev is done
+  for (int i = threadIdx.x; i < k; i += 256) {
+    const double l = ev[i];
+    out[i] = fabs(l) > cut ? 1.0 / l : 0.0;
+  }
+}
+
 int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
                   int32_t theta_mode, int32_t slice, int32_t nslices, double* evals_out, double* evecs_out,
                   double* theta_out, int32_t* iters_out, hipStream_t st) {
@@ -1512,16 +1531,20 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     OCM_HIP(hipMemcpyAsync(theta_out, tr2, 2 * sizeof(double), hipMemcpyDeviceToDevice, st));
     // θ3: this slice's rows of the Δ / O expansion (k_theta3_diag), then the
     // i8×3 Gram of those rows of O.  The Gram takes the context workspace, so
-    // O (f32), its Gram and the partials live in stream-ordered allocations and
-    // everything the eigensolver's carve-outs feed is already in the outputs.
+    // O (f32), its Gram and the partials live in the context's second arena
+    // (two hipMallocAsync calls here cost ≈ 50 µs of host time, with the GPU
+    // idle behind them) and everything the eigensolver's carve-outs feed is
+    // already in the outputs.
     const int r0 = (int)((int64_t)p * slice / nslices), r1 = (int)((int64_t)p * (slice + 1) / nslices);
     if (theta_mode >= 2 && r1 > r0) {
       const int nr = r1 - r0;
-      float* O32 = nullptr;
-      double* Gp = nullptr;
       const size_t pp = (size_t)p * p;
-      OCM_HIP(hipMallocAsync(reinterpret_cast<void**>(&O32), pp * sizeof(float), st));
-      OCM_HIP(hipMallocAsync(reinterpret_cast<void**>(&Gp), (pp + 3 * (size_t)p + 8) * sizeof(double), st));
+      const size_t o32_bytes = (pp * sizeof(float) + 255) / 256 * 256;
+      char* aux = static_cast<char*>(
+          ocm::workspace_aux(ctx, o32_bytes + (pp + 3 * (size_t)p + 8) * sizeof(double), st));
+      if (!aux) return OCM_ERR_NOMEM;
+      float* O32 = reinterpret_cast<float*>(aux);
+      double* Gp = reinterpret_cast<double*>(aux + o32_bytes);
       double* csum = Gp + pp;
       double* dpart3 = csum + p;  // p row partials of the Δ terms
       double* opart = dpart3 + p;  // p row partials of the O·O² term
@@ -1540,9 +1563,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
         hipLaunchKernelGGL(k_add3, dim3(1), dim3(64), 0, st, t3, t3 + 1, theta_out + 2);
         OCM_CHECK_LAUNCH("k_trace_og");
       }
-      const hipError_t e1 = hipFreeAsync(O32, st), e2 = hipFreeAsync(Gp, st);
       if (rc) return rc;
-      if (e1 != hipSuccess || e2 != hipSuccess) return ocm::fail(OCM_ERR_HIP, "hipFreeAsync (theta3)");
     } else {
       OCM_HIP(hipMemsetAsync(theta_out + 2, 0, sizeof(double), st));
     }
@@ -1574,6 +1595,14 @@ int ocm_eig_topk_ex(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double 
               "ocm_eig_topk_ex: need 0 <= theta3_slice < theta3_nslices");
   return eig_topk_impl(ctx, C, p, k, tol, max_iter, theta_mode, theta3_slice, theta3_nslices, evals_out, evecs_out,
                        theta_out, iters_out, (hipStream_t)stream);
+}
+
+int ocm_inv_evals_f64(ocm_ctx* ctx, const double* evals, int32_t k, double rcond, double* out, void* stream) {
+  OCM_REQUIRE(ctx && evals && out, "ocm_inv_evals_f64: NULL argument");
+  OCM_REQUIRE(k >= 1, "ocm_inv_evals_f64: k >= 1");
+  hipLaunchKernelGGL(k_inv_evals, dim3(1), dim3(256), 0, (hipStream_t)stream, evals, k, rcond, out);
+  OCM_CHECK_LAUNCH("k_inv_evals");
+  return OCM_OK;
 }
 
 int ocm_sym_pinv_f64(ocm_ctx* ctx, const double* A, int32_t d, double rcond, double* out, void* stream) {

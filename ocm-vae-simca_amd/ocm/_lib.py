@@ -82,6 +82,7 @@ SIGNATURES = {
     "ocm_gram_pack": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_i32, c_void_p, c_void_p]),
     "ocm_cov_from_packed": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p]),
     "ocm_sym_pinv_f64": (c_i32, [c_void_p, c_void_p, c_i32, c_f64, c_void_p, c_void_p]),
+    "ocm_inv_evals_f64": (c_i32, [c_void_p, c_void_p, c_i32, c_f64, c_void_p, c_void_p]),
     "ocm_score_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_void_p,
                               c_i32, c_void_p, c_void_p, c_void_p, ctypes.POINTER(OcmDecision), c_void_p, c_i64,
                               c_void_p, c_void_p]),
@@ -155,7 +156,7 @@ SIGNATURES = {
                                         ctypes.POINTER(OcmDecision), c_void_p, c_i64, c_void_p, c_void_p]),
 }
 
-ABI_VERSION = 8  # include/ocm.h OCM_ABI_VERSION
+ABI_VERSION = 9  # include/ocm.h OCM_ABI_VERSION
 
 _lib = None
 _lib_lock = threading.Lock()

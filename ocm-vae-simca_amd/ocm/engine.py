@@ -84,7 +84,7 @@ class ClassFit:
     mean64: torch.Tensor
     evals: torch.Tensor          # (k,) f64
     P64: torch.Tensor            # (k, p) f64, svd_flip sign convention (scoring operand)
-    invcov: torch.Tensor         # (k, k) f64 = pinv(cov(T)) = diag(1/λ)
+    invcov: torch.Tensor | None = None  # (k, k) f64 = pinv(cov(T)) = diag(1/λ); built on first use (invcov_mat)
     inv_diag: torch.Tensor = None  # (k,) f64: its diagonal (the scoring kernels' operand)
     thetas: tuple = (0.0, 0.0, 0.0)
     evals_host: np.ndarray = None
@@ -95,6 +95,11 @@ class ClassFit:
     eig_iters: int = 0
     C: torch.Tensor | None = None
     extra: dict = field(default_factory=dict)
+
+    def invcov_mat(self) -> torch.Tensor:
+        if self.invcov is None:
+            self.invcov = torch.diag(self.inv_diag)
+        return self.invcov
 
     def _stats(self) -> np.ndarray:
         # read on first use only: nothing on the Fdist / jm path waits for the
@@ -465,9 +470,11 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
 def inv_evals(evals: torch.Tensor, rcond=1e-15) -> torch.Tensor:
     """Diagonal of pinv(cov(T)) for T = centred scores on the eigenbasis:
     cov(T) = diag(λ) (utils/SIMCA.py:69 with np.linalg.pinv's rcond=1e-15 cutoff)."""
-    lam = evals.to(torch.float64)
-    cut = rcond * lam.abs().max()
-    return torch.where(lam.abs() > cut, 1.0 / lam, torch.zeros_like(lam))
+    lam = evals.to(torch.float64).contiguous()
+    out = torch.empty_like(lam)
+    check(_lib.load().ocm_inv_evals_f64(Context.get(lam.device.index).handle, ptr(lam), lam.numel(), float(rcond),
+                                        ptr(out), _stream(lam.device)), "ocm_inv_evals_f64")
+    return out
 
 
 def invcov_from_evals(evals: torch.Tensor, rcond=1e-15) -> torch.Tensor:
@@ -617,7 +624,7 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
     stats = sc["stats"]
     if allreduce is not None and need_stats:
         allreduce([stats])  # stream-ordered: no host wait
-    fit = ClassFit(k=k, n=n_total, p=p, mean64=mean64, evals=evals, P64=evecs, invcov=torch.diag(inv), inv_diag=inv, thetas=th,
+    fit = ClassFit(k=k, n=n_total, p=p, mean64=mean64, evals=evals, P64=evecs, inv_diag=inv, thetas=th,
                    evals_host=ev_h, T=sc["T"], T2=sc["T2"], Q=sc["Q"], stats_dev=stats, eig_iters=iters,
                    C=C if keep_C else None)
     fit.extra["shift32"] = shift32

@@ -7,11 +7,26 @@ overwritten per class; unknown limit names leave the result unbound).
 """
 from __future__ import annotations
 
+import functools
 import math
 
 import numpy as np
 from scipy import stats
 from scipy.special import erfinv
+
+
+# The quantiles are pure functions of (level, degrees of freedom); SciPy's
+# rv_continuous.ppf costs ≈ 140 µs of argument handling per call, the whole
+# host side of a refit at 125k rows, so repeated fits with the same (n, k,
+# level) look them up.  Results are SciPy's own, bit for bit.
+@functools.lru_cache(maxsize=4096)
+def _f_ppf(q: float, dfn: float, dfd: float) -> float:
+    return stats.f.ppf(q, dfn, dfd)
+
+
+@functools.lru_cache(maxsize=4096)
+def _chi2_ppf(q: float, df: float) -> float:
+    return stats.chi2.ppf(q, df)
 
 
 class Moments:
@@ -63,20 +78,20 @@ def t2_limit(est, T2: Moments, k: int) -> float:
     if est.t2lim == "perc":
         return T2.percentile(est.t2cl * 100)
     if est.t2lim == "Fdistrig":
-        F = stats.f.ppf(est.t2cl, k, n - k)
+        F = _f_ppf(est.t2cl, k, n - k)
         return (k / n) * (n ** 2 - 1) / (n - k) * F
     if est.t2lim == "Fdist":
-        F = stats.f.ppf(est.t2cl, k, n - k)
+        F = _f_ppf(est.t2cl, k, n - k)
         return k * (n - 1) / (n - k) * F
     if est.t2lim == "chi2":
-        return stats.chi2.ppf(est.t2cl, k)
+        return _chi2_ppf(est.t2cl, k)
     if est.t2lim == "chi2pom":
         h0 = float(T2.mean)
         v = float(T2.var(ddof=1)) if n > 1 else 0.0
         Nh = max(int(np.round(2 * (h0 ** 2) / v)) if v > 0 else 1, 1)
         est._t2dof = Nh
         est._t2scfact = h0
-        return h0 * stats.chi2.ppf(est.t2cl, Nh) / Nh
+        return h0 * _chi2_ppf(est.t2cl, Nh) / Nh
     raise UnboundLocalError(f"local variable 'T2_limit' referenced before assignment (t2lim={est.t2lim!r})")
 
 
@@ -100,13 +115,13 @@ def q_limit(est, Q: Moments, thetas) -> float:
         Ng = (th1 ** 2) / th2
         print("here we are")  # reference prints these (utils/SIMCA.py:207-208)
         print(th1, th2, g, Ng)
-        return g * stats.chi2.ppf(est.qcl, Ng)
+        return g * _chi2_ppf(est.qcl, Ng)
     if est.qlim == "chi2pom":
         v0 = np.float64(Q.mean)
         Nv = max(round(2 * (v0 ** 2) / np.float64(Q.var(ddof=1))), 1)
         est._qdof = Nv
         est._qscfact = float(v0)
-        return float(v0 * stats.chi2.ppf(est.qcl, Nv) / Nv)
+        return float(v0 * _chi2_ppf(est.qcl, Nv) / Nv)
     raise UnboundLocalError(f"local variable 'Q_limit' referenced before assignment (qlim={est.qlim!r})")
 
 
@@ -122,9 +137,9 @@ def critic_distance(est, T2_limit, Q_limit, thetas, k: int):
         tr2 = (k / T2_limit ** 2) + (th2 / Q_limit ** 2)
         gd = tr2 / tr1
         hd = tr1 ** 2 / tr2
-        return gd * stats.chi2.ppf(est.dcl, hd)
+        return gd * _chi2_ppf(est.dcl, hd)
     if est.type == "dd":
-        return stats.chi2.ppf(est.dcl, est._t2dof + est._qdof)
+        return _chi2_ppf(est.dcl, est._t2dof + est._qdof)
     raise UnboundLocalError(f"local variable 'dlim' referenced before assignment (type={est.type!r})")
 
 

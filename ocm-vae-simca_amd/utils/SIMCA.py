@@ -212,7 +212,7 @@ class SIMCA(BaseEstimator, ClassifierMixin):
             "pca_model": EnginePCA(fit, dt),
             "n_components": k,
             "xmean": _Lazy(lambda: _np(fit.mean64, dt)),
-            "invcovT": _Lazy(lambda: _np(fit.invcov)),
+            "invcovT": _Lazy(lambda: _np(fit.invcov_mat())),
             "eigs_all": _Lazy(lambda: _all_eigs(fit, n)),
             "T": _Lazy(lambda: _np(fit.T, dt)),
             "P": _Lazy(lambda: _np(fit.P64, dt)),

@@ -239,6 +239,9 @@ class _Fit:
         self.__dict__.update(kw)
         self.extra = {}
 
+    def invcov_mat(self):
+        return self.invcov
+
 
 def invcov_from_evals(evals, rcond=1e-15):
     lam = evals.to(torch.float64)
