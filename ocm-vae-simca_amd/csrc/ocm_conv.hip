@@ -234,6 +234,189 @@ __global__ __launch_bounds__(CV_T) void k_conv_wgrad(const TP* __restrict__ P, i
   }
 }
 
+// wgrad on the matrix cores (bf16 activations, the autocast training step):
+// G[o][c] = Σ_pos P[o][pos] · Qc[pos] is a (O × ncol) GEMM over B·Lp positions,
+// columns c = i·K + t (Qc[pos] = Q[b][i][l·s + t − pad], zero outside the row)
+// plus, with WB, a column of ones whose sum is the bias gradient.  One
+// v_mfma_f32_16x16x32_bf16 per 32 positions and 16 columns: A = P (16 channel
+// rows × 32 positions, one 16-B load per lane), B = the Q windows, built from
+// an LDS copy of the chunk's Q rows (all input channels, one wide load per 8
+// values).  A workgroup takes chunks of WM_CH positions of one row b, loading
+// the next chunk into registers while the MFMAs of this one run; products are
+// exact in f32, and every WM_FL chunks the MFMA accumulators (16 products
+// deep) are added into f32 running sums on the VALU (the bf16 MFMA truncates
+// its internal sum).  The workgroups' partials are summed in a fixed order by
+// the last workgroup of each 16 and then by the last of those (deterministic).
+// The VALU kernel above gave each (input channel, 4 outputs) group its own
+// pass over the positions: the C4 layers took 34–39 µs per call for a few MB.
+using bf16x8 = __attribute__((ext_vector_type(8))) short;
+constexpr int WM_CH = 256, WM_NT = 6, WM_IMAX = 12, WM_OMAX = 16, WM_FL = 8, WM_WG = 256;
+constexpr int WM_NOUT = WM_OMAX * WM_NT * 16;  // partial floats per workgroup, at most
+template <int S>
+__host__ __device__ constexpr int wm_qwp() {  // LDS row of one input channel (bf16 values): window + alignment slack
+  return ((7 + (WM_CH - 1) * S + CV_KMAX + 7) / 8) * 8;
+}
+
+template <bool WB, int S>
+__global__ __launch_bounds__(256) void k_conv_wgrad_mfma(const bf16_t* __restrict__ P, int O, int Lp,
+                                                         const bf16_t* __restrict__ Q, int I, int Lq, int B, int K,
+                                                         int pad, float* __restrict__ part,
+                                                         unsigned* __restrict__ ticket, float* __restrict__ G,
+                                                         float* __restrict__ db) {
+  constexpr int QWP = wm_qwp<S>(), N8 = QWP / 8;
+  constexpr int QI = (WM_IMAX * N8 + 255) / 256;  // staged 16-B pieces per thread
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[WM_IMAX * QWP];
+  __shared__ float red[4][WM_OMAX][WM_NT * 16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = lane & 15, kg = lane >> 4;
+  const int ncol = I * K + (WB ? 1 : 0);
+  const int NT = (ncol + 15) / 16;
+  const int NOUT = O * ncol;
+  const int cpr = Lp / WM_CH, nch = B * cpr;
+  // this lane's column of each N tile: LDS offset i·QWP + t (≥ 0), ones (−2), zero (−1)
+  int cb[WM_NT];
+#pragma unroll
+  for (int nt = 0; nt < WM_NT; ++nt) {
+    const int c = 16 * nt + n;
+    cb[nt] = c < I * K ? (c / K) * QWP + c % K : (WB && c == I * K ? -2 : -1);
+  }
+  f32x4 qv[QI];
+  bf16x8 av[2];
+  auto window = [&](int ch, int& b, int& l0, int& base) __attribute__((always_inline)) {
+    b = ch / cpr;
+    l0 = (ch - b * cpr) * WM_CH;
+    const int a = l0 * S - pad;
+    base = a >= 0 ? (a & ~7) : -((7 - a) & ~7);  // ⌊a / 8⌋ · 8
+  };
+  auto load_chunk = [&](int ch) __attribute__((always_inline)) {
+    int b, l0, base;
+    window(ch, b, l0, base);
+#pragma unroll
+    for (int r = 0; r < QI; ++r) {
+      const int e = tid + 256 * r, i = e / N8, j0 = base + 8 * (e - i * N8);
+      // Lq % 8 == 0: an aligned piece lies wholly inside the row or wholly outside
+      const bool ok = e < I * N8 && j0 >= 0 && j0 + 8 <= Lq;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(Q + ((int64_t)b * I + (i < I ? i : I - 1)) * Lq + (ok ? j0 : 0));
+      qv[r] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int pos = l0 + 64 * w + 32 * ks + 8 * kg;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(P + ((int64_t)b * O + (n < O ? n : O - 1)) * Lp + pos);
+      av[ks] = __builtin_bit_cast(bf16x8, n < O ? v : f32x4{0.f, 0.f, 0.f, 0.f});
+    }
+  };
+  f32x4 acc[WM_NT], run[WM_NT];
+#pragma unroll
+  for (int nt = 0; nt < WM_NT; ++nt) acc[nt] = run[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int done = 0;
+  int ch = blockIdx.x;
+  if (ch < nch) load_chunk(ch);
+  for (; ch < nch; ch += gridDim.x) {
+    int b, l0, base;
+    window(ch, b, l0, base);
+    const int off = l0 * S - pad - base;
+    __syncthreads();  // the previous chunk's windows are read
+#pragma unroll
+    for (int r = 0; r < QI; ++r) {
+      const int e = tid + 256 * r;
+      if (e < I * N8) *reinterpret_cast<f32x4*>(&Qs[(e / N8) * QWP + 8 * (e % N8)]) = qv[r];
+    }
+    const bf16x8 a0 = av[0], a1 = av[1];
+    __syncthreads();
+    if (ch + (int)gridDim.x < nch) load_chunk(ch + gridDim.x);  // in flight under this chunk's MFMAs
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int p0 = (64 * w + 32 * ks + 8 * kg) * S + off;
+#pragma unroll
+      for (int nt = 0; nt < WM_NT; ++nt) {
+        if (nt >= NT) break;
+        const int c0 = cb[nt];
+        const int ix = c0 >= 0 ? c0 + p0 : 0;
+        const short fill = c0 == -2 ? (short)0x3F80 : (short)0;  // bf16 1.0 / 0
+        bf16x8 bf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const short v = (short)Qs[ix + j * S];
+          bf[j] = c0 >= 0 ? v : fill;
+        }
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ks ? a1 : a0, bf, acc[nt], 0, 0, 0);
+      }
+    }
+    if (++done == WM_FL) {
+      done = 0;
+#pragma unroll
+      for (int nt = 0; nt < WM_NT; ++nt) {
+        run[nt] += acc[nt];
+        acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+#pragma unroll
+  for (int nt = 0; nt < WM_NT; ++nt) run[nt] += acc[nt];
+  // D layout: column 16·nt + (lane & 15), rows 4·(lane >> 4) + r
+#pragma unroll
+  for (int nt = 0; nt < WM_NT; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][4 * kg + r][16 * nt + n] = run[nt][r];
+  __syncthreads();
+  for (int e = tid; e < NOUT; e += 256) {
+    const int o = e / ncol, c = e - o * ncol;
+    st_agent(part + (int64_t)blockIdx.x * NOUT + e, (red[0][o][c] + red[1][o][c]) + (red[2][o][c] + red[3][o][c]));
+  }
+  // the last of each 16 workgroups sums their partials, the last of those the groups'
+  constexpr int EPT = WM_NOUT / 256;
+  const int g = blockIdx.x / 16, ng = (gridDim.x + 15) / 16;
+  const int gsize = min(16, (int)gridDim.x - 16 * g);
+  float* gpart = part + (int64_t)gridDim.x * NOUT;
+  auto sum16 = [&](const float* src, int cnt, float* dst_part, bool final_) __attribute__((always_inline)) {
+    float v[EPT][16];
+#pragma unroll
+    for (int r = 0; r < EPT; ++r) {
+      const int e = tid + 256 * r, ec = e < NOUT ? e : 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[r][k] = ld_agent(src + (int64_t)(k < cnt ? k : 0) * NOUT + ec);
+    }
+#pragma unroll
+    for (int r = 0; r < EPT; ++r) {
+      const int e = tid + 256 * r;
+      float sm = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) sm += k < cnt ? v[r][k] : 0.f;
+      if (e >= NOUT) continue;
+      if (!final_) {
+        st_agent(dst_part + e, sm);
+      } else {
+        const int o = e / ncol, c = e - o * ncol;
+        if (c < I * K) G[(int64_t)o * I * K + c] = sm;
+        else db[o] = sm;
+      }
+    }
+  };
+  __shared__ bool last_;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    unsigned* sub = ticket + (1 + g) * TICKET_STRIDE;
+    const bool l = __hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)gsize - 1;
+    if (l) __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_ = l;
+  }
+  __syncthreads();
+  if (!last_) return;
+  sum16(part + (int64_t)16 * g * NOUT, gsize, gpart + (int64_t)g * NOUT, false);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const bool l = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)ng - 1;
+    if (l) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_ = l;
+  }
+  __syncthreads();
+  if (!last_) return;
+  sum16(gpart, ng, nullptr, true);
+}
+
 // per-channel sums of (B, C, L): grid (WG_SPLIT, C) partials; the channel's
 // last workgroup sums them in order (fp64)
 template <typename T>
@@ -344,6 +527,22 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
   const int want = std::min(one, std::max(four, (1024 + groups - 1) / groups));
   const int split = std::max(1, std::min({WG_MAXSPLIT, std::max(1, 8192 / groups), want}));
   const bool wb = psum_out != nullptr;
+  const int ncol = I * K + (wb ? 1 : 0);
+  if (dtype_p == OCM_DTYPE_BF16 && dtype_q == OCM_DTYPE_BF16 && O <= WM_OMAX && I <= WM_IMAX && ncol <= 16 * WM_NT &&
+      (stride == 1 || stride == 2) && Lp % WM_CH == 0 && Lq % 8 == 0 && pad <= 7 &&
+      (reinterpret_cast<uintptr_t>(P) & 15) == 0 && (reinterpret_cast<uintptr_t>(Q) & 15) == 0) {
+    // the matrix-core path (bf16): ≤ WM_WG workgroups, two-level partial sums
+    const int nch = (int)((int64_t)B * Lp / WM_CH);
+    const int nwg = std::min(WM_WG, nch);
+#define OCM_WM(WB, S)                                                                                              hipLaunchKernelGGL((k_conv_wgrad_mfma<WB, S>), dim3((unsigned)nwg), dim3(256), 0, st,                                               static_cast<const bf16_t*>(P), O, Lp, static_cast<const bf16_t*>(Q), I, Lq, B, K, pad, part,                      ticket, G_out, psum_out)
+    if (wb && stride == 1) OCM_WM(true, 1);
+    else if (wb) OCM_WM(true, 2);
+    else if (stride == 1) OCM_WM(false, 1);
+    else OCM_WM(false, 2);
+#undef OCM_WM
+    OCM_CHECK_LAUNCH("k_conv_wgrad_mfma");
+    return OCM_OK;
+  }
   dim3 g((unsigned)split, (unsigned)groups);
 #define OCM_WG_K(KT, WB, TP, TQ)                                                                            \
   hipLaunchKernelGGL((k_conv_wgrad<KT, WB, TP, TQ>), g, dim3(CV_T), 0, st, static_cast<const TP*>(P), O, Lp,   \

@@ -1416,10 +1416,13 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     return OCM_OK;
   };
 
-  hipLaunchKernelGGL(k_randn, dim3((unsigned)((pb + 255) / 256)), dim3(256), 0, st, T1, (int64_t)pb, 0x5EEDull);
+  // V₀: a Gaussian block, used as it is — the subspace after i iterations is
+  // span(Cⁱ V₀) whatever basis V₀ has, so only the Rayleigh–Ritz steps need an
+  // orthonormal basis (every iteration before one ends with CholQR2), and an
+  // orthonormalisation of V₀ costs a CholQR pass (≈ 36 µs) for nothing
+  hipLaunchKernelGGL(k_randn, dim3((unsigned)((pb + 255) / 256)), dim3(256), 0, st, V, (int64_t)pb, 0x5EEDull);
   OCM_CHECK_LAUNCH("k_randn");
-  int rc = orth(T1, V, 1, 1);  // a Gaussian block is well conditioned: one pass
-  if (rc) return rc;
+  int rc = OCM_OK;
 
   // Iterations are plain orthogonal iterations V ← orth(C V) except at the
   // Rayleigh–Ritz steps, which are the only ones that can test convergence:
@@ -1438,6 +1441,12 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   // preprocessing (simca_nuts.py:47-52) at ~33.
   constexpr int PLAIN = 4;
   int it = 0, next_rr = std::min(PLAIN + 1, max_iter), prev_it = 0;
+  if (next_rr == 1) {  // Rayleigh–Ritz on the first product: V₀ must be orthonormal
+    hipLaunchKernelGGL(k_randn, dim3((unsigned)((pb + 255) / 256)), dim3(256), 0, st, T1, (int64_t)pb, 0x5EEDull);
+    OCM_CHECK_LAUNCH("k_randn");
+    rc = orth(T1, V, 1, 2);
+    if (rc) return rc;
+  }
   double prev_rmax = 0.0;
   bool converged = false;
   for (it = 1; it <= max_iter; ++it) {
