@@ -250,15 +250,19 @@ __global__ __launch_bounds__(CV_T) void k_conv_wgrad(const TP* __restrict__ P, i
 // The VALU kernel above gave each (input channel, 4 outputs) group its own
 // pass over the positions: the C4 layers took 34–39 µs per call for a few MB.
 using bf16x8 = __attribute__((ext_vector_type(8))) short;
-constexpr int WM_CH = 256, WM_NT = 6, WM_IMAX = 12, WM_OMAX = 16, WM_FL = 8, WM_WG = 256;
-constexpr int WM_NOUT = WM_OMAX * WM_NT * 16;  // partial floats per workgroup, at most
+// ≤ WM_WG workgroups, four per CU (37.5 KB of LDS each): each loads one chunk
+// ahead, so the chunks in flight per CU — the memory-level parallelism of a
+// few-MB layer — come from the resident workgroups
+constexpr int WM_CH = 256, WM_NT = 6, WM_IMAX = 12, WM_OMAX = 16, WM_FL = 8, WM_WG = 1024;
+constexpr int WM_NOUT = 768;  // partial floats per workgroup (O · ncol), at most
+constexpr int WM_LEVELS = 3;  // 16-way partial-sum levels: 1024 → 64 → 4 → 1
 template <int S>
 __host__ __device__ constexpr int wm_qwp() {  // LDS row of one input channel (bf16 values): window + alignment slack
   return ((7 + (WM_CH - 1) * S + CV_KMAX + 7) / 8) * 8;
 }
 
-template <bool WB, int S>
-__global__ __launch_bounds__(256) void k_conv_wgrad_mfma(const bf16_t* __restrict__ P, int O, int Lp,
+template <bool WB, int S, int NTT>
+__global__ __launch_bounds__(256, 4) void k_conv_wgrad_mfma(const bf16_t* __restrict__ P, int O, int Lp,
                                                          const bf16_t* __restrict__ Q, int I, int Lq, int B, int K,
                                                          int pad, float* __restrict__ part,
                                                          unsigned* __restrict__ ticket, float* __restrict__ G,
@@ -274,9 +278,9 @@ __global__ __launch_bounds__(256) void k_conv_wgrad_mfma(const bf16_t* __restric
   const int NOUT = O * ncol;
   const int cpr = Lp / WM_CH, nch = B * cpr;
   // this lane's column of each N tile: LDS offset i·QWP + t (≥ 0), ones (−2), zero (−1)
-  int cb[WM_NT];
+  int cb[NTT];
 #pragma unroll
-  for (int nt = 0; nt < WM_NT; ++nt) {
+  for (int nt = 0; nt < NTT; ++nt) {
     const int c = 16 * nt + n;
     cb[nt] = c < I * K ? (c / K) * QWP + c % K : (WB && c == I * K ? -2 : -1);
   }
@@ -306,9 +310,9 @@ __global__ __launch_bounds__(256) void k_conv_wgrad_mfma(const bf16_t* __restric
       av[ks] = __builtin_bit_cast(bf16x8, n < O ? v : f32x4{0.f, 0.f, 0.f, 0.f});
     }
   };
-  f32x4 acc[WM_NT], run[WM_NT];
+  f32x4 acc[NTT], run[NTT];
 #pragma unroll
-  for (int nt = 0; nt < WM_NT; ++nt) acc[nt] = run[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int nt = 0; nt < NTT; ++nt) acc[nt] = run[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   int done = 0;
   int ch = blockIdx.x;
   if (ch < nch) load_chunk(ch);
@@ -329,7 +333,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad_mfma(const bf16_t* __restric
     for (int ks = 0; ks < 2; ++ks) {
       const int p0 = (64 * w + 32 * ks + 8 * kg) * S + off;
 #pragma unroll
-      for (int nt = 0; nt < WM_NT; ++nt) {
+      for (int nt = 0; nt < NTT; ++nt) {
         if (nt >= NT) break;
         const int c0 = cb[nt];
         const int ix = c0 >= 0 ? c0 + p0 : 0;
@@ -346,17 +350,17 @@ __global__ __launch_bounds__(256) void k_conv_wgrad_mfma(const bf16_t* __restric
     if (++done == WM_FL) {
       done = 0;
 #pragma unroll
-      for (int nt = 0; nt < WM_NT; ++nt) {
+      for (int nt = 0; nt < NTT; ++nt) {
         run[nt] += acc[nt];
         acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
   }
 #pragma unroll
-  for (int nt = 0; nt < WM_NT; ++nt) run[nt] += acc[nt];
+  for (int nt = 0; nt < NTT; ++nt) run[nt] += acc[nt];
   // D layout: column 16·nt + (lane & 15), rows 4·(lane >> 4) + r
 #pragma unroll
-  for (int nt = 0; nt < WM_NT; ++nt)
+  for (int nt = 0; nt < NTT; ++nt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[w][4 * kg + r][16 * nt + n] = run[nt][r];
   __syncthreads();
@@ -364,57 +368,56 @@ __global__ __launch_bounds__(256) void k_conv_wgrad_mfma(const bf16_t* __restric
     const int o = e / ncol, c = e - o * ncol;
     st_agent(part + (int64_t)blockIdx.x * NOUT + e, (red[0][o][c] + red[1][o][c]) + (red[2][o][c] + red[3][o][c]));
   }
-  // the last of each 16 workgroups sums their partials, the last of those the groups'
+  // the last of each 16 workgroups sums their partials, the last of each 16 of
+  // those the group sums, … (fixed membership and order: deterministic)
   constexpr int EPT = WM_NOUT / 256;
-  const int g = blockIdx.x / 16, ng = (gridDim.x + 15) / 16;
-  const int gsize = min(16, (int)gridDim.x - 16 * g);
-  float* gpart = part + (int64_t)gridDim.x * NOUT;
-  auto sum16 = [&](const float* src, int cnt, float* dst_part, bool final_) __attribute__((always_inline)) {
+  __shared__ bool last_;
+  int idx = blockIdx.x, cnt = gridDim.x;
+  const float* src = part;
+  float* dst = part + (int64_t)gridDim.x * NOUT;
+  unsigned* tk = ticket;
+  for (int lvl = 0; lvl < WM_LEVELS; ++lvl) {
+    const int g = idx / 16, ng = (cnt + 15) / 16, gsize = min(16, cnt - 16 * g);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have left
+    __syncthreads();
+    if (tid == 0) {
+      unsigned* sub = tk + (int64_t)g * TICKET_STRIDE;
+      const bool l = __hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)gsize - 1;
+      if (l) __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_ = l;
+    }
+    __syncthreads();
+    if (!last_) return;
     float v[EPT][16];
+    const float* gs = src + (int64_t)16 * g * NOUT;
 #pragma unroll
     for (int r = 0; r < EPT; ++r) {
       const int e = tid + 256 * r, ec = e < NOUT ? e : 0;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) v[r][k] = ld_agent(src + (int64_t)(k < cnt ? k : 0) * NOUT + ec);
+      for (int k = 0; k < 16; ++k) v[r][k] = ld_agent(gs + (int64_t)(k < gsize ? k : 0) * NOUT + ec);
     }
 #pragma unroll
     for (int r = 0; r < EPT; ++r) {
       const int e = tid + 256 * r;
       float sm = 0.f;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) sm += k < cnt ? v[r][k] : 0.f;
+      for (int k = 0; k < 16; ++k) sm += k < gsize ? v[r][k] : 0.f;
       if (e >= NOUT) continue;
-      if (!final_) {
-        st_agent(dst_part + e, sm);
+      if (ng > 1) {
+        st_agent(dst + (int64_t)g * NOUT + e, sm);
       } else {
         const int o = e / ncol, c = e - o * ncol;
         if (c < I * K) G[(int64_t)o * I * K + c] = sm;
         else db[o] = sm;
       }
     }
-  };
-  __shared__ bool last_;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    unsigned* sub = ticket + (1 + g) * TICKET_STRIDE;
-    const bool l = __hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)gsize - 1;
-    if (l) __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_ = l;
+    if (ng == 1) return;
+    tk += (int64_t)ng * TICKET_STRIDE;
+    src = dst;
+    dst += (int64_t)ng * NOUT;
+    idx = g;
+    cnt = ng;
   }
-  __syncthreads();
-  if (!last_) return;
-  sum16(part + (int64_t)16 * g * NOUT, gsize, gpart + (int64_t)g * NOUT, false);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const bool l = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)ng - 1;
-    if (l) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_ = l;
-  }
-  __syncthreads();
-  if (!last_) return;
-  sum16(gpart, ng, nullptr, true);
 }
 
 // per-channel sums of (B, C, L): grid (WG_SPLIT, C) partials; the channel's
@@ -483,8 +486,11 @@ int launch_conv(int dti, int dto, const void* x, int B, int I, int Lin, const fl
 extern "C" {
 
 size_t ocm_conv1d_scratch_bytes(int32_t O, int32_t I, int32_t K) {
-  return CV_TICKETS * sizeof(unsigned) +
-         (size_t)((int64_t)O * I * (K + 1) + (int64_t)(O > I ? O : I)) * WG_MAXSPLIT * sizeof(float) + 256;
+  // VALU wgrad: ≤ WG_MAXSPLIT partials of O·I·(K + 1) (+ the channel sums);
+  // matrix-core wgrad: WM_WG + 64 + 4 partials of O·(I·K + 1)
+  const int64_t valu = ((int64_t)O * I * (K + 1) + (int64_t)(O > I ? O : I)) * WG_MAXSPLIT;
+  const int64_t mfma = (int64_t)O * (I * K + 1) * (WM_WG + 64 + 4);
+  return CV_TICKETS * sizeof(unsigned) + (size_t)(valu > mfma ? valu : mfma) * sizeof(float) + 256;
 }
 
 int ocm_conv1d(ocm_ctx* ctx, int32_t mode, int32_t dtype_in, const void* x, int32_t B, int32_t I, int32_t Lin,
@@ -529,17 +535,30 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
   const bool wb = psum_out != nullptr;
   const int ncol = I * K + (wb ? 1 : 0);
   if (dtype_p == OCM_DTYPE_BF16 && dtype_q == OCM_DTYPE_BF16 && O <= WM_OMAX && I <= WM_IMAX && ncol <= 16 * WM_NT &&
+      O * ncol <= WM_NOUT &&
       (stride == 1 || stride == 2) && Lp % WM_CH == 0 && Lq % 8 == 0 && pad <= 7 &&
       (reinterpret_cast<uintptr_t>(P) & 15) == 0 && (reinterpret_cast<uintptr_t>(Q) & 15) == 0) {
     // the matrix-core path (bf16): ≤ WM_WG workgroups, two-level partial sums
     const int nch = (int)((int64_t)B * Lp / WM_CH);
     const int nwg = std::min(WM_WG, nch);
-#define OCM_WM(WB, S)                                                                                              hipLaunchKernelGGL((k_conv_wgrad_mfma<WB, S>), dim3((unsigned)nwg), dim3(256), 0, st,                                               static_cast<const bf16_t*>(P), O, Lp, static_cast<const bf16_t*>(Q), I, Lq, B, K, pad, part,                      ticket, G_out, psum_out)
+    const int nt = (ncol + 15) / 16;
+#define OCM_WM3(WB, S, NTT)                                                                                      \
+  hipLaunchKernelGGL((k_conv_wgrad_mfma<WB, S, NTT>), dim3((unsigned)nwg), dim3(256), 0, st,                     \
+                     static_cast<const bf16_t*>(P), O, Lp, static_cast<const bf16_t*>(Q), I, Lq, B, K, pad, part, \
+                     ticket, G_out, psum_out)
+#define OCM_WM(WB, S)                    \
+  do {                                   \
+    if (nt == 1) OCM_WM3(WB, S, 1);      \
+    else if (nt == 2) OCM_WM3(WB, S, 2); \
+    else if (nt == 3) OCM_WM3(WB, S, 3); \
+    else OCM_WM3(WB, S, 6);              \
+  } while (0)
     if (wb && stride == 1) OCM_WM(true, 1);
     else if (wb) OCM_WM(true, 2);
     else if (stride == 1) OCM_WM(false, 1);
     else OCM_WM(false, 2);
 #undef OCM_WM
+#undef OCM_WM3
     OCM_CHECK_LAUNCH("k_conv_wgrad_mfma");
     return OCM_OK;
   }
