@@ -64,17 +64,22 @@ __device__ __forceinline__ bool cv_last(unsigned* ticket, int slot) {
   return last_arrival2(ticket, slot, gridDim.x, blockIdx.x);
 }
 
-// down / up: grid (ceil(Lout / CV_T), ceil(O / 4), B).  KT ≥ K is the
+// down / up: grid (ceil(Lout / CV_T), ceil(O / OG), B).  KT ≥ K is the
 // compile-time tap count, so the taps of one input channel unroll and their
 // loads issue together (a runtime tap loop waits out one load latency per tap).
-template <bool UP, int KT, typename TI, typename TO>
+// Each thread computes OG output channels of its position (OG ≥ O for the C4
+// layers: one pass over x per layer — with four channels per thread the
+// 6 → 12 layers read every tap three times, 2-byte loads each)
+template <bool UP, int KT, int OG, typename TI, typename TO>
 __global__ __launch_bounds__(CV_T) void k_conv(const TI* __restrict__ x, int I, int Lin, const float* __restrict__ w,
                                               const float* __restrict__ bias, int O, int Lout, int K, int s, int pad,
                                               TO* __restrict__ y) {
-  // the four output channels' weights as [input channel][tap][channel u]: one
-  // ds_read_b128 serves the four FMAs of a tap (CV_KMAX slots, zero past K)
-  __shared__ f32x4 sw[CV_CMAX * CV_KMAX];
-  const int o0 = blockIdx.y * CV_OG, b = blockIdx.z;
+  static_assert(OG % 4 == 0, "channel quads");
+  constexpr int NQ = OG / 4;
+  // the OG output channels' weights as [input channel][tap][channel quad]: one
+  // ds_read_b128 serves four FMAs of a tap (CV_KMAX slots, zero past K)
+  extern __shared__ f32x4 sw[];  // I · CV_KMAX · NQ (dynamic: only the layer's input channels)
+  const int o0 = blockIdx.y * OG, b = blockIdx.z;
   const int l = blockIdx.x * CV_T + threadIdx.x;  // this thread's output position (≥ Lout: none)
   const TI* xb = x + (int64_t)b * I * Lin;
   // up: the taps that reach output l are t ≡ (l + pad) mod s, input l' = (l + pad − t)/s;
@@ -104,44 +109,44 @@ __global__ __launch_bounds__(CV_T) void k_conv(const TI* __restrict__ x, int I, 
   // latencies overlap; the loads are clamped, so idle threads issue them too)
   float va[KT], vb[KT];
   taps(0, va);
-  for (int e = threadIdx.x; e < I * CV_KMAX; e += CV_T) {
-    const int i = e / CV_KMAX, t = e - i * CV_KMAX;
+  for (int e = threadIdx.x; e < I * CV_KMAX * NQ; e += CV_T) {
+    const int qd = e % NQ, it = e / NQ, i = it / CV_KMAX, t = it - i * CV_KMAX;
     f32x4 wv;
 #pragma unroll
-    for (int u = 0; u < CV_OG; ++u) {
-      const int o = o0 + u;
+    for (int u = 0; u < 4; ++u) {
+      const int o = o0 + 4 * qd + u;
       wv[u] = (o < O && t < K) ? (UP ? w[((int64_t)i * O + o) * K + t] : w[((int64_t)o * I + i) * K + t]) : 0.f;
     }
     sw[e] = wv;
   }
   __syncthreads();
   if (l >= Lout) return;
-  float acc[CV_OG];
+  float acc[OG];
 #pragma unroll
-  for (int u = 0; u < CV_OG; ++u) acc[u] = (bias && o0 + u < O) ? bias[o0 + u] : 0.f;
-  for (int i = 0; i < I; i += 2) {
-    if (i + 1 < I) taps(i + 1, vb);
+  for (int u = 0; u < OG; ++u) acc[u] = (bias && o0 + u < O) ? bias[o0 + u] : 0.f;
+  auto fmas = [&](int i, const float (&v)[KT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
       // raw tap of v[t] (clamped into the slot row: v[t] = 0 there)
       const int tw = UP ? min(t0 + t * s, CV_KMAX - 1) : t;
-      const f32x4 wv = sw[i * CV_KMAX + tw];
 #pragma unroll
-      for (int u = 0; u < CV_OG; ++u) acc[u] = fmaf(wv[u], va[t], acc[u]);
+      for (int qd = 0; qd < NQ; ++qd) {
+        const f32x4 wv = sw[(i * CV_KMAX + tw) * NQ + qd];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[4 * qd + u] = fmaf(wv[u], v[t], acc[4 * qd + u]);
+      }
     }
+  };
+  for (int i = 0; i < I; i += 2) {
+    if (i + 1 < I) taps(i + 1, vb);
+    fmas(i, va);
     if (i + 1 >= I) break;
     if (i + 2 < I) taps(i + 2, va);
-#pragma unroll
-    for (int t = 0; t < KT; ++t) {
-      const int tw = UP ? min(t0 + t * s, CV_KMAX - 1) : t;
-      const f32x4 wv = sw[(i + 1) * CV_KMAX + tw];
-#pragma unroll
-      for (int u = 0; u < CV_OG; ++u) acc[u] = fmaf(wv[u], vb[t], acc[u]);
-    }
+    fmas(i + 1, vb);
   }
   TO* yb = y + (int64_t)b * O * Lout;
 #pragma unroll
-  for (int u = 0; u < CV_OG; ++u)
+  for (int u = 0; u < OG; ++u)
     if (o0 + u < O) cv_st(yb, (int64_t)(o0 + u) * Lout + l, acc[u]);
 }
 
@@ -454,13 +459,13 @@ __global__ __launch_bounds__(CV_T) void k_chan_sum(const T* __restrict__ v, int 
   if (threadIdx.x == 0) out[c] = (float)s;
 }
 
-template <bool UP, int KT>
+template <bool UP, int KT, int OG>
 int launch_conv_k(int dti, int dto, const void* x, int B, int I, int Lin, const float* w, const float* bias, int O,
                   int Lout, int K, int s, int pad, void* y, hipStream_t st) {
-  dim3 g((unsigned)((Lout + CV_T - 1) / CV_T), (unsigned)((O + CV_OG - 1) / CV_OG), (unsigned)B);
+  dim3 g((unsigned)((Lout + CV_T - 1) / CV_T), (unsigned)((O + OG - 1) / OG), (unsigned)B);
 #define OCM_CONV_L(TI, TO)                                                                                        \
-  hipLaunchKernelGGL((k_conv<UP, KT, TI, TO>), g, dim3(CV_T), 0, st, static_cast<const TI*>(x), I, Lin, w, bias, O, \
-                     Lout, K, s, pad, static_cast<TO*>(y))
+  hipLaunchKernelGGL((k_conv<UP, KT, OG, TI, TO>), g, dim3(CV_T), (size_t)I * CV_KMAX * (OG / 4) * sizeof(f32x4), st, \
+                     static_cast<const TI*>(x), I, Lin, w, bias, O, Lout, K, s, pad, static_cast<TO*>(y))
   if (dti == OCM_DTYPE_F32 && dto == OCM_DTYPE_F32) OCM_CONV_L(float, float);
   else if (dti == OCM_DTYPE_F32) OCM_CONV_L(float, bf16_t);
   else if (dto == OCM_DTYPE_F32) OCM_CONV_L(bf16_t, float);
@@ -470,15 +475,25 @@ int launch_conv_k(int dti, int dto, const void* x, int B, int I, int Lin, const 
   return OCM_OK;
 }
 
+template <bool UP, int KT>
+int launch_conv_og(int dti, int dto, const void* x, int B, int I, int Lin, const float* w, const float* bias, int O,
+                   int Lout, int K, int s, int pad, void* y, hipStream_t st) {
+  // output channels per thread: all of them up to 12, else groups of 16
+  if (O <= 4) return launch_conv_k<UP, KT, 4>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
+  if (O <= 8) return launch_conv_k<UP, KT, 8>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
+  if (O <= 12) return launch_conv_k<UP, KT, 12>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
+  return launch_conv_k<UP, KT, 16>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
+}
+
 template <bool UP>
 int launch_conv(int dti, int dto, const void* x, int B, int I, int Lin, const float* w, const float* bias, int O,
                 int Lout, int K, int s, int pad, void* y, hipStream_t st) {
   // up: KT counts the taps of one residue class, ⌈K / s⌉
   const int kt = UP ? (K + s - 1) / s : K;
-  if (kt == 1) return launch_conv_k<UP, 1>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
-  if (kt <= 4) return launch_conv_k<UP, 4>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
-  if (kt <= 7) return launch_conv_k<UP, 7>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
-  return launch_conv_k<UP, CV_KMAX>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
+  if (kt == 1) return launch_conv_og<UP, 1>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
+  if (kt <= 4) return launch_conv_og<UP, 4>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
+  if (kt <= 7) return launch_conv_og<UP, 7>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
+  return launch_conv_og<UP, CV_KMAX>(dti, dto, x, B, I, Lin, w, bias, O, Lout, K, s, pad, y, st);
 }
 
 }  // namespace
