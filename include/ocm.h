@@ -441,6 +441,13 @@ int ocm_bn_fwd_train(ocm_ctx* ctx, int32_t dtype, const void* x, int32_t N, int3
                      const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
                      float* running_var, int64_t* num_batches_tracked, int32_t act, void* y, float* save_mean,
                      float* save_invstd, void* scratch, void* stream);
+/* Eval-mode BatchNorm1d (running statistics, vae_model.py:45-47 in model.eval(), the
+ * latent encoding of utils/final_vaesimca.py:406-442): y = (x − rm)·γ/√(rv + ε) + β,
+ * then the fused ELU with act = OCM_ACT_ELU; gamma / beta nullable.  No scratch,
+ * any N (one flat grid).  ABI 9. */
+int ocm_bn_fwd_eval(ocm_ctx* ctx, int32_t dtype, const void* x, int32_t N, int32_t C, int32_t L,
+                    const float* running_mean, const float* running_var, float eps, const float* gamma,
+                    const float* beta, int32_t act, void* y, void* stream);
 /* dx = γ·invstd·(dz − mean(dz) − x̂·mean(dz·x̂)), dz = dy (act NONE) or the ELU's input gradient;
  * dgamma = Σ dz·x̂, dbeta = Σ dz (either may be NULL); y [act ELU] the forward's output. */
 int ocm_bn_bwd(ocm_ctx* ctx, int32_t dtype, const void* x, const void* dy, int32_t N, int32_t C, int32_t L,

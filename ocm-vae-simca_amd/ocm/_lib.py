@@ -119,6 +119,8 @@ SIGNATURES = {
     "ocm_bn_fwd_train": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, ctypes.c_float,
                                  ctypes.c_float, c_void_p, c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p]),
+    "ocm_bn_fwd_eval": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, ctypes.c_float,
+                                c_void_p, c_void_p, c_i32, c_void_p, c_void_p]),
     "ocm_bn_bwd": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p,
                            c_i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ocm_conv1d_scratch_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),

@@ -96,6 +96,22 @@ class FastBatchNorm1d(nn.BatchNorm1d):
         return self
 
     def forward(self, x):
+        if (not self.training and x.is_cuda and x.dim() == 3 and x.dtype in _DT and self.track_running_stats
+                and self.running_mean is not None and self.running_mean.dtype == torch.float32
+                and not (torch.is_grad_enabled()
+                         and (x.requires_grad or (self.affine and self.weight.requires_grad)))):
+            # eval with running statistics and no autograd (the latent encoding):
+            # one libocm launch (MIOpen's inference kernel: 3.3 ms per 8192-row batch)
+            x = x.contiguous()
+            y = torch.empty_like(x)
+            N, C, L = x.shape
+            w = self.weight if self.affine else None
+            b = self.bias if self.affine else None
+            check(_lib.load().ocm_bn_fwd_eval(Context.get(x.device.index).handle, _DT[x.dtype], ptr(x), N, C, L,
+                                              ptr(self.running_mean), ptr(self.running_var), float(self.eps),
+                                              ptr(w) if w is not None else None, ptr(b) if b is not None else None,
+                                              self.act, ptr(y), stream_handle(x.device)), "ocm_bn_fwd_eval")
+            return y
         if not (self.training and x.is_cuda and x.dim() == 3 and x.dtype in _DT) or self.momentum is None:
             # eval (running statistics), host tensors, cumulative-average momentum: the stock module
             y = super().forward(x)

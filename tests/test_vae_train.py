@@ -141,6 +141,43 @@ def test_fast_batchnorm_matches_torch(dtype, shape):
 @pytest.mark.gpu
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8192, 3, 2048), (40000, 12, 16), (7, 5, 33)])
+@pytest.mark.parametrize("elu", [False, True])
+def test_eval_batchnorm_matches_torch(dtype, shape, elu):
+    """Eval-mode FastBatchNorm1d under no_grad (ocm_bn_fwd_eval, the latent
+    encoding) == nn.BatchNorm1d(.eval()) (+ ELU) on trained running statistics,
+    including N·C past a 65535-row grid and a length that is not a multiple of 8."""
+    from ocm.bn import FastBatchNorm1d
+
+    dev = torch.device("cuda", 0)
+    N, C, L = shape
+    g = torch.Generator(device="cpu").manual_seed(C * L + 7)
+    ref = torch.nn.BatchNorm1d(C).to(dev)
+    fast = FastBatchNorm1d(C).to(dev)
+    if elu:
+        fast.fuse_elu()
+    with torch.no_grad():
+        ref.weight.copy_(torch.linspace(0.5, 1.5, C))
+        ref.bias.copy_(torch.linspace(-0.2, 0.3, C))
+        ref.running_mean.copy_(torch.linspace(-1.0, 2.0, C))
+        ref.running_var.copy_(torch.linspace(0.3, 4.0, C))
+    fast.load_state_dict(ref.state_dict())
+    ref.eval()
+    fast.eval()
+    x = (0.5 + 2.0 * torch.randn(N, C, L, generator=g)).to(dev).to(dtype)
+    with torch.no_grad():
+        yr = ref(x.float())
+        if elu:
+            yr = torch.nn.functional.elu(yr)
+        yf = fast(x)
+    assert yf.dtype == dtype and yf.shape == x.shape
+    tol = dict(rtol=1e-2, atol=1e-2) if dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(yf.float(), yr, **tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(512, 3, 2048), (64, 12, 512), (7, 5, 33)])
 def test_fused_batchnorm_elu_matches_torch(dtype, shape):
     """FastBatchNorm1d.fuse_elu() == nn.BatchNorm1d followed by nn.ELU: output,
