@@ -797,19 +797,27 @@ __global__ __launch_bounds__(256) void k_cq_gram32(double* W, int p, const doubl
     wpart[wave][2][r][lane] = s11[r];
   }
   __syncthreads();
+  // hand-off without fences (ocm_internal.h: write-through stores, drained,
+  // then the ticket; the last workgroup reads them back write-through, all
+  // CQ_G of an element in flight together — a loop of loads waited out one
+  // memory round trip per partial)
   for (int e = tid; e < 768; e += 256) {
     const double* w0 = &wpart[0][0][0][0];
-    part[(int64_t)blockIdx.x * 768 + e] = (w0[e] + w0[768 + e]) + (w0[1536 + e] + w0[2304 + e]);
+    st_agent(&part[(int64_t)blockIdx.x * 768 + e], (w0[e] + w0[768 + e]) + (w0[1536 + e] + w0[2304 + e]));
   }
-  __threadfence();  // this workgroup's partial is visible before its ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) last = (atomicAdd(ticket, 1u) % CQ_G) == CQ_G - 1;
+  if (tid == 0)
+    last = (__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % CQ_G) == CQ_G - 1;
   __syncthreads();
   if (!last) return;
-  __threadfence();  // acquire: every partial is complete
   for (int e = tid; e < 768; e += 256) {
+    double pv[CQ_G];
+#pragma unroll
+    for (int wg = 0; wg < CQ_G; ++wg) pv[wg] = ld_agent(&part[(int64_t)wg * 768 + e]);
     double v = 0.0;
-    for (int wg = 0; wg < CQ_G; ++wg) v += __builtin_nontemporal_load(&part[(int64_t)wg * 768 + e]);
+#pragma unroll
+    for (int wg = 0; wg < CQ_G; ++wg) v += pv[wg];
     const int blk = e >> 8, r = (e >> 6) & 3, l = e & 63;
     const int row = 16 * (blk == 2) + (l >> 4) + 4 * r, col = 16 * (blk != 0) + (l & 15);
     sS[row][col] = v;

@@ -95,6 +95,53 @@ def test_sharded_simca_two_ranks_real_engine(tmp_path):
         assert diff.sum() <= 2, (cfg, int(diff.sum()))  # rows on the decision boundary only
 
 
+def _offset_data():
+    """spectra on a large baseline with small variance (μ ≈ 1e3,
+    tail λ ≈ 1e-6): each rank's moments are packed about ONE all-reduced
+    shift, so nothing of size |μ|² cancels in the covariance."""
+    X, bounds = _data()
+    return (X.astype(np.float64) * 1e-2 + 1e3).astype(np.float32), bounds
+
+
+def _simca_offset_worker(rank, world, port, path):
+    import torch.distributed as dist
+
+    from ocm.dist import ShardedSIMCA
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        X, bounds = _offset_data()
+        lo, hi = bounds[rank]
+        m = ShardedSIMCA(n_components=8, type="alt", t2lim="Fdist", qlim="jm").fit(torch.from_numpy(X[lo:hi]).cuda())
+        if rank == 0:
+            np.savez(path, lim=np.array([m.T2_limit, m.Q_limit, float(m.D_limit)]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_simca_large_offset(tmp_path):
+    """Two ranks on offset spectra == the single-process fit, and the jm Q limit
+    == the fp64 oracle's (θ1..θ3 of the tail eigenvalues survive the offset)."""
+    from ocm.dist import ShardedSIMCA
+
+    path = str(tmp_path / "off.npz")
+    _spawn(_simca_offset_worker, path)
+    got = np.load(path)["lim"]
+    X, _ = _offset_data()
+    ref = ShardedSIMCA(n_components=8, type="alt", t2lim="Fdist", qlim="jm").fit(torch.from_numpy(X).cuda())
+    np.testing.assert_allclose(got, [ref.T2_limit, ref.Q_limit, float(ref.D_limit)], rtol=1e-5)
+    Xc = X.astype(np.float64) - X.astype(np.float64).mean(0)
+    lam = np.linalg.eigvalsh(Xc.T @ Xc / (X.shape[0] - 1))[::-1]
+    tail = lam[8:]
+    th = (tail.sum(), (tail ** 2).sum(), (tail ** 3).sum())
+    h0 = 1 - 2 * th[0] * th[2] / (3 * th[1] ** 2)
+    from scipy.special import erfinv
+    ca = np.sqrt(2) * erfinv(2 * 0.95 - 1)
+    q_ref = th[0] * (ca * np.sqrt(2 * th[1] * h0 ** 2) / th[0] + 1 + th[1] * h0 * (h0 - 1) / th[0] ** 2) ** (1 / h0)
+    np.testing.assert_allclose(got[1], q_ref, rtol=1e-4)
+
+
 def _cv_worker(rank, world, port, path):
     import torch.distributed as dist
 
