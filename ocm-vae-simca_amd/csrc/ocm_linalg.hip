@@ -478,10 +478,15 @@ __global__ __launch_bounds__(256) void k_jacobi_blk(const double* __restrict__ A
         const double apq = A[cur][2 * tid][2 * tid + 1];
         double c = 1.0, sn = 0.0;
         if (apq != 0.0) {
-          const double theta = (aqq - app) / (2.0 * apq);
-          const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-          c = 1.0 / sqrt(t * t + 1.0);
-          sn = t * c;
+          // t = sgn(θ)/(|θ| + √(θ² + 1)), θ = d/e (d = aqq − app, e = 2apq), c = 1/√(1 + t²),
+          // s = t·c, rewritten with u = |d| + √(d² + e²): c = u/√(u² + e²), s = ±e/√(u² + e²)
+          // — one square root and one reciprocal square root on the round's serial
+          // path instead of three divisions and two square roots
+          const double d = aqq - app, e = 2.0 * apq;
+          const double u = fabs(d) + sqrt(fma(d, d, e * e));
+          const double w = rsqrt(fma(u, u, e * e));
+          c = u * w;
+          sn = (d >= 0.0 ? e : -e) * w;
         }
         rc[tid] = c;
         rs[tid] = sn;
