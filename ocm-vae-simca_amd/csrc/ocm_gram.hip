@@ -1246,6 +1246,18 @@ __global__ __launch_bounds__(1024) void k_q8_thresholds(int p, int P8, float* __
     thr[c] = c < p ? Q8TAU * fmaxf(thr[c], floor_) : __builtin_inff();
 }
 
+// zero nf flag words and 4 counters, fill n3 words of b3 with v3 (one launch)
+__global__ __launch_bounds__(256) void k_guard_init(uint32_t* __restrict__ flags, size_t nf,
+                                                    uint32_t* __restrict__ counters, uint32_t* __restrict__ b3,
+                                                    size_t n3, uint32_t v3) {
+  const size_t tot = nf + 4 + n3;
+  for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < tot; e += (size_t)gridDim.x * 256) {
+    if (e < nf) flags[e] = 0u;
+    else if (e < nf + 4) counters[e - nf] = 0u;
+    else b3[e - nf - 4] = v3;
+  }
+}
+
 // Marked-row compaction, in processed-row order: per 4096-row block the
 // number of marked rows, then each block writes its rows at the prefix of the
 // counts before it (ordered lists → a deterministic fix-up sum).
@@ -2463,12 +2475,19 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   auto* host = static_cast<uint32_t*>(ocm::host_staging(ctx, 64));
   if (!host) return OCM_ERR_NOMEM;
 
-  OCM_HIP(hipMemsetAsync(flags, 0, (size_t)n * fw * 4, st));
-  OCM_HIP(hipMemsetAsync(counters, 0, 16, st));
-  if (unguarded) {
-    OCM_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(thr), 0x7f800000, (size_t)P8, st));  // +inf
-  } else {
-    OCM_HIP(hipMemsetAsync(xhist, 0, (size_t)p * QX_BINS * 4, st));
+  // the guard's buffers in one launch (three memsets cost ≈ 5 µs each plus
+  // their gaps): row flags and counters zero, then the thresholds +inf
+  // (unguarded) or the exponent histogram zero
+  {
+    const size_t nf = (size_t)n * fw, third = unguarded ? (size_t)P8 : (size_t)p * QX_BINS;
+    const uint32_t v3 = unguarded ? 0x7f800000u : 0u;  // +inf / 0
+    uint32_t* b3 = unguarded ? reinterpret_cast<uint32_t*>(thr) : xhist;
+    const size_t tot = nf + 4 + third;
+    hipLaunchKernelGGL(k_guard_init, dim3((unsigned)std::min<size_t>((tot + 255) / 256, 4096)), dim3(256), 0, st,
+                       flags, nf, counters, b3, third, v3);
+    OCM_CHECK_LAUNCH("k_guard_init");
+  }
+  if (!unguarded) {
     hipLaunchKernelGGL(k_colexp_hist, dim3((p + 63) / 64, nsplit), dim3(256), 0, st, X, ldx, rows, nsamp, p, shift,
                        rps, xhist, pa);
     hipLaunchKernelGGL(k_q8_colmed, dim3((p + 3) / 4), dim3(256), 0, st, xhist, nsamp, p, thr);

@@ -942,9 +942,14 @@ __device__ __forceinline__ double hash_normal(uint64_t a) {
   return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
 }
 
-__global__ void k_randn(double* __restrict__ V, int64_t count, uint64_t seed) {
+// (+ zeroes nz words at z: the eigensolver's ticket counters, one launch
+// instead of two memsets ahead of it)
+__global__ void k_randn(double* __restrict__ V, int64_t count, uint64_t seed, unsigned* __restrict__ z0 = nullptr,
+                        int nz0 = 0, unsigned* __restrict__ z1 = nullptr, int nz1 = 0) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < count) V[i] = hash_normal(seed * 0x100000001B3ull + (uint64_t)i);
+  if (i < nz0) z0[i] = 0u;
+  if (i < nz1) z1[i] = 0u;
 }
 
 // Normalise each column of a tall p×b matrix; an (almost) zero column is
@@ -1332,17 +1337,17 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   double* Z = cv.take<double>(bb);
   double* S = cv.take<double>(bb);
   double* L = cv.take<double>(bb);
-  double* theta = cv.take<double>(b);
-  double* res = cv.take<double>(b);
+  double* theta = cv.take<double>(2 * (size_t)b);  // θ (b), then the residuals (b): one read-back
+  double* res = theta + b;
   double* planes = cv.take<double>(plane_cap);
   double* apart = wide ? nullptr : cv.take<double>((size_t)nblk * bb);
   double* cq_part = cv.take<double>((size_t)CQ_G * 768);
   double* cq_M = cv.take<double>(2048);
+  // k_cq_gram32's ticket counts from a multiple of CQ_G, k_cv32's parity tickets
+  // start even: both zeroed by the k_randn launch below (contiguous)
   unsigned* cq_ticket = cv.take<unsigned>(64);
-  OCM_HIP(hipMemsetAsync(cq_ticket, 0, sizeof(unsigned), st));  // k_cq_gram32's tickets count from a multiple of CQ_G
   double* cv_part = cv.take<double>((size_t)cv_rb * 2 * 512);
   unsigned* cv_ticket = cv.take<unsigned>(cv_rb);
-  OCM_HIP(hipMemsetAsync(cv_ticket, 0, (size_t)cv_rb * sizeof(unsigned), st));  // parity tickets start even
   auto* hres = static_cast<double*>(ocm::host_staging(ctx, (wide ? 3 * bb + b : 2 * b) * sizeof(double)));
   if (!hres) return OCM_ERR_NOMEM;
   double* hmat = hres + 2 * b;  // wide: b×b host staging (+ b×b result, + b values)
@@ -1433,7 +1438,8 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   // span(Cⁱ V₀) whatever basis V₀ has, so only the Rayleigh–Ritz steps need an
   // orthonormal basis (every iteration before one ends with CholQR2), and an
   // orthonormalisation of V₀ costs a CholQR pass (≈ 36 µs) for nothing
-  hipLaunchKernelGGL(k_randn, dim3((unsigned)((pb + 255) / 256)), dim3(256), 0, st, V, (int64_t)pb, 0x5EEDull);
+  hipLaunchKernelGGL(k_randn, dim3((unsigned)((std::max<size_t>(pb, cv_rb) + 255) / 256)), dim3(256), 0, st, V,
+                     (int64_t)pb, 0x5EEDull, cq_ticket, 1, cv_ticket, cv_rb);
   OCM_CHECK_LAUNCH("k_randn");
   int rc = OCM_OK;
 
@@ -1495,12 +1501,11 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     std::swap(W, T2);
     hipLaunchKernelGGL(k_ritz_residual, dim3(k), dim3(256), 0, st, W, V, theta, p, b, res);
     OCM_CHECK_LAUNCH("k_ritz_residual");
-    OCM_HIP(hipMemcpyAsync(hres, res, k * sizeof(double), hipMemcpyDeviceToHost, st));
-    OCM_HIP(hipMemcpyAsync(hres + b, theta, b * sizeof(double), hipMemcpyDeviceToHost, st));
+    OCM_HIP(hipMemcpyAsync(hres, theta, 2 * (size_t)b * sizeof(double), hipMemcpyDeviceToHost, st));
     OCM_HIP(hipStreamSynchronize(st));
     double rmax = 0.0;
-    for (int i = 0; i < k; ++i) rmax = std::max(rmax, hres[i]);
-    const double scale = std::fabs(hres[b]);
+    for (int i = 0; i < k; ++i) rmax = std::max(rmax, hres[b + i]);  // hres: θ (b) then the residuals
+    const double scale = std::fabs(hres[0]);
     if (!(rmax == rmax)) return ocm::fail(OCM_ERR_ARG, "ocm_eig_topk: NaN in covariance");
     const double target = tol * (scale > 0 ? scale : 1.0);
     if (rmax <= target) {
@@ -1509,8 +1514,8 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     }
     if (it == max_iter) break;  // keep V, W, theta consistent for the outputs
     // predicted iterations to the tolerance (at least one, at most 64 untested)
-    const double tk = std::fabs(hres[b + k - 1]);
-    double rate = tk > 0 ? std::fabs(hres[2 * b - 1]) / tk : 1.0;
+    const double tk = std::fabs(hres[k - 1]);
+    double rate = tk > 0 ? std::fabs(hres[b - 1]) / tk : 1.0;
     if (prev_it > 0 && prev_rmax > 0) rate = std::max(rate, std::pow(rmax / prev_rmax, 1.0 / (it - prev_it)));
     int ahead = 1;
     if (rate < 0.999) ahead = (int)std::ceil(std::log(target / rmax) / std::log(std::max(rate, 1e-3)));
