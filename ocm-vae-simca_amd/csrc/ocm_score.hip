@@ -383,8 +383,13 @@ __device__ __forceinline__ float xlane(int src, float v) {
 // columns).  B operands straight from the AGPR tile; four (six) interleaved
 // chains, none waits on its predecessor.  The s_nop covers a VALU/LDS write
 // of a or b right before.
+#ifdef OCM_S1P_DIAG_NOMFMA  // diagnostic builds only (make exp): both sweeps' MFMAs removed, timing only
+#define OCM_MF(ACC, A, B) ""
+#define OCM_M4(ACC, A, B) ""
+#else
 #define OCM_MF(ACC, A, B) "v_mfma_f32_16x16x4_f32 %[" #ACC "], %[" #A "], %[" #B "], %[" #ACC "]\n\t"
 #define OCM_M4(ACC, A, B) "v_mfma_f32_4x4x1_16b_f32 %[" #ACC "], %[" #A "], %[" #B "], %[" #ACC "]\n\t"
+#endif
 template <bool EX>
 __device__ __forceinline__ void s1_block(f32x4& acA, f32x4& acB, f32x4& acC, f32x4& acD, f32x4& acE, f32x4& acF,
                                          const f32x4& a, const float (&b)[4], const f32x4& x) {
@@ -411,7 +416,11 @@ __device__ __forceinline__ void s1_block(f32x4& acA, f32x4& acB, f32x4& acC, f32
 // and with it the next MFMA); the caller refills p0, p1 afterwards.  No
 // trailing wait: the next reader of x0, x1 is the next pair's statement or
 // the drain, which opens with its own s_nop.
+#ifdef OCM_S1P_DIAG_NOMFMA
+#define OCM_M2(R, A, T) ""
+#else
 #define OCM_M2(R, A, T) "v_mfma_f32_16x16x4_f32 %[" #R "], %[" #A "], %[" #T "], %[" #R "]\n\t"
+#endif
 #define OCM_RD(S, P) "v_accvgpr_read_b32 %[" #S "], %[" #P "]\n\t"
 #define OCM_FM(Q, S) "v_fmac_f32_e32 %[" #Q "], %[" #S "], %[" #S "]\n\t"
 template <bool EX, bool QW>
