@@ -1006,7 +1006,10 @@ __global__ __launch_bounds__(256) void k_ritz_residual(const double* __restrict_
 // evecs[i][j] = s_i · V[j][i] with s_i making the max-|entry| of row i positive
 // (sklearn svd_flip(u_based_decision=False), first index on ties like argmax).
 __global__ __launch_bounds__(256) void k_extract_signfix(const double* __restrict__ V, int p, int b, int k,
-                                                         double* __restrict__ evecs) {
+                                                         double* __restrict__ evecs,
+                                                         const double* __restrict__ theta = nullptr,
+                                                         double* __restrict__ evals = nullptr) {
+  if (evals && threadIdx.x == 0) evals[blockIdx.x] = theta[blockIdx.x];  // λ_i (no separate copy)
   __shared__ double bv[256];
   __shared__ int bi[256];
   const int i = blockIdx.x;
@@ -1530,8 +1533,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   }
   if (iters_out) *iters_out = std::min(it, max_iter);
 
-  OCM_HIP(hipMemcpyAsync(evals_out, theta, k * sizeof(double), hipMemcpyDeviceToDevice, st));
-  hipLaunchKernelGGL(k_extract_signfix, dim3(k), dim3(256), 0, st, V, p, b, k, evecs_out);
+  hipLaunchKernelGGL(k_extract_signfix, dim3(k), dim3(256), 0, st, V, p, b, k, evecs_out, theta, evals_out);
   OCM_CHECK_LAUNCH("k_extract_signfix");
 
   if (theta_mode) {
@@ -1543,7 +1545,6 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     if (rc) return rc;
     double* Ct = cv.take<double>((size_t)p * p);
     double* dpart = cv.take<double>(2 * def_blocks);
-    double* tr2 = cv.take<double>(2);
     double* U = cv.take<double>((size_t)2 * k * p);
     double* Wt = cv.take<double>((size_t)2 * k * p);
     hipLaunchKernelGGL(k_deflate_operands, dim3((unsigned)(((size_t)p * k + 255) / 256)), dim3(256), 0, st, V, W,
@@ -1553,9 +1554,8 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     hipLaunchKernelGGL(k_dgemm<2>, gd, dim3(256), 0, st, U, (int64_t)(2 * k), Wt, (int64_t)p, Ct, (int64_t)p, p, p,
                        2 * k, 2 * k, C, (int64_t)p, dpart, 0);
     OCM_CHECK_LAUNCH("k_dgemm deflate");
-    hipLaunchKernelGGL(k_sum_pairs, dim3(1), dim3(256), 0, st, dpart, (int)(gd.x * gd.y), tr2);
+    hipLaunchKernelGGL(k_sum_pairs, dim3(1), dim3(256), 0, st, dpart, (int)(gd.x * gd.y), theta_out);  // θ1, θ2
     OCM_CHECK_LAUNCH("k_sum_pairs");
-    OCM_HIP(hipMemcpyAsync(theta_out, tr2, 2 * sizeof(double), hipMemcpyDeviceToDevice, st));
     // θ3: this slice's rows of the Δ / O expansion (k_theta3_diag), then the
     // i8×3 Gram of those rows of O.  The Gram takes the context workspace, so
     // O (f32), its Gram and the partials live in the context's second arena
