@@ -94,6 +94,31 @@ def test_conv_bf16_autocast(shape):
                                atol=1e-5 * scale)
 
 
+@pytest.mark.parametrize("shape", [SHAPES[0], SHAPES[2], SHAPES[3], SHAPES[5]])
+def test_conv_bf16_wgrad_full_batch(shape):
+    """The C4 batch (B = 512): the matrix-core weight gradient at its full
+    workgroup count (1024 workgroups for the 1M-position layers, three levels of
+    partial sums) against the fp64 host gradient of the same bf16 operands."""
+    transposed, I, O, K, s, pad, op, L = shape
+    fast, ref = _mods(transposed, I, O, K, s, pad, op)
+    B = 512
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, I, L, generator=g).bfloat16()
+    xd = x.to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = fast(xd)
+    xr = x.double().requires_grad_(True)
+    yr = ref(xr)
+    gy = torch.randn(yr.shape, generator=g).bfloat16()
+    y.backward(gy.to(DEV))
+    yr.backward(gy.double())
+    scale = np.abs(ref.weight.grad.numpy()).max()
+    np.testing.assert_allclose(fast.weight.grad.cpu().numpy(), ref.weight.grad.numpy(), rtol=1e-4,
+                               atol=1e-5 * scale)
+    bscale = np.abs(ref.bias.grad.numpy()).max()
+    np.testing.assert_allclose(fast.bias.grad.cpu().numpy(), ref.bias.grad.numpy(), rtol=1e-4, atol=1e-5 * bscale)
+
+
 def test_conv_stock_fallback_for_unsupported():
     """Shapes outside the direct kernels' range take the stock module."""
     from ocm.conv import FastConv1d
