@@ -506,7 +506,8 @@ int ocm_chan_sum(ocm_ctx* ctx, int32_t dtype, const void* v, int32_t B, int32_t 
  * ocm_vae_recon_bwd: dxs = dtotal·gxs (n values, written in dtype), dkl_out = β·dtotal (nullable).
  * ocm_adam_step: torch.optim.Adam (L2 weight_decay, no amsgrad) over `ntensors` tensors of
  *   `table` [dev] (offsets: prefix of numel, total = Σ numel); step [dev] f32 counter, advanced by
- *   one per call (bias corrections 1 − βᵗ). */
+ *   one per call (bias corrections 1 − βᵗ); scratch [dev] ocm_vae_scratch_bytes(4096) bytes,
+ *   zero-filled once (completion counters, left zero). */
 #define OCM_VAE_LOSS_BCE 0
 #define OCM_VAE_LOSS_MSE 1
 typedef struct ocm_adam_tensor {

@@ -140,7 +140,8 @@ __global__ __launch_bounds__(VT) void k_recon_fwd(int kind, const float* __restr
   }
   const double ps = block_sum_d(s, red);
   if (threadIdx.x == 0) st_agent(part + b, ps);  // write-through (ocm_internal.h last_arrival)
-  if (!last_arrival(ticket, gridDim.x)) return;
+  // two-level counter: B = 512 arrivals at one counter queue up at the atomic unit
+  if (!last_arrival2(ticket, 0, gridDim.x, blockIdx.x)) return;
   const double t = threadIdx.x < 64 ? lane_sum_agent<double, double>(part, 1, (int)gridDim.x, threadIdx.x) : 0.0;
   const double tot = block_sum_d(t, red);
   if (threadIdx.x == 0) {
@@ -212,8 +213,9 @@ __global__ __launch_bounds__(VT) void k_adam(const ocm_adam_tensor* __restrict__
     }
   }
   // the last workgroup advances the counter: every workgroup read it before
-  // its own arrival (no data hand-off, so no fence)
-  if (last_arrival(ticket, gridDim.x) && threadIdx.x == 0) *step = t;
+  // its own arrival (no data hand-off, so no fence); two-level counters (≈ 800
+  // arrivals at one counter queue up at the atomic unit)
+  if (last_arrival2(ticket, 0, gridDim.x, blockIdx.x) && threadIdx.x == 0) *step = t;
 }
 
 // up to CAST_MAX tensors converted in one launch (the arguments by value:
@@ -288,7 +290,10 @@ int ocm_vae_standardise(ocm_ctx* ctx, const float* x, int32_t B, int32_t L, cons
   return OCM_OK;
 }
 
-size_t ocm_vae_scratch_bytes(int32_t B) { return (size_t)(B + 64) * sizeof(double) + 256; }
+size_t ocm_vae_scratch_bytes(int32_t B) {
+  // row partials (B + 32 doubles), then the two-level completion counters
+  return (size_t)(B + 32) * sizeof(double) + (size_t)tickets_per_slot(B) * TICKET_STRIDE * sizeof(unsigned) + 256;
+}
 size_t ocm_vae_bottleneck_scratch_bytes() { return 4096 * sizeof(double) + tickets_per_slot(4096) * TICKET_STRIDE * sizeof(unsigned); }
 
 int ocm_vae_bottleneck_fwd(ocm_ctx* ctx, int32_t dtype, const void* mu, const void* logvar, const void* eps, int32_t B,

@@ -174,7 +174,9 @@ class FusedAdam:
         self.total = sum(p.numel() for p in self.params)
         n = len(self.params)
         self.table = torch.empty(n * ctypes.sizeof(self._Entry), dtype=torch.uint8, device=dev)
-        self.scratch = torch.zeros(64, dtype=torch.int32, device=dev)
+        # completion counters of the two-level last-arrival (ocm_adam_step)
+        self.scratch = torch.zeros((int(_lib.load().ocm_vae_scratch_bytes(4096)) + 3) // 4, dtype=torch.int32,
+                                   device=dev)
         self._key = None
 
     def zero_grad(self, set_to_none=True):
