@@ -110,33 +110,59 @@ __global__ __launch_bounds__(VT) void k_recon_fwd(int kind, const float* __restr
   const int b = blockIdx.x;
   const float* xr = x + (int64_t)b * L;
   const double inv = 1.0 / ((double)B * L);
+  // the row's values in registers, every load of a pass issued together (RP
+  // per thread covers L ≤ RP·VT; longer rows stream through the same code in
+  // RP·VT pieces, each loaded twice)
+  constexpr int RP = 8;
   float lo = 0.f, den = 1.f;
   if (kind == OCM_VAE_LOSS_BCE) {
     float mn = __builtin_inff(), mx = -__builtin_inff();
-    for (int j = threadIdx.x; j < L; j += VT) {
-      mn = fminf(mn, xr[j]);
-      mx = fmaxf(mx, xr[j]);
+    for (int j0 = threadIdx.x; j0 < L; j0 += RP * VT) {
+      float v[RP];
+#pragma unroll
+      for (int r = 0; r < RP; ++r) {
+        const int j = j0 + r * VT;
+        v[r] = xr[j < L ? j : 0];
+      }
+#pragma unroll
+      for (int r = 0; r < RP; ++r)
+        if (j0 + r * VT < L) {
+          mn = fminf(mn, v[r]);
+          mx = fmaxf(mx, v[r]);
+        }
     }
     lo = block_minmax(mn, false, redf);
     const float hi = block_minmax(mx, true, redf);
     den = hi - lo + eps;
   }
   double s = 0.0;
-  for (int j = threadIdx.x; j < L; j += VT) {
-    const int64_t e = (int64_t)b * L + j;
-    const float z = ld_act(xs, dt, e) * sd[j] + mean[j];
-    float g;
-    if (kind == OCM_VAE_LOSS_BCE) {
-      const float t = fminf(fmaxf((xr[j] - lo) / den, 0.f), 1.f);
-      s += (double)(fmaxf(z, 0.f) - z * t + log1pf(expf(-fabsf(z))));
-      const float sg = 1.f / (1.f + expf(-z));
-      g = (float)((double)(sg - t) * inv);
-    } else {  // MSE
-      const float d = z - xr[j];
-      s += (double)d * d;
-      g = (float)(2.0 * d * inv);
+  for (int j0 = threadIdx.x; j0 < L; j0 += RP * VT) {
+    float xv[RP], zv[RP], sv[RP];
+#pragma unroll
+    for (int r = 0; r < RP; ++r) {
+      const int j = j0 + r * VT, jc = j < L ? j : 0;
+      xv[r] = xr[jc];
+      sv[r] = sd[jc];
+      zv[r] = ld_act(xs, dt, (int64_t)b * L + jc) * sv[r] + mean[jc];
     }
-    gxs[e] = g * sd[j];
+#pragma unroll
+    for (int r = 0; r < RP; ++r) {
+      const int j = j0 + r * VT;
+      if (j >= L) continue;
+      const float z = zv[r];
+      float g;
+      if (kind == OCM_VAE_LOSS_BCE) {
+        const float t = fminf(fmaxf((xv[r] - lo) / den, 0.f), 1.f);
+        s += (double)(fmaxf(z, 0.f) - z * t + log1pf(expf(-fabsf(z))));
+        const float sg = 1.f / (1.f + expf(-z));
+        g = (float)((double)(sg - t) * inv);
+      } else {  // MSE
+        const float d = z - xv[r];
+        s += (double)d * d;
+        g = (float)(2.0 * d * inv);
+      }
+      gxs[(int64_t)b * L + j] = g * sv[r];
+    }
   }
   const double ps = block_sum_d(s, red);
   if (threadIdx.x == 0) st_agent(part + b, ps);  // write-through (ocm_internal.h last_arrival)
