@@ -150,3 +150,35 @@ def test_sharded_simca_gloo_world2_matches_single(tmp_path, cfg, p):
     np.testing.assert_allclose([got["T2"], got["Q"], got["D"]], [ref.T2_limit, ref.Q_limit, float(ref.D_limit)],
                                rtol=1e-9)
     np.testing.assert_array_equal(got["acc"], acc)
+
+
+def test_sharded_simca_gloo_world4_with_empty_rank(tmp_path):
+    """Four ranks (the θ3 trace tiles split four ways), one of them holding no
+    rows, against the single-process run: the zero-row rank contributes zero
+    moments to the one all-reduce and still scores its (empty) block."""
+    import ocm.dist as od
+    from oracle import simca_oracle as O
+
+    cfg = dict(type="alt", t2lim="Fdist", qlim="jm")
+    X = O.synth_spectra(1500, 160, 4, rank=10, seed=4, outlier_frac=0.05)
+    bounds = [(0, 400), (400, 400), (400, 900), (900, 1500)]
+    path = str(tmp_path / "r4.npz")
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_simca_worker, args=(r, 4, port, path, X, bounds, cfg)) for r in range(4)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    got = np.load(path)
+    saved = od.engine
+    od.engine = fake_engine
+    try:
+        ref = od.ShardedSIMCA(n_components=4, **cfg).fit(torch.from_numpy(X))
+        acc = ref.predict(torch.from_numpy(X)).numpy()
+    finally:
+        od.engine = saved
+    np.testing.assert_allclose([got["T2"], got["Q"], got["D"]], [ref.T2_limit, ref.Q_limit, float(ref.D_limit)],
+                               rtol=1e-9)
+    np.testing.assert_array_equal(got["acc"], acc)
