@@ -129,6 +129,8 @@ class ShardedSIMCA:
         m = X_local.shape[0]
         if out is None:
             out = torch.empty(m, dtype=torch.float64, device=X_local.device)
+        if m == 0:  # a rank without rows has nothing to score (its block is empty)
+            return out
         fit = self.fit_
         engine.score(X_local, None, m, fit.P64, fit.mean64, fit.inv_diag, want_T2=False, want_Q=False,
                      decision=self.decision, accept_out=out, accept_stride=1)

@@ -95,6 +95,43 @@ def test_sharded_simca_two_ranks_real_engine(tmp_path):
         assert diff.sum() <= 2, (cfg, int(diff.sum()))  # rows on the decision boundary only
 
 
+def _simca4_worker(rank, world, port, path):
+    import torch.distributed as dist
+
+    from ocm.dist import ShardedSIMCA
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        X, _ = _data()
+        bounds = [(0, 2100), (2100, 2100), (2100, 5000), (5000, 9000)]
+        lo, hi = bounds[rank]
+        m = ShardedSIMCA(n_components=8, type="alt", t2lim="Fdist", qlim="jm").fit(torch.from_numpy(X[lo:hi]).cuda())
+        acc = m.predict(torch.from_numpy(X[lo:hi]).cuda()).cpu()
+        got = [torch.empty(0)] * world
+        dist.all_gather_object(got, acc)
+        if rank == 0:
+            np.savez(path, lim=np.array([m.T2_limit, m.Q_limit, float(m.D_limit)]), acc=torch.cat(got).numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_simca_four_ranks_with_empty_rank(tmp_path):
+    """Four ranks on the one GPU (θ3 trace split four ways, one rank without
+    rows) against the single-process run of the real engine."""
+    from ocm.dist import ShardedSIMCA
+
+    path = str(tmp_path / "r4.npz")
+    _spawn(_simca4_worker, path, world=4, timeout=300)
+    got = np.load(path)
+    X, _ = _data()
+    Xd = torch.from_numpy(X).cuda()
+    ref = ShardedSIMCA(n_components=8, type="alt", t2lim="Fdist", qlim="jm").fit(Xd)
+    acc = ref.predict(Xd).cpu().numpy()
+    np.testing.assert_allclose(got["lim"], [ref.T2_limit, ref.Q_limit, float(ref.D_limit)], rtol=1e-5)
+    assert (got["acc"] != acc).sum() <= 2
+
+
 def _offset_data():
     """spectra on a large baseline with small variance (μ ≈ 1e3,
     tail λ ≈ 1e-6): each rank's moments are packed about ONE all-reduced
