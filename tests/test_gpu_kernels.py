@@ -116,6 +116,44 @@ def test_eig_no_gap_converges(eng):
     np.testing.assert_allclose(theta.cpu().numpy()[:2], [tail.sum(), (tail ** 2).sum()], rtol=1e-8)
 
 
+def test_eig_slow_decay_adaptive_rayleigh_ritz(eng):
+    """A spectrum whose k-th / (b+1)-th eigenvalue ratio is close to 1 (the
+    derivative spectra of the nuts preprocessing converge in ~30 iterations):
+    the predicted Rayleigh–Ritz schedule must still stop only at the tolerance,
+    with eigenpairs and θ equal to eigh's."""
+    rng = np.random.default_rng(21)
+    p, k = 512, 20
+    lam = np.geomspace(100.0, 0.01, p) * (1 + 0.01 * rng.random(p))
+    lam = np.sort(lam)[::-1]
+    Qm, _ = np.linalg.qr(rng.standard_normal((p, p)))
+    C = (Qm * lam) @ Qm.T
+    C = 0.5 * (C + C.T)
+    evals, evecs, theta, iters = eng.eig_topk(_dev(C), k, 2)
+    assert iters > 6  # the slow case really took the adaptive path
+    w, V = np.linalg.eigh(C)
+    w, V = w[::-1], V[:, ::-1]
+    np.testing.assert_allclose(evals.cpu().numpy(), w[:k], rtol=1e-9)
+    P = evecs.cpu().numpy()
+    for i in range(k):
+        v = V[:, i] * np.sign(V[np.argmax(np.abs(V[:, i])), i])
+        np.testing.assert_allclose(P[i], v, atol=1e-6)
+    tail = w[k:]
+    np.testing.assert_allclose(theta.cpu().numpy(), [tail.sum(), (tail ** 2).sum(), (tail ** 3).sum()],
+                               rtol=1e-8)
+
+
+def test_inv_evals_pinv_cutoff(eng):
+    """ocm_inv_evals_f64 = the diagonal of np.linalg.pinv(diag(λ)) (rcond 1e-15
+    relative to max |λ|): tiny and zero eigenvalues map to 0."""
+    import torch
+
+    lam = np.array([5.0, 1.0, 3e-15, 6e-15, 0.0, -2.0, 1e-3])
+    got = eng.inv_evals(torch.from_numpy(lam).cuda()).cpu().numpy()
+    want = np.diag(np.linalg.pinv(np.diag(lam), rcond=1e-15))
+    np.testing.assert_allclose(got, want, rtol=1e-14, atol=0)
+    assert got[2] == 0.0 and got[4] == 0.0 and got[3] != 0.0
+
+
 @pytest.mark.parametrize("k", [4, 20, 40])
 def test_score_matches_oracle(eng, k):
     import torch
