@@ -324,7 +324,9 @@ int ocm_snv_savgol_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, int
  * Householder tridiagonalisation on the GPU, QL eigenvalues and inverse-iteration vectors of the
  * tridiagonal on the host, back-transformation on the GPU.  Replaces the full spectrum of the
  * reference's SVD (utils/SIMCA.py:64-66,88 `eigs_all`; sklearn _pca.py:584-598) and is the fallback of
- * ocm_eig_topk when its subspace iteration does not converge.  Synchronises the stream. */
+ * ocm_eig_topk when its subspace iteration does not converge.  Synchronises the stream.
+ * Limits: 1 ≤ p ≤ 16384 for eigenvalues only (k = 0); p ≤ 12288 when k > 0 (checked before any
+ * work).  OCM_ERR_NOCONV if the implicit QL of the tridiagonal does not converge. */
 int ocm_eigh_f64(ocm_ctx* ctx, const double* C, int32_t p, double* evals_out, int32_t k, double* evecs_out,
                  void* stream);
 
@@ -396,9 +398,10 @@ int ocm_score_f32_diag_prep(ocm_ctx* ctx, const float* X, int64_t ldx, const int
  *   fp64 MFMA (v_mfma_f64_16x16x4f64), no digit split; arguments and outputs as
  *   ocm_gram_f32 (the float shift is exact in fp64), so ocm_cov_from_gram /
  *   ocm_gram_pack apply unchanged.
- * ocm_score_f64_diag: t = P·(x − μ), T² = Σ t²·a_diag, Q = ‖x − μ‖² − ‖t‖²
- *   (fp64: no cancellation issue at ≈1e-13 relative), fused decision and the
- *   moments, as ocm_score_f32_diag; T_out m×k float64, Q_out m float64; any
+ * ocm_score_f64_diag: t = P·(x − μ), T² = Σ t²·a_diag, and Q = ‖(x − μ) − Pᵀt‖²
+ *   as the explicit residual of the reconstruction X̂ = T·P + μ
+ *   (utils/SIMCA.py:67-68, 71), fused decision and the moments, as
+ *   ocm_score_f32_diag; T_out m×k float64 (nullable), Q_out m float64; any
  *   1 ≤ k ≤ p (component blocks of 64 beyond that).
  * ocm_decide_f64: ocm_decide with float64 Q. */
 int ocm_colmean_f64(ocm_ctx* ctx, const double* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,

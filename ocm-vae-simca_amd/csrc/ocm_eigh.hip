@@ -221,6 +221,8 @@ __global__ __launch_bounds__(TR_T) void k_rows_signfix(double* __restrict__ ev, 
 
 namespace ocm {
 
+constexpr int EIGH_VEC_MAXP = 96 * 1024 / (int)sizeof(double);  // 12288
+
 int eigh_dense(ocm_ctx* ctx, const double* C, int p, double* evals_out, int k, double* evecs_out, hipStream_t st) {
   const size_t pp = (size_t)p * p;
   const int nblk_max = (p + TR_T / 64 - 1) / (TR_T / 64);
@@ -259,14 +261,16 @@ int eigh_dense(ocm_ctx* ctx, const double* C, int p, double* evals_out, int k, d
   OCM_HIP(hipMemcpyAsync(hd.data(), d, (size_t)p * sizeof(double), hipMemcpyDeviceToHost, st));
   OCM_HIP(hipMemcpyAsync(he.data(), e, (size_t)p * sizeof(double), hipMemcpyDeviceToHost, st));
   OCM_HIP(hipStreamSynchronize(st));
-  host_tridiag_eigvals(hd.data(), he.data(), p, hev.data());
+  if (!host_tridiag_eigvals(hd.data(), he.data(), p, hev.data())) {
+    ocm::set_error("ocm_eigh_f64: implicit QL did not converge");
+    return OCM_ERR_NOCONV;
+  }
   OCM_HIP(hipMemcpyAsync(evals_out, hev.data(), (size_t)p * sizeof(double), hipMemcpyHostToDevice, st));
   if (k > 0 && evecs_out) {
     std::vector<double> hx((size_t)p * k);
     host_tridiag_invit(hd.data(), he.data(), p, hev.data(), k, hx.data());
     OCM_HIP(hipMemcpyAsync(X, hx.data(), hx.size() * sizeof(double), hipMemcpyHostToDevice, st));
     const size_t lds = (size_t)p * sizeof(double);
-    OCM_REQUIRE(lds <= 96 * 1024, "ocm_eigh_f64: eigenvectors need p <= 12288");
     hipLaunchKernelGGL(k_tri_backtransform, dim3(k), dim3(TR_T), lds, st, A, p, tau, X, k, evecs_out);
     hipLaunchKernelGGL(k_rows_signfix, dim3(k), dim3(TR_T), 0, st, evecs_out, p);
     OCM_CHECK_LAUNCH("k_tri_backtransform");
@@ -285,6 +289,9 @@ int ocm_eigh_f64(ocm_ctx* ctx, const double* C, int32_t p, double* evals_out, in
   OCM_REQUIRE(ctx && C && evals_out, "ocm_eigh_f64: NULL argument");
   OCM_REQUIRE(p >= 1 && p <= 16384, "ocm_eigh_f64: 1 <= p <= 16384");
   OCM_REQUIRE(k >= 0 && k <= p && (k == 0 || evecs_out), "ocm_eigh_f64: 0 <= k <= p (evecs_out for k > 0)");
+  // the back-transformation stages one p-vector in LDS (96 KiB): checked
+  // before any work starts
+  OCM_REQUIRE(k == 0 || p <= ocm::EIGH_VEC_MAXP, "ocm_eigh_f64: eigenvectors (k > 0) need p <= 12288");
   return ocm::eigh_dense(ctx, C, p, evals_out, k, evecs_out, (hipStream_t)stream);
 }
 

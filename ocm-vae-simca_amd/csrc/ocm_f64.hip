@@ -12,10 +12,13 @@
 //              split into chunks whose fp64 partials are summed in a fixed order.
 //              MFMA-bound: n·p(p+1) flops at the fp64 matrix rate.
 // k_score_f64  t = P·(x − μ) on the same MFMA (M = 16 components, N = 16
-//              spectra, K = 4 wavelengths per step), ‖x − μ‖² beside it, then
-//              Q = ‖y‖² − ‖t‖² (exact to ~1e-13 relative in fp64 — the identity
-//              the f32 kernels cannot afford), T² = Σ t²/λ, fused decision and
-//              the χ² moment partials.  One HBM pass; HBM/MFMA balanced at k ≤ 32.
+//              spectra, K = 4 wavelengths per step) and T² = Σ t²/λ.
+// k_qres_f64   Q = ‖(x − μ) − Pᵀt‖² as the reference forms it: the explicit
+//              residual X − (T·P + μ) (utils/SIMCA.py:67-68, 71), not the
+//              identity ‖y‖² − ‖t‖², which loses eps·‖y‖²/Q of Q's relative
+//              accuracy on nearly low-rank data; Pᵀt on the same MFMA (M = 16
+//              spectra, N = 16 wavelengths, K = 4 components per step), then the
+//              fused decision and the χ² moment partials.  Two reads of X.
 #include "ocm_internal.h"
 
 #include <algorithm>
@@ -196,9 +199,9 @@ __global__ __launch_bounds__(256) void k_gram_f64_reduce(const double* __restric
 // components (kb ≤ 16·NB); lane (row r16, k-slot ks) reads wavelengths
 // c0 + 4·ks + e of its row for the four MFMA steps e of a 16-column chunk (the
 // K order is permuted identically for P and y).
-// T²_in / TT_in (nullable): T² and ‖t‖² of earlier component blocks (k > 64).
-// TT_out (nullable): running ‖t‖² for the next block; the last block writes
-// Q = ‖y‖² − ‖t‖², T², the decision and the moments.
+// T2_in (nullable): T² of earlier component blocks (k > 64); T2_out: the sum
+// so far.  T_out (m × ldt, this block's columns) is always written: the
+// residual pass reads it.
 // ---------------------------------------------------------------------------
 template <int NB, int RB>
 __global__ __launch_bounds__(256) void k_score_f64(const double* __restrict__ X, int64_t ldx,
@@ -206,12 +209,7 @@ __global__ __launch_bounds__(256) void k_score_f64(const double* __restrict__ X,
                                                    const double* __restrict__ P, const double* __restrict__ mu,
                                                    const double* __restrict__ a_diag, int kb,
                                                    double* __restrict__ T_out, int64_t ldt,
-                                                   const double* T2_in, const double* TT_in,  // alias T2_out / TT_out
-                                                   double* T2_out, double* TT_out,
-                                                   double* __restrict__ Q_out, DecF64 dec,
-                                                   double* __restrict__ acc_out, int64_t acc_stride,
-                                                   double* __restrict__ stat_part) {
-  __shared__ double sred[16];
+                                                   const double* T2_in, double* T2_out) {  // T2_in may alias T2_out
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, ks = lane >> 4;
   const int64_t rbase = ((int64_t)blockIdx.x * 4 + wave) * (16 * RB);
@@ -237,9 +235,6 @@ __global__ __launch_bounds__(256) void k_score_f64(const double* __restrict__ X,
   for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) acc[nb][rb] = (f64x4){0.0, 0.0, 0.0, 0.0};
-  double yy[RB];
-#pragma unroll
-  for (int rb = 0; rb < RB; ++rb) yy[rb] = 0.0;
 
   struct Ld {
     double x[RB][4];
@@ -264,7 +259,6 @@ __global__ __launch_bounds__(256) void k_score_f64(const double* __restrict__ X,
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
         const double y = L.x[rb][e] - L.u[e];
-        yy[rb] += y * y;
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) acc[nb][rb] = __builtin_amdgcn_mfma_f64_16x16x4f64(L.w[nb][e], y, acc[nb][rb], 0, 0, 0);
       }
@@ -281,11 +275,10 @@ __global__ __launch_bounds__(256) void k_score_f64(const double* __restrict__ X,
 
   // lane (r16, ks) holds t for spectrum r16 of each row block, components
   // 16·nb + ks + 4r; the four k-slot lanes of a spectrum combine by shuffles
-  double st[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     const int64_t g = rbase + 16 * rb + r16;
-    double t2 = 0.0, tt = 0.0;
+    double t2 = 0.0;
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
@@ -294,35 +287,98 @@ __global__ __launch_bounds__(256) void k_score_f64(const double* __restrict__ X,
         const double t = acc[nb][rb][r];
         if (c < kb) {
           t2 += t * t * a_diag[c];
-          tt += t * t;
-          if (T_out && g < m) T_out[g * ldt + c] = t;
+          if (g < m) T_out[g * ldt + c] = t;
         }
       }
-    double y2 = yy[rb];
     t2 += __shfl_xor(t2, 16, 64);
     t2 += __shfl_xor(t2, 32, 64);
-    tt += __shfl_xor(tt, 16, 64);
-    tt += __shfl_xor(tt, 32, 64);
-    y2 += __shfl_xor(y2, 16, 64);
-    y2 += __shfl_xor(y2, 32, 64);
-    if (ks == 0 && g < m) {
-      if (T2_in) t2 += T2_in[g];
-      if (TT_in) tt += TT_in[g];
-      if (TT_out) {  // not the last block: carry the running sums
-        T2_out[g] = t2;
-        TT_out[g] = tt;
-      } else {
-        const double q = fmax(y2 - tt, 0.0);
-        if (T2_out) T2_out[g] = t2;
-        if (Q_out) Q_out[g] = q;
+    if (ks == 0 && g < m) T2_out[g] = T2_in ? T2_in[g] + t2 : t2;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_qres_f64: one wave per 16 spectra.  For each 16-wavelength chunk the
+// reconstruction (T·P)[i][c] is one 16×16 MFMA tile over the k components
+// (A = T rows: lane (i = l&15, kk = l>>4) holds T[i][4s + kk]; B = P: lane
+// (kk = l>>4, j = l&15) holds P[4s + kk][c0 + j]; D[i][j] in lane (j = l&15),
+// register r, i = (l>>4) + 4r); lane (j, kk) then forms r = (x − μ) − D for
+// its four spectra at wavelength c0 + j and accumulates r².  The 16 wavelength
+// lanes of a spectrum combine by shuffles.  Q, the fused decision (on the
+// final T²) and the χ² moment partials follow.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_qres_f64(const double* __restrict__ X, int64_t ldx,
+                                                  const int64_t* __restrict__ rows, int64_t m, int p,
+                                                  const double* __restrict__ P, const double* __restrict__ mu, int k,
+                                                  const double* __restrict__ T, const double* __restrict__ T2,
+                                                  double* __restrict__ Q_out, DecF64 dec,
+                                                  double* __restrict__ acc_out, int64_t acc_stride,
+                                                  double* __restrict__ stat_part) {
+  __shared__ double sred[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 15, kk = lane >> 4;
+  const int64_t rbase = ((int64_t)blockIdx.x * 4 + wave) * 16;
+  // A operand row (spectrum rbase + j) and the four spectra this lane's
+  // accumulator registers belong to (rbase + kk + 4r)
+  const int64_t ga = rbase + j;
+  const double* trow = T + (ga < m ? ga : m - 1) * (int64_t)k;
+  const double amask = ga < m ? 1.0 : 0.0;
+  const double* xr[4];
+  double rmask[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t g = rbase + kk + 4 * r;
+    const int64_t gc = g < m ? g : m - 1;
+    xr[r] = X + (rows ? rows[gc] : gc) * ldx;
+    rmask[r] = g < m ? 1.0 : 0.0;
+  }
+  const int nsteps = (k + 3) / 4;
+  double q[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int c0 = 0; c0 < p; c0 += 16) {
+    const int c = c0 + j;
+    const int cc = c < p ? c : p - 1;
+    const double cmask = c < p ? 1.0 : 0.0;
+    double y[4];
+    const double u = mu[cc];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] = xr[r][cc] - u;
+    f64x4 d = (f64x4){0.0, 0.0, 0.0, 0.0};
+    for (int s = 0; s < nsteps; ++s) {
+      const int comp = 4 * s + kk;
+      const int ce = comp < k ? comp : k - 1;
+      const double okc = comp < k ? 1.0 : 0.0;
+      const double a = trow[ce] * (amask * okc);
+      const double b = P[(int64_t)ce * p + cc] * (okc * cmask);
+      d = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, d, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double res = (y[r] - d[r]) * (cmask * rmask[r]);
+      q[r] += res * res;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    q[r] += __shfl_xor(q[r], 1, 64);
+    q[r] += __shfl_xor(q[r], 2, 64);
+    q[r] += __shfl_xor(q[r], 4, 64);
+    q[r] += __shfl_xor(q[r], 8, 64);
+  }
+  double st[4] = {0.0, 0.0, 0.0, 0.0};
+  if (j == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t g = rbase + kk + 4 * r;
+      if (g < m) {
+        const double t2 = T2[g];
+        Q_out[g] = q[r];
         if (dec.enabled) {
-          const double d = ocm::dred_of(dec.type, t2 * dec.t2_scale, q * dec.q_scale);
-          acc_out[g * acc_stride] = d < dec.dlim ? 1.0 : 0.0;
+          const double dd = ocm::dred_of(dec.type, t2 * dec.t2_scale, q[r] * dec.q_scale);
+          acc_out[g * acc_stride] = dd < dec.dlim ? 1.0 : 0.0;
         }
         st[0] += t2;
         st[1] += t2 * t2;
-        st[2] += q;
-        st[3] += q * q;
+        st[2] += q[r];
+        st[3] += q[r] * q[r];
       }
     }
   }
@@ -372,10 +428,9 @@ constexpr int SF_RB = 4;  // row blocks of 16 per wave
 template <int NB>
 void launch_score_f64(dim3 g, hipStream_t st, const double* X, int64_t ldx, const int64_t* rows, int64_t m, int p,
                       const double* P, const double* mu, const double* a, int kb, double* T, int64_t ldt,
-                      const double* T2_in, const double* TT_in, double* T2_out, double* TT_out, double* Q_out,
-                      DecF64 d, double* acc, int64_t acc_stride, double* part) {
+                      const double* T2_in, double* T2_out) {
   hipLaunchKernelGGL((k_score_f64<NB, SF_RB>), g, dim3(256), 0, st, X, ldx, rows, m, p, P, mu, a, kb, T, ldt, T2_in,
-                     TT_in, T2_out, TT_out, Q_out, d, acc, acc_stride, part);
+                     T2_out);
 }
 
 }  // namespace
@@ -463,49 +518,45 @@ int ocm_score_f64_diag(ocm_ctx* ctx, const double* X, int64_t ldx, const int64_t
   }
   const int64_t rows_per_wg = 4 * 16 * SF_RB;
   const int64_t nblk = (m + rows_per_wg - 1) / rows_per_wg;
-  OCM_REQUIRE(nblk < (1LL << 31), "ocm_score_f64_diag: too many rows");
+  const int64_t nblk_q = (m + 63) / 64;  // k_qres_f64: 64 spectra per workgroup
+  OCM_REQUIRE(nblk_q < (1LL << 31), "ocm_score_f64_diag: too many rows");
   constexpr int KB = 64;
   const int nkb = (k + KB - 1) / KB;
-  const size_t part_n = stats_out ? (size_t)nblk * 4 : 0;
-  const size_t run_n = nkb > 1 ? 2 * (size_t)m + (T2_out ? 0 : (size_t)m) : 0;
-  void* w = ocm::workspace(ctx, (part_n + run_n) * sizeof(double) + 1024, st);
+  const size_t part_n = stats_out ? (size_t)nblk_q * 4 : 0;
+  const size_t t_n = T_out ? 0 : (size_t)m * k;  // the residual pass needs T
+  const size_t t2_n = T2_out ? 0 : (size_t)m;
+  const size_t q_n = Q_out ? 0 : (size_t)m;
+  void* w = ocm::workspace(ctx, (part_n + t_n + t2_n + q_n) * sizeof(double) + 1024, st);
   if (!w) return OCM_ERR_NOMEM;
   ocm::Carve cv{static_cast<char*>(w)};
   double* part = stats_out ? cv.take<double>(part_n) : nullptr;
-  double* TTa = nkb > 1 ? cv.take<double>(m) : nullptr;
-  double* TTb = nkb > 1 ? cv.take<double>(m) : nullptr;
-  double* T2run = nkb > 1 ? (T2_out ? T2_out : cv.take<double>(m)) : T2_out;
+  double* Tw = T_out ? T_out : cv.take<double>((size_t)m * k);
+  double* T2w = T2_out ? T2_out : cv.take<double>(m);
+  double* Qw = Q_out ? Q_out : cv.take<double>(m);
   DecF64 d{};
   if (dec) d = DecF64{1, dec->type, dec->t2_scale, dec->q_scale, dec->dlim};
   const dim3 g((unsigned)nblk);
   for (int bk = 0; bk < nkb; ++bk) {
     const int c0 = bk * KB, kb = std::min(KB, k - c0);
-    const bool first = bk == 0, last = bk == nkb - 1;
-    double* Tb = T_out ? T_out + c0 : nullptr;
-    const double* T2i = first ? nullptr : T2run;
-    const double* TTi = first ? nullptr : (bk % 2 ? TTa : TTb);
-    double* TTo = last ? nullptr : (bk % 2 ? TTb : TTa);
-    double* T2o = last ? T2_out : T2run;
-    DecF64 db = last ? d : DecF64{};
     ocm::TimedRegion tr(ctx, OCM_KERNEL_SCORE, st);
     const double* Pb = P + (size_t)c0 * p;
     const double* ab = a_diag + c0;
-    double* acc = last ? accept_out : nullptr;
-    double* pt = last ? part : nullptr;
-    double* Qo = last ? Q_out : nullptr;
+    const double* T2i = bk == 0 ? nullptr : T2w;
     if (kb <= 16)
-      launch_score_f64<1>(g, st, X, ldx, rows, m, p, Pb, mu, ab, kb, Tb, k, T2i, TTi, T2o, TTo, Qo, db, acc,
-                          accept_stride, pt);
+      launch_score_f64<1>(g, st, X, ldx, rows, m, p, Pb, mu, ab, kb, Tw + c0, k, T2i, T2w);
     else if (kb <= 32)
-      launch_score_f64<2>(g, st, X, ldx, rows, m, p, Pb, mu, ab, kb, Tb, k, T2i, TTi, T2o, TTo, Qo, db, acc,
-                          accept_stride, pt);
+      launch_score_f64<2>(g, st, X, ldx, rows, m, p, Pb, mu, ab, kb, Tw + c0, k, T2i, T2w);
     else
-      launch_score_f64<4>(g, st, X, ldx, rows, m, p, Pb, mu, ab, kb, Tb, k, T2i, TTi, T2o, TTo, Qo, db, acc,
-                          accept_stride, pt);
+      launch_score_f64<4>(g, st, X, ldx, rows, m, p, Pb, mu, ab, kb, Tw + c0, k, T2i, T2w);
     OCM_CHECK_LAUNCH("k_score_f64");
   }
+  if (Q_out || dec || stats_out) {
+    hipLaunchKernelGGL(k_qres_f64, dim3((unsigned)nblk_q), dim3(256), 0, st, X, ldx, rows, m, p, P, mu, k, Tw, T2w,
+                       Qw, d, accept_out, accept_stride, part);
+    OCM_CHECK_LAUNCH("k_qres_f64");
+  }
   if (stats_out) {
-    hipLaunchKernelGGL(k_stats_reduce_f64, dim3(1), dim3(1024), 0, st, part, nblk, stats_out);
+    hipLaunchKernelGGL(k_stats_reduce_f64, dim3(1), dim3(1024), 0, st, part, nblk_q, stats_out);
     OCM_CHECK_LAUNCH("k_stats_reduce_f64");
   }
   return OCM_OK;

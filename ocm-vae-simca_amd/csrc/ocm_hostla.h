@@ -13,6 +13,10 @@
 
 namespace ocm {
 
+// implicit QL sweeps per eigenvalue before it counts as not converged (LAPACK
+// dsteqr allows 30·n in total; one eigenvalue takes 2-3 on average)
+constexpr int QL_MAX_ITER = 90;
+
 // S = L Lᵀ with the device kernels' pivot clamp (1e-14·max diag); M = L⁻ᵀ.
 inline void host_chol_inv_t(const double* S, int b, double* M) {
   std::vector<double> L((size_t)b * b, 0.0), Li((size_t)b * b, 0.0);
@@ -45,7 +49,9 @@ inline void host_chol_inv_t(const double* S, int b, double* M) {
 // Symmetric eigen-decomposition of n×n A (row-major; the symmetric part is
 // used): eigenvalues descending into ev, Z[i·n + j] = component i of
 // eigenvector j.
-inline void host_sym_eig(const double* A, int n, double* ev, double* Z) {
+// Returns false if some eigenvalue did not converge within QL_MAX_ITER implicit
+// QL sweeps (its value and vectors are then unreliable).
+inline bool host_sym_eig(const double* A, int n, double* ev, double* Z) {
   std::vector<double> a((size_t)n * n), d(n), e(n, 0.0), v(n), pv(n), z((size_t)n * n, 0.0);
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) a[(size_t)i * n + j] = 0.5 * (A[(size_t)i * n + j] + A[(size_t)j * n + i]);
@@ -102,8 +108,13 @@ inline void host_sym_eig(const double* A, int n, double* ev, double* Z) {
   }
   // implicit QL on (d, e), rotations accumulated into the columns of z
   const double eps = std::numeric_limits<double>::epsilon();
+  bool converged = true;
   for (int l = 0; l < n; ++l) {
-    for (int iter = 0; iter < 60; ++iter) {
+    for (int iter = 0;; ++iter) {
+      if (iter == QL_MAX_ITER) {
+        converged = false;
+        break;
+      }
       int m = l;
       for (; m + 1 < n; ++m) {
         const double dd = std::fabs(d[m]) + std::fabs(d[m + 1]);
@@ -152,16 +163,23 @@ inline void host_sym_eig(const double* A, int n, double* ev, double* Z) {
     ev[j] = d[ord[j]];
     for (int i = 0; i < n; ++i) Z[(size_t)i * n + j] = z[(size_t)i * n + ord[j]];
   }
+  return converged;
 }
 
 // Eigenvalues of the symmetric tridiagonal matrix (d[0..n-1] diagonal,
 // e[0..n-2] off-diagonal) by implicit QL without vectors; descending into ev.
-inline void host_tridiag_eigvals(const double* d_in, const double* e_in, int n, double* ev) {
+// Returns false if some eigenvalue did not converge within QL_MAX_ITER sweeps.
+inline bool host_tridiag_eigvals(const double* d_in, const double* e_in, int n, double* ev) {
   std::vector<double> d(d_in, d_in + n), e(n, 0.0);
   for (int i = 0; i + 1 < n; ++i) e[i] = e_in[i];
   const double eps = std::numeric_limits<double>::epsilon();
+  bool converged = true;
   for (int l = 0; l < n; ++l) {
-    for (int iter = 0; iter < 60; ++iter) {
+    for (int iter = 0;; ++iter) {
+      if (iter == QL_MAX_ITER) {
+        converged = false;
+        break;
+      }
       int m = l;
       for (; m + 1 < n; ++m) {
         const double dd = std::fabs(d[m]) + std::fabs(d[m + 1]);
@@ -200,6 +218,7 @@ inline void host_tridiag_eigvals(const double* d_in, const double* e_in, int n, 
   }
   std::sort(d.begin(), d.end(), [](double a, double b) { return a > b; });
   for (int i = 0; i < n; ++i) ev[i] = d[i];
+  return converged;
 }
 
 // Eigenvectors of the tridiagonal matrix for the k eigenvalues lam[0..k-1]

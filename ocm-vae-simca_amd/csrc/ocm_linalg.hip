@@ -1431,7 +1431,10 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     }
     int rc = proj_to_host(V, W);
     if (rc) return rc;
-    host_sym_eig(hmat, b, hmat + 2 * bb, hmat + bb);
+    if (!host_sym_eig(hmat, b, hmat + 2 * bb, hmat + bb)) {
+      ocm::set_error("ocm_eig_topk: implicit QL of the Rayleigh-Ritz problem did not converge");
+      return OCM_ERR_NOCONV;
+    }
     OCM_HIP(hipMemcpyAsync(Z, hmat + bb, bb * sizeof(double), hipMemcpyHostToDevice, st));
     OCM_HIP(hipMemcpyAsync(theta, hmat + 2 * bb, b * sizeof(double), hipMemcpyHostToDevice, st));
     return OCM_OK;

@@ -22,7 +22,8 @@ Aggregation is the reference's: spec = mean over folds of TN/(TN+FP)·100
 their own fold's prediction and other-class rows the LAST fold's
 (:190, 205-207), eff = √(sens·spec) (:208).
 
-Multi-GPU (``group`` given): each rank holds a contiguous row block of X
+Multi-GPU (``group`` given; the drop-in ``grid`` passes dist.group.WORLD
+when the process runs as one of W > 1 ranks): each rank holds a contiguous row block of X
 (``row_offset``) and the full label vector.  Fold f's eigensolve runs on
 its owner rank f mod W: every rank forms its local TRAIN Gram of fold f
 (Σ_g G_g − G_f, fp64 downdating on the device) and one RCCL reduce brings
@@ -115,7 +116,30 @@ def grid(base_est, X, y, cv, lv_values, param_grid, class_index, store_predictio
         class_index = [tl]
     y = np.asarray(y)
     folds = [cls_idx[test_rel] for _, test_rel in cv.kf.split(cls_idx)]
-    return cv_grid(X, y, folds, cls_idx, lv_values, combos, base, class_index, store_predictions)
+    group = _world_group_for(X, y)
+    if group is None:
+        return cv_grid(X, y, folds, cls_idx, lv_values, combos, base, class_index, store_predictions)
+    # Under torchrun (an initialised world of W > 1 ranks, each holding all
+    # len(y) rows, as an unchanged driver does) the drop-in is collective: rank
+    # r keeps its contiguous row block and the fold engine runs sharded (C3,
+    # SURVEY.md §8e).  Every rank returns the same records and predictions.
+    from .synth import shard_bounds
+
+    lo, hi = shard_bounds(int(y.shape[0]), dist.get_rank(group), dist.get_world_size(group))
+    return cv_grid(X[lo:hi], y, folds, cls_idx, lv_values, combos, base, class_index, store_predictions,
+                   row_offset=lo, group=group)
+
+
+def _world_group_for(X, y):
+    """dist.group.WORLD when a process group of more than one rank is
+    initialised and X holds every row of y; otherwise None (single process)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() < 2:
+        return None
+    if int(X.shape[0]) != int(np.asarray(y).shape[0]):
+        raise ValueError(f"cross_validate_simca_grid under a process group of {dist.get_world_size()} ranks: X has "
+                         f"{int(X.shape[0])} rows but y has {int(np.asarray(y).shape[0])}; pass every rank the full "
+                         "X (the drop-in shards it), or call ocm.cv.cv_grid(..., row_offset=, group=) with a block")
+    return dist.group.WORLD
 
 
 class FoldModels:
@@ -169,8 +193,9 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
     lo, hi = row_offset, row_offset + n_loc
     y = np.asarray(y)
     n_glob = y.shape[0]
-    distributed = group is not None or (dist.is_available() and dist.is_initialized()
-                                        and dist.get_world_size() > 1)
+    # cross-rank only when a group is passed explicitly (``grid`` passes WORLD
+    # under torchrun); an initialised process group alone changes nothing
+    distributed = group is not None
     W = dist.get_world_size(group) if distributed else 1
     R = dist.get_rank(group) if distributed else 0
     K = len(folds)

@@ -68,9 +68,16 @@ def _moments(v: torch.Tensor, group=None):
 
 
 def _world(group) -> int:
+    """Ranks a statistic spans: 1 unless a process group is passed EXPLICITLY.
+    An initialised default group alone never makes a statistic cross-rank —
+    the reference's statistics are per call (compute_q_h_f per batch,
+    vae_model.py:162-182), so a DDP driver that calls them per rank must get
+    per-rank numbers; pass ``group=dist.group.WORLD`` to pool every rank's rows."""
+    if group is None:
+        return 1
     import torch.distributed as dist
 
-    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    return dist.get_world_size(group)
 
 
 def _latent_cov(Z: torch.Tensor, group=None):

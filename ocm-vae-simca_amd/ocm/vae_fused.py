@@ -187,36 +187,46 @@ class FusedAdam:
                 p.grad.zero_()
 
     def _write_table(self, capturing: bool):
-        key = tuple(p.grad.data_ptr() for p in self.params)
+        """Entries for the parameters that have a gradient this step; like
+        torch.optim.Adam, a parameter whose .grad is None is skipped (its
+        moments are left alone).  The step counter is shared, so a parameter
+        skipped on some steps sees the optimizer's step count in its bias
+        correction, not its own (torch keeps one per parameter)."""
+        key = tuple(p.grad.data_ptr() if p.grad is not None else None for p in self.params)
         if key == self._key:
             return
-        arr = (self._Entry * len(self.params))()
+        live = [i for i, p in enumerate(self.params) if p.grad is not None]
+        arr = (self._Entry * max(len(live), 1))()
         o = 0
-        for i, p in enumerate(self.params):
+        for j, i in enumerate(live):
+            p = self.params[i]
             if not (p.is_contiguous() and p.grad.is_contiguous() and p.grad.dtype == torch.float32):
                 raise RuntimeError("FusedAdam: contiguous float32 parameters and gradients only")
-            arr[i] = self._Entry(p.data_ptr(), p.grad.data_ptr(), self.exp_avg[i].data_ptr(),
+            arr[j] = self._Entry(p.data_ptr(), p.grad.data_ptr(), self.exp_avg[i].data_ptr(),
                                  self.exp_avg_sq[i].data_ptr(), o, p.numel())
             o += p.numel()
+        self._n_live, self._total_live = len(live), o
         raw = torch.frombuffer(bytearray(arr), dtype=torch.uint8)
         if capturing:  # written once after the capture (the graph replays the capture's addresses)
             self._pending = raw.clone()
         else:  # eager steps: a synchronous copy (the host staging is reused next step)
-            self.table.copy_(raw.to(self.table.device))
+            self.table[:raw.numel()].copy_(raw.to(self.table.device))
         self._key = key
 
     def flush_pending(self):
         """After a graph capture: the table of the captured step's gradients."""
         if getattr(self, "_pending", None) is not None:
-            self.table.copy_(self._pending.to(self.table.device))
+            self.table[:self._pending.numel()].copy_(self._pending.to(self.table.device))
             torch.cuda.synchronize(self.table.device)
             self._pending = None
 
     def step(self):
         capturing = torch.cuda.is_current_stream_capturing()
         self._write_table(capturing)
+        if self._n_live == 0:
+            return
         dev = self.table.device
-        check(_lib.load().ocm_adam_step(_h(dev), ptr(self.table), len(self.params), self.total, ptr(self.step_t),
+        check(_lib.load().ocm_adam_step(_h(dev), ptr(self.table), self._n_live, self._total_live, ptr(self.step_t),
                                         self.lr, self.b1, self.b2, self.eps, self.wd, ptr(self.scratch),
                                         stream_handle(dev)), "ocm_adam_step")
 
@@ -236,16 +246,20 @@ def _cast_multi(srcs, dsts, sdt, ddt, dev):
 
 class _CastBF16(torch.autograd.Function):
     """float32 parameters → bfloat16 copies (one launch); the backward turns
-    their bfloat16 gradients into float32 ones (one launch), written straight
-    into the parameters' .grad views when every parameter has one (the flat
-    all-reduce buffer of the data-parallel step), else returned."""
+    their bfloat16 gradients into float32 ones (one launch) and returns them,
+    so autograd accumulates them into .grad like any gradient.  Only when the
+    caller says every .grad is a freshly zeroed view (``into_zeroed_grads``:
+    the data-parallel step zeroes its flat all-reduce buffer first) are they
+    written straight into the views instead (no accumulate kernel); that
+    equals accumulation because the views hold zeros."""
 
     @staticmethod
-    def forward(ctx, *params):
+    def forward(ctx, into_zeroed_grads, *params):
         outs = [torch.empty_like(p, dtype=torch.bfloat16, memory_format=torch.contiguous_format) for p in params]
         _cast_multi([p.detach().contiguous() for p in params], outs, _DT[torch.float32], _DT[torch.bfloat16],
                     params[0].device)
         ctx.params = params
+        ctx.into_zeroed = bool(into_zeroed_grads)
         ctx.set_materialize_grads(False)
         return tuple(outs)
 
@@ -254,15 +268,15 @@ class _CastBF16(torch.autograd.Function):
         params = ctx.params
         live = [(p, g) for p, g in zip(params, grads) if g is not None]
         if not live:
-            return (None,) * len(params)
-        into_views = all(p.grad is not None and p.grad.is_contiguous() for p, _ in live)
+            return (None,) * (len(params) + 1)
+        into_views = ctx.into_zeroed and all(p.grad is not None and p.grad.is_contiguous() for p, _ in live)
         outs = [p.grad if into_views else torch.empty_like(p, memory_format=torch.contiguous_format)
                 for p, _ in live]
         _cast_multi([g.contiguous() for _, g in live], outs, _DT[torch.bfloat16], _DT[torch.float32],
                     params[0].device)
         if into_views:
-            return (None,) * len(params)
-        res, k = [], 0
+            return (None,) * (len(params) + 1)
+        res, k = [None], 0
         for g in grads:
             if g is None:
                 res.append(None)
@@ -272,8 +286,9 @@ class _CastBF16(torch.autograd.Function):
         return tuple(res)
 
 
-def cast_bf16(*params):
-    return _CastBF16.apply(*params)
+def cast_bf16(*params, into_zeroed_grads: bool = False):
+    """bf16 copies of ``params``; see _CastBF16 for ``into_zeroed_grads``."""
+    return _CastBF16.apply(into_zeroed_grads, *params)
 
 
 def standardise(x: torch.Tensor, mean: torch.Tensor, std: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:

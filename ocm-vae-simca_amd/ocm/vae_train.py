@@ -16,18 +16,18 @@ autocast (the loss, BN statistics and Adam state stay fp32).
 Multi-GPU (C5): one process per GPU, pass the bare model and
 the process group.  The trainer broadcasts rank 0's parameters and buffers,
 points every parameter's .grad into one flat fp32 buffer, and after the
-backward pass all-reduces that buffer once (one RCCL call over xGMI, 3.2 MB
-at L = 2048, 6.4 MB at L = 4096) and divides by the world size — DDP's
-gradient averaging, captured into the same HIP graph as the step, so a
-replay is still one launch.  BatchNorm statistics stay per rank, as in DDP;
+backward pass all-reduces that buffer once with ncclAvg (one RCCL call over
+xGMI, 3.2 MB at L = 2048, 6.4 MB at L = 4096) — DDP's gradient averaging,
+captured into the same HIP graph as the step, so a replay is still one
+launch.  The trainer's collectives run on an RCCL communicator of its own
+(ocm/rccl.py), never on ProcessGroupNCCL, whose watchdog aborts the process
+if it polls an event during a capture.  BatchNorm statistics stay per rank, as in DDP;
 ``sync_buffers()`` copies rank 0's running statistics to every rank
 (DDP's broadcast_buffers) before evaluation.
 """
 from __future__ import annotations
 
 import os
-
-import time
 
 import torch
 import torch.distributed as dist
@@ -80,7 +80,17 @@ class GraphedVAETrainer:
         self.world = dist.get_world_size(group) if distributed else 1
         # data-parallel gradient averaging (None: whenever the world has > 1 rank)
         self.allreduce = (self.world > 1) if grad_allreduce is None else bool(grad_allreduce and distributed)
+        # the trainer's collectives run on an RCCL communicator of its own
+        # (ocm/rccl.py) when the group is RCCL's: none of them is ever tracked
+        # by a ProcessGroupNCCL watchdog, which would abort the process if it
+        # polled one while the step is being captured; gloo groups (CPU, or
+        # several ranks sharing one GPU in tests) use torch.distributed
+        self._comm = None
         if self.allreduce:
+            if dev.type == "cuda" and "nccl" in str(dist.get_backend(group)):
+                from .rccl import Communicator
+
+                self._comm = Communicator(group, dev)
             self._flatten_grads(dev)
             self._broadcast_state()
         self.beta = float(beta)
@@ -140,19 +150,33 @@ class GraphedVAETrainer:
             o += p.numel()
 
     def _broadcast_state(self):
-        src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+        self._broadcast(self.module.state_dict().values())
+
+    def _broadcast(self, tensors):
+        """Group rank 0's values of ``tensors`` on every rank, in place."""
         with torch.no_grad():
-            for t in self.module.state_dict().values():
+            if self._comm is not None:
+                for t in tensors:
+                    self._comm.broadcast(t, 0)
+                return
+            src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+            for t in tensors:
                 dist.broadcast(t, src=src, group=self.group)
+
+    def _average_grads(self):
+        """DDP averaging: one all-reduce of the flat gradient (ncclAvg on the
+        trainer's communicator: the division runs inside the collective)."""
+        if self._comm is not None:
+            self._comm.all_reduce(self.flat_grad, average=True)
+        else:
+            dist.all_reduce(self.flat_grad, group=self.group)
+            self.flat_grad.div_(self.world)
 
     def sync_buffers(self):
         """Rank 0's BatchNorm running statistics on every rank (DDP broadcast_buffers)."""
         if not self.allreduce:
             return
-        src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
-        with torch.no_grad():
-            for b in self.module.buffers():
-                dist.broadcast(b, src=src, group=self.group)
+        self._broadcast(list(self.module.buffers()))
 
     def _body(self):
         # one process: gradients set to None, so backward hands each parameter
@@ -179,9 +203,8 @@ class GraphedVAETrainer:
         kl = V.kl_term(mu, logvar)
         total = recon + self.beta * kl
         total.backward()
-        if self.allreduce:  # DDP averaging: one RCCL all-reduce of the flat gradient
-            dist.all_reduce(self.flat_grad, group=self.group)
-            self.flat_grad.div_(self.world)
+        if self.allreduce:
+            self._average_grads()
         self.opt.step()
         return total.detach(), recon.detach(), kl.detach()
 
@@ -192,7 +215,9 @@ class GraphedVAETrainer:
         reconstruction term and the total (one launch)."""
         m = self.module
         if self.dtype == torch.bfloat16 and self._lin:
-            casted = self._vf.cast_bf16(*[p for _, p in self._lin])
+            # the flat all-reduce buffer was zeroed above: the cast's backward
+            # may write the Linear gradients straight into its views
+            casted = self._vf.cast_bf16(*[p for _, p in self._lin], into_zeroed_grads=self.allreduce)
             xin = self._vf.standardise(self.x, m.spec_mean, m.spec_std)
             with torch.autocast("cuda", dtype=self.dtype):
                 xs, kl = torch.func.functional_call(self._fwd, dict(zip([n for n, _ in self._lin], casted)), (xin,))
@@ -201,9 +226,8 @@ class GraphedVAETrainer:
                 xs, kl = self._fwd((self.x - m.spec_mean) / m.spec_std)
         total, recon = self._vf.recon_total(self.x, xs, kl, self._rbufs, self.loss, self.beta)
         total.backward()
-        if self.allreduce:  # DDP averaging: one RCCL all-reduce of the flat gradient
-            dist.all_reduce(self.flat_grad, group=self.group)
-            self.flat_grad.div_(self.world)
+        if self.allreduce:
+            self._average_grads()
         self.opt.step()
         return total.detach(), recon, kl.detach()
 
@@ -220,19 +244,20 @@ class GraphedVAETrainer:
                 self._body()
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        # With the gradient all-reduce in the graph the process group's watchdog
-        # thread polls the warm-up collectives' events; under the default
-        # (global) capture mode such a query from another thread during the
-        # capture fails with hipErrorStreamCaptureUnsupported and the watchdog
-        # aborts the process.  Drain the warm-up work first and capture in
-        # thread-local mode, which leaves other threads' HIP calls alone.
+        # A ProcessGroupNCCL watchdog that polls a collective's end event while
+        # any stream is capturing is refused by HIP and aborts the process
+        # (round 4, DESIGN.md §5 caveat 5).  The trainer's own collectives are
+        # on its RCCL communicator and never tracked (ocm/rccl.py); eager
+        # collectives the CALLER issued on its process group just before are
+        # waited out on the watchdogs' own records (flight recorder).
         mode = "global"
         if self.allreduce:
-            torch.cuda.synchronize()
-            # the watchdog drops a finished collective on its next poll (every
-            # 100 ms); one still listed is queried during the capture, which
-            # HIP refuses even in thread-local mode (seen once in round 4)
-            time.sleep(0.35)
+            if self._comm is None:
+                raise ValueError("GraphedVAETrainer(graph=True) with a gradient all-reduce needs an RCCL ('nccl') "
+                                 "process group; pass graph=False for a gloo group")
+            from .rccl import wait_pg_collectives_retired
+
+            self.pending_at_capture = wait_pg_collectives_retired()
             mode = "thread_local"
         with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.out = self._body()

@@ -30,6 +30,13 @@ def main():
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    # the round-4 abort: an eager ProcessGroupNCCL collective still tracked by
+    # its watchdog when the step is captured.  Issue one right before the
+    # trainer, so its capture has to wait it out (ocm/rccl.py)
+    from ocm.rccl import pending_pg_collectives
+
+    dist.all_reduce(torch.ones(4, device=dev))
+    pending_before = pending_pg_collectives()
     tr = GraphedVAETrainer(m1, B, lr=1e-3, dtype=torch.bfloat16, graph=True, grad_allreduce=True)
     lo, hi = tr.flat_grad.data_ptr(), tr.flat_grad.data_ptr() + tr.flat_grad.numel() * 4
     views = all(lo <= p.grad.data_ptr() < hi for p in m1.parameters())
@@ -43,6 +50,8 @@ def main():
     tr.sync_buffers()
     torch.cuda.synchronize()
     print(json.dumps({"allreduce": tr.allreduce, "graphed": tr.graphed, "grads_are_views": views,
+                      "own_comm": tr._comm is not None, "pending_before": pending_before,
+                      "pending_at_capture": tr.pending_at_capture, "pending_after": pending_pg_collectives(),
                       "loss_ddp": la.cpu().tolist(), "loss_single": lb.cpu().tolist(),
                       "params_finite": all(bool(torch.isfinite(p).all()) for p in m1.parameters())}), flush=True)
     sys.stdout.flush()

@@ -116,7 +116,8 @@ def _worker(rank, world, port, path, X, y, bounds, grid):
 
         od.percentile_sharded = pct_sharded
         lo, hi = bounds[rank]
-        recs, by = _run_fold_engine(X, y, 4, [2, 3, 4], grid, row_offset=lo, Xlocal=X[lo:hi])
+        recs, by = _run_fold_engine(X, y, 4, [2, 3, 4], grid, row_offset=lo, group=dist.group.WORLD,
+                                    Xlocal=X[lo:hi])
         if rank == 0:
             np.savez(path, spec=[r["spec"] for r in recs], sens=[r["sens"] for r in recs],
                      pred=np.stack([b["prediction"] for b in by]))
@@ -158,3 +159,74 @@ def test_generic_loop_accepts_tensor_predictions():
 
     got = _fold_predictions(Est(), torch.zeros((5, 3)), np.zeros(5))
     assert isinstance(got, np.ndarray) and got.shape == (5,) and got.sum() == 5
+
+
+def _grid_hook_worker(rank, world, port, path, X, y, grid):
+    """Both ranks call the drop-in hook ocm.cv.grid with the FULL X, as
+    utils.cross_validate_simca_grid does under torchrun."""
+    import torch.distributed as dist
+
+    import ocm.cv as fe
+    import ocm.dist as od
+    from utils.CVSIMCA import ClasswiseKFoldWithExternalVal
+    from utils.SIMCA import SIMCA
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        fe.engine = fake_engine
+
+        def pct_sharded(v, pct, n_total, group=None):
+            got = [None] * world
+            dist.all_gather_object(got, v.numpy(), group=group)
+            return float(np.percentile(np.concatenate(got), pct))
+
+        od.percentile_sharded = pct_sharded
+        seen = []
+        orig = fe.cv_grid
+
+        def spy(*a, **k):
+            seen.append((k.get("group") is not None, int(k.get("row_offset", 0)), int(a[0].shape[0])))
+            return orig(*a, **k)
+
+        fe.cv_grid = spy
+        recs, by = fe.grid(SIMCA(verbose=False), X, y, ClasswiseKFoldWithExternalVal(n_splits=4, cls_label=0),
+                           [2, 3, 4], grid, None, True)
+        np.savez(path + f".{rank}.npz", spec=[r["spec"] for r in recs], sens=[r["sens"] for r in recs],
+                 pred=np.stack([b["prediction"] for b in by]), seen=np.array(seen))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dropin_hook_shards_under_world_group(golden_dir, tmp_path, restore_engine):
+    """under an initialised world of two ranks the drop-in hook
+    gives each rank its contiguous row block (group = WORLD) and both ranks get
+    the single-process records; with no process group it runs on all rows."""
+    import ocm.cv as fe
+    from utils.CVSIMCA import ClasswiseKFoldWithExternalVal
+    from utils.SIMCA import SIMCA
+
+    g = _load(golden_dir, "cv_a.npz")
+    X, y = g["X"], g["y"]
+    grid = {"type": ["alt", "ci"], "t2lim": ["perc", "Fdist"], "qlim": ["perc", "jm"]}
+    path = str(tmp_path / "hook")
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_grid_hook_worker, args=(r, 2, port, path, X, y, grid)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    fe.engine = fake_engine
+    recs, by = fe.grid(SIMCA(verbose=False), X, y, ClasswiseKFoldWithExternalVal(n_splits=4, cls_label=0),
+                       [2, 3, 4], grid, None, True)
+    n = X.shape[0]
+    for r in range(2):
+        got = np.load(path + f".{r}.npz")
+        from ocm.synth import shard_bounds
+
+        lo, hi = shard_bounds(n, r, 2)
+        assert got["seen"].tolist() == [[1, lo, hi - lo]]
+        np.testing.assert_allclose(got["spec"], [x["spec"] for x in recs], atol=1e-9)
+        np.testing.assert_allclose(got["sens"], [x["sens"] for x in recs], atol=1e-9)
+        np.testing.assert_array_equal(got["pred"], np.stack([b["prediction"] for b in by]))

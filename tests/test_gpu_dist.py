@@ -211,8 +211,10 @@ def _cv_run(rank=0, world=1):
     combos = [{"type": "alt", "t2lim": "Fdist", "qlim": "jm"}, {"type": "ci", "t2lim": "perc", "qlim": "chi2pom"}]
     base = dict(n_components=2, model_class=None, type="alt", t2lim="Fdist", t2cl=0.95, qlim="jm", qcl=0.95,
                 dcl=0.95, maxPC=20, criteria="compl", verbose=False)
+    import torch.distributed as dist
+
     recs, by = fe.cv_grid(torch.from_numpy(X[lo:hi]).cuda(), y, folds, cls_idx, [6, 7, 8], combos, base, [0], True,
-                          row_offset=lo)
+                          row_offset=lo, group=dist.group.WORLD if world > 1 else None)
     return {"spec": np.array([r["spec"] for r in recs]), "sens": np.array([r["sens"] for r in recs]),
             "pred": np.stack([np.asarray(b["prediction"]) for b in by])}
 
@@ -226,3 +228,96 @@ def test_cv_fold_engine_two_ranks_real_engine(tmp_path):
     np.testing.assert_allclose(got["sens"], ref["sens"], atol=1e-9)
     diff = got["pred"] != ref["pred"]
     assert diff.sum() <= 2, int(diff.sum())
+
+
+def _cv_dropin_data():
+    from oracle import simca_oracle as O
+
+    X0 = O.synth_spectra(2400, 256, 8, rank=24, seed=21)
+    X1 = O.synth_spectra(600, 256, 8, rank=24, seed=22, outlier_frac=1.0)
+    X = np.concatenate([X0, X1]).astype(np.float32)
+    y = np.concatenate([np.zeros(2400, np.int64), np.ones(600, np.int64)])
+    return X, y
+
+
+CV_GRID = {"type": ["alt", "ci"], "t2lim": ["Fdist", "perc"], "qlim": ["jm", "perc"]}
+
+
+def _cv_dropin_run():
+    """The reference entry point, unchanged: utils.cross_validate_simca_grid on
+    the FULL X (utils/CVSIMCA.py:103-269).  Returns its records and pooled
+    predictions plus the ``group`` the fold engine was called with."""
+    import contextlib
+    import io
+
+    import ocm.cv as fe
+    from utils import SIMCA, ClasswiseKFoldWithExternalVal, cross_validate_simca_grid
+
+    X, y = _cv_dropin_data()
+    seen = []
+    orig = fe.cv_grid
+
+    def spy(*a, **k):
+        seen.append((k.get("group") is not None, int(k.get("row_offset", 0)), int(a[0].shape[0])))
+        return orig(*a, **k)
+
+    fe.cv_grid = spy
+    try:
+        with contextlib.redirect_stdout(io.StringIO()):
+            res = cross_validate_simca_grid(SIMCA(verbose=False), X, y, ClasswiseKFoldWithExternalVal(n_splits=5,
+                                            cls_label=0), LV_min=6, LV_max=8, param_grid=CV_GRID,
+                                            print_summary=False, store_predictions=True)
+    finally:
+        fe.cv_grid = orig
+    recs = res["results"]
+    return {"spec": np.array([r["spec"] for r in recs]), "sens": np.array([r["sens"] for r in recs]),
+            "pred": np.stack([np.asarray(b["prediction"]) for b in res["by_combo"]]),
+            "best_lv": np.array(res["best_LV"]), "seen": np.array(seen, dtype=np.int64)}
+
+
+def _cv_dropin_worker(rank, world, port, path):
+    import os
+
+    import torch.distributed as dist
+
+    import vae_model as V
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        res = _cv_dropin_run()
+        # compute_q_h_f under an initialised group stays per batch
+        # (vae_model.py:162-182): every rank gets the reference's numbers
+        g = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "qhf.npz")))
+        q, h, f, qc, hc, fc = V.compute_q_h_f(torch.from_numpy(g["x"]).cuda(), torch.from_numpy(g["x_rec"]).cuda(),
+                                              torch.from_numpy(g["z"]).cuda())
+        res.update(q=q.cpu().numpy(), h=h.cpu().numpy(), f=f.cpu().numpy(), crit=np.array([qc, hc, fc]))
+        np.savez(path + f".{rank}.npz", **res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cv_dropin_under_process_group_shards_and_matches(tmp_path, golden_dir):
+    """an unchanged driver under torchrun (two ranks, each
+    calling utils.cross_validate_simca_grid on the full X, a perc combo
+    included) runs the fold engine row-sharded — each rank on its contiguous
+    block, group = WORLD — and both ranks return the single-process records
+    and pooled predictions; compute_q_h_f under the same group equals the
+    reference fixture (qhf.npz) on every rank."""
+    path = str(tmp_path / "dropin")
+    _spawn(_cv_dropin_worker, path)
+    ref = _cv_dropin_run()
+    assert ref["seen"].tolist() == [[0, 0, 3000]]  # one process: no group, all rows
+    g = np.load(f"{golden_dir}/qhf.npz")
+    for r in range(2):
+        got = np.load(path + f".{r}.npz")
+        assert got["seen"].tolist() == [[1, [0, 1500][r], 1500]], got["seen"]
+        np.testing.assert_allclose(got["spec"], ref["spec"], atol=1e-9)
+        np.testing.assert_allclose(got["sens"], ref["sens"], atol=1e-9)
+        diff = got["pred"] != ref["pred"]
+        assert diff.sum() <= 2 * got["pred"].shape[0], int(diff.sum())  # boundary rows only
+        assert int(got["best_lv"]) == int(ref["best_lv"])
+        np.testing.assert_allclose(got["q"], g["q"], rtol=1e-5)
+        np.testing.assert_allclose(got["h"], g["h"], rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(got["f"], g["f"], rtol=1e-4)
+        np.testing.assert_allclose(got["crit"], g["crit"], rtol=1e-4)

@@ -137,3 +137,56 @@ def test_drop_in_float64_vs_fp64_oracle():
     np.testing.assert_array_equal(pred[clear], (d < dl)[clear].astype(float))
     T2, _, Q, _ = est.transform(Xt)
     assert Q.dtype == np.float64
+
+
+def _near_low_rank(n=6000, p=512, k=20, seed=31):
+    """Rank-k spectra (λ₁ ≈ 100) plus an isotropic tail of λ ≈ 1e-8 = 1e-10·λ₁,
+    on a baseline of 3: ‖y‖² is ~1e10 × Q, so Q = ‖y‖² − ‖t‖² would keep only
+    ≈ 6 of its 16 digits (eps·‖y‖²/Q ≈ 1e-6)."""
+    rng = np.random.default_rng(seed)
+    scores = rng.standard_normal((n, k)) * np.geomspace(10, 1, k)
+    basis = np.linalg.qr(rng.standard_normal((p, k)))[0].T
+    return scores @ basis + 1e-4 * rng.standard_normal((n, p)) + 3.0
+
+
+def test_score_f64_q_is_explicit_residual_near_low_rank():
+    """on nearly exact low-rank data Q is the explicit residual
+    Σ(x − (t·P + μ))² (utils/SIMCA.py:67-68, 71) to 1e-8 relative — the
+    identity ‖y‖² − ‖t‖² misses that by orders of magnitude here."""
+    from ocm import engine
+
+    X = _near_low_rank()
+    k = 20
+    mu = X.mean(0)
+    Y = X - mu
+    P = np.linalg.svd(Y, full_matrices=False)[2][:k].copy()
+    lam = (Y @ P.T).var(0, ddof=1)
+    out = engine.score(_dev(X), None, X.shape[0], _dev(P), _dev(mu), _dev(1.0 / lam), want_T=True)
+    T = Y @ P.T
+    Q = ((Y - T @ P) ** 2).sum(1)
+    q_ident = (Y ** 2).sum(1) - (T ** 2).sum(1)
+    assert np.max(np.abs(q_ident - Q) / Q) > 1e-7  # the identity is NOT good enough on this data
+    np.testing.assert_allclose(out["Q"].cpu().numpy(), Q, rtol=1e-8)
+    np.testing.assert_allclose(out["T2"].cpu().numpy(), (T * T / lam).sum(1), rtol=1e-10)
+
+
+@pytest.mark.timeout(300)
+def test_drop_in_float64_near_low_rank_vs_oracle():
+    """The drop-in's float64 fit and predict on the same data against the fp64
+    oracle (explicit residuals): Q at rtol 1e-6, T² 1e-8, both limits."""
+    from oracle import simca_oracle as O
+    from utils import SIMCA
+
+    X = _near_low_rank()
+    Xf, Xt = X[:5000], X[5000:]
+    y = np.zeros(len(Xf), dtype=np.int64)
+    est = SIMCA(n_components=20, model_class=0, verbose=False).fit(Xf, y)
+    orc = O.OracleSIMCA(n_components=20, model_class=0, precision="gram").fit(Xf, y)
+    m, mo = est._model[0], orc._model[0]
+    np.testing.assert_allclose(m["Q"], mo["Q"], rtol=1e-6)
+    np.testing.assert_allclose(m["T2"], mo["T2"], rtol=1e-8)
+    np.testing.assert_allclose([m["T2_limit"], m["Q_limit"]], [mo["T2_limit"], mo["Q_limit"]], rtol=1e-6)
+    T2, _, Q, _ = est.transform(Xt)
+    _, T2o, Qo = orc._scores(Xt, mo)
+    np.testing.assert_allclose(Q, Qo, rtol=1e-6)
+    np.testing.assert_allclose(T2, T2o, rtol=1e-8)

@@ -30,12 +30,12 @@ int main(int argc, char** argv) {
   if (std::fread(A.data(), 8, A.size(), f) != A.size()) return 2;
   std::fclose(f);
   if (mode[0] == 'e') {
-    ocm::host_sym_eig(A.data(), n, out.data() + (size_t)n * n, out.data());
+    if (!ocm::host_sym_eig(A.data(), n, out.data() + (size_t)n * n, out.data())) return 3;  // QL cap hit
   } else if (mode[0] == 't') {  // tridiagonal: eigenvalues by QL, the top k vectors by inverse iteration
     std::vector<double> d(n), e(n > 1 ? n - 1 : 1);
     for (int i = 0; i < n; ++i) d[i] = A[(size_t)i * n + i];
     for (int i = 0; i + 1 < n; ++i) e[i] = A[(size_t)(i + 1) * n + i];
-    ocm::host_tridiag_eigvals(d.data(), e.data(), n, out.data() + (size_t)n * n);
+    if (!ocm::host_tridiag_eigvals(d.data(), e.data(), n, out.data() + (size_t)n * n)) return 3;
     const int k = n < 12 ? n : 12;
     ocm::host_tridiag_invit(d.data(), e.data(), n, out.data() + (size_t)n * n, k, out.data());
   } else {

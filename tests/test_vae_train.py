@@ -239,6 +239,10 @@ def test_c4_graph_step_with_grad_allreduce():
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["allreduce"] and res["graphed"] and res["grads_are_views"]
+    # the trainer's collectives ran on its own RCCL communicator; the caller's
+    # eager all-reduce was retired by the watchdog before the capture started
+    assert res["own_comm"] and not res["pending_after"]
+    print("flight recorder: pending before", res["pending_before"], "at capture", res["pending_at_capture"])
     la, lb = np.array(res["loss_ddp"]), np.array(res["loss_single"])
     assert np.isfinite(la).all() and np.isfinite(lb).all() and res["params_finite"]
     assert la[-5:].mean() < la[0]
@@ -347,3 +351,87 @@ def test_fused_adam_matches_torch_adam():
         ta.step()
     for a, b in zip(p1, p2):
         torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+@pytest.mark.parametrize("layout", ["grad_none", "flat_views"])
+def test_bf16_fused_step_matches_bf16_torch_step(layout):
+    """the production step (bf16, fused: cast_bf16 +
+    functional_call, libocm losses, FusedAdam) against the fused=False bf16
+    step (torch autocast, torch losses, torch Adam) with the same ε seeds, at
+    the C4 network's layer plan (L = 512).  Losses to 1e-2 and every parameter
+    gradient to 5e-2 of its norm (bf16 roundings sit in different places),
+    once with .grad = None before backward (one process) and once with the
+    gradients as views of the flat all-reduce buffer (world-1 gloo group), the
+    layout in which the cast's backward writes straight into the views."""
+    import socket
+
+    import torch.distributed as dist
+
+    from ocm.vae_train import GraphedVAETrainer
+
+    dev = torch.device("cuda", 0)
+    L, d, B = 512, 16, 128
+    g = torch.Generator(device="cpu").manual_seed(11)
+    X = (1.0 + 0.3 * torch.randn(B * 2, L, generator=g)).to(dev)
+    mean, std = X.mean(0).cpu().numpy(), X.std(0).cpu().numpy()
+    torch.manual_seed(0)
+    m1 = V.ConvVAE1D(L, d, mean, std, conv_blocks=3, n_filters=3, kernel_size=7, hidden_fc=64).to(dev)
+    m2 = copy.deepcopy(m1)
+    flat = layout == "flat_views"
+    if flat:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        tf = GraphedVAETrainer(m1, B, lr=1e-3, dtype=torch.bfloat16, graph=False, grad_allreduce=flat)
+        tt = GraphedVAETrainer(m2, B, lr=1e-3, dtype=torch.bfloat16, graph=False, grad_allreduce=flat, fused=False)
+        assert tf.fused and not tt.fused and tf.allreduce == flat
+        for i in range(2):
+            xb = X[i * B:(i + 1) * B]
+            torch.manual_seed(70 + i)
+            a = [float(v) for v in tf.step(xb)]
+            torch.manual_seed(70 + i)
+            b = [float(v) for v in tt.step(xb)]
+            np.testing.assert_allclose(a, b, rtol=1e-2)
+            if i == 0:
+                if flat:
+                    lo = tf.flat_grad.data_ptr()
+                    hi = lo + tf.flat_grad.numel() * 4
+                    assert all(lo <= p.grad.data_ptr() < hi for p in m1.parameters())
+                gmax = max(float(p.grad.norm()) for p in m2.parameters())
+                for (n1, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+                    scale = float(p2.grad.norm())
+                    tol = 5e-2 * scale if scale > 1e-3 * gmax else 5e-4 * gmax
+                    assert float((p1.grad - p2.grad).norm()) <= tol, (n1, float((p1.grad - p2.grad).norm()), scale)
+    finally:
+        if flat:
+            dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+def test_cast_bf16_accumulates_into_existing_grads():
+    """without the caller's 'freshly zeroed' promise the cast's
+    backward returns its gradients, so autograd adds them to a .grad that is
+    already there (gradient accumulation keeps working); FusedAdam skips a
+    parameter without a gradient, as torch.optim.Adam does."""
+    from ocm import vae_fused as vf
+
+    dev = torch.device("cuda", 0)
+    w = torch.randn(8, 4, device=dev, requires_grad=True)
+    u = torch.randn(3, device=dev, requires_grad=True)
+    x = torch.randn(5, 4, device=dev, dtype=torch.bfloat16)
+    (wb,) = vf.cast_bf16(w)
+    (x @ wb.t()).float().sum().backward()
+    g1 = w.grad.clone()
+    (wb,) = vf.cast_bf16(w)
+    (x @ wb.t()).float().sum().backward()  # accumulates: 2 × the first gradient
+    torch.testing.assert_close(w.grad, 2 * g1)
+    u_before, w_before = u.detach().clone(), w.detach().clone()
+    opt = vf.FusedAdam([w, u], lr=1e-2)
+    opt.step()  # u.grad is None: u is left alone, w takes its step
+    torch.testing.assert_close(u.detach(), u_before)
+    assert float((w.detach() - w_before).abs().max()) > 1e-3
