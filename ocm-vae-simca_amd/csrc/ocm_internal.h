@@ -29,6 +29,12 @@ struct ocm_ctx {
   // side stream + events of the quantiser / Gram overlap (created on first use)
   hipStream_t side = nullptr;
   std::vector<hipEvent_t> fork_ev;
+  // the eigensolver's θ work beside its Jacobi (created on first use): a side
+  // stream, fork / join events, and a sub-context whose workspaces the θ3
+  // Gram takes (the main workspace holds the eigensolver's live buffers)
+  hipStream_t eig_side = nullptr;
+  hipEvent_t eig_ev[3] = {nullptr, nullptr, nullptr};
+  ocm_ctx* eig_sub = nullptr;
 };
 
 namespace ocm {

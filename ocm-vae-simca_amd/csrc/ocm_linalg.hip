@@ -747,6 +747,95 @@ __device__ __forceinline__ void cq_apply_block(const double* src, int p, int rb,
   }
 }
 
+// The CholQR factor of a 32×32 Gram S (in sS): column scaling r_i = 1/√S_ii,
+// S' = D S D = L Lᵀ by wave 0 in registers (lane i holds row i, v_readlane
+// broadcasts, pivot clamp 1e-14 as k_chol), X = L⁻¹ by back substitution and
+// M = D·Xᵀ (upper triangular), so that W·M has orthonormal columns.  A
+// (numerically) zero column of W (rank-deficient C, fix_zero) is replaced by
+// a pseudo-random one and S formed again from all of W by this workgroup.
+// Called by every thread of ONE workgroup (any blockDim ≥ 64).
+__device__ __forceinline__ void cq_finalize(double (*sS)[33], double* rsc, int* degen_flag, double* W, int p, int fix_zero,
+                            uint64_t seed, double* __restrict__ Mout) {
+  const int tid = threadIdx.x, lane = tid & 63, nt = blockDim.x;
+  int& degen = *degen_flag;
+  __shared__ double sm[32][33];
+  if (tid == 0) degen = 0;
+  __syncthreads();
+  if (tid < 32) {
+    const double nrm = sqrt(sS[tid][tid]);
+    const bool zero = !(nrm > 1e-280);
+    if (zero && fix_zero) atomicOr(&degen, 1);
+    rsc[tid] = zero ? 0.0 : 1.0 / nrm;
+  }
+  __syncthreads();
+  if (degen) {
+    // rank-deficient C: a (numerically) zero column of W is replaced by the
+    // pseudo-random column k_colnormalize uses, and S is formed again here
+    // from all of W by this one workgroup (rare; the first pass only)
+    for (int cc = 0; cc < 32; ++cc) {
+      if (rsc[cc] != 0.0) continue;
+      for (int r = tid; r < p; r += nt) W[(int64_t)r * 32 + cc] = hash_normal(seed * 0x9E3779B1ull + (uint64_t)r * 131 + cc);
+    }
+    __threadfence();
+    __syncthreads();
+    for (int e = tid; e < 32 * 32; e += nt) {
+      const int i = e >> 5, j = e & 31;
+      double v = 0.0;
+      for (int r = 0; r < p; ++r) v += ld_agent(&W[(int64_t)r * 32 + i]) * ld_agent(&W[(int64_t)r * 32 + j]);
+      sS[i][j] = v;
+    }
+    __syncthreads();
+    if (tid < 32) rsc[tid] = 1.0 / sqrt(fmax(sS[tid][tid], 1e-300));
+    __syncthreads();
+  }
+  if (tid < 64) {
+    // Cholesky of S' = D S D in registers (lanes 32..63 mirror 0..31)
+    const int i = lane & 31;
+    const double ri = rsc[i];
+    double a[32];
+#pragma unroll
+    for (int cc = 0; cc < 32; ++cc) a[cc] = sS[i][cc] * ri * rsc[cc];
+    double lrow[32], invd[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const double ajj = fmax(readlane_f64(a[j], j), 1e-14);  // diag(S') = 1: clamp 1e-14 · max diag
+      const double inv = rsqrt(ajj);
+      const double djj = ajj * inv;
+      invd[j] = inv;
+      const double lij = i > j ? a[j] * inv : (i == j ? djj : 0.0);
+      lrow[j] = lij;
+#pragma unroll
+      for (int l = j + 1; l < 32; ++l) {
+        const double llj = readlane_f64(lij, l);
+        if (l <= i) a[l] -= lij * llj;
+      }
+    }
+    if (lane < 32) {
+#pragma unroll
+      for (int cc = 0; cc < 32; ++cc) sm[i][cc] = lrow[cc];
+    }
+    __builtin_amdgcn_wave_barrier();
+    // lane i: row i of X = L⁻¹ by X·L = I, columns j = 31 … 0, right-looking:
+    // once X[i][j] is known its products with row j of L go into the pending
+    // sums of columns < j (independent FMAs; the serial chain is one FMA and
+    // one multiply per column)
+    double xr[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) xr[j] = 0.0;
+#pragma unroll
+    for (int j = 31; j >= 0; --j) {
+      xr[j] = j > i ? 0.0 : ((j == i ? 1.0 : 0.0) - xr[j]) * invd[j];
+#pragma unroll
+      for (int jj = 0; jj < j; ++jj) xr[jj] = fma(xr[j], sm[j][jj], xr[jj]);
+    }
+    // M[k][i] = r_k · X[i][k]
+    if (lane < 32) {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) Mout[k * 32 + i] = rsc[k] * xr[k];
+    }
+  }
+}
+
 template <bool APPLY>
 __global__ __launch_bounds__(256) void k_cq_gram32(double* W, int p, const double* __restrict__ Mprev, double* T,
                                                    double* __restrict__ part, unsigned* __restrict__ ticket,
@@ -828,81 +917,7 @@ __global__ __launch_bounds__(256) void k_cq_gram32(double* W, int p, const doubl
     sS[row][col] = v;
     if (blk == 1) sS[col][row] = v;
   }
-  if (tid == 0) degen = 0;
-  __syncthreads();
-  if (tid < 32) {
-    const double nrm = sqrt(sS[tid][tid]);
-    const bool zero = !(nrm > 1e-280);
-    if (zero && fix_zero) atomicOr(&degen, 1);
-    rsc[tid] = zero ? 0.0 : 1.0 / nrm;
-  }
-  __syncthreads();
-  if (degen) {
-    // rank-deficient C: a (numerically) zero column of W is replaced by the
-    // pseudo-random column k_colnormalize uses, and S is formed again here
-    // from all of W by this one workgroup (rare; the first pass only)
-    for (int cc = 0; cc < 32; ++cc) {
-      if (rsc[cc] != 0.0) continue;
-      for (int r = tid; r < p; r += 256) W[(int64_t)r * 32 + cc] = hash_normal(seed * 0x9E3779B1ull + (uint64_t)r * 131 + cc);
-    }
-    __threadfence();
-    __syncthreads();
-    for (int e = tid; e < 32 * 32; e += 256) {
-      const int i = e >> 5, j = e & 31;
-      double v = 0.0;
-      for (int r = 0; r < p; ++r) v += W[(int64_t)r * 32 + i] * W[(int64_t)r * 32 + j];
-      sS[i][j] = v;
-    }
-    __syncthreads();
-    if (tid < 32) rsc[tid] = 1.0 / sqrt(fmax(sS[tid][tid], 1e-300));
-    __syncthreads();
-  }
-  if (tid < 64) {
-    // Cholesky of S' = D S D in registers (lanes 32..63 mirror 0..31)
-    const int i = lane & 31;
-    const double ri = rsc[i];
-    double a[32];
-#pragma unroll
-    for (int cc = 0; cc < 32; ++cc) a[cc] = sS[i][cc] * ri * rsc[cc];
-    double lrow[32], invd[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const double ajj = fmax(readlane_f64(a[j], j), 1e-14);  // diag(S') = 1: clamp 1e-14 · max diag
-      const double inv = rsqrt(ajj);
-      const double djj = ajj * inv;
-      invd[j] = inv;
-      const double lij = i > j ? a[j] * inv : (i == j ? djj : 0.0);
-      lrow[j] = lij;
-#pragma unroll
-      for (int l = j + 1; l < 32; ++l) {
-        const double llj = readlane_f64(lij, l);
-        if (l <= i) a[l] -= lij * llj;
-      }
-    }
-    if (lane < 32) {
-#pragma unroll
-      for (int cc = 0; cc < 32; ++cc) sm[i][cc] = lrow[cc];
-    }
-    __builtin_amdgcn_wave_barrier();
-    // lane i: row i of X = L⁻¹ by X·L = I, columns j = 31 … 0, right-looking:
-    // once X[i][j] is known its products with row j of L go into the pending
-    // sums of columns < j (independent FMAs; the serial chain is one FMA and
-    // one multiply per column)
-    double xr[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) xr[j] = 0.0;
-#pragma unroll
-    for (int j = 31; j >= 0; --j) {
-      xr[j] = j > i ? 0.0 : ((j == i ? 1.0 : 0.0) - xr[j]) * invd[j];
-#pragma unroll
-      for (int jj = 0; jj < j; ++jj) xr[jj] = fma(xr[j], sm[j][jj], xr[jj]);
-    }
-    // M[k][i] = r_k · X[i][k]
-    if (lane < 32) {
-#pragma unroll
-      for (int k = 0; k < 32; ++k) Mout[k * 32 + i] = rsc[k] * xr[k];
-    }
-  }
+  cq_finalize(sS, rsc, &degen, W, p, fix_zero, seed, Mout);
 }
 
 __global__ __launch_bounds__(256) void k_cq_apply32(const double* __restrict__ src, int p, const double* __restrict__ M,
@@ -926,6 +941,156 @@ __global__ __launch_bounds__(256) void k_cq_apply32(const double* __restrict__ s
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// One plain subspace iteration for b = 32 in ONE launch (the product, the
+// basis change and the next CholQR factor):
+//   Wout = (C · Win) · Min     (Min = the CholQR factor of Win: Win·Min is the
+//                               orthonormal basis; nullptr = identity)
+//   Mout = CholQR factor of Wout (cq_finalize)
+// so V = Win·Min is never stored: span(C·V) = span(Wout), and only the
+// Rayleigh–Ritz step materialises an orthonormal basis.  The product is
+// k_cv32's (two half-K workgroups per 16 rows, parity ticket); the second of a
+// pair to finish applies Min to its 16 rows in LDS, stores them and their
+// 32×32 Gram partial (write-through); the last of each CVQ_G1 row blocks sums
+// its group's partials in row-block order, the last group sums the group
+// partials in order (two-level last arrival: deterministic, ≤ 16 + ⌈rb/16⌉
+// counter adds in a row) and factors the Gram.  Replaces k_cv32 +
+// k_cq_gram32 + k_cq_apply32 (three launches, ≈ 49 µs per iteration, r04zf).
+// gpart: cv_rb·1024 row-block partials, then ⌈cv_rb/16⌉·1024 group partials;
+// gtick: 1 + ⌈cv_rb/16⌉ counters TICKET_STRIDE words apart (zeroed once).
+// ---------------------------------------------------------------------------
+constexpr int CVQ_G1 = 16;
+__global__ __launch_bounds__(512) void k_cvq32(const double* __restrict__ C, int p, const double* __restrict__ Win,
+                                             const double* __restrict__ Min, double* __restrict__ Wout,
+                                             double* __restrict__ part, unsigned* __restrict__ ticket,
+                                             double* __restrict__ gpart, unsigned* __restrict__ gtick,
+                                             uint64_t seed, double* __restrict__ Mout) {
+  __shared__ double red[CV_W][16 * 33];
+  __shared__ double sm[32][33];
+  __shared__ double sv[16][33];
+  __shared__ double sS[32][33];
+  __shared__ double rsc[32];
+  __shared__ int last, degen;
+  const int rb = blockIdx.x >> 1, half = blockIdx.x & 1;
+  const int nrb = (p + 15) / 16;
+  const int r0 = rb * 16;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int i = lane & 15, g = lane >> 4;
+  const int kslice = (p + 2 * CV_W * 32 - 1) / (2 * CV_W * 32) * 32;
+  const int kb = (half * CV_W + wave) * kslice;
+  const int ke = min(p, kb + kslice);
+  const double* crow = C + (int64_t)min(r0 + i, p - 1) * p;
+  f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = acc0;
+  for (int k0 = kb; k0 < ke; k0 += 32) {
+    double a[8], b0[8], b1[8];
+    const int kk0 = k0 + 8 * g;
+    if (k0 + 32 <= ke) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        a[s] = crow[kk0 + s];
+        b0[s] = Win[(int64_t)(kk0 + s) * 32 + i];
+        b1[s] = Win[(int64_t)(kk0 + s) * 32 + 16 + i];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int kk = kk0 + s;
+        const bool ok = kk < ke;
+        a[s] = ok ? crow[kk] : 0.0;
+        b0[s] = ok ? Win[(int64_t)kk * 32 + i] : 0.0;
+        b1[s] = ok ? Win[(int64_t)kk * 32 + 16 + i] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b0[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b1[s], acc1, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[wave][(g + 4 * r) * 33 + i] = acc0[r];
+    red[wave][(g + 4 * r) * 33 + 16 + i] = acc1[r];
+  }
+  if (Min)
+    for (int e = tid; e < 32 * 32; e += 512) sm[e >> 5][e & 31] = Min[e];
+  __syncthreads();
+  const int orow = tid >> 5, ocol = tid & 31;
+  double v = 0.0;
+#pragma unroll
+  for (int w = 0; w < CV_W; ++w) v += red[w][orow * 33 + ocol];
+  part[(int64_t)blockIdx.x * 512 + tid] = v;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = (__hip_atomic_fetch_add(&ticket[rb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u) == 1u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  const double o = part[(int64_t)(blockIdx.x ^ 1) * 512 + tid];
+  double y = half == 0 ? v + o : o + v;  // (C·Win)[r0 + orow][ocol]
+  const bool rok = r0 + orow < p;
+  if (Min) {  // basis change on the output rows: (C·Win)·Min
+    sv[orow][ocol] = y;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) t = fma(sv[orow][j], sm[j][ocol], t);
+    y = t;
+    __syncthreads();
+  }
+  // write-through: the finishing workgroup may re-read Wout (rank-deficient C)
+  if (rok) st_agent(&Wout[(int64_t)(r0 + orow) * 32 + ocol], y);
+  sv[orow][ocol] = rok ? y : 0.0;
+  __syncthreads();
+  // this row block's Gram partial (entries tid and tid + 512 of the 32×32)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int e = tid + 512 * h, a = e >> 5, b = e & 31;
+    double gs = 0.0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gs = fma(sv[r][a], sv[r][b], gs);
+    st_agent(&gpart[(int64_t)rb * 1024 + e], gs);
+  }
+  const int ngrp = (nrb + CVQ_G1 - 1) / CVQ_G1;
+  const int grp = rb / CVQ_G1, g0 = grp * CVQ_G1, gsize = min(CVQ_G1, nrb - g0);
+  if (!last_arrival(gtick + (1 + grp) * TICKET_STRIDE, (unsigned)gsize)) return;
+  double* gsum = gpart + (int64_t)nrb * 1024;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int e = tid + 512 * h;
+    double pv[CVQ_G1];
+#pragma unroll
+    for (int q = 0; q < CVQ_G1; ++q) pv[q] = q < gsize ? ld_agent(&gpart[(int64_t)(g0 + q) * 1024 + e]) : 0.0;
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < CVQ_G1; ++q) acc += pv[q];
+    st_agent(&gsum[(int64_t)grp * 1024 + e], acc);
+  }
+  if (!last_arrival(gtick, (unsigned)ngrp)) return;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int e = tid + 512 * h;
+    double acc = 0.0;
+    for (int q0 = 0; q0 < ngrp; q0 += 16) {
+      double pv[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) pv[q] = q0 + q < ngrp ? ld_agent(&gsum[(int64_t)(q0 + q) * 1024 + e]) : 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc += pv[q];
+    }
+    sS[e >> 5][e & 31] = acc;
+  }
+  __syncthreads();
+  cq_finalize(sS, rsc, &degen, Wout, p, 1, seed, Mout);
 }
 
 __device__ __forceinline__ double hash_normal(uint64_t a) {
@@ -983,6 +1148,209 @@ __global__ __launch_bounds__(256) void k_colnormalize(double* __restrict__ W, in
   }
   const double inv = 1.0 / nrm;
   for (int r = threadIdx.x; r < p; r += 256) W[(int64_t)r * b + c] *= inv;
+}
+
+// ---------------------------------------------------------------------------
+// Rayleigh–Ritz for b = 32 without rotating the block (round 5):
+//   k_atb32        out = AᵀB (32×32) of tall p×32 blocks on fp64 MFMA, CQ_G
+//                  workgroups, the last to finish sums the partials in order
+//                  (H = VᵀW, and G2 = Rᵀ(C·R) for θ3);
+//   k_rr_resid32   R = W − V·H (the projection residual, stored) and
+//                  S = RᵀR (same hand-off);
+//   k_rr_test32    the Ritz residuals ‖C v_i − θ_i v_i‖ = ‖R z_i‖ =
+//                  √(z_iᵀ S z_i) of the top-k pairs from the Jacobi output —
+//                  no rotated block is formed for the convergence test;
+//   k_theta_combine θ1..θ3 of the deflated matrix (I − P_k)C(I − P_k) from the
+//                  b-block deflation Ct_b = (I − P_b)C(I − P_b) (traces,
+//                  computed beside the Jacobi on a side stream) plus the
+//                  Ritz block's exact corrections, block form with
+//                  E = (P_b − P_k)C(I − P_b):
+//                    θ1 = Σ_t θ_i + tr Ct_b
+//                    θ2 = Σ_t θ_i² + 2 Σ_t z_iᵀSz_i + ‖Ct_b‖²
+//                    θ3 = Σ_t θ_i³ + 3 Σ_t θ_i z_iᵀSz_i + 3 Σ_t z_iᵀ G2 z_i + tr Ct_b³
+//                  (t: Ritz pairs k..b−1; every term ≥ 0 for PSD C: no
+//                  cancellation against the leading eigenvalues).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_atb32(const double* __restrict__ A, const double* __restrict__ B, int p,
+                                               double* __restrict__ part, unsigned* __restrict__ ticket,
+                                               double* __restrict__ out) {
+  __shared__ double wpart[4][4][4][64];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  int lo, hi;
+  cq_blocks(p, lo, hi);
+  f64x4 s[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s[q] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int rb = lo + wave; rb < hi; rb += 4) {
+    double a[2][4], bq[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 16 * rb + g + 4 * j;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        a[cb][j] = r < p ? A[(int64_t)r * 32 + 16 * cb + c] : 0.0;
+        bq[cb][j] = r < p ? B[(int64_t)r * 32 + 16 * cb + c] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        s[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q >> 1][j], bq[q & 1][j], s[q], 0, 0, 0);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) wpart[wave][q][r][lane] = s[q][r];
+  __syncthreads();
+  for (int e = tid; e < 1024; e += 256) {
+    const double* w0 = &wpart[0][0][0][0];
+    st_agent(&part[(int64_t)blockIdx.x * 1024 + e], (w0[e] + w0[1024 + e]) + (w0[2048 + e] + w0[3072 + e]));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    last = (__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % CQ_G) == CQ_G - 1;
+  __syncthreads();
+  if (!last) return;
+  for (int e = tid; e < 1024; e += 256) {
+    double pv[CQ_G];
+#pragma unroll
+    for (int wg = 0; wg < CQ_G; ++wg) pv[wg] = ld_agent(&part[(int64_t)wg * 1024 + e]);
+    double v = 0.0;
+#pragma unroll
+    for (int wg = 0; wg < CQ_G; ++wg) v += pv[wg];
+    const int q = e >> 8, r = (e >> 6) & 3, l = e & 63;
+    out[(16 * (q >> 1) + (l >> 4) + 4 * r) * 32 + 16 * (q & 1) + (l & 15)] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rr_resid32(const double* __restrict__ V, const double* __restrict__ W, int p,
+                                                    const double* __restrict__ H, double* __restrict__ R,
+                                                    double* __restrict__ part, unsigned* __restrict__ ticket,
+                                                    double* __restrict__ S) {
+  __shared__ double wpart[4][3][4][64];
+  __shared__ double sm[32][33];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  int lo, hi;
+  cq_blocks(p, lo, hi);
+  for (int e = tid; e < 32 * 32; e += 256) sm[e >> 5][e & 31] = H[e];
+  __syncthreads();
+  f64x4 s00 = {0.0, 0.0, 0.0, 0.0}, s01 = s00, s11 = s00;
+  for (int rb = lo + wave; rb < hi; rb += 4) {
+    f64x4 o0, o1;
+    cq_apply_block(V, p, rb, sm, g, c, o0, o1);  // (V·H)[16rb + g + 4r][16cb + c]
+    double x[2][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * rb + g + 4 * r;
+      const bool ok = row < p;
+      const double r0 = ok ? W[(int64_t)row * 32 + c] - o0[r] : 0.0;
+      const double r1 = ok ? W[(int64_t)row * 32 + 16 + c] - o1[r] : 0.0;
+      x[0][r] = r0;
+      x[1][r] = r1;
+      if (ok) {
+        R[(int64_t)row * 32 + c] = r0;
+        R[(int64_t)row * 32 + 16 + c] = r1;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s00 = __builtin_amdgcn_mfma_f64_16x16x4f64(x[0][j], x[0][j], s00, 0, 0, 0);
+      s01 = __builtin_amdgcn_mfma_f64_16x16x4f64(x[0][j], x[1][j], s01, 0, 0, 0);
+      s11 = __builtin_amdgcn_mfma_f64_16x16x4f64(x[1][j], x[1][j], s11, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    wpart[wave][0][r][lane] = s00[r];
+    wpart[wave][1][r][lane] = s01[r];
+    wpart[wave][2][r][lane] = s11[r];
+  }
+  __syncthreads();
+  for (int e = tid; e < 768; e += 256) {
+    const double* w0 = &wpart[0][0][0][0];
+    st_agent(&part[(int64_t)blockIdx.x * 768 + e], (w0[e] + w0[768 + e]) + (w0[1536 + e] + w0[2304 + e]));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    last = (__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % CQ_G) == CQ_G - 1;
+  __syncthreads();
+  if (!last) return;
+  for (int e = tid; e < 768; e += 256) {
+    double pv[CQ_G];
+#pragma unroll
+    for (int wg = 0; wg < CQ_G; ++wg) pv[wg] = ld_agent(&part[(int64_t)wg * 768 + e]);
+    double v = 0.0;
+#pragma unroll
+    for (int wg = 0; wg < CQ_G; ++wg) v += pv[wg];
+    const int blk = e >> 8, r = (e >> 6) & 3, l = e & 63;
+    const int row = 16 * (blk == 2) + (l >> 4) + 4 * r, col = 16 * (blk != 0) + (l & 15);
+    S[row * 32 + col] = v;
+    if (blk == 1) S[col * 32 + row] = v;
+  }
+}
+
+// z_iᵀ M z_i for columns i of Z (b×b, column i = vector i), one wave per
+// column block; lane l of the wave handling column i sums rows l, l + 64, …
+__device__ __forceinline__ double quad_form_col(const double* __restrict__ M, const double* __restrict__ Z, int b,
+                                                int i, int lane) {
+  double acc = 0.0;
+  for (int r = lane; r < b; r += 64) {
+    double mz = 0.0;
+    for (int q = 0; q < b; ++q) mz = fma(M[r * b + q], Z[q * b + i], mz);
+    acc = fma(Z[r * b + i], mz, acc);
+  }
+  return wave_sum_f64(acc);
+}
+
+// res[i] = √max(z_iᵀ S z_i, 0) for i < k (one workgroup; wave w takes i ≡ w mod 4)
+__global__ __launch_bounds__(256) void k_rr_test32(const double* __restrict__ S, const double* __restrict__ Z, int b,
+                                                   int k, double* __restrict__ res) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = wave; i < k; i += 4) {
+    const double q = quad_form_col(S, Z, b, i, lane);
+    if (lane == 0) res[i] = sqrt(fmax(q, 0.0));
+  }
+}
+
+// tr3[0..2] = tr Ct_b, ‖Ct_b‖², tr Ct_b³ (this slice's part); θ3 corrections
+// only on slice 0 (the slices' θ3 partials are summed over ranks)
+__global__ __launch_bounds__(256) void k_theta_combine(const double* __restrict__ th, const double* __restrict__ Z,
+                                                       const double* __restrict__ S, const double* __restrict__ G2,
+                                                       const double* __restrict__ tr3, int b, int k, int slice0,
+                                                       int want3, double* __restrict__ theta_out) {
+  __shared__ double qs[64], qg[64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = k + wave; i < b; i += 4) {
+    const double a = quad_form_col(S, Z, b, i, lane);
+    const double g2 = want3 ? quad_form_col(G2, Z, b, i, lane) : 0.0;
+    if (lane == 0) {
+      qs[i] = a;
+      qg[i] = g2;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t1 = 0.0, t2 = 0.0, t3 = 0.0, e2 = 0.0, e3 = 0.0, g3 = 0.0;
+    for (int i = k; i < b; ++i) {
+      const double l = th[i];
+      t1 += l;
+      t2 += l * l;
+      t3 += l * l * l;
+      e2 += qs[i];
+      e3 += l * qs[i];
+      g3 += qg[i];
+    }
+    theta_out[0] = t1 + tr3[0];
+    theta_out[1] = (t2 + 2.0 * e2) + tr3[1];
+    theta_out[2] = want3 ? (slice0 ? (t3 + 3.0 * e3 + 3.0 * g3) : 0.0) + tr3[2] : 0.0;
+  }
 }
 
 // res[i] = ‖W_i − θ_i V_i‖ for i < kk
@@ -1288,6 +1656,18 @@ __global__ __launch_bounds__(256) void k_inv_evals(const double* __restrict__ ev
   }
 }
 
+// the eigensolver's side stream, its events and the θ3 Gram's sub-context
+int eig_side_init(ocm_ctx* ctx) {
+  if (ctx->eig_side) return OCM_OK;
+  OCM_HIP(hipStreamCreateWithFlags(&ctx->eig_side, hipStreamNonBlocking));
+  for (auto& e : ctx->eig_ev) OCM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  auto* sub = new ocm_ctx();
+  sub->device = ctx->device;
+  sub->num_cus = ctx->num_cus;
+  ctx->eig_sub = sub;
+  return OCM_OK;
+}
+
 int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
                   int32_t theta_mode, int32_t slice, int32_t nslices, double* evals_out, double* evecs_out,
                   double* theta_out, int32_t* iters_out, hipStream_t st) {
@@ -1324,10 +1704,16 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   const size_t def_blocks = (size_t)((p + DT - 1) / DT) * ((p + DT - 1) / DT);  // deflate GEMM tiles
   const size_t plane_cap = std::max((size_t)ksplit * pb, wide ? 16 * bb : 0);
   size_t need = (6 * pb + 6 * bb + plane_cap + (wide ? 0 : (size_t)nblk * bb) + 4 * b + 64) * sizeof(double);
-  need += ((size_t)CQ_G * 768 + 2048 + 64) * sizeof(double) + 3 * 256;  // CholQR partials, M1/M2, ticket
+  need += ((size_t)CQ_G * 1024 + 2048 + 64) * sizeof(double) + 3 * 256;  // CholQR / k_atb32 partials, M1/M2, ticket
   const int cv_rb = (p + 15) / 16;  // k_cv32 row blocks
   need += ((size_t)cv_rb * 2 * 512) * sizeof(double) + (size_t)cv_rb * sizeof(unsigned) + 2 * 256;
-  if (theta_mode) need += ((size_t)p * p + 4 * (size_t)k * p + 2 * def_blocks + 8) * sizeof(double);
+  // fused plain iterations (k_cvq32, b = 32): two blocks, two factors, the
+  // Gram partials (row blocks + groups) and the two-level counters
+  const bool fused = !wide && b == QB;
+  const int cvq_ng = (cv_rb + CVQ_G1 - 1) / CVQ_G1;
+  const int gt_words = (1 + cvq_ng) * TICKET_STRIDE;
+  if (fused) need += (2 * pb + 2048 + (size_t)(cv_rb + cvq_ng) * 1024) * sizeof(double) + gt_words * 4 + 4 * 256;
+  if (theta_mode) need += ((size_t)p * p + 4 * (size_t)b * p + 2 * def_blocks + 8) * sizeof(double) + 4 * 256;
   void* w = ocm::workspace(ctx, need + 16 * 256, st);
   if (!w) return OCM_ERR_NOMEM;
   ocm::Carve cv{static_cast<char*>(w)};
@@ -1344,13 +1730,28 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   double* res = theta + b;
   double* planes = cv.take<double>(plane_cap);
   double* apart = wide ? nullptr : cv.take<double>((size_t)nblk * bb);
-  double* cq_part = cv.take<double>((size_t)CQ_G * 768);
+  double* cq_part = cv.take<double>((size_t)CQ_G * 1024);
   double* cq_M = cv.take<double>(2048);
   // k_cq_gram32's ticket counts from a multiple of CQ_G, k_cv32's parity tickets
   // start even: both zeroed by the k_randn launch below (contiguous)
   unsigned* cq_ticket = cv.take<unsigned>(64);
   double* cv_part = cv.take<double>((size_t)cv_rb * 2 * 512);
-  unsigned* cv_ticket = cv.take<unsigned>(cv_rb);
+  // k_cv32's parity tickets, then k_cvq32's counters: one range, zeroed once
+  unsigned* cv_ticket = cv.take<unsigned>(cv_rb + (fused ? gt_words + TICKET_STRIDE : 0));
+  unsigned* gtick = fused ? cv_ticket + (cv_rb + TICKET_STRIDE - 1) / TICKET_STRIDE * TICKET_STRIDE : nullptr;
+  const int nzero_cv = fused ? (int)(gtick - cv_ticket) + gt_words : cv_rb;
+  double* Wa = fused ? cv.take<double>(pb) : nullptr;
+  double* Wb = fused ? cv.take<double>(pb) : nullptr;
+  double* Mf = fused ? cv.take<double>(2048) : nullptr;
+  double* gpart = fused ? cv.take<double>((size_t)(cv_rb + cvq_ng) * 1024) : nullptr;
+  // θ work buffers (the deflated matrix, its tile partials, the rank-2kd
+  // operands, three traces), carved up front: the fused path fills them during
+  // its Rayleigh–Ritz step, on a side stream
+  double* Ct = theta_mode ? cv.take<double>((size_t)p * p) : nullptr;
+  double* dpart = theta_mode ? cv.take<double>(2 * def_blocks) : nullptr;
+  double* Ud = theta_mode ? cv.take<double>((size_t)2 * b * p) : nullptr;
+  double* Wd = theta_mode ? cv.take<double>((size_t)2 * b * p) : nullptr;
+  double* tr3 = theta_mode ? cv.take<double>(8) : nullptr;
   auto* hres = static_cast<double*>(ocm::host_staging(ctx, (wide ? 3 * bb + b : 2 * b) * sizeof(double)));
   if (!hres) return OCM_ERR_NOMEM;
   double* hmat = hres + 2 * b;  // wide: b×b host staging (+ b×b result, + b values)
@@ -1440,12 +1841,68 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     return OCM_OK;
   };
 
+  // θ1..θ3 of (I − P)C(I − P), P the projector on the first kd columns of the
+  // orthonormal block Vb (Wb_ = C·Vb, Hb = Vbᵀ Wb_): the rank-2kd deflation
+  // GEMM with its trace and Frobenius epilogue → out3[0..1], and this slice's
+  // θ3 rows → out3[2], all on stream s; the θ3 Gram runs on gctx's workspaces.
+  auto theta_into = [&](const double* Vb, const double* Wb_, const double* Hb, int kd, hipStream_t s,
+                        ocm_ctx* gctx, double* out3) -> int {
+    // N = Vb[:, :kd] · Hb[:kd, :]
+    int rc2 = dgemm(Vb, b, Hb, b, Nm, b, p, b, kd, 1, nullptr, s);
+    if (rc2) return rc2;
+    hipLaunchKernelGGL(k_deflate_operands, dim3((unsigned)(((size_t)p * kd + 255) / 256)), dim3(256), 0, s, Vb, Wb_,
+                       Nm, p, b, kd, Ud, Wd);
+    OCM_CHECK_LAUNCH("k_deflate_operands");
+    const dim3 gd((p + DT - 1) / DT, (p + DT - 1) / DT, 1);
+    hipLaunchKernelGGL(k_dgemm<2>, gd, dim3(256), 0, s, Ud, (int64_t)(2 * kd), Wd, (int64_t)p, Ct, (int64_t)p, p, p,
+                       2 * kd, 2 * kd, C, (int64_t)p, dpart, 0);
+    OCM_CHECK_LAUNCH("k_dgemm deflate");
+    hipLaunchKernelGGL(k_sum_pairs, dim3(1), dim3(256), 0, s, dpart, (int)(gd.x * gd.y), out3);  // tr, ‖·‖²
+    OCM_CHECK_LAUNCH("k_sum_pairs");
+    // θ3: this slice's rows of the Δ / O expansion (k_theta3_diag), then the
+    // i8×3 Gram of those rows of O.  The Gram takes gctx's workspace, so O
+    // (f32), its Gram and the partials live in gctx's second arena (two
+    // hipMallocAsync calls here cost ≈ 50 µs of host time, with the GPU idle
+    // behind them).
+    const int r0 = (int)((int64_t)p * slice / nslices), r1 = (int)((int64_t)p * (slice + 1) / nslices);
+    if (theta_mode >= 2 && r1 > r0) {
+      const int nr = r1 - r0;
+      const size_t pp = (size_t)p * p;
+      const size_t o32_bytes = (pp * sizeof(float) + 255) / 256 * 256;
+      char* aux = static_cast<char*>(
+          ocm::workspace_aux(gctx, o32_bytes + (pp + 3 * (size_t)p + 8) * sizeof(double), s));
+      if (!aux) return OCM_ERR_NOMEM;
+      float* O32 = reinterpret_cast<float*>(aux);
+      double* Gp = reinterpret_cast<double*>(aux + o32_bytes);
+      double* csum = Gp + pp;
+      double* dpart3 = csum + p;  // p row partials of the Δ terms
+      double* opart = dpart3 + p;  // p row partials of the O·O² term
+      double* t3 = opart + p;
+      hipLaunchKernelGGL(k_theta3_diag, dim3(nr), dim3(256), 0, s, Ct, p, r0, r1, O32, dpart3);
+      hipLaunchKernelGGL(k_offdiag_f32, dim3((unsigned)((pp + 255) / 256)), dim3(256), 0, s, Ct, p, O32);
+      hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, s, dpart3, nr, t3);
+      OCM_CHECK_LAUNCH("k_theta3_diag");
+      // the shift of the Gram is zero: a p-vector of zeros (taken from the partials' tail)
+      float* zshift = reinterpret_cast<float*>(opart);
+      OCM_HIP(hipMemsetAsync(zshift, 0, (size_t)p * sizeof(float), s));
+      rc2 = ocm::gram_rows_i8(gctx, O32 + (size_t)r0 * p, p, nr, p, zshift, Gp, csum, s);
+      if (rc2) return rc2;
+      hipLaunchKernelGGL(k_trace_og, dim3(p), dim3(256), 0, s, O32, Gp, p, opart);
+      hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, s, opart, p, t3 + 1);
+      hipLaunchKernelGGL(k_add3, dim3(1), dim3(64), 0, s, t3, t3 + 1, out3 + 2);
+      OCM_CHECK_LAUNCH("k_trace_og");
+    } else {
+      OCM_HIP(hipMemsetAsync(out3 + 2, 0, sizeof(double), s));
+    }
+    return OCM_OK;
+  };
+
   // V₀: a Gaussian block, used as it is — the subspace after i iterations is
   // span(Cⁱ V₀) whatever basis V₀ has, so only the Rayleigh–Ritz steps need an
   // orthonormal basis (every iteration before one ends with CholQR2), and an
   // orthonormalisation of V₀ costs a CholQR pass (≈ 36 µs) for nothing
-  hipLaunchKernelGGL(k_randn, dim3((unsigned)((std::max<size_t>(pb, cv_rb) + 255) / 256)), dim3(256), 0, st, V,
-                     (int64_t)pb, 0x5EEDull, cq_ticket, 1, cv_ticket, cv_rb);
+  hipLaunchKernelGGL(k_randn, dim3((unsigned)((std::max<size_t>(pb, nzero_cv) + 255) / 256)), dim3(256), 0, st, V,
+                     (int64_t)pb, 0x5EEDull, cq_ticket, 1, cv_ticket, nzero_cv);
   OCM_CHECK_LAUNCH("k_randn");
   int rc = OCM_OK;
 
@@ -1474,7 +1931,32 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   }
   double prev_rmax = 0.0;
   bool converged = false;
+  // fused chain state (b = 32): the current unnormalised block Wc and its
+  // CholQR factor Mc (nullptr: Wc is the start block, used as it is)
+  double* Wc = V;
+  double* Wn = Wa;
+  const double* Mc = nullptr;
+  int mslot = 0;
   for (it = 1; it <= max_iter; ++it) {
+    if (fused && it < next_rr) {  // W ← (C·Wc)·Mc and its factor, one launch
+      double* Mn = Mf + 1024 * mslot;
+      hipLaunchKernelGGL(k_cvq32, dim3(2 * cv_rb), dim3(512), 0, st, C, p, Wc, Mc, Wn, cv_part, cv_ticket, gpart,
+                         gtick, (uint64_t)(500 + it), Mn);
+      OCM_CHECK_LAUNCH("k_cvq32");
+      Wc = Wn;
+      Wn = (Wn == Wa) ? Wb : Wa;
+      Mc = Mn;
+      mslot ^= 1;
+      continue;
+    }
+    if (fused && Mc) {  // the Rayleigh–Ritz basis: V = CholQR2 of the chain's block (Wc·Mc, then its factor)
+      hipLaunchKernelGGL(k_cq_gram32<true>, dim3(CQ_G), dim3(256), 0, st, Wc, p, Mc, Wc, cq_part, cq_ticket, 0,
+                         (uint64_t)(700 + it), cq_M);
+      OCM_CHECK_LAUNCH("k_cq_gram32 rr");
+      hipLaunchKernelGGL(k_cq_apply32, dim3(CQ_G), dim3(256), 0, st, Wc, p, cq_M, V);
+      OCM_CHECK_LAUNCH("k_cq_apply32 rr");
+      Mc = nullptr;
+    }
     if (!wide && b == 32) {  // W = C V
       hipLaunchKernelGGL(k_cv32, dim3(2 * cv_rb), dim3(512), 0, st, C, p, V, W, cv_part, cv_ticket);
       OCM_CHECK_LAUNCH("k_cv32");
@@ -1489,6 +1971,86 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
       // rounding.
       rc = orth(W, V, 500 + it, it == next_rr - 1 ? 2 : 1);
       if (rc) return rc;
+      continue;
+    }
+    if (fused) {
+      // Rayleigh–Ritz on the unrotated block: H = VᵀW, the projection
+      // residual R = W − V·H and S = RᵀR, Jacobi on H; the test reads
+      // ‖R z_i‖ (k_rr_test32).  With θ wanted, R/S, C·R, G2 = Rᵀ(C·R) and the
+      // deflation of the whole block run on a side stream beside the Jacobi
+      // (they need no Ritz rotation: k_theta_combine adds its terms later).
+      hipLaunchKernelGGL(k_atb32, dim3(CQ_G), dim3(256), 0, st, V, W, p, cq_part, cq_ticket, H);
+      OCM_CHECK_LAUNCH("k_atb32 H");
+      hipStream_t rs = st;
+      if (theta_mode) {
+        rc = eig_side_init(ctx);
+        if (rc) return rc;
+        rs = ctx->eig_side;
+        OCM_HIP(hipEventRecord(ctx->eig_ev[0], st));
+        OCM_HIP(hipStreamWaitEvent(rs, ctx->eig_ev[0], 0));
+      }
+      double* R = T1;
+      double* CR = T2;
+      hipLaunchKernelGGL(k_rr_resid32, dim3(CQ_G), dim3(256), 0, rs, V, W, p, H, R, cq_part, cq_ticket, S);
+      OCM_CHECK_LAUNCH("k_rr_resid32");
+      if (theta_mode) OCM_HIP(hipEventRecord(ctx->eig_ev[1], rs));
+      rc = jacobi(H, b, 40, theta, Z, st);
+      if (rc) return rc;
+      if (theta_mode) OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[1], 0));
+      hipLaunchKernelGGL(k_rr_test32, dim3(1), dim3(256), 0, st, S, Z, b, k, res);
+      OCM_CHECK_LAUNCH("k_rr_test32");
+      if (theta_mode) {
+        hipLaunchKernelGGL(k_cv32, dim3(2 * cv_rb), dim3(512), 0, rs, C, p, R, CR, cv_part, cv_ticket);
+        OCM_CHECK_LAUNCH("k_cv32 CR");
+        if (theta_mode >= 2) {
+          hipLaunchKernelGGL(k_atb32, dim3(CQ_G), dim3(256), 0, rs, R, CR, p, cq_part, cq_ticket, L);  // G2
+          OCM_CHECK_LAUNCH("k_atb32 G2");
+        }
+        rc = theta_into(V, W, H, b, rs, ctx->eig_sub, tr3);
+        if (rc) return rc;
+        OCM_HIP(hipEventRecord(ctx->eig_ev[2], rs));
+      }
+      OCM_HIP(hipMemcpyAsync(hres, theta, 2 * (size_t)b * sizeof(double), hipMemcpyDeviceToHost, st));
+      OCM_HIP(hipStreamSynchronize(st));
+      double rmax = 0.0;
+      for (int i = 0; i < k; ++i) rmax = std::max(rmax, hres[b + i]);
+      const double scale = std::fabs(hres[0]);
+      if (!(rmax == rmax)) {
+        if (theta_mode) (void)hipStreamSynchronize(rs);
+        return ocm::fail(OCM_ERR_ARG, "ocm_eig_topk: NaN in covariance");
+      }
+      const double target = tol * (scale > 0 ? scale : 1.0);
+      converged = rmax <= target;
+      if (theta_mode) OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[2], 0));  // R, CR, Ct, the θ3 arena reused
+      if (converged || it == max_iter) {
+        if (theta_mode) {
+          hipLaunchKernelGGL(k_theta_combine, dim3(1), dim3(256), 0, st, theta, Z, S, L, tr3, b, k, slice == 0 ? 1 : 0,
+                             theta_mode >= 2 ? 1 : 0, theta_out);
+          OCM_CHECK_LAUNCH("k_theta_combine");
+        }
+        hipLaunchKernelGGL(k_cq_apply32, dim3(CQ_G), dim3(256), 0, st, V, p, Z, T1);  // Ritz vectors
+        OCM_CHECK_LAUNCH("k_cq_apply32 ritz");
+        std::swap(V, T1);
+        break;
+      }
+      const double tk = std::fabs(hres[k - 1]);
+      double rate = tk > 0 ? std::fabs(hres[b - 1]) / tk : 1.0;
+      if (prev_it > 0 && prev_rmax > 0) rate = std::max(rate, std::pow(rmax / prev_rmax, 1.0 / (it - prev_it)));
+      int ahead = 1;
+      if (rate < 0.999) ahead = (int)std::ceil(std::log(target / rmax) / std::log(std::max(rate, 1e-3)));
+      ahead = std::max(1, std::min(ahead, 64));
+      next_rr = std::min(it + ahead, max_iter);
+      prev_it = it;
+      prev_rmax = rmax;
+      // the chain continues from W = C·V (span is all it needs) and its factor
+      OCM_HIP(hipMemcpyAsync(Wa, W, pb * sizeof(double), hipMemcpyDeviceToDevice, st));
+      hipLaunchKernelGGL(k_cq_gram32<false>, dim3(CQ_G), dim3(256), 0, st, Wa, p, nullptr, nullptr, cq_part, cq_ticket,
+                         1, (uint64_t)(1000 + it), Mf);
+      OCM_CHECK_LAUNCH("k_cq_gram32 chain");
+      Wc = Wa;
+      Wn = Wb;
+      Mc = Mf;
+      mslot = 1;
       continue;
     }
     rc = ritz();
@@ -1539,64 +2101,13 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   hipLaunchKernelGGL(k_extract_signfix, dim3(k), dim3(256), 0, st, V, p, b, k, evecs_out, theta, evals_out);
   OCM_CHECK_LAUNCH("k_extract_signfix");
 
-  if (theta_mode) {
-    // H_k = V_kᵀ (C V_k): the projected block; N = V H restricted to k columns
+  if (theta_mode && !fused) {
+    // H_k = V_kᵀ (C V_k): the projected block of the Ritz vectors; deflate
+    // the leading k of them
     rc = project(V, W, H);
     if (rc) return rc;
-    // N = V_k H_k (K = k: only the leading k Ritz directions are deflated)
-    rc = dgemm(V, b, H, b, Nm, b, p, b, k, 1, nullptr, st);
+    rc = theta_into(V, W, H, k, st, ctx, theta_out);
     if (rc) return rc;
-    double* Ct = cv.take<double>((size_t)p * p);
-    double* dpart = cv.take<double>(2 * def_blocks);
-    double* U = cv.take<double>((size_t)2 * k * p);
-    double* Wt = cv.take<double>((size_t)2 * k * p);
-    hipLaunchKernelGGL(k_deflate_operands, dim3((unsigned)(((size_t)p * k + 255) / 256)), dim3(256), 0, st, V, W,
-                       Nm, p, b, k, U, Wt);
-    OCM_CHECK_LAUNCH("k_deflate_operands");
-    const dim3 gd((p + DT - 1) / DT, (p + DT - 1) / DT, 1);
-    hipLaunchKernelGGL(k_dgemm<2>, gd, dim3(256), 0, st, U, (int64_t)(2 * k), Wt, (int64_t)p, Ct, (int64_t)p, p, p,
-                       2 * k, 2 * k, C, (int64_t)p, dpart, 0);
-    OCM_CHECK_LAUNCH("k_dgemm deflate");
-    hipLaunchKernelGGL(k_sum_pairs, dim3(1), dim3(256), 0, st, dpart, (int)(gd.x * gd.y), theta_out);  // θ1, θ2
-    OCM_CHECK_LAUNCH("k_sum_pairs");
-    // θ3: this slice's rows of the Δ / O expansion (k_theta3_diag), then the
-    // i8×3 Gram of those rows of O.  The Gram takes the context workspace, so
-    // O (f32), its Gram and the partials live in the context's second arena
-    // (two hipMallocAsync calls here cost ≈ 50 µs of host time, with the GPU
-    // idle behind them) and everything the eigensolver's carve-outs feed is
-    // already in the outputs.
-    const int r0 = (int)((int64_t)p * slice / nslices), r1 = (int)((int64_t)p * (slice + 1) / nslices);
-    if (theta_mode >= 2 && r1 > r0) {
-      const int nr = r1 - r0;
-      const size_t pp = (size_t)p * p;
-      const size_t o32_bytes = (pp * sizeof(float) + 255) / 256 * 256;
-      char* aux = static_cast<char*>(
-          ocm::workspace_aux(ctx, o32_bytes + (pp + 3 * (size_t)p + 8) * sizeof(double), st));
-      if (!aux) return OCM_ERR_NOMEM;
-      float* O32 = reinterpret_cast<float*>(aux);
-      double* Gp = reinterpret_cast<double*>(aux + o32_bytes);
-      double* csum = Gp + pp;
-      double* dpart3 = csum + p;  // p row partials of the Δ terms
-      double* opart = dpart3 + p;  // p row partials of the O·O² term
-      double* t3 = opart + p;
-      hipLaunchKernelGGL(k_theta3_diag, dim3(nr), dim3(256), 0, st, Ct, p, r0, r1, O32, dpart3);
-      hipLaunchKernelGGL(k_offdiag_f32, dim3((unsigned)((pp + 255) / 256)), dim3(256), 0, st, Ct, p, O32);
-      hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, dpart3, nr, t3);
-      OCM_CHECK_LAUNCH("k_theta3_diag");
-      // the shift of the Gram is zero: a p-vector of zeros (taken from the partials' tail)
-      float* zshift = reinterpret_cast<float*>(opart);
-      OCM_HIP(hipMemsetAsync(zshift, 0, (size_t)p * sizeof(float), st));
-      rc = ocm::gram_rows_i8(ctx, O32 + (size_t)r0 * p, p, nr, p, zshift, Gp, csum, st);
-      if (rc == OCM_OK) {
-        hipLaunchKernelGGL(k_trace_og, dim3(p), dim3(256), 0, st, O32, Gp, p, opart);
-        hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, st, opart, p, t3 + 1);
-        hipLaunchKernelGGL(k_add3, dim3(1), dim3(64), 0, st, t3, t3 + 1, theta_out + 2);
-        OCM_CHECK_LAUNCH("k_trace_og");
-      }
-      if (rc) return rc;
-    } else {
-      OCM_HIP(hipMemsetAsync(theta_out + 2, 0, sizeof(double), st));
-    }
   }
   return converged ? OCM_OK : ocm::fail(OCM_ERR_NOCONV, "ocm_eig_topk: max_iter reached before tolerance");
 }
