@@ -90,9 +90,11 @@ int ocm_ctx_destroy(ocm_ctx* ctx) {
   if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   for (auto e : ctx->fork_ev) (void)hipEventDestroy(e);
-  if (ctx->eig_side) (void)hipStreamSynchronize(ctx->eig_side);
+  for (auto s : ctx->eig_side)
+    if (s) (void)hipStreamSynchronize(s);
   if (ctx->eig_sub) (void)ocm_ctx_destroy(ctx->eig_sub);
-  if (ctx->eig_side) (void)hipStreamDestroy(ctx->eig_side);
+  for (auto s : ctx->eig_side)
+    if (s) (void)hipStreamDestroy(s);
   for (auto e : ctx->eig_ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& v : ctx->ev)

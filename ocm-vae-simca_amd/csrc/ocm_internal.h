@@ -32,8 +32,8 @@ struct ocm_ctx {
   // the eigensolver's θ work beside its Jacobi (created on first use): a side
   // stream, fork / join events, and a sub-context whose workspaces the θ3
   // Gram takes (the main workspace holds the eigensolver's live buffers)
-  hipStream_t eig_side = nullptr;
-  hipEvent_t eig_ev[3] = {nullptr, nullptr, nullptr};
+  hipStream_t eig_side[2] = {nullptr, nullptr};
+  hipEvent_t eig_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   ocm_ctx* eig_sub = nullptr;
 };
 

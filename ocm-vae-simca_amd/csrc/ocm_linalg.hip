@@ -40,14 +40,22 @@ namespace {
 // ---------------------------------------------------------------------------
 constexpr int DT = 64, DBK = 16, DPAD = 16;
 
+// MODE 3: as MODE 2 without storing D in fp64: the off-diagonal part goes to
+//         O32 (float32, zero diagonal, row-major p×p), the diagonal to D[row],
+//         each row's Σ_{col≠row} D² over this tile's 64 columns to
+//         rowpart[blockIdx.y·M + row] (the θ3 expansion's Δ terms), plus the
+//         {Σ diag, Σ D²} pair partials of MODE 2.
 template <int MODE, bool TA = false>
 __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
                                                int64_t ldb, double* __restrict__ D, int64_t ldd, int M, int N, int K,
                                                int kper, const double* __restrict__ E, int64_t lde,
-                                               double* __restrict__ part, int tile0 = 0) {
+                                               double* __restrict__ part, int tile0 = 0,
+                                               float* __restrict__ O32 = nullptr,
+                                               double* __restrict__ rowpart = nullptr) {
   __shared__ double As[DBK][DT + DPAD];
   __shared__ double Bs[DBK][DT + DPAD];
   __shared__ double red[8];
+  __shared__ double rsum[2][2][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   int bx = blockIdx.x, by = blockIdx.y;
@@ -117,6 +125,7 @@ __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int
     __syncthreads();
   }
   double tr = 0.0, fro = 0.0;
+  double rs[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -131,6 +140,17 @@ __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int
             D[(int64_t)blockIdx.z * M * ldd + (int64_t)row * ldd + col] = acc[a][b][r];
           } else if (MODE == 1) {
             tr += acc[a][b][r] * E[(int64_t)row * lde + col];
+          } else if (MODE == 3) {
+            const double v = E[(int64_t)row * lde + col] - acc[a][b][r];
+            fro += v * v;
+            if (row == col) {
+              tr += v;
+              D[row] = v;
+              O32[(int64_t)row * N + col] = 0.f;
+            } else {
+              O32[(int64_t)row * N + col] = (float)v;
+              rs[a][r] += v * v;
+            }
           } else {
             const double v = E[(int64_t)row * lde + col] - acc[a][b][r];
             D[(int64_t)row * ldd + col] = v;
@@ -139,9 +159,28 @@ __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int
           }
         }
       }
+  if (MODE == 3) {
+    // row sums over the 16 column lanes of each row, then the two column waves
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double v = rs[a][r];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        if ((lane & 15) == 0) rsum[wm][wn][a * 16 + (lane >> 4) + 4 * r] = v;
+      }
+    __syncthreads();
+    if (tid < 64) {
+      const int row = m0 + tid;
+      if (row < M) rowpart[(int64_t)by * M + row] = rsum[tid >> 5][0][tid & 31] + rsum[tid >> 5][1][tid & 31];
+    }
+  }
   if (MODE >= 1) {
     tr = wave_sum_f64(tr);
-    if (MODE == 2) fro = wave_sum_f64(fro);
+    if (MODE >= 2) fro = wave_sum_f64(fro);
     if (lane == 0) {
       red[wave] = tr;
       red[4 + wave] = fro;
@@ -1296,27 +1335,40 @@ __global__ __launch_bounds__(256) void k_rr_resid32(const double* __restrict__ V
   }
 }
 
-// z_iᵀ M z_i for columns i of Z (b×b, column i = vector i), one wave per
-// column block; lane l of the wave handling column i sums rows l, l + 64, …
-__device__ __forceinline__ double quad_form_col(const double* __restrict__ M, const double* __restrict__ Z, int b,
-                                                int i, int lane) {
-  double acc = 0.0;
-  for (int r = lane; r < b; r += 64) {
-    double mz = 0.0;
-    for (int q = 0; q < b; ++q) mz = fma(M[r * b + q], Z[q * b + i], mz);
-    acc = fma(Z[r * b + i], mz, acc);
+// q[i] = z_iᵀ M z_i for the 32 columns z_i of Z (32×32, column i = vector i):
+// M and Z staged in LDS, Y = M·Z by the workgroup (four entries per thread),
+// then the column dots Σ_r Z[r][i]·Y[r][i] — one workgroup of 256 threads.
+__device__ __forceinline__ void quad_forms32(const double* __restrict__ M, double (*sz)[33], double (*sy)[33],
+                                             double (*smm)[33], double* q) {
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 1024; e += 256) smm[e >> 5][e & 31] = M[e];
+  __syncthreads();
+  for (int e = tid; e < 1024; e += 256) {
+    const int r = e >> 5, i = e & 31;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int j = 0; j < 32; ++j) acc = fma(smm[r][j], sz[j][i], acc);
+    sy[r][i] = acc;
   }
-  return wave_sum_f64(acc);
+  __syncthreads();
+  if (tid < 32) {
+    double acc = 0.0;
+#pragma unroll 8
+    for (int r = 0; r < 32; ++r) acc = fma(sz[r][tid], sy[r][tid], acc);
+    q[tid] = acc;
+  }
+  __syncthreads();
 }
 
-// res[i] = √max(z_iᵀ S z_i, 0) for i < k (one workgroup; wave w takes i ≡ w mod 4)
+// res[i] = √max(z_iᵀ S z_i, 0) for i < k (b = 32, one workgroup)
 __global__ __launch_bounds__(256) void k_rr_test32(const double* __restrict__ S, const double* __restrict__ Z, int b,
                                                    int k, double* __restrict__ res) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int i = wave; i < k; i += 4) {
-    const double q = quad_form_col(S, Z, b, i, lane);
-    if (lane == 0) res[i] = sqrt(fmax(q, 0.0));
-  }
+  __shared__ double sz[32][33], sy[32][33], smm[32][33];
+  __shared__ double q[32];
+  for (int e = threadIdx.x; e < 1024; e += 256) sz[e >> 5][e & 31] = Z[e];
+  quad_forms32(S, sz, sy, smm, q);
+  if (threadIdx.x < k) res[threadIdx.x] = sqrt(fmax(q[threadIdx.x], 0.0));
+  (void)b;
 }
 
 // tr3[0..2] = tr Ct_b, ‖Ct_b‖², tr Ct_b³ (this slice's part); θ3 corrections
@@ -1325,16 +1377,11 @@ __global__ __launch_bounds__(256) void k_theta_combine(const double* __restrict_
                                                        const double* __restrict__ S, const double* __restrict__ G2,
                                                        const double* __restrict__ tr3, int b, int k, int slice0,
                                                        int want3, double* __restrict__ theta_out) {
-  __shared__ double qs[64], qg[64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int i = k + wave; i < b; i += 4) {
-    const double a = quad_form_col(S, Z, b, i, lane);
-    const double g2 = want3 ? quad_form_col(G2, Z, b, i, lane) : 0.0;
-    if (lane == 0) {
-      qs[i] = a;
-      qg[i] = g2;
-    }
-  }
+  __shared__ double sz[32][33], sy[32][33], smm[32][33];
+  __shared__ double qs[32], qg[32];
+  for (int e = threadIdx.x; e < 1024; e += 256) sz[e >> 5][e & 31] = Z[e];
+  quad_forms32(S, sz, sy, smm, qs);
+  if (want3) quad_forms32(G2, sz, sy, smm, qg);
   __syncthreads();
   if (threadIdx.x == 0) {
     double t1 = 0.0, t2 = 0.0, t3 = 0.0, e2 = 0.0, e3 = 0.0, g3 = 0.0;
@@ -1345,7 +1392,7 @@ __global__ __launch_bounds__(256) void k_theta_combine(const double* __restrict_
       t3 += l * l * l;
       e2 += qs[i];
       e3 += l * qs[i];
-      g3 += qg[i];
+      g3 += want3 ? qg[i] : 0.0;
     }
     theta_out[0] = t1 + tr3[0];
     theta_out[1] = (t2 + 2.0 * e2) + tr3[1];
@@ -1587,37 +1634,29 @@ int dgemm_ta(const double* A, const double* B, int p, int b, double* S, double* 
 // off-diagonal part), expanded so that only O goes through a Gram:
 //   trace(D³) = Σ_i Δ_i³ + 3 Σ_i Δ_i Σ_j O_ij² + Σ_ij O_ij (O²)_ij
 // (the terms with one O vanish: O_ii = 0).  The first two are exact fp64 sums
-// over rows [r0, r1) (this slice's rows); O² is the i8×3 Gram of O's rows
-// [r0, r1) (a Gram over a row subset is a partial of O², and the trace is
-// linear in it), and the last term pairs it with all of O.  O has no
-// dominant diagonal, so the Gram's outlier guard stays quiet.
-__global__ __launch_bounds__(256) void k_theta3_diag(const double* __restrict__ D, int p, int r0, int r1,
-                                                      float* __restrict__ O32, double* __restrict__ part) {
+// over rows [r0, r1) (this slice's rows) of k_dgemm<3>'s diagonal and row
+// sums; O² is the i8×3 Gram of O's rows [r0, r1) (a Gram over a row subset is
+// a partial of O², and the trace is linear in it), and the last term pairs it
+// with all of O.  O has no dominant diagonal, so the Gram's outlier guard
+// stays quiet.
+// rows [r0, r1) of the Δ terms of θ3 from k_dgemm<3>'s outputs: per
+// workgroup Σ_i (Δ_i³ + 3 Δ_i Σ_t rowpart[t][i]) over its 256 rows
+__global__ __launch_bounds__(256) void k_theta3_rows(const double* __restrict__ diag,
+                                                     const double* __restrict__ rowpart, int ntc, int p, int r0,
+                                                     int r1, double* __restrict__ part) {
   __shared__ double red[4];
-  const int i = r0 + blockIdx.x;
+  const int i = r0 + blockIdx.x * 256 + threadIdx.x;
   double acc = 0.0;
   if (i < r1) {
-    const double* row = D + (int64_t)i * p;
-    const double di = row[i];
-    double s = 0.0;
-    for (int j = threadIdx.x; j < p; j += 256) {
-      const double o = j == i ? 0.0 : row[j];
-      s += o * o;
-    }
-    acc = 3.0 * di * s;
-    if (threadIdx.x == 0) acc += di * di * di;
+    double s2 = 0.0;
+    for (int t = 0; t < ntc; ++t) s2 += rowpart[(int64_t)t * p + i];
+    const double di = diag[i];
+    acc = di * di * di + 3.0 * di * s2;
   }
   acc = wave_sum_f64(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
-}
-
-__global__ __launch_bounds__(256) void k_offdiag_f32(const double* __restrict__ D, int p, float* __restrict__ O32) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (int64_t)p * p) return;
-  const int i = (int)(e / p), j = (int)(e % p);
-  O32[e] = i == j ? 0.f : (float)D[e];
 }
 
 // partial Σ_ij O_ij G_ij, one row per workgroup (rows in order: deterministic)
@@ -1658,8 +1697,8 @@ __global__ __launch_bounds__(256) void k_inv_evals(const double* __restrict__ ev
 
 // the eigensolver's side stream, its events and the θ3 Gram's sub-context
 int eig_side_init(ocm_ctx* ctx) {
-  if (ctx->eig_side) return OCM_OK;
-  OCM_HIP(hipStreamCreateWithFlags(&ctx->eig_side, hipStreamNonBlocking));
+  if (ctx->eig_sub) return OCM_OK;
+  for (auto& s : ctx->eig_side) OCM_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   for (auto& e : ctx->eig_ev) OCM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   auto* sub = new ocm_ctx();
   sub->device = ctx->device;
@@ -1713,7 +1752,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   const int cvq_ng = (cv_rb + CVQ_G1 - 1) / CVQ_G1;
   const int gt_words = (1 + cvq_ng) * TICKET_STRIDE;
   if (fused) need += (2 * pb + 2048 + (size_t)(cv_rb + cvq_ng) * 1024) * sizeof(double) + gt_words * 4 + 4 * 256;
-  if (theta_mode) need += ((size_t)p * p + 4 * (size_t)b * p + 2 * def_blocks + 8) * sizeof(double) + 4 * 256;
+  if (theta_mode) need += (4 * (size_t)b * p + 2 * def_blocks + 8) * sizeof(double) + 4 * 256;
   void* w = ocm::workspace(ctx, need + 16 * 256, st);
   if (!w) return OCM_ERR_NOMEM;
   ocm::Carve cv{static_cast<char*>(w)};
@@ -1747,7 +1786,6 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   // θ work buffers (the deflated matrix, its tile partials, the rank-2kd
   // operands, three traces), carved up front: the fused path fills them during
   // its Rayleigh–Ritz step, on a side stream
-  double* Ct = theta_mode ? cv.take<double>((size_t)p * p) : nullptr;
   double* dpart = theta_mode ? cv.take<double>(2 * def_blocks) : nullptr;
   double* Ud = theta_mode ? cv.take<double>((size_t)2 * b * p) : nullptr;
   double* Wd = theta_mode ? cv.take<double>((size_t)2 * b * p) : nullptr;
@@ -1853,36 +1891,40 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     hipLaunchKernelGGL(k_deflate_operands, dim3((unsigned)(((size_t)p * kd + 255) / 256)), dim3(256), 0, s, Vb, Wb_,
                        Nm, p, b, kd, Ud, Wd);
     OCM_CHECK_LAUNCH("k_deflate_operands");
-    const dim3 gd((p + DT - 1) / DT, (p + DT - 1) / DT, 1);
-    hipLaunchKernelGGL(k_dgemm<2>, gd, dim3(256), 0, s, Ud, (int64_t)(2 * kd), Wd, (int64_t)p, Ct, (int64_t)p, p, p,
-                       2 * kd, 2 * kd, C, (int64_t)p, dpart, 0);
+    // the deflated matrix D = C − U·Wdᵀ is never stored in fp64: k_dgemm<3>
+    // writes its off-diagonal part O (float32, the θ3 Gram's input), its
+    // diagonal Δ, per-tile row sums of O² and the {tr D, ‖D‖²} partials.  O,
+    // its Gram and the partials live in gctx's second arena (the Gram takes
+    // gctx's workspace).
+    const size_t pp = (size_t)p * p;
+    const int ntc = (p + DT - 1) / DT;
+    const size_t o32_bytes = (pp * sizeof(float) + 255) / 256 * 256;
+    char* aux = static_cast<char*>(ocm::workspace_aux(
+        gctx, o32_bytes + (pp + 4 * (size_t)p + (size_t)ntc * p + 64) * sizeof(double), s));
+    if (!aux) return OCM_ERR_NOMEM;
+    float* O32 = reinterpret_cast<float*>(aux);
+    double* Gp = reinterpret_cast<double*>(aux + o32_bytes);
+    double* csum = Gp + pp;
+    double* diag = csum + p;
+    double* opart = diag + p;  // p row partials of the O·O² term (then the zero shift)
+    double* rowpart = opart + p;
+    double* dpart3 = rowpart + (size_t)ntc * p;  // ≤ p/256 + 1 workgroup partials
+    double* t3 = dpart3 + p;
+    const dim3 gd(ntc, ntc, 1);
+    hipLaunchKernelGGL(k_dgemm<3>, gd, dim3(256), 0, s, Ud, (int64_t)(2 * kd), Wd, (int64_t)p, diag, (int64_t)p, p,
+                       p, 2 * kd, 2 * kd, C, (int64_t)p, dpart, 0, O32, rowpart);
     OCM_CHECK_LAUNCH("k_dgemm deflate");
     hipLaunchKernelGGL(k_sum_pairs, dim3(1), dim3(256), 0, s, dpart, (int)(gd.x * gd.y), out3);  // tr, ‖·‖²
     OCM_CHECK_LAUNCH("k_sum_pairs");
-    // θ3: this slice's rows of the Δ / O expansion (k_theta3_diag), then the
-    // i8×3 Gram of those rows of O.  The Gram takes gctx's workspace, so O
-    // (f32), its Gram and the partials live in gctx's second arena (two
-    // hipMallocAsync calls here cost ≈ 50 µs of host time, with the GPU idle
-    // behind them).
+    // θ3 = Σ Δ³ + 3 Σ Δ_i Σ_j O_ij² + Σ O∘(O²): this slice's rows of the Δ
+    // terms, then the i8×3 Gram of its rows of O against all of O
     const int r0 = (int)((int64_t)p * slice / nslices), r1 = (int)((int64_t)p * (slice + 1) / nslices);
     if (theta_mode >= 2 && r1 > r0) {
       const int nr = r1 - r0;
-      const size_t pp = (size_t)p * p;
-      const size_t o32_bytes = (pp * sizeof(float) + 255) / 256 * 256;
-      char* aux = static_cast<char*>(
-          ocm::workspace_aux(gctx, o32_bytes + (pp + 3 * (size_t)p + 8) * sizeof(double), s));
-      if (!aux) return OCM_ERR_NOMEM;
-      float* O32 = reinterpret_cast<float*>(aux);
-      double* Gp = reinterpret_cast<double*>(aux + o32_bytes);
-      double* csum = Gp + pp;
-      double* dpart3 = csum + p;  // p row partials of the Δ terms
-      double* opart = dpart3 + p;  // p row partials of the O·O² term
-      double* t3 = opart + p;
-      hipLaunchKernelGGL(k_theta3_diag, dim3(nr), dim3(256), 0, s, Ct, p, r0, r1, O32, dpart3);
-      hipLaunchKernelGGL(k_offdiag_f32, dim3((unsigned)((pp + 255) / 256)), dim3(256), 0, s, Ct, p, O32);
-      hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, s, dpart3, nr, t3);
-      OCM_CHECK_LAUNCH("k_theta3_diag");
-      // the shift of the Gram is zero: a p-vector of zeros (taken from the partials' tail)
+      const int nb3 = (nr + 255) / 256;
+      hipLaunchKernelGGL(k_theta3_rows, dim3(nb3), dim3(256), 0, s, diag, rowpart, ntc, p, r0, r1, dpart3);
+      hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, s, dpart3, nb3, t3);
+      OCM_CHECK_LAUNCH("k_theta3_rows");
       float* zshift = reinterpret_cast<float*>(opart);
       OCM_HIP(hipMemsetAsync(zshift, 0, (size_t)p * sizeof(float), s));
       rc2 = ocm::gram_rows_i8(gctx, O32 + (size_t)r0 * p, p, nr, p, zshift, Gp, csum, s);
@@ -1981,47 +2023,52 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
       // (they need no Ritz rotation: k_theta_combine adds its terms later).
       hipLaunchKernelGGL(k_atb32, dim3(CQ_G), dim3(256), 0, st, V, W, p, cq_part, cq_ticket, H);
       OCM_CHECK_LAUNCH("k_atb32 H");
-      hipStream_t rs = st;
+      // two side streams when θ is wanted: A deflates the block and runs
+      // θ3; B forms R and S (the test waits for S), then C·R and G2
+      hipStream_t sa = st, sb = st;
       if (theta_mode) {
         rc = eig_side_init(ctx);
         if (rc) return rc;
-        rs = ctx->eig_side;
+        sa = ctx->eig_side[0];
+        sb = ctx->eig_side[1];
         OCM_HIP(hipEventRecord(ctx->eig_ev[0], st));
-        OCM_HIP(hipStreamWaitEvent(rs, ctx->eig_ev[0], 0));
+        OCM_HIP(hipStreamWaitEvent(sa, ctx->eig_ev[0], 0));
+        OCM_HIP(hipStreamWaitEvent(sb, ctx->eig_ev[0], 0));
+        rc = theta_into(V, W, H, b, sa, ctx->eig_sub, tr3);
+        if (rc) return rc;
+        OCM_HIP(hipEventRecord(ctx->eig_ev[2], sa));
       }
       double* R = T1;
       double* CR = T2;
-      hipLaunchKernelGGL(k_rr_resid32, dim3(CQ_G), dim3(256), 0, rs, V, W, p, H, R, cq_part, cq_ticket, S);
+      hipLaunchKernelGGL(k_rr_resid32, dim3(CQ_G), dim3(256), 0, sb, V, W, p, H, R, cq_part, cq_ticket, S);
       OCM_CHECK_LAUNCH("k_rr_resid32");
-      if (theta_mode) OCM_HIP(hipEventRecord(ctx->eig_ev[1], rs));
+      if (theta_mode) {
+        OCM_HIP(hipEventRecord(ctx->eig_ev[1], sb));
+        hipLaunchKernelGGL(k_cv32, dim3(2 * cv_rb), dim3(512), 0, sb, C, p, R, CR, cv_part, cv_ticket);
+        OCM_CHECK_LAUNCH("k_cv32 CR");
+        if (theta_mode >= 2) {
+          hipLaunchKernelGGL(k_atb32, dim3(CQ_G), dim3(256), 0, sb, R, CR, p, cq_part, cq_ticket, L);  // G2
+          OCM_CHECK_LAUNCH("k_atb32 G2");
+        }
+        OCM_HIP(hipEventRecord(ctx->eig_ev[3], sb));
+      }
       rc = jacobi(H, b, 40, theta, Z, st);
       if (rc) return rc;
       if (theta_mode) OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[1], 0));
       hipLaunchKernelGGL(k_rr_test32, dim3(1), dim3(256), 0, st, S, Z, b, k, res);
       OCM_CHECK_LAUNCH("k_rr_test32");
-      if (theta_mode) {
-        hipLaunchKernelGGL(k_cv32, dim3(2 * cv_rb), dim3(512), 0, rs, C, p, R, CR, cv_part, cv_ticket);
-        OCM_CHECK_LAUNCH("k_cv32 CR");
-        if (theta_mode >= 2) {
-          hipLaunchKernelGGL(k_atb32, dim3(CQ_G), dim3(256), 0, rs, R, CR, p, cq_part, cq_ticket, L);  // G2
-          OCM_CHECK_LAUNCH("k_atb32 G2");
-        }
-        rc = theta_into(V, W, H, b, rs, ctx->eig_sub, tr3);
-        if (rc) return rc;
-        OCM_HIP(hipEventRecord(ctx->eig_ev[2], rs));
-      }
       OCM_HIP(hipMemcpyAsync(hres, theta, 2 * (size_t)b * sizeof(double), hipMemcpyDeviceToHost, st));
       OCM_HIP(hipStreamSynchronize(st));
       double rmax = 0.0;
       for (int i = 0; i < k; ++i) rmax = std::max(rmax, hres[b + i]);
       const double scale = std::fabs(hres[0]);
-      if (!(rmax == rmax)) {
-        if (theta_mode) (void)hipStreamSynchronize(rs);
-        return ocm::fail(OCM_ERR_ARG, "ocm_eig_topk: NaN in covariance");
+      if (theta_mode) {  // R, CR, the deflation operands and the θ3 arena are reused
+        OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[2], 0));
+        OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[3], 0));
       }
+      if (!(rmax == rmax)) return ocm::fail(OCM_ERR_ARG, "ocm_eig_topk: NaN in covariance");
       const double target = tol * (scale > 0 ? scale : 1.0);
       converged = rmax <= target;
-      if (theta_mode) OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[2], 0));  // R, CR, Ct, the θ3 arena reused
       if (converged || it == max_iter) {
         if (theta_mode) {
           hipLaunchKernelGGL(k_theta_combine, dim3(1), dim3(256), 0, st, theta, Z, S, L, tr3, b, k, slice == 0 ? 1 : 0,

@@ -23,7 +23,8 @@ def main():
     for r in rows[a:b]:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         busy += e - s
-        print(f"{(s - t0) / 1e3:9.1f} us  +{(e - s) / 1e3:7.1f}  gap {(s - prev_end) / 1e3:6.1f}  {r['Kernel_Name'][:90]}")
+        q = r.get("Stream_Id") or r.get("Queue_Id") or "?"
+        print(f"{(s - t0) / 1e3:9.1f} us  +{(e - s) / 1e3:7.1f}  gap {(s - prev_end) / 1e3:6.1f}  q{q:>3}  {r['Kernel_Name'][:80]}")
         prev_end = e
     span = int(rows[b]["Start_Timestamp"]) - t0
     print(f"span {span / 1e3:.1f} us, kernels busy {busy / 1e3:.1f} us, idle {(span - busy) / 1e3:.1f} us")
