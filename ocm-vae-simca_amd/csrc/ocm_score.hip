@@ -469,6 +469,13 @@ __device__ __forceinline__ void s1_block_v(f32x4& acA, f32x4& acB, f32x4& acC, f
 #undef OCM_FM
 }  // namespace s1p
 
+#ifdef OCM_S1P_W8  // make exp A/B: OCM_S1P_W8_ON=0 selects the four-wave kernel in the same process
+static bool s1p_w8_enabled() {
+  const char* v = getenv("OCM_S1P_W8_ON");
+  return !v || v[0] != '0';
+}
+#endif
+
 // HH ≥ 0: a lazy view (include/ocm.h ocm_prep, window 2·HH + 1, or SNV only
 // at HH = 0).  Each raw tile is transformed in registers inside sweep 1, block
 // by block one block behind its loads: the quads of the neighbouring lanes of
@@ -479,8 +486,14 @@ __device__ __forceinline__ void s1_block_v(f32x4& acA, f32x4& acB, f32x4& acC, f
 // y replaces x in the AGPR tile, so sweep 2 and the epilogue are unchanged;
 // sweep 1 takes y from VGPRs.  The first / last HH columns of the row (wave 0
 // block 0, wave 3 block NJ − 1) use the least-squares edge rows.
-template <int NJ, bool EX, int HH = -1>
-__global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X, int64_t ldx,
+// WV: waves per workgroup.  4 (the default) = one wave per SIMD with two row
+// tiles in AGPRs; 8 = two waves per SIMD, each with half the columns (NJ
+// halves at the same p) and the same two tiles (half the AGPRs), so one wave's
+// MFMA stream can run under the other's loads and waits.  WV = 8 keeps one
+// tpart buffer (P₀ takes 128 KiB of the 160 KiB of LDS at p = 2048) and adds a
+// barrier before sweep 1 writes it.
+template <int NJ, bool EX, int HH = -1, int WV = 4>
+__global__ __launch_bounds__(64 * WV, 1) void k_score_1p(const float* __restrict__ X, int64_t ldx,
                                                      const int64_t* __restrict__ rows, int64_t m,
                                                      const double* __restrict__ P, const double* __restrict__ mu,
                                                      const double* __restrict__ adiag, int k,
@@ -491,6 +504,9 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
                                                      PrepArgs pa, const float* __restrict__ ptaps,
                                                      const float* __restrict__ prow) {
   using namespace s1p;
+  constexpr int W = WV;             // waves (column slices) per workgroup
+  constexpr int NT = 64 * WV;       // threads
+  constexpr int TPB = WV == 4 ? 2 : 1;  // tpart buffers
   constexpr bool PREP = HH >= 0;
   constexpr int GL = NJ + (HH > 0 ? 1 : 0);  // loads per tile group (the halo quad first)
   constexpr int PW = 16 * NJ;  // columns per wave
@@ -500,7 +516,7 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
   __shared__ f32x4 P0s[16 * NCH];
   __shared__ float nmuL[PP];               // −μ (the sweep-2 μ step's A operand)
   __shared__ double pmuL[20];              // P·μ (fp64)
-  __shared__ double tpart[2][W * 20 * R];  // [buffer][wave][comp][row]
+  __shared__ double tpart[TPB][W * 20 * R];  // [buffer][wave][comp][row]
   __shared__ double qpart[2][W * R];       // [buffer][wave][row]
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -508,7 +524,7 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
 
   // ---- prologue: loadings (f64 → f32) and −μ into LDS, P·μ (fp64), comps
   // 16..19 and diag(A) into registers
-  for (int e = tid; e < 16 * NCH; e += 256) {
+  for (int e = tid; e < 16 * NCH; e += NT) {
     const int c = e / NCH, ch = e - c * NCH;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (c < k)
@@ -516,7 +532,7 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
       for (int u = 0; u < 4; ++u) v[u] = (float)P[(int64_t)c * PP + 4 * ch + u];
     P0s[c * NCH + (ch ^ sw(c))] = v;
   }
-  for (int c = tid; c < PP; c += 256) nmuL[c] = -(float)mu[c];
+  for (int c = tid; c < PP; c += NT) nmuL[c] = -(float)mu[c];
   for (int c = w; c < 20; c += W) {  // wave w: comps w, w + 4, ...
     double s = 0.0;
     if (c < k)
@@ -534,7 +550,7 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
   // (the widest lazy-view variant, HH = 7 at NJ = 32, has no VGPRs to spare for
   // p1b: its sweep 1 reads p1a at the equivalent lane, 16c + 4lq + e, and takes
   // the 2-way conflicts back — round 3 measured them at no cost in time)
-  constexpr bool NOP1B = EX && NJ == 32 && HH > 4;
+  constexpr bool NOP1B = EX && ((NJ == 32 && HH > 4) || WV == 8);  // WV = 8: no registers to spare either
   float p1b[EX && !NOP1B ? NJ : 1];
   if constexpr (EX)
 #pragma unroll
@@ -543,9 +559,16 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
       p1a[j] = 16 + lq < k ? (float)P[rowp + ln] : 0.f;
       if constexpr (!NOP1B) p1b[j] = 16 + lq < k ? (float)P[rowp + (ln ^ (8 * (lq >> 1)))] : 0.f;
     }
-  double ad[5];
+  // diag(A) of this lane's comps lq + 4s: registers at WV = 4, LDS at WV = 8
+  // (read once per tile, in compute_t; the registers went to the tiles)
+  __shared__ double adL[WV == 8 ? 20 : 1];
+  double ad[WV == 8 ? 1 : 5];
+  if constexpr (WV == 8) {
+    if (tid < 20) adL[tid] = tid < k ? adiag[tid] : 0.0;
+  } else {
 #pragma unroll
-  for (int s = 0; s < 5; ++s) ad[s] = lq + 4 * s < k ? adiag[lq + 4 * s] : 0.0;
+    for (int s = 0; s < 5; ++s) ad[s] = lq + 4 * s < k ? adiag[lq + 4 * s] : 0.0;
+  }
   // sweep-1 A operand: chunk (w·PW/4 + 4j + lq) ^ sw(ln) of comp ln; the XOR
   // only touches the low 4 bits, so j = 4a + b reads b1[b] + 16a chunks
   int b1[4];
@@ -862,7 +885,14 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
         }
       });
     }
-    double* tp = tpart[buf];
+    if constexpr (TPB == 1) {
+      // one buffer: every wave has read the previous tile's t (compute_t,
+      // right after the last barrier) before any wave overwrites it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    double* tp = tpart[TPB == 1 ? 0 : buf];
 #pragma unroll
     for (int i = 0; i < 4; ++i) tp[(w * 20 + 4 * lq + i) * R + ln] = t64[i];
     if constexpr (EX) {  // comps 16..19: lane (ln, lq) holds the partial over its column quarter lq
@@ -878,7 +908,7 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
   };
   // ---- full t of this lane's comps lq + 4s (row ln) from tpart[buf]; T², T --
   auto compute_t = [&](int64_t t, int buf) {
-    const double* tp = tpart[buf];
+    const double* tp = tpart[TPB == 1 ? 0 : buf];
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
       double v = 0.0;
@@ -891,7 +921,7 @@ __global__ __launch_bounds__(256, 1) void k_score_1p(const float* __restrict__ X
     }
     T2 = 0.0;
 #pragma unroll
-    for (int s = 0; s < 5; ++s) T2 += tt[s] * tt[s] * ad[s];
+    for (int s = 0; s < 5; ++s) T2 += tt[s] * tt[s] * (WV == 8 ? adL[lq + 4 * s] : ad[s < (WV == 8 ? 1 : 5) ? s : 0]);
     T2 += __shfl_xor(T2, 16, 64);
     T2 += __shfl_xor(T2, 32, 64);
     const int64_t row = t * R + ln;
@@ -1280,7 +1310,7 @@ int score_diag_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* ro
                     const PrepArgs* pp, const double* P, const double* mu, const double* a_diag, int32_t k,
                     float* T_out, double* T2_out, float* Q_out, const ocm_decision* dec, double* accept_out,
                     int64_t accept_stride, double* stats_out, hipStream_t st) {
-  const int nj = p / 64;
+  int nj = p / 64;
   const bool vec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
   bool one_pass = vec && p % 64 == 0 && (nj == 4 || nj == 8 || nj == 16 || nj == 32) && k <= 20;
   const PrepArgs pa = pp ? *pp : PrepArgs{};
@@ -1329,6 +1359,19 @@ int score_diag_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* ro
 #define OCM_S1P_H(NJ_, EX_, H_)                                                                                 \
   hipLaunchKernelGGL((k_score_1p<NJ_, EX_, H_>), dim3(grid), dim3(256), 0, st, X, ldx, rows, m, P, mu, a_diag, k, \
                      T_out, T2_out, Q_out, d, accept_out, accept_stride, part, ntiles, pa, pa.taps, pa.rowstat)
+#ifdef OCM_S1P_W8  // make exp A/B: two waves per SIMD at p = 2048 (plain rows)
+    if (nj == 32 && !pp && s1p_w8_enabled()) {
+      if (k > 16)
+        hipLaunchKernelGGL((k_score_1p<16, true, -1, 8>), dim3(grid), dim3(512), 0, st, X, ldx, rows, m, P, mu, a_diag,
+                           k, T_out, T2_out, Q_out, d, accept_out, accept_stride, part, ntiles, pa, pa.taps,
+                           pa.rowstat);
+      else
+        hipLaunchKernelGGL((k_score_1p<16, false, -1, 8>), dim3(grid), dim3(512), 0, st, X, ldx, rows, m, P, mu,
+                           a_diag, k, T_out, T2_out, Q_out, d, accept_out, accept_stride, part, ntiles, pa, pa.taps,
+                           pa.rowstat);
+      nj = 0;  // launched
+    }
+#endif
 #define OCM_S1P(NJ_, EX_)                                  \
   if (!pp)                                                 \
     OCM_S1P_H(NJ_, EX_, -1);                               \
@@ -1344,7 +1387,8 @@ int score_diag_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* ro
   } else {             \
     OCM_S1P(NJ_, false) \
   }
-    if (nj == 32) {
+    if (nj == 0) {
+    } else if (nj == 32) {
       OCM_S1P_K(32)
     } else if (nj == 16) {
       OCM_S1P_K(16)
