@@ -321,3 +321,25 @@ def test_cv_dropin_under_process_group_shards_and_matches(tmp_path, golden_dir):
         np.testing.assert_allclose(got["h"], g["h"], rtol=1e-4, atol=1e-6)
         np.testing.assert_allclose(got["f"], g["f"], rtol=1e-4)
         np.testing.assert_allclose(got["crit"], g["crit"], rtol=1e-4)
+
+
+def test_cv_engine_over_rccl_world1():
+    """The nccl branches of the distributed CV fold engine on a real RCCL
+    group (one rank: the box has one GPU) equal the engine without a group."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "nccl_world1_worker.py")], capture_output=True, text=True,
+                       timeout=240, cwd=os.path.dirname(here))
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["backend"] == "nccl"
+    # the distributed path packs the train moments about a zero shift and
+    # rebuilds C from the packed triangle (a different fp64 summation than the
+    # one-process path): rows on the decision boundary may flip
+    np.testing.assert_allclose(res["spec"], res["spec_ref"], atol=0.2)
+    np.testing.assert_allclose(res["sens"], res["sens_ref"], atol=0.2)
+    assert res["pred_diff"] <= 3
