@@ -820,25 +820,47 @@ __device__ __forceinline__ void q8_tail(f32x4 (&v)[16], int tid, int cq, int rs,
   }
   // row quads outermost: v[4k .. 4k+3] are dead after quad k, so the digits
   // take the registers the values free (peak ≈ 64 + 12, not 64 + 48: no spills
-  // at the 168-VGPR budget of three waves per SIMD)
+  // at the 168-VGPR budget of three waves per SIMD).
+  // Digits by the round-to-nearest-even of an add of 1.5·2²³ (round 5): for
+  // |x| < 2²² the f32 sum x + 1.5·2²³ is 0x4B400000 + rint(x), so its low byte
+  // IS the int8 digit (no v_rndne / v_cvt_i32) and subtracting 1.5·2²³ back
+  // gives rint(x) exactly; in pairs of rows on packed f32 (v_pk_add / v_pk_mul):
+  // the same digits as rintf, bit for bit (the Gram of the bench workload
+  // hashes identically with either split: profiles/r05h_quant_ab.json; the
+  // quantiser is HBM-bound, 3.03 vs 3.05 ms).  No implicit FMA contraction
+  // (t2 is rounded before the add that rounds it to an integer, as rintf(t2)
+  // saw it); the third digit's remainder is the one explicit FMA,
+  // (t − a1)·254 − a2 with the exact product, as the contracted rintf form
+  // computed it.
+  {
+#pragma clang fp contract(off)
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2 MG = {12582912.f, 12582912.f}, BASE = {Q8BASE, Q8BASE};
+    auto bits = [](float f) { return __builtin_bit_cast(uint32_t, f); };
+    auto pack = [&](f32x2 lo, f32x2 hi) -> int {  // low bytes of four sums → one dword (rows u = 0..3)
+      const uint32_t l = __builtin_amdgcn_perm(bits(lo.y), bits(lo.x), 0x0c0c0400u);
+      const uint32_t h = __builtin_amdgcn_perm(bits(hi.y), bits(hi.x), 0x04000c0cu);
+      return (int)(l | h);
+    };
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 4; ++k) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float d1[4], d2[4], d3[4];
+      for (int e = 0; e < 4; ++e) {
+        const f32x2 ie = {inv[e], inv[e]};
+        f32x2 A[2], B[2], Cd[2];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float t = v[4 * k + u][e] * inv[e];  // exact (power of two), |t| ≤ 127
-        const float a1 = rintf(t);
-        const float t2 = (t - a1) * Q8BASE;
-        const float a2 = rintf(t2);
-        d1[u] = a1;
-        d2[u] = a2;
-        d3[u] = rintf((t2 - a2) * Q8BASE);
+        for (int h = 0; h < 2; ++h) {
+          const f32x2 t = f32x2{v[4 * k + 2 * h][e], v[4 * k + 2 * h + 1][e]} * ie;  // exact, |t| ≤ 127
+          A[h] = t + MG;
+          const f32x2 d = t - (A[h] - MG);  // exact
+          const f32x2 t2 = d * BASE;
+          B[h] = t2 + MG;
+          Cd[h] = __builtin_elementwise_fma(d, BASE, MG - B[h]) * BASE + MG;  // MG − B = −a2 exactly
+        }
+        w[0][e][k] = pack(A[0], A[1]);
+        w[1][e][k] = pack(B[0], B[1]);
+        w[2][e][k] = pack(Cd[0], Cd[1]);
       }
-      w[0][e][k] = (int)q8_pack4(d1[0], d1[1], d1[2], d1[3]);
-      w[1][e][k] = (int)q8_pack4(d2[0], d2[1], d2[2], d2[3]);
-      w[2][e][k] = (int)q8_pack4(d3[0], d3[1], d3[2], d3[3]);
     }
   }
   // stage image: [group][column 0..31][32 B]; copy-out: 16 B per thread and
