@@ -369,11 +369,12 @@ def run_simca(args, rk, n_total):
 
 
 def run_prep(args, rk, n_total):
-    """the drivers' preprocessing before SIMCA, two ways, on
-    the same raw rows: the eager pass (``snv_savgol``: X′ written to HBM) then
-    fit + predict on X′, against the lazy view (``lazy=True``: the transform
-    runs in the Gram quantiser's and the scoring kernel's load paths, X′ never
-    exists).  Settings: simca_nuts.py:47-52 (SNV, w 5, p 2, deriv 1) and
+    """the drivers' preprocessing before SIMCA, three ways,
+    on the same raw rows: the eager pass (``snv_savgol``: X′ written to HBM)
+    then fit + predict on X′; the no-copy lazy view (``lazy=True``: the
+    transform runs in the Gram quantiser's and the scoring kernel's load paths,
+    X′ never exists); and the write-through view (``lazy="write"``: the
+    quantiser writes X′ as it forms it, the scoring reads X′).  Settings: simca_nuts.py:47-52 (SNV, w 5, p 2, deriv 1) and
     simca_new_cheese.py:37-39 (w 15, p 2, deriv 1, no SNV)."""
     import torch
 
@@ -390,9 +391,10 @@ def run_prep(args, rk, n_total):
     out = {"metric": "spectra/s, preprocessing + SIMCA fit + predict", "rows": n_total, "p": p, "k": k}
     for name, (snv, w) in {"nuts_snv_sg5_d1": (True, 5), "cheese_sg15_d1": (False, 15)}.items():
         res = {}
-        for mode in ("materialised", "fused"):
+        for mode in ("materialised", "fused", "fused_write"):
             def step():
-                Xp = preprocess.snv_savgol(X, w, 2, 1, 1.0, snv=snv, lazy=(mode == "fused"))
+                lazy = {"materialised": False, "fused": True, "fused_write": "write"}[mode]
+                Xp = preprocess.snv_savgol(X, w, 2, 1, 1.0, snv=snv, lazy=lazy)
                 model = SIMCA(n_components=k, model_class=0, type="alt", t2lim="Fdist", qlim="jm", verbose=False)
                 model.fit(Xp, y)
                 return model.predict(Xp)
@@ -410,7 +412,7 @@ def run_prep(args, rk, n_total):
                          "quantise_ms": round(t["quant"][0] / max(t["quant"][1], 1), 4),
                          "score_ms": round(t["score"][0] / max(t["score"][1], 1), 4),
                          "gram_ms": round(t["gram"][0] / max(t["gram"][1], 1), 4)}
-            if mode == "fused":
+            if mode != "materialised":
                 res[mode]["materialised_views"] = materialised_count(rk.device.index) - c0
         out[name] = res
     del X, y

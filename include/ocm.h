@@ -379,6 +379,15 @@ int ocm_colmean_f32_prep(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_
 int ocm_gram_f32_prep(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
                       const float* shift, const int64_t* seg_offsets, int32_t nseg, int32_t mode,
                       int64_t chunk_rows, const ocm_prep* prep, double* G_out, double* colsum_out, void* stream);
+/* Write-through (round 5): ocm_gram_f32_prep (i8×3, all n rows of X, no gather list) whose quantiser
+ * also writes the preprocessed rows to xout [dev] n×p (ldo % 4 == 0, 16-B aligned) as it forms them:
+ * the stencil runs once, in the Gram's read of X, and the consumers after the Gram (scoring of the fit
+ * and predict sets) read X′ with the plain kernels.  The values are those of ocm_prep_apply_f32 bit for
+ * bit.  Shapes and transforms the fused quantiser does not cover run the eager pass into xout, then the
+ * Gram on it. */
+int ocm_gram_f32_prep_write(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t n, int32_t p, const float* shift,
+                            const int64_t* seg_offsets, int32_t nseg, int64_t chunk_rows, const ocm_prep* prep,
+                            double* G_out, double* colsum_out, float* xout, int64_t ldo, void* stream);
 /* Number of times this context materialised a lazy view (the fallback paths above), for tests and
  * diagnostics: 0 after any call on the fused paths. */
 int ocm_prep_materialised(ocm_ctx* ctx, int64_t* count_out);

@@ -722,18 +722,24 @@ constexpr int Q8QT = Q8QS * (Q8QC / 4);    // threads (768)
 // and their LDS-staged stores (shared by k_q8_quant and k_q8_quant_prep).
 // q8_tail's LDS (the caller declares it: k_q8_quant_prep overlays its own
 // load-phase buffers on it)
-struct Q8TailLds {
-  __attribute__((aligned(16))) char stage[Q8SPB * Q8QC * 32];  // one digit plane: 24 KiB
-  __attribute__((aligned(16))) float wmax[Q8QS][Q8QC];
-  __attribute__((aligned(16))) double wsum[Q8QS][Q8QC];
-  float pmax[8][Q8QC];
-  double psum[8][Q8QC];
-  __attribute__((aligned(16))) float fmax_[Q8QC];
+template <int QC = Q8QC>
+struct Q8TailLdsT {
+  __attribute__((aligned(16))) char stage[Q8SPB * QC * 32];  // one digit plane: 24 KiB at QC = 32
+  __attribute__((aligned(16))) float wmax[Q8QS][QC];
+  __attribute__((aligned(16))) double wsum[Q8QS][QC];
+  float pmax[8][QC];
+  double psum[8][QC];
+  __attribute__((aligned(16))) float fmax_[QC];
 };
+using Q8TailLds = Q8TailLdsT<>;
+template <int QC = Q8QC>
+// th: the thresholds of the thread's four columns, loaded by the caller in
+// its load phase (a global load here would wait, through vmcnt, for every
+// store the caller has issued — the write-through X′ rows)
 __device__ __forceinline__ void q8_tail(f32x4 (&v)[16], int tid, int cq, int rs, int cg0, int c0, int64_t rb,
                                         const Q8Plan& q, int chunk, int b, const SegTable& st,
-                                        double* __restrict__ colblk, Q8TailLds& L) {
-  constexpr int QC = Q8QC;
+                                        double* __restrict__ colblk, Q8TailLdsT<QC>& L, const f32x4 th) {
+  constexpr int NT = Q8QS * (QC / 4);  // threads
   char* stage = L.stage;
   auto& wmax = L.wmax;
   auto& wsum = L.wsum;
@@ -749,16 +755,14 @@ __device__ __forceinline__ void q8_tail(f32x4 (&v)[16], int tid, int cq, int rs,
   // outlier screen: rows with a value above the threshold in this column group are
   // taken out of its scale and digits (k_gram_fixup adds them exactly)
   {
-    const f32x4 th = *reinterpret_cast<const f32x4*>(q.thr + c0);
     uint32_t ext = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) ext |= (fabsf(v[j][e]) > th[e]) ? (1u << j) : 0u;
-    // OR over the 8 threads (consecutive lanes) that share this row slice
-    ext |= __shfl_xor(ext, 1, 64);
-    ext |= __shfl_xor(ext, 2, 64);
-    ext |= __shfl_xor(ext, 4, 64);
+    // OR over the QC / 4 threads (consecutive lanes) that share this row slice
+#pragma unroll
+    for (int o = 1; o < QC / 4; o *= 2) ext |= __shfl_xor(ext, o, 64);
     if (ext) {
 #pragma unroll
       for (int j = 0; j < 16; ++j)
@@ -874,9 +878,10 @@ __device__ __forceinline__ void q8_tail(f32x4 (&v)[16], int tid, int cq, int rs,
     for (int e = 0; e < 4; ++e)
       *reinterpret_cast<i32x4*>(&stage[grp * GIMG + q8_qslot(2 * (4 * cq + e) + half) * 16]) = w[dg][e];
     __syncthreads();
+    static_assert(Q8SPB * GIMG % (16 * NT) == 0, "copy-out passes");
 #pragma unroll
-    for (int k = 0; k < Q8SPB * GIMG / (16 * Q8QT); ++k) {
-      const int o = 16 * (tid + Q8QT * k);  // byte offset in the stage image
+    for (int k = 0; k < Q8SPB * GIMG / (16 * NT); ++k) {
+      const int o = 16 * (tid + NT * k);  // byte offset in the stage image
       const int g = o / GIMG, within = o - g * GIMG;
       *reinterpret_cast<i32x4*>(gdst + (size_t)dg * q.plane + (size_t)g * q.P8 * 32 + within) =
           *reinterpret_cast<const i32x4*>(&stage[g * GIMG + q8_qslot(within >> 4) * 16]);
@@ -885,19 +890,22 @@ __device__ __forceinline__ void q8_tail(f32x4 (&v)[16], int tid, int cq, int rs,
   }
 }
 
-template <bool GATHER, int CG = 1>
-__global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ X, int64_t ldx,
-                                                      const int64_t* __restrict__ rows, int p,
-                                                      const float* __restrict__ shift, SegTable st, Q8Plan q,
-                                                      double* __restrict__ colblk, int cb0) {
-  constexpr int QC = Q8QC;
+// QC: columns per workgroup.  16-column workgroups (384 threads, two per CU)
+// measured 4.25 against 3.02 ms for the default at 1M × 2048: rows read as
+// 16 × 64 B per wave instruction lose more than the second workgroup per CU
+// gains (profiles/r05j_quant_qc16_ab.json)
+template <bool GATHER, int CG = 1, int QC = Q8QC>
+__global__ __launch_bounds__(Q8QS * (QC / 4), 1) void k_q8_quant(const float* __restrict__ X, int64_t ldx,
+                                                                 const int64_t* __restrict__ rows, int p,
+                                                                 const float* __restrict__ shift, SegTable st,
+                                                                 Q8Plan q, double* __restrict__ colblk, int cb0) {
   // CG > 1 (A/B): CG neighbouring 32-column groups of one row block on
   // consecutive workgroups (they run at the same time on other CUs), so each
   // row's CG·128 bytes are read close in time
   const int gbk = (int)(blockIdx.x / CG) + cb0;  // (chunk, block) of the call's chunk range
   const int chunk = gbk / q.nblk, b = gbk - chunk * q.nblk;
   const int tid = threadIdx.x;
-  const int cq = tid & 7, rs = tid >> 3;
+  const int cq = tid % (QC / 4), rs = tid / (QC / 4);
   int s = 0;
   while (s + 1 < st.nseg && chunk >= st.cprefix[s + 1]) ++s;
   const int64_t r0 = st.begin[s] + (int64_t)(chunk - st.cprefix[s]) * st.chunk_rows;
@@ -948,8 +956,8 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant(const float* __restrict__ 
       for (int e = 0; e < 4; ++e) v[j][e] = (g < r1 && c0 + e < p) ? x[e] - sh[e] : 0.f;
     }
   }
-  __shared__ Q8TailLds lds;
-  q8_tail(v, tid, cq, rs, cg0, c0, rb, q, chunk, b, st, colblk, lds);
+  __shared__ Q8TailLdsT<QC> lds;
+  q8_tail<QC>(v, tid, cq, rs, cg0, c0, rb, q, chunk, b, st, colblk, lds, *reinterpret_cast<const f32x4*>(q.thr + c0));
 }
 
 // k_q8_quant with the preprocessing of a lazy view applied in the load path
@@ -976,12 +984,16 @@ union Q8PrepUnion {
   Q8TailLds tail;
   Q8PrepLds<HH> ld;
 };
-template <bool GATHER, int HH>
+// WR (write-through, round 5): the preprocessed rows also go to xout (ldo),
+// so the consumers after the Gram read X′ plainly and the stencil runs once
+// (ocm_gram_f32_prep_write; contiguous rows only)
+template <bool GATHER, int HH, bool WR = false>
 __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restrict__ X, int64_t ldx,
                                                            const int64_t* __restrict__ rows, int p,
                                                            const float* __restrict__ shift, SegTable st, Q8Plan q,
                                                            double* __restrict__ colblk, int cb0, int ncg,
-                                                           PrepArgs pa) {
+                                                           PrepArgs pa, float* __restrict__ xout, int64_t ldo) {
+  static_assert(!(WR && GATHER), "write-through takes contiguous rows");
   constexpr int HQ = (HH + 3) / 4;
   constexpr int WN = 2 * HH + 1;
   __shared__ Q8PrepUnion<HH> lds;
@@ -1023,6 +1035,7 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restri
   f32x4 sh;
 #pragma unroll
   for (int e = 0; e < 4; ++e) sh[e] = c0 + e < p ? shift[c0 + e] : 0.f;
+  const f32x4 th = *reinterpret_cast<const f32x4*>(q.thr + c0);
   const float* c = pa.taps + HH;  // interior taps, offset -HH..HH (scalar loads)
   float ct[HH + 1];
 #pragma unroll
@@ -1044,6 +1057,8 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restri
   const int64_t nvalid = max((int64_t)0, min(r1 - rblk, (int64_t)Q8BLK));
   const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(X + (bufd ? rblk * ldx : 0)), 0, bufd ? (uint32_t)(nvalid * ldx * 4) : 0u, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(WR ? xout + rblk * ldo : nullptr), 0, WR ? (uint32_t)(nvalid * ldo * 4) : 0u, 0x00020000);
   auto load_q = [&](int jr, int col) -> f32x4 {  // the quad at column col of slice row jr
     if constexpr (bufd)
       return __builtin_bit_cast(
@@ -1155,11 +1170,17 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restri
       }
     }
     __builtin_amdgcn_wave_barrier();  // the image is rewritten by the next row
+    if constexpr (WR) {  // eight lanes: one row's 128 B (p % 4 == 0: a quad is all in or all out);
+                         // rows past r1 fall outside the descriptor and are dropped
+      if (c0 < p)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, y), rs_o, (int)(((16 * rs + j) * ldo + c0) * 4),
+                                               0, 0);
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[j][e] = (g < r1 && c0 + e < p) ? __fsub_rn(y[e], sh[e]) : 0.f;
   }
   __syncthreads();  // q8_tail's LDS overlays the load phase's
-  q8_tail(v, tid, cq, rs, cg0, c0, rb, q, chunk, b, st, colblk, lds.tail);
+  q8_tail(v, tid, cq, rs, cg0, c0, rb, q, chunk, b, st, colblk, lds.tail, th);
 }
 
 // Column sums of the quantiser's per-block partials: rows [c0, c1) of colblk
@@ -2446,7 +2467,7 @@ int gram_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, in
 int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
                const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
                hipStream_t st, int64_t chunk_rows, bool k32, const PrepArgs& pa = PrepArgs{},
-               bool unguarded = false) {
+               bool unguarded = false, float* xout = nullptr, int64_t ldo = 0) {
   // unguarded: an internal Gram (the eigensolver's θ3 of the off-diagonal
   // deflated covariance) — no outlier screen (thresholds +inf, nothing marked,
   // no read-back), not timed, ctx->last_gram_marks left alone
@@ -2614,15 +2635,15 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     if (prep) {
       const int ncg = P8 / Q8QC;
       const dim3 gp((unsigned)((c1 - c0) * nblk * ncg));
-#define Q8P_LAUNCH(G_, H_)                                                                                        \
-  hipLaunchKernelGGL((k_q8_quant_prep<G_, H_>), gp, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, col_g, \
-                     (int)(c0 * nblk), ncg, pa)
+#define Q8P_LAUNCH(G_, H_, W_)                                                                                \
+  hipLaunchKernelGGL((k_q8_quant_prep<G_, H_, W_>), gp, dim3(Q8QT), 0, qs, X, ldx, rows, p, shift, tabs[t], q, \
+                     col_g, (int)(c0 * nblk), ncg, pa, xout, ldo)
       if (pa.h == 0) {
-        if (rows) Q8P_LAUNCH(true, 0); else Q8P_LAUNCH(false, 0);
+        if (rows) Q8P_LAUNCH(true, 0, false); else if (xout) Q8P_LAUNCH(false, 0, true); else Q8P_LAUNCH(false, 0, false);
       } else if (pa.h == 2) {
-        if (rows) Q8P_LAUNCH(true, 2); else Q8P_LAUNCH(false, 2);
+        if (rows) Q8P_LAUNCH(true, 2, false); else if (xout) Q8P_LAUNCH(false, 2, true); else Q8P_LAUNCH(false, 2, false);
       } else {
-        if (rows) Q8P_LAUNCH(true, 7); else Q8P_LAUNCH(false, 7);
+        if (rows) Q8P_LAUNCH(true, 7, false); else if (xout) Q8P_LAUNCH(false, 7, true); else Q8P_LAUNCH(false, 7, false);
       }
 #undef Q8P_LAUNCH
     } else if (rows)
@@ -2876,6 +2897,35 @@ int ocm_gram_f32_prep(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* 
   }
   return gram_materialised(ctx, X, ldx, rows, n, p, shift, seg_offsets, nseg, mode, chunk_rows, pa, G_out,
                            colsum_out, st);
+}
+
+int ocm_gram_f32_prep_write(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t n, int32_t p, const float* shift,
+                            const int64_t* seg_offsets, int32_t nseg, int64_t chunk_rows, const ocm_prep* prep,
+                            double* G_out, double* colsum_out, float* xout, int64_t ldo, void* stream) {
+  OCM_REQUIRE(ctx && X && shift && seg_offsets && G_out && colsum_out && xout,
+              "ocm_gram_f32_prep_write: NULL argument");
+  OCM_REQUIRE(n > 0 && p > 0 && ldx >= p && ldo >= p && nseg > 0, "ocm_gram_f32_prep_write: bad shape");
+  OCM_REQUIRE(seg_offsets[0] == 0 && seg_offsets[nseg] == n, "ocm_gram_f32_prep_write: seg_offsets must span [0, n]");
+  for (int s = 0; s < nseg; ++s)
+    OCM_REQUIRE(seg_offsets[s + 1] >= seg_offsets[s], "ocm_gram_f32_prep_write: seg_offsets not ascending");
+  if (int rc = ocm::check_prep(prep, p, "ocm_gram_f32_prep_write")) return rc;
+  const PrepArgs pa = ocm::prep_args(prep);
+  hipStream_t st = (hipStream_t)stream;
+  const bool wr_ok = ldo % 4 == 0 && (reinterpret_cast<uintptr_t>(xout) & 15) == 0 &&
+                     (int64_t)Q8BLK * ldo * 4 < (1LL << 31);  // the store descriptor's 32-bit offsets
+  if (wr_ok && prep_fused_gram(X, ldx, p, OCM_GRAM_I8X3, pa)) {
+    const int rc = gram_impl8(ctx, X, ldx, nullptr, n, p, shift, seg_offsets, nseg, G_out, colsum_out, st, chunk_rows,
+                              false, pa, false, xout, ldo);
+    if (rc != 1) return rc;
+    // too many screened rows: the quantiser has written every row, so the
+    // exact split runs on X′
+    return gram_dispatch(ctx, xout, ldo, nullptr, n, p, shift, seg_offsets, nseg, OCM_GRAM_BF16X3, chunk_rows, G_out,
+                         colsum_out, st);
+  }
+  // no fused quantiser for this shape or transform: the eager pass into xout
+  if (int rc = ocm::prep_apply(ctx, X, ldx, nullptr, n, p, pa, xout, ldo, st)) return rc;
+  return gram_dispatch(ctx, xout, ldo, nullptr, n, p, shift, seg_offsets, nseg, OCM_GRAM_I8X3, chunk_rows, G_out,
+                       colsum_out, st);
 }
 
 int ocm_colmean_f32_prep(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,

@@ -334,7 +334,7 @@ __global__ __launch_bounds__(256, 2) void k_score_direct(const float* X, int64_t
 // reference forms X − (T·P + μ) in float32 (utils/SIMCA.py:67, 105).
 // ---------------------------------------------------------------------------
 namespace s1p {
-constexpr int W = 4, R = 16;
+constexpr int R = 16;  // rows per tile (the waves per workgroup are k_score_1p's WV)
 // compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N-1
 template <class F, int... I>
 __device__ __forceinline__ void sfor_(F&& f, std::integer_sequence<int, I...>) {

@@ -153,6 +153,8 @@ SIGNATURES = {
     "ocm_gram_f32_prep": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p,
                                   ctypes.POINTER(c_i64), c_i32, c_i32, c_i64, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),
+    "ocm_gram_f32_prep_write": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_i32, c_void_p, ctypes.POINTER(c_i64),
+                                        c_i32, c_i64, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_void_p]),
     "ocm_score_f32_diag_prep": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p,
                                         ctypes.POINTER(OcmDecision), c_void_p, c_i64, c_void_p, c_void_p]),

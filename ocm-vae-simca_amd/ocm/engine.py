@@ -124,7 +124,15 @@ def _stream(dev):
     return stream_handle(dev)
 
 
+def _plain(X):
+    """A write-through view that has been written is its X′ tensor."""
+    if isinstance(X, PrepView) and X.written() is not None:
+        return X.written()
+    return X
+
+
 def colmean(X: torch.Tensor, rows: torch.Tensor | None, n: int) -> torch.Tensor:
+    X = _plain(X)
     ctx = Context.get(X.device.index)
     out = torch.empty(X.shape[1], dtype=torch.float64, device=X.device)
     if isinstance(X, PrepView):
@@ -165,6 +173,7 @@ def gram(X: torch.Tensor, rows: torch.Tensor | None, seg_offsets, shift32: torch
          chunk_rows: int = 0):
     """Per-segment shifted Gram (nseg, p, p) f64 and column sums (nseg, p).
     float64 X takes the fp64-MFMA Gram (``mode`` does not apply)."""
+    X = _plain(X)
     p = X.shape[1]
     seg = [int(s) for s in seg_offsets]
     nseg = len(seg) - 1
@@ -173,6 +182,16 @@ def gram(X: torch.Tensor, rows: torch.Tensor | None, seg_offsets, shift32: torch
     cs = torch.empty((nseg, p), dtype=torch.float64, device=X.device)
     arr = (ctypes.c_int64 * len(seg))(*seg)
     ctx = Context.get(X.device.index)
+    if (isinstance(X, PrepView) and X.through and rows is None and n == X.shape[0]
+            and (mode or _gram_mode) == "i8x3"):
+        # write-through: the quantiser also writes X′, which later consumers read
+        st = X.struct()
+        xp = torch.empty(X.shape, dtype=torch.float32, device=X.device)
+        check(_lib.load().ocm_gram_f32_prep_write(ctx.handle, ptr(X.X), X.X.stride(0), n, p, ptr(shift32), arr, nseg,
+                                                  int(chunk_rows), ctypes.byref(st), ptr(G), ptr(cs), ptr(xp),
+                                                  xp.stride(0), _stream(X.device)), "ocm_gram_f32_prep_write")
+        X._set_written(xp)
+        return G, cs
     if isinstance(X, PrepView):  # the preprocessing runs in the quantiser's load path
         st = X.struct()
         check(_lib.load().ocm_gram_f32_prep(ctx.handle, ptr(X.X), X.X.stride(0), ptr(rows), n, p, ptr(shift32), arr,
@@ -287,6 +306,7 @@ def score(X: torch.Tensor, rows: torch.Tensor | None, m: int, P64: torch.Tensor,
     """Fused scoring: P64 (k, p) f64 orthonormal rows, mean64 (p,) f64, A the
     (k, k) quadratic form (ocm_score_f32) or its diagonal (k,) (ocm_score_f32_diag,
     the single-HBM-pass kernel for the SIMCA shapes).  Returns dict of device tensors."""
+    X = _plain(X)
     k, p = P64.shape
     dev = X.device
     out = {}

@@ -62,18 +62,25 @@ def snv_savgol(X, window_length: int | None = None, polyorder: int = 2, deriv: i
     ``lazy=True`` returns a ``PrepView``: nothing is computed here (SNV row
     statistics on first use), and ``utils.SIMCA`` fit / predict / transform,
     the CV engine and the engine entry points apply the transform in their
-    load paths, so the preprocessed matrix is never written to HBM."""
+    load paths, so the preprocessed matrix is never written to HBM.
+
+    ``lazy="write"`` returns a write-through ``PrepView``: the first Gram over
+    all its rows (a fit) forms X′ in its quantiser and writes it as a side
+    output, and every later consumer reads that X′ (the stencil runs once; X′
+    costs its memory, as the eager pass does)."""
     Xd = engine.as_device_f32(X)
     if isinstance(Xd, PrepView):
         Xd = Xd.materialize()
     m, p = Xd.shape
     if window_length is not None and int(window_length) > p:
         raise ValueError("If mode is 'interp', window_length must be less than or equal to the size of x.")
+    if lazy not in (False, True, "write"):
+        raise ValueError('snv_savgol: lazy must be False, True or "write"')
     if lazy:
         if out is not None:
-            raise ValueError("snv_savgol: `out` and lazy=True exclude each other")
+            raise ValueError("snv_savgol: `out` and a lazy view exclude each other")
         tp = savgol_taps(int(window_length), int(polyorder), int(deriv), float(delta)) if window_length else None
-        return PrepView(Xd, window_length, polyorder, deriv, delta, snv, tp)
+        return PrepView(Xd, window_length, polyorder, deriv, delta, snv, tp, through=(lazy == "write"))
     if out is None:
         out = torch.empty((m, p), dtype=torch.float32, device=Xd.device)
     w = 0

@@ -11,6 +11,15 @@ samples and the exact outlier fix-up.  The preprocessed matrix is never
 written to HBM on those paths.  ``materialize()`` writes it (the same float32
 values the fused kernels use).
 
+Write-through views (``through=True``, ``snv_savgol(..., lazy="write")``,
+round 5): the Gram of all the view's rows (a fit) runs the stencil in its
+quantiser as above and also writes X′ from there
+(``ocm_gram_f32_prep_write``); from then on the view IS that tensor to every
+consumer (the fit-set and predict scoring read it with the plain single-pass
+kernel).  The stencil runs once and the eager pass's separate read of X and
+the quantiser's read of X′ become one read: it costs X′'s memory, which the
+no-copy view does not.
+
 The view quacks like the (m, p) float32 device tensor it stands for where the
 engine looks (``shape``, ``dtype``, ``device``, ``ndim``, ``len``); anything
 else (slicing, arithmetic) is done on ``materialize()``.
@@ -44,7 +53,7 @@ class PrepView:
     evaluated lazily inside the kernels that consume it."""
 
     def __init__(self, X: torch.Tensor, window_length: int | None, polyorder: int, deriv: int, delta: float,
-                 snv: bool, taps64=None):
+                 snv: bool, taps64=None, through: bool = False):
         if not (isinstance(X, torch.Tensor) and X.is_cuda and X.dtype == torch.float32 and X.dim() == 2):
             raise TypeError("PrepView wraps a 2-D float32 CUDA tensor")
         if X.stride(1) != 1:
@@ -60,6 +69,15 @@ class PrepView:
         self._taps = (torch.from_numpy(taps64).to(torch.float32).to(X.device)
                       if self.window else None)
         self._rowstat = None
+        self.through = bool(through)
+        self._xp = None  # X′ once a write-through Gram has formed it
+
+    def written(self) -> torch.Tensor | None:
+        """X′ when a write-through Gram has written it (else None)."""
+        return self._xp
+
+    def _set_written(self, xp: torch.Tensor):
+        self._xp = xp
 
     # ---- tensor-like surface the engine reads ----
     @property
@@ -96,7 +114,8 @@ class PrepView:
 
     def __repr__(self):
         return (f"PrepView(shape={tuple(self.shape)}, snv={self.snv}, window={self.window or None}, "
-                f"polyorder={self.polyorder}, deriv={self.deriv})")
+                f"polyorder={self.polyorder}, deriv={self.deriv}, through={self.through}, "
+                f"written={self._xp is not None})")
 
     # ---- the transform ----
     def rowstat(self) -> torch.Tensor | None:
@@ -121,6 +140,8 @@ class PrepView:
 
     def materialize(self, rows: torch.Tensor | None = None) -> torch.Tensor:
         """The preprocessed rows (all, or X[rows]) as a float32 tensor."""
+        if self._xp is not None:
+            return self._xp if rows is None else self._xp.index_select(0, rows)
         m = self.X.shape[0] if rows is None else int(rows.numel())
         p = self.X.shape[1]
         out = torch.empty((m, p), dtype=torch.float32, device=self.X.device)
@@ -133,7 +154,10 @@ class PrepView:
     def __getitem__(self, idx):
         """Row selection (``X[rows]``, ``X[rows, :]``, as the CV refit loop
         does): a view of the selected raw rows (the reference's X[rows] is a
-        copy too); anything else indexes the materialised matrix."""
+        copy too); anything else indexes the materialised matrix.  A written
+        write-through view indexes X′."""
+        if self._xp is not None:
+            return self._xp[idx]
         if isinstance(idx, tuple):
             if len(idx) == 2 and isinstance(idx[1], slice) and idx[1] == slice(None):
                 idx = idx[0]
@@ -153,6 +177,7 @@ class PrepView:
             raise IndexError("PrepView: select rows (a 2-D view)")
         sub.X = sub.X.contiguous()
         sub._rowstat = self._rowstat[sel].contiguous() if self._rowstat is not None else None
+        sub._xp = None
         return sub
 
     def __array__(self, dtype=None, copy=None):

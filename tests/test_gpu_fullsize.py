@@ -215,19 +215,26 @@ def test_lazy_view_at_1m(snv, w, d):
     c0 = materialised_count(0)
     ests = []
     preds = []
-    for data in (v, None):
+    vw = preprocess.snv_savgol(X, w, 2, d, 1.0, snv=snv, lazy="write")  # write-through
+    for data in (v, vw, None):
         if data is None:
             data = v.materialize()
         est = SIMCA(n_components=K, model_class=0, type="alt", t2lim="Fdist", qlim="jm", verbose=False).fit(data, y)
         preds.append(est.predict(data).cpu().numpy())
         ests.append(est)
-        if len(ests) == 1:
+        if len(ests) <= 2:
             assert materialised_count(0) == c0
+        if len(ests) == 2:
+            assert vw.written() is not None
+            torch.testing.assert_close(vw.written(), v.materialize(), rtol=0, atol=0)
         del data
-    fa, fb = ests[0]._fits[0], ests[1]._fits[0]
-    assert torch.equal(fa.evals, fb.evals)
-    assert torch.equal(fa.T2, fb.T2) and torch.equal(fa.Q, fb.Q)
-    np.testing.assert_array_equal(preds[0], preds[1])
+    vw = None
+    fa = ests[0]._fits[0]
+    for e, pr in zip(ests[1:], preds[1:]):
+        fb = e._fits[0]
+        assert torch.equal(fa.evals, fb.evals)
+        assert torch.equal(fa.T2, fb.T2) and torch.equal(fa.Q, fb.Q)
+        np.testing.assert_array_equal(preds[0], pr)
     n = N
     np.testing.assert_allclose(float(fa.T2.double().sum()), K * (n - 1), rtol=1e-4)
     np.testing.assert_allclose(float(fa.Q.double().sum()), (n - 1) * fa.thetas[0], rtol=1e-4)

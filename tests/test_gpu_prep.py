@@ -129,6 +129,69 @@ def test_view_gram_outlier_rows_bit_identical():
     assert torch.equal(Ga, Gb) and torch.equal(ca, cb)
 
 
+@pytest.mark.parametrize("snv,w,po,d", DRIVERS + OTHERS)
+@pytest.mark.parametrize("n,p", [(20000, 2048), (5000, 300)])
+def test_write_through_gram_and_xprime_bit_identical(snv, w, po, d, n, p):
+    """Write-through views (lazy="write"): the quantiser
+    writes X′ as a side output of the pass that forms it.  X′ = the no-copy
+    view's materialised rows to the bit, the Gram and column sums = the
+    materialised Gram (segments too), the view then reads as X′ everywhere,
+    and nothing is materialised on the fused forms (the others run the eager
+    pass into X′ inside ocm_gram_f32_prep_write)."""
+    import torch
+
+    from ocm import engine, preprocess
+    from ocm.prepview import materialised_count
+
+    X = _spectra(n, p, seed=n + p)
+    Xd = torch.from_numpy(X).cuda()
+    Y = _view(Xd, snv, w, po, d).materialize()
+    for seg in ([0, n], [0, n // 3, n // 3, n]):
+        vw = preprocess.snv_savgol(Xd, w, po, d, 1.0, snv=snv, lazy="write")
+        sh = engine.cast_f32(engine.colmean(vw, None, 4096))
+        assert torch.equal(sh, engine.cast_f32(engine.colmean(Y, None, 4096)))
+        c0 = materialised_count(0)
+        Ga, ca = engine.gram(vw, None, seg, sh)
+        assert materialised_count(0) == c0
+        assert vw.written() is not None and torch.equal(vw.written(), Y)
+        Gb, cb = engine.gram(Y, None, seg, sh)
+        assert torch.equal(Ga, Gb) and torch.equal(ca, cb)
+        assert torch.equal(vw.materialize(), Y) and torch.equal(vw[5:9], Y[5:9])
+    # a gather list does not write: the view stays lazy
+    rows = torch.arange(0, n, 2, device="cuda")
+    vw = preprocess.snv_savgol(Xd, w, po, d, 1.0, snv=snv, lazy="write")
+    sh = engine.cast_f32(engine.colmean(Y, rows, min(4096, rows.numel())))
+    Ga, ca = engine.gram(vw, rows, [0, rows.numel()], sh)
+    Gb, cb = engine.gram(Y, rows, [0, rows.numel()], sh)
+    assert vw.written() is None and torch.equal(Ga, Gb) and torch.equal(ca, cb)
+
+
+@pytest.mark.parametrize("frac", [0.002, 0.2])
+def test_write_through_outlier_rows(frac):
+    """Screened rows on a write-through view: the exact fix-up (few rows) and
+    the bf16×3 recompute past n/8 marked rows (which runs on the X′ the
+    quantiser has written) = the materialised Gram."""
+    import torch
+
+    from ocm import engine, preprocess
+
+    n, p = 8000, 1024
+    X = _spectra(n, p, seed=77)
+    rng = np.random.default_rng(4)
+    bad = rng.choice(n, int(frac * n), replace=False)
+    X[bad] *= np.float32(400.0)
+    Xd = torch.from_numpy(X).cuda()
+    Y = _view(Xd, False, 5, 2, 1).materialize()
+    vw = preprocess.snv_savgol(Xd, 5, 2, 1, 1.0, snv=False, lazy="write")
+    sh = engine.cast_f32(engine.colmean(Y, None, 4096))
+    Ga, ca = engine.gram(vw, None, [0, n], sh)
+    ma = engine.last_gram_marks(0)
+    Gb, cb = engine.gram(Y, None, [0, n], sh)
+    assert ma == engine.last_gram_marks(0) and ma > 0
+    assert torch.equal(vw.written(), Y)
+    assert torch.equal(Ga, Gb) and torch.equal(ca, cb)
+
+
 def _score_pair(v, rows, m, k, seed=3):
     import torch
 
