@@ -476,6 +476,61 @@ __global__ __launch_bounds__(256) void k_gram_reduce(const float* __restrict__ p
   }
 }
 
+// Σ_ij O_ij G_ij straight from the chunk partials of one segment (the
+// eigensolver's θ3 term tr(O·O²), O symmetric, G = the Gram of rows of O):
+// the chunk sums as k_gram_reduce forms them, weighted by O and by the
+// tile's multiplicity (off-diagonal tiles and the strict upper triangle of
+// diagonal tiles stand for their mirror too); one partial per workgroup,
+// tile-major (fixed order).  Replaces the fp64 G, its reduce, the column sums
+// and a separate trace pass.
+template <int GT>
+__global__ __launch_bounds__(256) void k_gram_trace(const float* __restrict__ part, int nt, int ntiles, int p,
+                                                    int c0, int c1, const float* __restrict__ O,
+                                                    double* __restrict__ tr_part) {
+  const int tile = blockIdx.y;
+  const int e4 = blockIdx.x * blockDim.x + threadIdx.x;  // float4 index in tile
+  int ti, tj;
+  tile_coords(tile, nt, ti, tj);
+  double acc = 0.0;
+  if (e4 < GT * GT / 4) {
+    const size_t stride = (size_t)ntiles * (GT * GT) / 4;
+    const f32x4* src = reinterpret_cast<const f32x4*>(part) + (size_t)tile * (GT * GT) / 4 + e4;
+    double s[4][4] = {};
+    int c = c0;
+    for (; c + 4 <= c1; c += 4) {
+      f32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = src[(size_t)(c + u) * stride];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[u][q] += (double)v[u][q];
+    }
+    for (; c < c1; ++c) {
+      const f32x4 v = src[(size_t)c * stride];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s[0][q] += (double)v[q];
+    }
+    const int e = 4 * e4;
+    const int i = e / GT, j0 = e % GT;
+    const int gi = ti * GT + i;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = j0 + q, gj = tj * GT + j;
+      if (gi < p && gj < p && !(ti == tj && i > j)) {
+        const double v = (s[0][q] + s[1][q]) + (s[2][q] + s[3][q]);
+        const double w = (ti == tj && i == j) ? 1.0 : 2.0;
+        acc += w * v * (double)O[(size_t)gi * p + gj];
+      }
+    }
+  }
+  __shared__ double red[4];
+  acc = wave_sum_f64(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) tr_part[(size_t)tile * gridDim.x + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 // Column mean over n rows: per (column, row-split) f64 partial sums.
 __global__ void k_colsum_part(const float* __restrict__ X, int64_t ldx, const int64_t* __restrict__ rows, int64_t n,
                               int p, int64_t rows_per_split, double* __restrict__ part, PrepArgs pa = PrepArgs{}) {
@@ -916,9 +971,9 @@ __global__ __launch_bounds__(Q8QS * (QC / 4), 1) void k_q8_quant(const float* __
   const int cg0 = (int)(blockIdx.y * CG + blockIdx.x % CG) * QC;  // first column of the workgroup
   const int c0 = cg0 + 4 * cq;                                    // first of this thread's 4 columns
   const bool vec = (ldx % 4 == 0) && (c0 + 3 < p) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
-  f32x4 sh;
+  f32x4 sh;  // shift == nullptr: a zero shift (internal Grams)
 #pragma unroll
-  for (int e = 0; e < 4; ++e) sh[e] = c0 + e < p ? shift[c0 + e] : 0.f;
+  for (int e = 0; e < 4; ++e) sh[e] = (shift && c0 + e < p) ? shift[c0 + e] : 0.f;
   f32x4 v[16];
   const int64_t rblk = r0 + (int64_t)b * Q8BLK;  // first row of the block
   if (!GATHER && vec && (int64_t)Q8BLK * ldx * 4 < (1LL << 31)) {
@@ -957,7 +1012,9 @@ __global__ __launch_bounds__(Q8QS * (QC / 4), 1) void k_q8_quant(const float* __
     }
   }
   __shared__ Q8TailLdsT<QC> lds;
-  q8_tail<QC>(v, tid, cq, rs, cg0, c0, rb, q, chunk, b, st, colblk, lds, *reinterpret_cast<const f32x4*>(q.thr + c0));
+  const float inf = __builtin_inff();  // q.thr == nullptr: no screen (internal Grams)
+  q8_tail<QC>(v, tid, cq, rs, cg0, c0, rb, q, chunk, b, st, colblk, lds,
+              q.thr ? *reinterpret_cast<const f32x4*>(q.thr + c0) : f32x4{inf, inf, inf, inf});
 }
 
 // k_q8_quant with the preprocessing of a lazy view applied in the load path
@@ -2467,10 +2524,14 @@ int gram_impl(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, in
 int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t n, int32_t p,
                const float* shift, const int64_t* seg_offsets, int32_t nseg, double* G_out, double* colsum_out,
                hipStream_t st, int64_t chunk_rows, bool k32, const PrepArgs& pa = PrepArgs{},
-               bool unguarded = false, float* xout = nullptr, int64_t ldo = 0) {
+               bool unguarded = false, float* xout = nullptr, int64_t ldo = 0, const float* tr_O = nullptr,
+               double* tr_part = nullptr) {
   // unguarded: an internal Gram (the eigensolver's θ3 of the off-diagonal
-  // deflated covariance) — no outlier screen (thresholds +inf, nothing marked,
-  // no read-back), not timed, ctx->last_gram_marks left alone
+  // deflated covariance) — no outlier screen (no thresholds, nothing marked,
+  // no read-back, no guard buffers to initialise), shift may be nullptr (zero),
+  // not timed, ctx->last_gram_marks left alone.  tr_O (unguarded, one
+  // segment): no G at all — tr_part[ntiles · 16] = the partials of
+  // Σ_ij tr_O_ij G_ij (k_gram_trace)
   const bool prep = pa.w > 0 || pa.snv;
   const int P8 = (int)ocm::align_up((size_t)p, Q8T);
   const int nt = P8 / Q8T;
@@ -2521,13 +2582,11 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
   // the guard's buffers in one launch (three memsets cost ≈ 5 µs each plus
   // their gaps): row flags and counters zero, then the thresholds +inf
   // (unguarded) or the exponent histogram zero
-  {
-    const size_t nf = (size_t)n * fw, third = unguarded ? (size_t)P8 : (size_t)p * QX_BINS;
-    const uint32_t v3 = unguarded ? 0x7f800000u : 0u;  // +inf / 0
-    uint32_t* b3 = unguarded ? reinterpret_cast<uint32_t*>(thr) : xhist;
+  if (!unguarded) {
+    const size_t nf = (size_t)n * fw, third = (size_t)p * QX_BINS;
     const size_t tot = nf + 4 + third;
     hipLaunchKernelGGL(k_guard_init, dim3((unsigned)std::min<size_t>((tot + 255) / 256, 4096)), dim3(256), 0, st,
-                       flags, nf, counters, b3, third, v3);
+                       flags, nf, counters, xhist, third, 0u);
     OCM_CHECK_LAUNCH("k_guard_init");
   }
   if (!unguarded) {
@@ -2564,7 +2623,7 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     q.scale = scale + (size_t)cprefix[s0] * nblk * P8;
     q.P8 = P8;
     q.nblk = nblk;
-    q.thr = thr;
+    q.thr = unguarded ? nullptr : thr;
     q.flags = flags;
     q.fw = fw;
     q.nmark = counters;
@@ -2731,6 +2790,12 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
     OCM_CHECK_LAUNCH("k_gram8e");
     OCM_HIP(hipStreamWaitEvent(st, ev, 0));  // the read-back is done before the workspace is reused
   }
+  if (tr_O) {
+    hipLaunchKernelGGL(k_gram_trace<Q8T>, dim3(Q8T * Q8T / 4 / 256, ntiles), dim3(256), 0, st, part, nt, ntiles, p, 0,
+                       cprefix[1], tr_O, tr_part);
+    OCM_CHECK_LAUNCH("k_gram_trace");
+    return OCM_OK;
+  }
   for (int s = 0; s < nseg; ++s) {
     double* Gs = G_out + (size_t)s * p * p;
     double* cs = colsum_out + (size_t)s * p;
@@ -2832,11 +2897,14 @@ int gram_dispatch(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows
 }  // namespace
 
 namespace ocm {
-int gram_rows_i8(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t n, int p, const float* shift, double* G,
-                 double* colsum, hipStream_t st) {
+int trace_gram_rows_i8(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t n, int p, const float* O, double* tr_part,
+                       int* ntr, hipStream_t st) {
+  const int nt = (int)(ocm::align_up((size_t)p, Q8T) / Q8T);
+  *ntr = nt * (nt + 1) / 2 * (Q8T * Q8T / 4 / 256);
+  if (p <= SMALL_P) return OCM_ERR_ARG;  // the caller takes the G path
   const int64_t seg[2] = {0, n};
-  if (p <= SMALL_P) return gram_small(ctx, X, ldx, nullptr, p, shift, seg, 1, G, colsum, st);
-  return gram_impl8(ctx, X, ldx, nullptr, n, p, shift, seg, 1, G, colsum, st, 0, false, PrepArgs{}, true);
+  return gram_impl8(ctx, X, ldx, nullptr, n, p, nullptr, seg, 1, nullptr, nullptr, st, 0, false, PrepArgs{}, true,
+                    nullptr, 0, O, tr_part);
 }
 }  // namespace ocm
 

@@ -51,21 +51,29 @@ inline void host_chol_inv_t(const double* S, int b, double* M) {
 // eigenvector j.
 // Returns false if some eigenvalue did not converge within QL_MAX_ITER implicit
 // QL sweeps (its value and vectors are then unreliable).
+// √(a² + b²) without std::hypot's cost (its overflow care is needed only far
+// from the magnitudes of a covariance's projections; those take the slow path)
+inline double fast_hypot(double a, double b) {
+  const double m = std::fmax(std::fabs(a), std::fabs(b));
+  if (m > 1e150 || (m < 1e-150 && m > 0.0)) return std::hypot(a, b);
+  return std::sqrt(a * a + b * b);
+}
+
 inline bool host_sym_eig(const double* A, int n, double* ev, double* Z) {
-  std::vector<double> a((size_t)n * n), d(n), e(n, 0.0), v(n), pv(n), z((size_t)n * n, 0.0);
+  // flat work arrays; zt[j·n + i] = component i of (eventually) eigenvector j,
+  // so reflectors and QL rotations update contiguous rows
+  std::vector<double> a((size_t)n * n), d(n), e(n, 0.0), v(n), pv(n), zt((size_t)n * n, 0.0), hw((size_t)n * n, 0.0);
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) a[(size_t)i * n + j] = 0.5 * (A[(size_t)i * n + j] + A[(size_t)j * n + i]);
-  std::vector<std::vector<double>> hv;  // Householder vectors (index k: entries k+1..n-1)
-  // A ← H A H, H = I − 2 w wᵀ, zeroing column k below the subdiagonal
-  for (int k = 0; k + 2 < n; ++k) {
+  // A ← H A H, H = I − 2 w wᵀ, zeroing column k below the subdiagonal;
+  // w_k (entries k+1..n-1) kept in row k of hw (zero row: no reflection)
+  const int nref = std::max(0, n - 2);
+  for (int k = 0; k < nref; ++k) {
+    double* w = &hw[(size_t)k * n];
     double nrm = 0.0;
     for (int i = k + 1; i < n; ++i) nrm += a[(size_t)i * n + k] * a[(size_t)i * n + k];
     nrm = std::sqrt(nrm);
-    std::vector<double> w(n, 0.0);
-    if (nrm == 0.0) {
-      hv.push_back(w);
-      continue;
-    }
+    if (nrm == 0.0) continue;
     const double x0 = a[(size_t)(k + 1) * n + k];
     const double alpha = x0 > 0 ? -nrm : nrm;
     for (int i = k + 1; i < n; ++i) w[i] = a[(size_t)i * n + k];
@@ -74,7 +82,7 @@ inline bool host_sym_eig(const double* A, int n, double* ev, double* Z) {
     for (int i = k + 1; i < n; ++i) wn += w[i] * w[i];
     wn = std::sqrt(wn);
     if (wn == 0.0) {
-      hv.push_back(std::vector<double>(n, 0.0));
+      for (int i = k + 1; i < n; ++i) w[i] = 0.0;
       continue;
     }
     for (int i = k + 1; i < n; ++i) w[i] /= wn;
@@ -82,31 +90,35 @@ inline bool host_sym_eig(const double* A, int n, double* ev, double* Z) {
     double K = 0.0;
     for (int i = k + 1; i < n; ++i) {
       double s = 0.0;
-      for (int j = k + 1; j < n; ++j) s += a[(size_t)i * n + j] * w[j];
+      const double* ar = &a[(size_t)i * n];
+      for (int j = k + 1; j < n; ++j) s += ar[j] * w[j];
       pv[i] = s;
       K += w[i] * s;
     }
     for (int i = k + 1; i < n; ++i) v[i] = pv[i] - K * w[i];
-    for (int i = k + 1; i < n; ++i)
-      for (int j = k + 1; j < n; ++j) a[(size_t)i * n + j] -= 2.0 * (w[i] * v[j] + v[i] * w[j]);
+    for (int i = k + 1; i < n; ++i) {
+      double* ar = &a[(size_t)i * n];
+      const double wi = w[i], vi = v[i];
+      for (int j = k + 1; j < n; ++j) ar[j] -= 2.0 * (wi * v[j] + vi * w[j]);
+    }
     a[(size_t)(k + 1) * n + k] = a[(size_t)k * n + k + 1] = alpha;
     for (int i = k + 2; i < n; ++i) a[(size_t)i * n + k] = a[(size_t)k * n + i] = 0.0;
-    hv.push_back(w);
   }
   for (int i = 0; i < n; ++i) d[i] = a[(size_t)i * n + i];
   for (int i = 0; i + 1 < n; ++i) e[i] = a[(size_t)(i + 1) * n + i];
-  // Q = H_0 H_1 … H_{n-3}: apply to the identity from the last reflector back
-  for (int i = 0; i < n; ++i) z[(size_t)i * n + i] = 1.0;
-  for (int k = (int)hv.size() - 1; k >= 0; --k) {
-    const std::vector<double>& w = hv[k];
-    for (int j = 0; j < n; ++j) {  // column j: z_j −= 2 w (wᵀ z_j)
+  // Q = H_0 H_1 … H_{n-3}: applied to the identity from the last reflector back
+  for (int i = 0; i < n; ++i) zt[(size_t)i * n + i] = 1.0;
+  for (int k = nref - 1; k >= 0; --k) {
+    const double* w = &hw[(size_t)k * n];
+    for (int j = 0; j < n; ++j) {  // column j of Q (row j of zt): z_j −= 2 w (wᵀ z_j)
+      double* zr = &zt[(size_t)j * n];
       double s = 0.0;
-      for (int i = k + 1; i < n; ++i) s += w[i] * z[(size_t)i * n + j];
+      for (int i = k + 1; i < n; ++i) s += w[i] * zr[i];
       if (s == 0.0) continue;
-      for (int i = k + 1; i < n; ++i) z[(size_t)i * n + j] -= 2.0 * s * w[i];
+      for (int i = k + 1; i < n; ++i) zr[i] -= 2.0 * s * w[i];
     }
   }
-  // implicit QL on (d, e), rotations accumulated into the columns of z
+  // implicit QL on (d, e), rotations accumulated into the rows of zt
   const double eps = std::numeric_limits<double>::epsilon();
   bool converged = true;
   for (int l = 0; l < n; ++l) {
@@ -122,14 +134,14 @@ inline bool host_sym_eig(const double* A, int n, double* ev, double* Z) {
       }
       if (m == l) break;
       double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
-      double r = std::hypot(g, 1.0);
+      double r = fast_hypot(g, 1.0);
       g = d[m] - d[l] + e[l] / (g + (g >= 0 ? r : -r));
       double s = 1.0, c = 1.0, p = 0.0;
       int i = m - 1;
       bool underflow = false;
       for (; i >= l; --i) {
         double f = s * e[i], bb = c * e[i];
-        r = std::hypot(f, g);
+        r = fast_hypot(f, g);
         e[i + 1] = r;
         if (r == 0.0) {
           d[i + 1] -= p;
@@ -144,10 +156,12 @@ inline bool host_sym_eig(const double* A, int n, double* ev, double* Z) {
         p = s * r;
         d[i + 1] = g + p;
         g = c * r - bb;
+        double* z0 = &zt[(size_t)i * n];
+        double* z1 = &zt[(size_t)(i + 1) * n];
         for (int q = 0; q < n; ++q) {
-          const double zf = z[(size_t)q * n + i + 1];
-          z[(size_t)q * n + i + 1] = s * z[(size_t)q * n + i] + c * zf;
-          z[(size_t)q * n + i] = c * z[(size_t)q * n + i] - s * zf;
+          const double zf = z1[q];
+          z1[q] = s * z0[q] + c * zf;
+          z0[q] = c * z0[q] - s * zf;
         }
       }
       if (underflow) continue;
@@ -161,7 +175,8 @@ inline bool host_sym_eig(const double* A, int n, double* ev, double* Z) {
   std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return d[x] > d[y]; });
   for (int j = 0; j < n; ++j) {
     ev[j] = d[ord[j]];
-    for (int i = 0; i < n; ++i) Z[(size_t)i * n + j] = z[(size_t)i * n + ord[j]];
+    const double* zr = &zt[(size_t)ord[j] * n];
+    for (int i = 0; i < n; ++i) Z[(size_t)i * n + j] = zr[i];
   }
   return converged;
 }

@@ -33,7 +33,7 @@ struct ocm_ctx {
   // stream, fork / join events, and a sub-context whose workspaces the θ3
   // Gram takes (the main workspace holds the eigensolver's live buffers)
   hipStream_t eig_side[2] = {nullptr, nullptr};
-  hipEvent_t eig_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t eig_ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   ocm_ctx* eig_sub = nullptr;
 };
 
@@ -254,11 +254,12 @@ inline PrepArgs prep_args(const ocm_prep* p) {
 }
 
 int check_prep(const ocm_prep* prep, int p, const char* who);
-// G = Σ_rows (x − shift)(x − shift)ᵀ of n float32 rows on the default i8×3 path
-// (ocm_gram.hip); uses the context workspace from offset 0 (callers must not
-// hold workspace carve-outs across it).
-int gram_rows_i8(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t n, int p, const float* shift, double* G,
-                 double* colsum, hipStream_t st);
+// Σ_ij O_ij (XᵀX)_ij for the rows X of a symmetric p×p float32 O (p > 64): the
+// i8×3 Gram without G, as ntr fp64 partials in tr_part (ntr ≤ 16·(p/128+1)²/2;
+// sum them in order); zero shift, no outlier screen.  Uses the context
+// workspace from offset 0 (callers must not hold workspace carve-outs across it).
+int trace_gram_rows_i8(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t n, int p, const float* O, double* tr_part,
+                       int* ntr, hipStream_t st);
 int prep_apply(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int p, const PrepArgs& pa,
                float* out, int64_t ldo, hipStream_t st);
 

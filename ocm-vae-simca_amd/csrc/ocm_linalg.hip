@@ -39,6 +39,9 @@ namespace {
 // the trace GEMM when the θ3 work is split over GPUs).
 // ---------------------------------------------------------------------------
 constexpr int DT = 64, DBK = 16, DPAD = 16;
+#ifndef OCM_JACOBI_TOL2
+#define OCM_JACOBI_TOL2 1e-26  // Jacobi stop: off-diagonal ‖·‖² ≤ this × diagonal ‖·‖²
+#endif
 
 // MODE 3: as MODE 2 without storing D in fp64: the off-diagonal part goes to
 //         O32 (float32, zero diagonal, row-major p×p), the diagonal to D[row],
@@ -198,6 +201,129 @@ __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int
   }
 }
 
+// k_dgemm<3> for K ≤ 64 (the fused path's rank-2b deflation, b = 32): every
+// global load is issued up front — the four K-steps' A / B pieces and this
+// thread's 16 elements of E (C) for the epilogue — so one memory latency
+// covers the workgroup instead of one per K-step plus one for E; the K-steps
+// then run from registers through LDS.  Same outputs as k_dgemm<3>.
+__global__ __launch_bounds__(256) void k_deflate64(const double* __restrict__ A, int64_t lda,
+                                                   const double* __restrict__ B, int64_t ldb,
+                                                   double* __restrict__ D, int M, int N, int K,
+                                                   const double* __restrict__ E, int64_t lde,
+                                                   double* __restrict__ part, float* __restrict__ O32,
+                                                   double* __restrict__ rowpart) {
+  constexpr int NS = 64 / DBK;  // K-steps
+  __shared__ double As[DBK][DT + DPAD];
+  __shared__ double Bs[DBK][DT + DPAD];
+  __shared__ double red[8];
+  __shared__ double rsum[2][2][32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * DT, n0 = blockIdx.y * DT;
+  const int arow = tid >> 2, akc = (tid & 3) * 4;
+  const int bk = tid >> 4, bcol = (tid & 15) * 4;
+  double ev[2][2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + a * 16 + (lane >> 4) + 4 * r;
+        const int col = n0 + wn * 32 + b * 16 + (lane & 15);
+        ev[a][b][r] = (row < M && col < N) ? E[(int64_t)row * lde + col] : 0.0;
+      }
+  double ra[NS][4], rb[NS][4];
+#pragma unroll
+  for (int st = 0; st < NS; ++st)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = m0 + arow, kk = st * DBK + akc + e;
+      ra[st][e] = (r < M && kk < K) ? A[(int64_t)r * lda + kk] : 0.0;
+      const int kr = st * DBK + bk, c = n0 + bcol + e;
+      rb[st][e] = (kr < K && c < N) ? B[(int64_t)kr * ldb + c] : 0.0;
+    }
+  f64x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (f64x4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    if (st * DBK >= K) break;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      As[akc + e][arow] = ra[st][e];
+      Bs[bk][bcol + e] = rb[st][e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kq = 0; kq < DBK / 4; ++kq) {
+      const int kr = kq * 4 + (lane >> 4);
+      const double a0 = As[kr][wm * 32 + (lane & 15)];
+      const double a1 = As[kr][wm * 32 + 16 + (lane & 15)];
+      const double b0 = Bs[kr][wn * 32 + (lane & 15)];
+      const double b1 = Bs[kr][wn * 32 + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  double tr = 0.0, fro = 0.0;
+  double rs[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + a * 16 + (lane >> 4) + 4 * r;
+        const int col = n0 + wn * 32 + b * 16 + (lane & 15);
+        if (row < M && col < N) {
+          const double v = ev[a][b][r] - acc[a][b][r];
+          fro += v * v;
+          if (row == col) {
+            tr += v;
+            D[row] = v;
+            O32[(int64_t)row * N + col] = 0.f;
+          } else {
+            O32[(int64_t)row * N + col] = (float)v;
+            rs[a][r] += v * v;
+          }
+        }
+      }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double v = rs[a][r];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      if ((lane & 15) == 0) rsum[wm][wn][a * 16 + (lane >> 4) + 4 * r] = v;
+    }
+  __syncthreads();
+  if (tid < 64) {
+    const int row = m0 + tid;
+    if (row < M) rowpart[(int64_t)blockIdx.y * M + row] = rsum[tid >> 5][0][tid & 31] + rsum[tid >> 5][1][tid & 31];
+  }
+  tr = wave_sum_f64(tr);
+  fro = wave_sum_f64(fro);
+  if (lane == 0) {
+    red[wave] = tr;
+    red[4 + wave] = fro;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int wg = blockIdx.y * gridDim.x + blockIdx.x;
+    part[2 * wg] = (red[0] + red[1]) + (red[2] + red[3]);
+    part[2 * wg + 1] = (red[4] + red[5]) + (red[6] + red[7]);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // W = C·V for a 32-column block (the subspace iteration's product, b = 32):
 // two workgroups of eight waves per 16 rows of C, each a half of K, each wave
@@ -295,17 +421,6 @@ __global__ void k_sum_planes(const double* __restrict__ P, int nz, int64_t plane
   D[i] = v;
 }
 
-// ordered sum of n partials into out[0] (single wave, deterministic)
-__global__ __launch_bounds__(256) void k_sum_partials(const double* __restrict__ part, int n, double* __restrict__ out) {
-  __shared__ double red[4];
-  double v = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) v += part[i];
-  v = wave_sum_f64(v);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) *out = (red[0] + red[1]) + (red[2] + red[3]);
-}
-
 // partial  S = Aᵀ B  for tall row-major A, B (p×b, ld = b): block = 64 rows
 __global__ __launch_bounds__(256) void k_atb_part(const double* __restrict__ A, const double* __restrict__ B, int p,
                                                   int b, double* __restrict__ part) {
@@ -381,7 +496,7 @@ __global__ __launch_bounds__(NT) void k_jacobi(const double* __restrict__ Ain, i
         d += wsum[NW + w];
       }
       // off-diagonal norm ≤ 1e-13 of the diagonal's: eigenvalue error ~ off²/gap
-      done = (o <= 1e-26 * d) || (o == 0.0);
+      done = (o <= OCM_JACOBI_TOL2 * d) || (o == 0.0);
     }
     __syncthreads();
     if (done) break;
@@ -507,7 +622,7 @@ __global__ __launch_bounds__(256) void k_jacobi_blk(const double* __restrict__ A
       const double o = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
       const double d = (wsum[4] + wsum[5]) + (wsum[6] + wsum[7]);
       // off-diagonal norm ≤ 1e-13 of the diagonal's: eigenvalue error ~ off²/gap
-      done = (o <= 1e-26 * d) || (o == 0.0);
+      done = (o <= OCM_JACOBI_TOL2 * d) || (o == 0.0);
     }
     __syncthreads();
     if (done) break;
@@ -1201,7 +1316,7 @@ __global__ __launch_bounds__(256) void k_colnormalize(double* __restrict__ W, in
 //                  no rotated block is formed for the convergence test;
 //   k_theta_combine θ1..θ3 of the deflated matrix (I − P_k)C(I − P_k) from the
 //                  b-block deflation Ct_b = (I − P_b)C(I − P_b) (traces,
-//                  computed beside the Jacobi on a side stream) plus the
+//                  computed beside the Jacobi on side streams) plus the
 //                  Ritz block's exact corrections, block form with
 //                  E = (P_b − P_k)C(I − P_b):
 //                    θ1 = Σ_t θ_i + tr Ct_b
@@ -1457,39 +1572,57 @@ __global__ __launch_bounds__(256) void k_extract_signfix(const double* __restric
 
 // Operands of the deflation update C⊥ = C − U·Wt (one fp64-MFMA GEMM):
 //   C⊥ = C − V_k M_kᵀ − M_k V_kᵀ + N_k V_kᵀ = C − [V_k | M_k − N_k]·[M_k | V_k]ᵀ
-// with V the Ritz basis, M = C V, N = V_k H_k (first k columns of p×b blocks).
-// U p×2k row-major, Wt 2k×p row-major.
-__global__ __launch_bounds__(256) void k_deflate_operands(const double* __restrict__ V, const double* __restrict__ M,
-                                                          const double* __restrict__ Nm, int p, int b, int k,
-                                                          double* __restrict__ U, double* __restrict__ Wt) {
+// with V the Ritz basis, M = C V, N = V_k H_k (H = VᵀM; first k columns of p×b
+// blocks).  U p×2k row-major, Wt 2k×p row-major.  Thread (i, l) forms its N
+// entry itself (H_k in LDS for k ≤ 64): one launch, no separate GEMM for N.
+__global__ __launch_bounds__(256) void k_deflate_operands_h(const double* __restrict__ V, const double* __restrict__ M,
+                                                            const double* __restrict__ H, int p, int b, int k,
+                                                            double* __restrict__ U, double* __restrict__ Wt) {
+  __shared__ double Hs[64 * 64];
+  const bool lds = k <= 64;
+  if (lds)
+    for (int e = threadIdx.x; e < k * k; e += 256) Hs[e] = H[(e / k) * b + e % k];
+  __syncthreads();
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= (int64_t)p * k) return;
   const int i = (int)(e / k), l = (int)(e % k);
-  const double v = V[(int64_t)i * b + l], m = M[(int64_t)i * b + l], nn = Nm[(int64_t)i * b + l];
+  const double* vr = V + (int64_t)i * b;
+  double nn = 0.0;
+  for (int t = 0; t < k; ++t) nn = fma(vr[t], lds ? Hs[t * k + l] : H[(int64_t)t * b + l], nn);
+  const double v = vr[l], m = M[(int64_t)i * b + l];
   U[(int64_t)i * 2 * k + l] = v;
   U[(int64_t)i * 2 * k + k + l] = m - nn;
   Wt[(int64_t)l * p + i] = m;
   Wt[(int64_t)(k + l) * p + i] = v;
 }
 
-__global__ __launch_bounds__(256) void k_sum_pairs(const double* __restrict__ part, int n, double* __restrict__ out2) {
-  __shared__ double red[8];
-  double a = 0.0, b = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) {
-    a += part[2 * i];
-    b += part[2 * i + 1];
+// θ's sums in one launch (fixed order): out3[0..1] = the deflation GEMM's
+// {tr, ‖·‖²} tile pairs (which & 1), out3[2] = Σ of the Δ-term partials + Σ
+// of the trace partials (which & 2; either count may be 0)
+__global__ __launch_bounds__(256) void k_theta_final(const double* __restrict__ pairs, int npairs,
+                                                     const double* __restrict__ d3, int nd3,
+                                                     const double* __restrict__ tr, int ntr,
+                                                     double* __restrict__ out3, int which) {
+  __shared__ double red[3][4];
+  double a = 0.0, b = 0.0, c = 0.0, t = 0.0;
+  for (int i = threadIdx.x; i < npairs; i += 256) {
+    a += pairs[2 * i];
+    b += pairs[2 * i + 1];
   }
+  for (int i = threadIdx.x; i < nd3; i += 256) c += d3[i];
+  for (int i = threadIdx.x; i < ntr; i += 256) t += tr[i];
+  c += t;
   a = wave_sum_f64(a);
   b = wave_sum_f64(b);
+  c = wave_sum_f64(c);
   if ((threadIdx.x & 63) == 0) {
-    red[threadIdx.x >> 6] = a;
-    red[4 + (threadIdx.x >> 6)] = b;
+    red[0][threadIdx.x >> 6] = a;
+    red[1][threadIdx.x >> 6] = b;
+    red[2][threadIdx.x >> 6] = c;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    out2[0] = (red[0] + red[1]) + (red[2] + red[3]);
-    out2[1] = (red[4] + red[5]) + (red[6] + red[7]);
-  }
+  if (threadIdx.x < 3 && (which & (threadIdx.x < 2 ? 1 : 2)))
+    out3[threadIdx.x] = (red[threadIdx.x][0] + red[threadIdx.x][1]) + (red[threadIdx.x][2] + red[threadIdx.x][3]);
 }
 
 // p ≤ 64 path: evecs (k×p) from Z (p×p columns), θ from the tail eigenvalues
@@ -1567,6 +1700,18 @@ int dgemm(const double* A, int64_t lda, const double* B, int64_t ldb, double* D,
 
 int jacobi(const double* A, int n, int max_sweeps, double* ev, double* Z, hipStream_t st) {
   // n = 32: the block kernel (0.95 ms per fit against 1.19 with the one-wave k_jacobi<32, 64>, r03z)
+#ifdef OCM_JACOBI_SWEEPS  // make exp diagnostic: print the sweep count of each 32×32 solve
+  if (n == 32) {
+    static int* dsw = nullptr;
+    if (!dsw) (void)hipMalloc(reinterpret_cast<void**>(&dsw), sizeof(int));
+    hipLaunchKernelGGL(k_jacobi_blk<32>, dim3(1), dim3(256), 0, st, A, max_sweeps, ev, Z, dsw);
+    int hsw = -1;
+    (void)hipMemcpyAsync(&hsw, dsw, sizeof(int), hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    fprintf(stderr, "jacobi32 sweeps %d\n", hsw);
+    return OCM_OK;
+  }
+#endif
   if (n == 32)
     hipLaunchKernelGGL(k_jacobi_blk<32>, dim3(1), dim3(256), 0, st, A, max_sweeps, ev, Z, nullptr);
   else if (n == 48)
@@ -1659,23 +1804,6 @@ __global__ __launch_bounds__(256) void k_theta3_rows(const double* __restrict__ 
   if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-// partial Σ_ij O_ij G_ij, one row per workgroup (rows in order: deterministic)
-__global__ __launch_bounds__(256) void k_trace_og(const float* __restrict__ O32, const double* __restrict__ G, int p,
-                                                   double* __restrict__ part) {
-  __shared__ double red[4];
-  const int64_t base = (int64_t)blockIdx.x * p;
-  double s = 0.0;
-  for (int j = threadIdx.x; j < p; j += 256) s += (double)O32[base + j] * G[base + j];
-  s = wave_sum_f64(s);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
-}
-
-__global__ void k_add3(const double* __restrict__ a, const double* __restrict__ b, double* __restrict__ out) {
-  if (threadIdx.x == 0) *out = *a + *b;
-}
-
 // 1/λ with np.linalg.pinv's cutoff (|λ| ≤ rcond·max|λ| → 0); one workgroup,
 // every thread reads all k values (k is the component count: ≤ p, small)
 __global__ __launch_bounds__(256) void k_inv_evals(const double* __restrict__ ev, int k, double rcond,
@@ -1742,7 +1870,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   const int nblk = (p + 63) / 64;
   const size_t def_blocks = (size_t)((p + DT - 1) / DT) * ((p + DT - 1) / DT);  // deflate GEMM tiles
   const size_t plane_cap = std::max((size_t)ksplit * pb, wide ? 16 * bb : 0);
-  size_t need = (6 * pb + 6 * bb + plane_cap + (wide ? 0 : (size_t)nblk * bb) + 4 * b + 64) * sizeof(double);
+  size_t need = (5 * pb + 6 * bb + plane_cap + (wide ? 0 : (size_t)nblk * bb) + 4 * b + 64) * sizeof(double);
   need += ((size_t)CQ_G * 1024 + 2048 + 64) * sizeof(double) + 3 * 256;  // CholQR / k_atb32 partials, M1/M2, ticket
   const int cv_rb = (p + 15) / 16;  // k_cv32 row blocks
   need += ((size_t)cv_rb * 2 * 512) * sizeof(double) + (size_t)cv_rb * sizeof(unsigned) + 2 * 256;
@@ -1760,7 +1888,6 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   double* W = cv.take<double>(pb);
   double* T1 = cv.take<double>(pb);
   double* T2 = cv.take<double>(pb);
-  double* Nm = cv.take<double>(pb);
   double* H = cv.take<double>(bb);
   double* Z = cv.take<double>(bb);
   double* S = cv.take<double>(bb);
@@ -1884,58 +2011,68 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   // GEMM with its trace and Frobenius epilogue → out3[0..1], and this slice's
   // θ3 rows → out3[2], all on stream s; the θ3 Gram runs on gctx's workspaces.
   auto theta_into = [&](const double* Vb, const double* Wb_, const double* Hb, int kd, hipStream_t s,
-                        ocm_ctx* gctx, double* out3) -> int {
-    // N = Vb[:, :kd] · Hb[:kd, :]
-    int rc2 = dgemm(Vb, b, Hb, b, Nm, b, p, b, kd, 1, nullptr, s);
-    if (rc2) return rc2;
-    hipLaunchKernelGGL(k_deflate_operands, dim3((unsigned)(((size_t)p * kd + 255) / 256)), dim3(256), 0, s, Vb, Wb_,
-                       Nm, p, b, kd, Ud, Wd);
-    OCM_CHECK_LAUNCH("k_deflate_operands");
+                        hipStream_t s2, ocm_ctx* gctx, double* out3) -> int {
+    // s2 (≠ s: the fused path's second side stream) takes the Δ terms beside
+    // the θ3 Gram; eig_ev[4] / [5] order them
+    hipLaunchKernelGGL(k_deflate_operands_h, dim3((unsigned)(((size_t)p * kd + 255) / 256)), dim3(256), 0, s, Vb,
+                       Wb_, Hb, p, b, kd, Ud, Wd);
+    OCM_CHECK_LAUNCH("k_deflate_operands_h");
     // the deflated matrix D = C − U·Wdᵀ is never stored in fp64: k_dgemm<3>
     // writes its off-diagonal part O (float32, the θ3 Gram's input), its
-    // diagonal Δ, per-tile row sums of O² and the {tr D, ‖D‖²} partials.  O,
-    // its Gram and the partials live in gctx's second arena (the Gram takes
-    // gctx's workspace).
+    // diagonal Δ, per-tile row sums of O² and the {tr D, ‖D‖²} partials.  O
+    // and the partials live in gctx's second arena (the Gram takes gctx's
+    // workspace).
     const size_t pp = (size_t)p * p;
     const int ntc = (p + DT - 1) / DT;
+    const int ntq = (p + 127) / 128;
+    const int ntr_cap = ntq * (ntq + 1) / 2 * 16;  // k_gram_trace partials
     const size_t o32_bytes = (pp * sizeof(float) + 255) / 256 * 256;
     char* aux = static_cast<char*>(ocm::workspace_aux(
-        gctx, o32_bytes + (pp + 4 * (size_t)p + (size_t)ntc * p + 64) * sizeof(double), s));
+        gctx, o32_bytes + (2 * (size_t)p + (size_t)ntc * p + ntr_cap + 64) * sizeof(double), s));
     if (!aux) return OCM_ERR_NOMEM;
     float* O32 = reinterpret_cast<float*>(aux);
-    double* Gp = reinterpret_cast<double*>(aux + o32_bytes);
-    double* csum = Gp + pp;
-    double* diag = csum + p;
-    double* opart = diag + p;  // p row partials of the O·O² term (then the zero shift)
-    double* rowpart = opart + p;
+    double* diag = reinterpret_cast<double*>(aux + o32_bytes);
+    double* rowpart = diag + p;
     double* dpart3 = rowpart + (size_t)ntc * p;  // ≤ p/256 + 1 workgroup partials
-    double* t3 = dpart3 + p;
+    double* trpart = dpart3 + p;
     const dim3 gd(ntc, ntc, 1);
-    hipLaunchKernelGGL(k_dgemm<3>, gd, dim3(256), 0, s, Ud, (int64_t)(2 * kd), Wd, (int64_t)p, diag, (int64_t)p, p,
-                       p, 2 * kd, 2 * kd, C, (int64_t)p, dpart, 0, O32, rowpart);
+    if (2 * kd <= 64)
+      hipLaunchKernelGGL(k_deflate64, gd, dim3(256), 0, s, Ud, (int64_t)(2 * kd), Wd, (int64_t)p, diag, p, p, 2 * kd, C,
+                         (int64_t)p, dpart, O32, rowpart);
+    else
+      hipLaunchKernelGGL(k_dgemm<3>, gd, dim3(256), 0, s, Ud, (int64_t)(2 * kd), Wd, (int64_t)p, diag, (int64_t)p, p,
+                         p, 2 * kd, 2 * kd, C, (int64_t)p, dpart, 0, O32, rowpart);
     OCM_CHECK_LAUNCH("k_dgemm deflate");
-    hipLaunchKernelGGL(k_sum_pairs, dim3(1), dim3(256), 0, s, dpart, (int)(gd.x * gd.y), out3);  // tr, ‖·‖²
-    OCM_CHECK_LAUNCH("k_sum_pairs");
+    // the tile pairs sit in this context's workspace, which the θ3 Gram takes
+    // over when gctx is this context (the unfused path): sum them first there
+    const bool own_ws = gctx == ctx;
+    if (own_ws) {
+      hipLaunchKernelGGL(k_theta_final, dim3(1), dim3(256), 0, s, dpart, (int)(gd.x * gd.y), nullptr, 0, nullptr, 0,
+                         out3, 1);
+      OCM_CHECK_LAUNCH("k_theta_final pairs");
+    }
     // θ3 = Σ Δ³ + 3 Σ Δ_i Σ_j O_ij² + Σ O∘(O²): this slice's rows of the Δ
-    // terms, then the i8×3 Gram of its rows of O against all of O
+    // terms (on s2), and the i8×3 Gram of its rows of O paired with all of O
+    // in the Gram's epilogue (k_gram_trace, on s)
     const int r0 = (int)((int64_t)p * slice / nslices), r1 = (int)((int64_t)p * (slice + 1) / nslices);
+    int nb3 = 0, ntr = 0;
     if (theta_mode >= 2 && r1 > r0) {
       const int nr = r1 - r0;
-      const int nb3 = (nr + 255) / 256;
-      hipLaunchKernelGGL(k_theta3_rows, dim3(nb3), dim3(256), 0, s, diag, rowpart, ntc, p, r0, r1, dpart3);
-      hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, s, dpart3, nb3, t3);
+      nb3 = (nr + 255) / 256;
+      if (s2 != s) {
+        OCM_HIP(hipEventRecord(ctx->eig_ev[4], s));
+        OCM_HIP(hipStreamWaitEvent(s2, ctx->eig_ev[4], 0));
+      }
+      hipLaunchKernelGGL(k_theta3_rows, dim3(nb3), dim3(256), 0, s2, diag, rowpart, ntc, p, r0, r1, dpart3);
       OCM_CHECK_LAUNCH("k_theta3_rows");
-      float* zshift = reinterpret_cast<float*>(opart);
-      OCM_HIP(hipMemsetAsync(zshift, 0, (size_t)p * sizeof(float), s));
-      rc2 = ocm::gram_rows_i8(gctx, O32 + (size_t)r0 * p, p, nr, p, zshift, Gp, csum, s);
+      if (s2 != s) OCM_HIP(hipEventRecord(ctx->eig_ev[5], s2));
+      int rc2 = ocm::trace_gram_rows_i8(gctx, O32 + (size_t)r0 * p, p, nr, p, O32, trpart, &ntr, s);
       if (rc2) return rc2;
-      hipLaunchKernelGGL(k_trace_og, dim3(p), dim3(256), 0, s, O32, Gp, p, opart);
-      hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(256), 0, s, opart, p, t3 + 1);
-      hipLaunchKernelGGL(k_add3, dim3(1), dim3(64), 0, s, t3, t3 + 1, out3 + 2);
-      OCM_CHECK_LAUNCH("k_trace_og");
-    } else {
-      OCM_HIP(hipMemsetAsync(out3 + 2, 0, sizeof(double), s));
+      if (s2 != s) OCM_HIP(hipStreamWaitEvent(s, ctx->eig_ev[5], 0));
     }
+    hipLaunchKernelGGL(k_theta_final, dim3(1), dim3(256), 0, s, dpart, own_ws ? 0 : (int)(gd.x * gd.y), dpart3, nb3,
+                       trpart, ntr, out3, own_ws ? 2 : 3);
+    OCM_CHECK_LAUNCH("k_theta_final");
     return OCM_OK;
   };
 
@@ -1973,6 +2110,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   }
   double prev_rmax = 0.0;
   bool converged = false;
+  bool extracted = false;  // the fused path writes evals / evecs itself
   // fused chain state (b = 32): the current unnormalised block Wc and its
   // CholQR factor Mc (nullptr: Wc is the start block, used as it is)
   double* Wc = V;
@@ -2019,24 +2157,24 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
       // Rayleigh–Ritz on the unrotated block: H = VᵀW, the projection
       // residual R = W − V·H and S = RᵀR, Jacobi on H; the test reads
       // ‖R z_i‖ (k_rr_test32).  With θ wanted, R/S, C·R, G2 = Rᵀ(C·R) and the
-      // deflation of the whole block run on a side stream beside the Jacobi
+      // deflation of the whole block run on side streams beside the Jacobi
       // (they need no Ritz rotation: k_theta_combine adds its terms later).
+      // (The eigenproblem of H on the host — implicit QL, ocm_hostla.h —
+      // measured slower: ≈ 50–90 µs of QL plus two round trips against the
+      // 135 µs Jacobi, profiles/r05m_eig_timeline.txt.)
       hipLaunchKernelGGL(k_atb32, dim3(CQ_G), dim3(256), 0, st, V, W, p, cq_part, cq_ticket, H);
       OCM_CHECK_LAUNCH("k_atb32 H");
       // two side streams when θ is wanted: A deflates the block and runs
       // θ3; B forms R and S (the test waits for S), then C·R and G2
       hipStream_t sa = st, sb = st;
+      rc = eig_side_init(ctx);  // the streams and events (the test's read-back event too)
+      if (rc) return rc;
       if (theta_mode) {
-        rc = eig_side_init(ctx);
-        if (rc) return rc;
         sa = ctx->eig_side[0];
         sb = ctx->eig_side[1];
         OCM_HIP(hipEventRecord(ctx->eig_ev[0], st));
         OCM_HIP(hipStreamWaitEvent(sa, ctx->eig_ev[0], 0));
         OCM_HIP(hipStreamWaitEvent(sb, ctx->eig_ev[0], 0));
-        rc = theta_into(V, W, H, b, sa, ctx->eig_sub, tr3);
-        if (rc) return rc;
-        OCM_HIP(hipEventRecord(ctx->eig_ev[2], sa));
       }
       double* R = T1;
       double* CR = T2;
@@ -2051,6 +2189,10 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
           OCM_CHECK_LAUNCH("k_atb32 G2");
         }
         OCM_HIP(hipEventRecord(ctx->eig_ev[3], sb));
+        // after B's test inputs: theta_into queues its Δ terms on B too
+        rc = theta_into(V, W, H, b, sa, sb, ctx->eig_sub, tr3);
+        if (rc) return rc;
+        OCM_HIP(hipEventRecord(ctx->eig_ev[2], sa));
       }
       rc = jacobi(H, b, 40, theta, Z, st);
       if (rc) return rc;
@@ -2058,26 +2200,33 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
       hipLaunchKernelGGL(k_rr_test32, dim3(1), dim3(256), 0, st, S, Z, b, k, res);
       OCM_CHECK_LAUNCH("k_rr_test32");
       OCM_HIP(hipMemcpyAsync(hres, theta, 2 * (size_t)b * sizeof(double), hipMemcpyDeviceToHost, st));
-      OCM_HIP(hipStreamSynchronize(st));
+      OCM_HIP(hipEventRecord(ctx->eig_ev[6], st));
+      // R (= T1) and CR are reused below: side stream B is done with them
+      if (theta_mode) OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[3], 0));
+      // the outputs of a converged test are queued before the host has read
+      // it (the GPU would idle through the round trip otherwise): the Ritz
+      // vectors V·Z into T1, λ and the eigenvectors, then θ once side stream
+      // A is done.  A test that fails leaves them to be overwritten.
+      hipLaunchKernelGGL(k_cq_apply32, dim3(CQ_G), dim3(256), 0, st, V, p, Z, T1);  // Ritz vectors
+      OCM_CHECK_LAUNCH("k_cq_apply32 ritz");
+      hipLaunchKernelGGL(k_extract_signfix, dim3(k), dim3(256), 0, st, T1, p, b, k, evecs_out, theta, evals_out);
+      OCM_CHECK_LAUNCH("k_extract_signfix");
+      if (theta_mode) {  // (the deflation operands and the θ3 arena are reused by the next test too)
+        OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[2], 0));
+        hipLaunchKernelGGL(k_theta_combine, dim3(1), dim3(256), 0, st, theta, Z, S, L, tr3, b, k, slice == 0 ? 1 : 0,
+                           theta_mode >= 2 ? 1 : 0, theta_out);
+        OCM_CHECK_LAUNCH("k_theta_combine");
+      }
+      OCM_HIP(hipEventSynchronize(ctx->eig_ev[6]));
       double rmax = 0.0;
       for (int i = 0; i < k; ++i) rmax = std::max(rmax, hres[b + i]);
       const double scale = std::fabs(hres[0]);
-      if (theta_mode) {  // R, CR, the deflation operands and the θ3 arena are reused
-        OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[2], 0));
-        OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[3], 0));
-      }
       if (!(rmax == rmax)) return ocm::fail(OCM_ERR_ARG, "ocm_eig_topk: NaN in covariance");
       const double target = tol * (scale > 0 ? scale : 1.0);
       converged = rmax <= target;
       if (converged || it == max_iter) {
-        if (theta_mode) {
-          hipLaunchKernelGGL(k_theta_combine, dim3(1), dim3(256), 0, st, theta, Z, S, L, tr3, b, k, slice == 0 ? 1 : 0,
-                             theta_mode >= 2 ? 1 : 0, theta_out);
-          OCM_CHECK_LAUNCH("k_theta_combine");
-        }
-        hipLaunchKernelGGL(k_cq_apply32, dim3(CQ_G), dim3(256), 0, st, V, p, Z, T1);  // Ritz vectors
-        OCM_CHECK_LAUNCH("k_cq_apply32 ritz");
         std::swap(V, T1);
+        extracted = true;
         break;
       }
       const double tk = std::fabs(hres[k - 1]);
@@ -2145,15 +2294,17 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   }
   if (iters_out) *iters_out = std::min(it, max_iter);
 
-  hipLaunchKernelGGL(k_extract_signfix, dim3(k), dim3(256), 0, st, V, p, b, k, evecs_out, theta, evals_out);
-  OCM_CHECK_LAUNCH("k_extract_signfix");
+  if (!extracted) {
+    hipLaunchKernelGGL(k_extract_signfix, dim3(k), dim3(256), 0, st, V, p, b, k, evecs_out, theta, evals_out);
+    OCM_CHECK_LAUNCH("k_extract_signfix");
+  }
 
   if (theta_mode && !fused) {
     // H_k = V_kᵀ (C V_k): the projected block of the Ritz vectors; deflate
     // the leading k of them
     rc = project(V, W, H);
     if (rc) return rc;
-    rc = theta_into(V, W, H, k, st, ctx, theta_out);
+    rc = theta_into(V, W, H, k, st, st, ctx, theta_out);
     if (rc) return rc;
   }
   return converged ? OCM_OK : ocm::fail(OCM_ERR_NOCONV, "ocm_eig_topk: max_iter reached before tolerance");

@@ -487,6 +487,20 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
     return _SIDE[key]
 
 
+_PINNED: dict = {}
+
+
+def _pinned(dev: torch.device, n: int) -> torch.Tensor:
+    """A per-device pinned float64 staging buffer of ≥ n values (fit_class
+    reads it back before it returns, so consecutive fits can share it; a fresh
+    pinned allocation per fit cost host time on the GPU's critical path)."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    buf = _PINNED.get(key)
+    if buf is None or buf.numel() < n:
+        buf = _PINNED[key] = torch.empty(max(n, 64), dtype=torch.float64, pin_memory=True)
+    return buf[:n]
+
+
 def inv_evals(evals: torch.Tensor, rcond=1e-15) -> torch.Tensor:
     """Diagonal of pinv(cov(T)) for T = centred scores on the eigenbasis:
     cov(T) = diag(λ) (utils/SIMCA.py:69 with np.linalg.pinv's rcond=1e-15 cutoff)."""
@@ -613,21 +627,14 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
             allreduce([theta[2:]])  # θ3 partials of the ranks' trace slices
     _mark("eig")
     # The host needs λ and θ for the limits (SciPy), the device needs 1/λ for
-    # the fit-set scoring.  The scalars go to pinned memory on a side stream
-    # that waits only for the eigensolve; 1/λ and the scoring are queued on the
-    # launch stream first, so the GPU never idles while the host issues the
-    # small ops or waits for the copy, and the limits overlap the scoring.
-    inv = inv_evals(evals)
-    host_buf = torch.empty(k + 3, dtype=torch.float64, pin_memory=True)
+    # the fit-set scoring.  The eigensolver has just synchronised on its
+    # convergence test, so the launch queue is nearly empty: 1/λ and the
+    # scoring are launched first (every host µs before that launch is GPU idle
+    # time), then λ and θ go to pinned memory on a side stream that waits only
+    # for the eigensolve, and the limits overlap the scoring.
     eig_done = torch.cuda.Event()
     eig_done.record(torch.cuda.current_stream(X.device))
-    side = _side_stream(X.device)
-    with torch.cuda.stream(side):
-        side.wait_event(eig_done)
-        host_buf[:k].copy_(evals, non_blocking=True)
-        host_buf[k:].copy_(theta, non_blocking=True)
-        copied = torch.cuda.Event()
-        copied.record(side)
+    inv = inv_evals(evals)
     if n > 0:
         sc = score(X, rows, n, evecs, mean64, inv, want_T=want_T, want_stats=True)
     else:  # T and Q in the dtype the other ranks' scoring produces (utils/SIMCA.py:65-71)
@@ -636,6 +643,14 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
               "T2": torch.empty(0, dtype=torch.float64, device=X.device),
               "Q": torch.empty(0, dtype=vdt, device=X.device),
               "stats": torch.zeros(4, dtype=torch.float64, device=X.device)}
+    host_buf = _pinned(X.device, k + 3)
+    side = _side_stream(X.device)
+    with torch.cuda.stream(side):
+        side.wait_event(eig_done)
+        host_buf[:k].copy_(evals, non_blocking=True)
+        host_buf[k:].copy_(theta, non_blocking=True)
+        copied = torch.cuda.Event()
+        copied.record(side)
     _mark("fit_score")
     copied.synchronize()
     host = host_buf.numpy().copy()
