@@ -1092,7 +1092,11 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restri
   f32x4 sh;
 #pragma unroll
   for (int e = 0; e < 4; ++e) sh[e] = c0 + e < p ? shift[c0 + e] : 0.f;
+#ifdef OCM_QP_NOSTENCIL
+  const f32x4 th = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
+#else
   const f32x4 th = *reinterpret_cast<const f32x4*>(q.thr + c0);
+#endif
   const float* c = pa.taps + HH;  // interior taps, offset -HH..HH (scalar loads)
   float ct[HH + 1];
 #pragma unroll
@@ -1189,9 +1193,13 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restri
       if constexpr (HH == 0) {
         a = win[o];
       } else {  // odd derivative
+#ifdef OCM_QP_NOSTENCIL  // make exp timing diagnostic: no stencil arithmetic (wrong values)
+        a = win[o + 1] - win[o - 1];
+#else
         a = 0.f;
 #pragma unroll
         for (int t = 1; t <= HH; ++t) a = fmaf(ct[t], __fsub_rn(win[o + t], win[o - t]), a);
+#endif
       }
       y[e] = ocm::mul_nc(a, srj);  // s_r = 1 without SNV (exact)
     }
