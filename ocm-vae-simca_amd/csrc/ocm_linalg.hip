@@ -1699,7 +1699,8 @@ int dgemm(const double* A, int64_t lda, const double* B, int64_t ldb, double* D,
 }
 
 int jacobi(const double* A, int n, int max_sweeps, double* ev, double* Z, hipStream_t st) {
-  // n = 32: the block kernel (0.95 ms per fit against 1.19 with the one-wave k_jacobi<32, 64>, r03z)
+  // n = 32: the block kernel (0.95 ms per fit against 1.19 with the one-wave k_jacobi<32, 64>, r03z; the
+  // same block rounds in one wave without barriers, round 5: 204 against 122–140 µs, r05s_eig_timeline.txt)
 #ifdef OCM_JACOBI_SWEEPS  // make exp diagnostic: print the sweep count of each 32×32 solve
   if (n == 32) {
     static int* dsw = nullptr;
