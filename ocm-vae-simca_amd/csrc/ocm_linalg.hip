@@ -901,6 +901,18 @@ __device__ __forceinline__ void cq_apply_block(const double* src, int p, int rb,
   }
 }
 
+#ifdef OCM_CVQ_STAMPS  // make exp diagnostic: phase times of k_cvq32 (wall clock, 100 MHz)
+__device__ unsigned long long g_cvq_st[10];
+__device__ __forceinline__ void cvq_stamp(int slot, bool is_min) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t = wall_clock64() + (unsigned long long)(threadIdx.x & 1);  // lane-dependent: a vector atomic
+    if (is_min) atomicMin(&g_cvq_st[slot], t); else atomicMax(&g_cvq_st[slot], t);
+  }
+}
+#define CVQ_STAMP(s_, m_) cvq_stamp(s_, m_)
+#else
+#define CVQ_STAMP(s_, m_)
+#endif
 // The CholQR factor of a 32×32 Gram S (in sS): column scaling r_i = 1/√S_ii,
 // S' = D S D = L Lᵀ by wave 0 in registers (lane i holds row i, v_readlane
 // broadcasts, pivot clamp 1e-14 as k_chol), X = L⁻¹ by back substitution and
@@ -988,6 +1000,69 @@ __device__ __forceinline__ void cq_finalize(double (*sS)[33], double* rsc, int* 
       for (int k = 0; k < 32; ++k) Mout[k * 32 + i] = rsc[k] * xr[k];
     }
   }
+}
+
+// The CholQR factor of a non-degenerate Gram (sS) computed by ONE wave, into
+// LDS: msm[k][i] = M[k][i], M = D·L⁻ᵀ as cq_finalize defines it (same pivot
+// clamp), but without cross-lane register broadcasts: the rows of L go
+// through LDS (Ls, rows 16-B aligned) and every lane reads row j of L with
+// 16-B broadcast loads (left-looking Cholesky, lane i builds row i; then lane
+// c solves L x = e_c for column c of L⁻¹).  k_cvq32<true>'s eighth wave runs
+// it beside the other seven's product: cq_finalize's readlane form took
+// ≈ 40 µs there (SGPR pressure next to the product waves) against 14 µs alone.
+// Not bit-identical to cq_finalize (the sums run in another order).
+__device__ __forceinline__ void cq_factor_wave(const double (*sS)[33], double (*Ls)[34], double* rsc, double* dinv,
+                                               double (*msm)[33], int lane) {
+  const int i = lane & 31;
+  if (lane < 32) rsc[i] = 1.0 / sqrt(sS[i][i]);
+  __builtin_amdgcn_wave_barrier();
+  const double ri = rsc[i];
+  double a[32], l[32];
+#pragma unroll
+  for (int c = 0; c < 32; ++c) a[c] = sS[i][c] * ri * rsc[c];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    double s0 = a[j], s1 = 0.0;
+#pragma unroll
+    for (int k = 0; k + 1 < j; k += 2) {
+      const double2 r2 = *reinterpret_cast<const double2*>(&Ls[j][k]);
+      s0 = fma(-l[k], r2.x, s0);
+      s1 = fma(-l[k + 1], r2.y, s1);
+    }
+    if (j & 1) s0 = fma(-l[j - 1], Ls[j][j - 1], s0);
+    const double sj = s0 + s1;
+    if (lane == j) {
+      const double ajj = fmax(sj, 1e-14);
+      const double inv = rsqrt(ajj);
+      Ls[j][j] = ajj * inv;
+      dinv[j] = inv;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const double inv = dinv[j];
+    l[j] = i > j ? sj * inv : (i == j ? Ls[j][j] : 0.0);
+    if (lane < 32 && i > j) Ls[i][j] = l[j];
+    __builtin_amdgcn_wave_barrier();
+  }
+  // column c = i of X = L⁻¹: x_r = (δ_rc − Σ_{k<r} L[r][k] x_k) / L[r][r], r ≥ c
+  double x[32];
+#pragma unroll
+  for (int r = 0; r < 32; ++r) {
+    double s0 = r == i ? 1.0 : 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = 0; k + 1 < r; k += 2) {
+      const double2 r2 = *reinterpret_cast<const double2*>(&Ls[r][k]);
+      s0 = fma(-r2.x, x[k], s0);
+      s1 = fma(-r2.y, x[k + 1], s1);
+    }
+    if (r & 1) s0 = fma(-Ls[r][r - 1], x[r - 1], s0);
+    x[r] = r < i ? 0.0 : (s0 + s1) * dinv[r];
+  }
+  // M[c][r] = r_c · X[r][c]
+  if (lane < 32) {
+#pragma unroll
+    for (int r = 0; r < 32; ++r) msm[i][r] = rsc[i] * x[r];
+  }
+  __builtin_amdgcn_wave_barrier();
 }
 
 template <bool APPLY>
@@ -1115,13 +1190,28 @@ __global__ __launch_bounds__(256) void k_cq_apply32(const double* __restrict__ s
 // gpart: cv_rb·1024 row-block partials, then ⌈cv_rb/16⌉·1024 group partials;
 // gtick: 1 + ⌈cv_rb/16⌉ counters TICKET_STRIDE words apart (zeroed once).
 // ---------------------------------------------------------------------------
+// Deferred factor (DEFER, round 5): Min is not given — the previous launch
+// left the Gram of Win (Sin[0..1023], Sin[1024] = 0) instead of factoring it,
+// and the eighth wave of every workgroup factors it (cq_factor_wave, the same
+// values as cq_finalize would have produced) while the other seven form the
+// product, so the ≈ 14 µs one-wave factorisation leaves the critical path.
+// Sin[1024] = 1: the previous launch met a zero column and factored (and
+// repaired W) itself; Min holds its factor.  defer_next: this launch leaves
+// its Gram in Sout (non-degenerate) instead of factoring it.
 constexpr int CVQ_G1 = 16;
+template <bool DEFER>
 __global__ __launch_bounds__(512) void k_cvq32(const double* __restrict__ C, int p, const double* __restrict__ Win,
                                              const double* __restrict__ Min, double* __restrict__ Wout,
                                              double* __restrict__ part, unsigned* __restrict__ ticket,
                                              double* __restrict__ gpart, unsigned* __restrict__ gtick,
-                                             uint64_t seed, double* __restrict__ Mout) {
+                                             uint64_t seed, double* __restrict__ Mout, const double* __restrict__ Sin,
+                                             double* __restrict__ Sout, int defer_next) {
+  // DEFER: the factor wave (7) shares a SIMD with wave 3 (waves w and w + 4
+  // share SIMD w), so the product runs on the six waves of the other SIMDs
+  constexpr int PW = DEFER ? CV_W - 2 : CV_W;  // product waves
   __shared__ double red[CV_W][16 * 33];
+  __shared__ __attribute__((aligned(16))) double lsc[DEFER ? 32 : 1][34];  // the factor wave's L
+  __shared__ double dinv[DEFER ? 32 : 1];
   __shared__ double sm[32][33];
   __shared__ double sv[16][33];
   __shared__ double sS[32][33];
@@ -1132,10 +1222,13 @@ __global__ __launch_bounds__(512) void k_cvq32(const double* __restrict__ C, int
   const int r0 = rb * 16;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int i = lane & 15, g = lane >> 4;
-  const int kslice = (p + 2 * CV_W * 32 - 1) / (2 * CV_W * 32) * 32;
-  const int kb = (half * CV_W + wave) * kslice;
-  const int ke = min(p, kb + kslice);
+  const int pwave = DEFER ? (wave < 3 ? wave : wave - 1) : wave;  // product slot (DEFER: waves 0-2, 4-6)
+  const bool prod = DEFER ? (wave != 3 && wave != 7) : true;
+  const int kslice = (p + 2 * PW * 32 - 1) / (2 * PW * 32) * 32;
+  const int kb = (half * PW + pwave) * kslice;
+  const int ke = prod ? min(p, kb + kslice) : kb;  // waves 3 and 7 form no product
   const double* crow = C + (int64_t)min(r0 + i, p - 1) * p;
+  CVQ_STAMP(0, true);
   f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = acc0;
   for (int k0 = kb; k0 < ke; k0 += 32) {
     double a[8], b0[8], b1[8];
@@ -1163,18 +1256,53 @@ __global__ __launch_bounds__(512) void k_cvq32(const double* __restrict__ C, int
       acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b1[s], acc1, 0, 0, 0);
     }
   }
+  if (prod) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    red[wave][(g + 4 * r) * 33 + i] = acc0[r];
-    red[wave][(g + 4 * r) * 33 + 16 + i] = acc1[r];
+    for (int r = 0; r < 4; ++r) {
+      red[pwave][(g + 4 * r) * 33 + i] = acc0[r];
+      red[pwave][(g + 4 * r) * 33 + 16 + i] = acc1[r];
+    }
+#ifdef OCM_CVQ_STAMPS
+    if (lane == 0) {
+      const unsigned long long t = wall_clock64() + (unsigned long long)(lane & 1);
+      atomicMax(&g_cvq_st[9], t);
+    }
+#endif
   }
-  if (Min)
+  if (DEFER) {
+    if (wave == 7) {  // the factor of Win: from the previous launch's Gram (or its own factor)
+      // all sixteen loads of a lane in flight at once: the product waves keep
+      // the memory system busy, and one load at a time cost ≈ 2 µs apiece
+      const bool ready = Sin[1024] != 0.0;
+      const double* src = ready ? Min : Sin;
+      double t[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) t[q] = src[lane + 64 * q];
+      if (ready) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) sm[(lane + 64 * q) >> 5][(lane + 64 * q) & 31] = t[q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) sS[(lane + 64 * q) >> 5][(lane + 64 * q) & 31] = t[q];
+        __builtin_amdgcn_wave_barrier();
+        cq_factor_wave(sS, lsc, rsc, dinv, sm, lane);
+      }
+#ifdef OCM_CVQ_STAMPS
+      if (lane == 0) {
+        const unsigned long long t = wall_clock64() + (unsigned long long)(lane & 1);
+        atomicMax(&g_cvq_st[8], t);
+      }
+#endif
+    }
+  } else if (Min) {
     for (int e = tid; e < 32 * 32; e += 512) sm[e >> 5][e & 31] = Min[e];
+  }
   __syncthreads();
+  CVQ_STAMP(1, false);
   const int orow = tid >> 5, ocol = tid & 31;
   double v = 0.0;
 #pragma unroll
-  for (int w = 0; w < CV_W; ++w) v += red[w][orow * 33 + ocol];
+  for (int w = 0; w < PW; ++w) v += red[w][orow * 33 + ocol];
   part[(int64_t)blockIdx.x * 512 + tid] = v;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1191,8 +1319,9 @@ __global__ __launch_bounds__(512) void k_cvq32(const double* __restrict__ C, int
   if (!last) return;
   const double o = part[(int64_t)(blockIdx.x ^ 1) * 512 + tid];
   double y = half == 0 ? v + o : o + v;  // (C·Win)[r0 + orow][ocol]
+  CVQ_STAMP(2, false);
   const bool rok = r0 + orow < p;
-  if (Min) {  // basis change on the output rows: (C·Win)·Min
+  if (DEFER || Min) {  // basis change on the output rows: (C·Win)·Min
     sv[orow][ocol] = y;
     __syncthreads();
     double t = 0.0;
@@ -1214,6 +1343,7 @@ __global__ __launch_bounds__(512) void k_cvq32(const double* __restrict__ C, int
     for (int r = 0; r < 16; ++r) gs = fma(sv[r][a], sv[r][b], gs);
     st_agent(&gpart[(int64_t)rb * 1024 + e], gs);
   }
+  CVQ_STAMP(3, false);
   const int ngrp = (nrb + CVQ_G1 - 1) / CVQ_G1;
   const int grp = rb / CVQ_G1, g0 = grp * CVQ_G1, gsize = min(CVQ_G1, nrb - g0);
   if (!last_arrival(gtick + (1 + grp) * TICKET_STRIDE, (unsigned)gsize)) return;
@@ -1229,7 +1359,9 @@ __global__ __launch_bounds__(512) void k_cvq32(const double* __restrict__ C, int
     for (int q = 0; q < CVQ_G1; ++q) acc += pv[q];
     st_agent(&gsum[(int64_t)grp * 1024 + e], acc);
   }
+  CVQ_STAMP(4, false);
   if (!last_arrival(gtick, (unsigned)ngrp)) return;
+  CVQ_STAMP(5, false);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int e = tid + 512 * h;
@@ -1244,7 +1376,22 @@ __global__ __launch_bounds__(512) void k_cvq32(const double* __restrict__ C, int
     sS[e >> 5][e & 31] = acc;
   }
   __syncthreads();
+  CVQ_STAMP(6, false);
+  if (defer_next) {  // hand the Gram on (the next launch factors it) unless a column is zero
+    if (tid == 0) degen = 0;
+    __syncthreads();
+    if (tid < 32 && !(sqrt(sS[tid][tid]) > 1e-280)) atomicOr(&degen, 1);
+    __syncthreads();
+    if (!degen) {
+      for (int e = tid; e < 32 * 32; e += 512) Sout[e] = sS[e >> 5][e & 31];
+      if (tid == 0) Sout[1024] = 0.0 + (double)(tid & 1);
+      return;
+    }
+    if (tid == 0) Sout[1024] = 1.0 + (double)(tid & 1);  // factored here (Mout), W repaired
+  }
   cq_finalize(sS, rsc, &degen, Wout, p, 1, seed, Mout);
+  __syncthreads();
+  CVQ_STAMP(7, false);
 }
 
 __device__ __forceinline__ double hash_normal(uint64_t a) {
@@ -1880,7 +2027,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   const bool fused = !wide && b == QB;
   const int cvq_ng = (cv_rb + CVQ_G1 - 1) / CVQ_G1;
   const int gt_words = (1 + cvq_ng) * TICKET_STRIDE;
-  if (fused) need += (2 * pb + 2048 + (size_t)(cv_rb + cvq_ng) * 1024) * sizeof(double) + gt_words * 4 + 4 * 256;
+  if (fused) need += (2 * pb + 2048 + (size_t)(cv_rb + cvq_ng) * 1024 + 2 * 1056) * sizeof(double) + gt_words * 4 + 5 * 256;
   if (theta_mode) need += (4 * (size_t)b * p + 2 * def_blocks + 8) * sizeof(double) + 4 * 256;
   void* w = ocm::workspace(ctx, need + 16 * 256, st);
   if (!w) return OCM_ERR_NOMEM;
@@ -1911,6 +2058,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   double* Wb = fused ? cv.take<double>(pb) : nullptr;
   double* Mf = fused ? cv.take<double>(2048) : nullptr;
   double* gpart = fused ? cv.take<double>((size_t)(cv_rb + cvq_ng) * 1024) : nullptr;
+  double* Sb = fused ? cv.take<double>(2 * 1056) : nullptr;  // two deferred Grams (+ their flags)
   // θ work buffers (the deflated matrix, its tile partials, the rank-2kd
   // operands, three traces), carved up front: the fused path fills them during
   // its Rayleigh–Ritz step, on a side stream
@@ -2118,12 +2266,38 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   double* Wn = Wa;
   const double* Mc = nullptr;
   int mslot = 0;
+  const double* Sprev = nullptr;  // the Gram the previous plain launch left unfactored (k_cvq32<true>)
+  int sslot = 0;
   for (it = 1; it <= max_iter; ++it) {
     if (fused && it < next_rr) {  // W ← (C·Wc)·Mc and its factor, one launch
       double* Mn = Mf + 1024 * mslot;
-      hipLaunchKernelGGL(k_cvq32, dim3(2 * cv_rb), dim3(512), 0, st, C, p, Wc, Mc, Wn, cv_part, cv_ticket, gpart,
-                         gtick, (uint64_t)(500 + it), Mn);
+      // the next launch is a plain iteration too: it factors this one's Gram
+      // in a wave of its own (k_cvq32<true>), off the critical path
+      const int defer_next = it + 1 < next_rr ? 1 : 0;
+      double* Sout = Sb + 1056 * sslot;
+      if (Sprev)
+        hipLaunchKernelGGL(k_cvq32<true>, dim3(2 * cv_rb), dim3(512), 0, st, C, p, Wc, Mc, Wn, cv_part, cv_ticket,
+                           gpart, gtick, (uint64_t)(500 + it), Mn, Sprev, Sout, defer_next);
+      else
+        hipLaunchKernelGGL(k_cvq32<false>, dim3(2 * cv_rb), dim3(512), 0, st, C, p, Wc, Mc, Wn, cv_part, cv_ticket,
+                           gpart, gtick, (uint64_t)(500 + it), Mn, nullptr, Sout, defer_next);
       OCM_CHECK_LAUNCH("k_cvq32");
+      Sprev = defer_next ? Sout : nullptr;
+      sslot ^= 1;
+#ifdef OCM_CVQ_STAMPS
+      {
+        unsigned long long h[10];
+        (void)hipStreamSynchronize(st);
+        (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_cvq_st), sizeof(h));
+        fprintf(stderr, "cvq32 us: product+factor %.2f (product waves end %.2f, factor wave end %.2f) pair %.2f "
+                "gram %.2f group %.2f last %.2f sum %.2f finalize %.2f\n",
+                (h[1] - h[0]) / 100.0, h[9] ? (h[9] - h[0]) / 100.0 : -1.0, h[8] ? (h[8] - h[0]) / 100.0 : -1.0,
+                (h[2] - h[1]) / 100.0, (h[3] - h[2]) / 100.0, (h[4] - h[3]) / 100.0,
+                (h[5] - h[4]) / 100.0, (h[6] - h[5]) / 100.0, (h[7] - h[6]) / 100.0);
+        unsigned long long z[10] = {~0ull, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_cvq_st), z, sizeof(z));
+      }
+#endif
       Wc = Wn;
       Wn = (Wn == Wa) ? Wb : Wa;
       Mc = Mn;
@@ -2248,6 +2422,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
       Wn = Wb;
       Mc = Mf;
       mslot = 1;
+      Sprev = nullptr;
       continue;
     }
     rc = ritz();
