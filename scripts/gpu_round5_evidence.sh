@@ -23,11 +23,13 @@ if [ "${TESTS:-1}" = 1 ]; then
   step tests 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider
   step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
 fi
-step bench 500 python3 -u bench.py
-step share125k 300 python3 -u bench.py --rows 125000 --no-cpu --no-vae --no-cv --no-prep --steps 20
-step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 -u bench.py --no-cpu --no-vae --no-cv --no-prep --steps 5
-python3 scripts/trace_by_grid.py "$O/prof/run_kernel_trace.csv" "$O/headline_by_grid.md" "headline workload (bench.py --no-cpu --no-vae --no-cv --no-prep --steps 5): kernel trace by launch shape" || exit 6
-rm -f "$O/prof/run_kernel_trace.csv"
+if [ "${BENCH:-1}" = 1 ]; then
+  step bench 500 python3 -u bench.py
+  step share125k 300 python3 -u bench.py --rows 125000 --no-cpu --no-vae --no-cv --no-prep --steps 20
+  step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 -u bench.py --no-cpu --no-vae --no-cv --no-prep --steps 5
+  python3 scripts/trace_by_grid.py "$O/prof/run_kernel_trace.csv" "$O/headline_by_grid.md" "headline workload (bench.py --no-cpu --no-vae --no-cv --no-prep --steps 5): kernel trace by launch shape" || exit 6
+  rm -f "$O/prof/run_kernel_trace.csv"
+fi
 if [ "${PMC:-1}" = 1 ]; then
   step pmc_gram 600 bash scripts/pmc_passes.sh "k_gram8e|k_q8_quant" "$O/pmc_gram" scripts/bench_gram.py --rounds 1 --variants i8x3:0
   step pmc_score 400 bash scripts/pmc_passes.sh "k_score_1p" "$O/pmc_score" scripts/bench_score.py --k 20 --reps 3 --kernels diag
