@@ -104,6 +104,32 @@ def test_eig_topk_and_thetas(eng, p, k):
                                rtol=1e-8)
 
 
+@pytest.mark.parametrize("rank", [12, 25])
+def test_eig_rank_deficient_block(eng, rank):
+    """C of rank < b = 32 (fewer spectra than the block width): the plain
+    iterations' CholQR meets zero columns, which the factor replaces by
+    pseudo-random ones — including in the launch that would otherwise hand
+    its Gram to the next one (k_cvq32<true>, round 5).  Eigenpairs and θ as
+    eigh's; the zero tail contributes nothing."""
+    rng = np.random.default_rng(100 + rank)
+    p, k = 256, 6
+    lam = np.concatenate([np.linspace(40, 20, k), np.geomspace(1.0, 1e-2, rank - k)])
+    Qm, _ = np.linalg.qr(rng.standard_normal((p, rank)))
+    C = (Qm * lam) @ Qm.T
+    C = 0.5 * (C + C.T)
+    evals, evecs, theta, iters = eng.eig_topk(_dev(C), k, 2)
+    w, V = np.linalg.eigh(C)
+    w, V = w[::-1], V[:, ::-1]
+    np.testing.assert_allclose(evals.cpu().numpy(), w[:k], rtol=1e-10)
+    P = evecs.cpu().numpy()
+    for i in range(k):
+        v = V[:, i] * np.sign(V[np.argmax(np.abs(V[:, i])), i])
+        np.testing.assert_allclose(P[i], v, atol=1e-7)
+    tail = lam[k:]
+    np.testing.assert_allclose(theta.cpu().numpy(), [tail.sum(), (tail ** 2).sum(), (tail ** 3).sum()],
+                               rtol=1e-8)
+
+
 def test_eig_no_gap_converges(eng):
     rng = np.random.default_rng(9)
     p, k = 512, 10
