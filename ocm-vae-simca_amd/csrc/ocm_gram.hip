@@ -777,13 +777,26 @@ constexpr int Q8QT = Q8QS * (Q8QC / 4);    // threads (768)
 // and their LDS-staged stores (shared by k_q8_quant and k_q8_quant_prep).
 // q8_tail's LDS (the caller declares it: k_q8_quant_prep overlays its own
 // load-phase buffers on it)
+// digit planes staged in LDS at once: 3 (one barrier, 147 KiB with the
+// reduction buffers overlaid — the quantiser is one workgroup per CU by its
+// registers anyway) or 1 (a barrier pair per plane); 3.02 vs 3.04 and 2.62 vs
+// 2.69 ms on two boxes, identical digits (profiles/r05zc_quant_stage_ab.json)
+#ifdef OCM_Q8_STAGE1
+constexpr int Q8NST = 1;
+#else
+constexpr int Q8NST = 3;
+#endif
 template <int QC = Q8QC>
 struct Q8TailLdsT {
-  __attribute__((aligned(16))) char stage[Q8SPB * QC * 32];  // one digit plane: 24 KiB at QC = 32
-  __attribute__((aligned(16))) float wmax[Q8QS][QC];
-  __attribute__((aligned(16))) double wsum[Q8QS][QC];
-  float pmax[8][QC];
-  double psum[8][QC];
+  union {  // the reduction buffers are dead once the block scales are known
+    struct {
+      __attribute__((aligned(16))) float wmax[Q8QS][QC];
+      __attribute__((aligned(16))) double wsum[Q8QS][QC];
+      float pmax[8][QC];
+      double psum[8][QC];
+    } r;
+    __attribute__((aligned(16))) char stage[Q8NST * Q8SPB * QC * 32];  // digit planes: 48 KiB each at QC = 32
+  } u;
   __attribute__((aligned(16))) float fmax_[QC];
 };
 using Q8TailLds = Q8TailLdsT<>;
@@ -795,11 +808,11 @@ __device__ __forceinline__ void q8_tail(f32x4 (&v)[16], int tid, int cq, int rs,
                                         const Q8Plan& q, int chunk, int b, const SegTable& st,
                                         double* __restrict__ colblk, Q8TailLdsT<QC>& L, const f32x4 th) {
   constexpr int NT = Q8QS * (QC / 4);  // threads
-  char* stage = L.stage;
-  auto& wmax = L.wmax;
-  auto& wsum = L.wsum;
-  auto& pmax = L.pmax;
-  auto& psum = L.psum;
+  char* stage = L.u.stage;
+  auto& wmax = L.u.r.wmax;
+  auto& wsum = L.u.r.wsum;
+  auto& pmax = L.u.r.pmax;
+  auto& psum = L.u.r.psum;
   float* fmax_ = L.fmax_;
   // column sums over every row (the fix-up does not touch them)
   double cs[4] = {0.0, 0.0, 0.0, 0.0};
@@ -927,6 +940,25 @@ __device__ __forceinline__ void q8_tail(f32x4 (&v)[16], int tid, int cq, int rs,
   constexpr int GIMG = QC * 32;  // bytes per group image
   char* gdst = q.digits + ((size_t)chunk * (st.chunk_rows / Q8K) + (size_t)b * Q8SPB) * q.P8 * 32 + (size_t)cg0 * 32;
   const int grp = rs >> 1, half = rs & 1;
+  if constexpr (Q8NST == 3) {
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        *reinterpret_cast<i32x4*>(&stage[dg * Q8SPB * GIMG + grp * GIMG + q8_qslot(2 * (4 * cq + e) + half) * 16]) =
+            w[dg][e];
+    __syncthreads();
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg)
+#pragma unroll
+      for (int k = 0; k < Q8SPB * GIMG / (16 * NT); ++k) {
+        const int o = 16 * (tid + NT * k);
+        const int g = o / GIMG, within = o - g * GIMG;
+        *reinterpret_cast<i32x4*>(gdst + (size_t)dg * q.plane + (size_t)g * q.P8 * 32 + within) =
+            *reinterpret_cast<const i32x4*>(&stage[dg * Q8SPB * GIMG + g * GIMG + q8_qslot(within >> 4) * 16]);
+      }
+    return;
+  }
 #pragma unroll
   for (int dg = 0; dg < 3; ++dg) {
 #pragma unroll

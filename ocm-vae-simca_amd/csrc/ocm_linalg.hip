@@ -1528,6 +1528,92 @@ __global__ __launch_bounds__(256) void k_atb32(const double* __restrict__ A, con
   }
 }
 
+// The Rayleigh–Ritz basis, W and H in one launch (round 5): with T = Wc·Mc
+// (k_cq_gram32<true>, its CholQR factor M2 in M2) and CW = C·Wc (k_cv32 on a
+// side stream, beside it), V = T·M2 and W = C·V = CW·(Mc·M2) need no second
+// product with C; each workgroup forms Mc·M2 in LDS, applies both to its row
+// blocks, stores V and W and its partial of H = VᵀW (k_atb32's MFMA layout and
+// hand-off).  Replaces k_cq_apply32 + k_cv32 + k_atb32 on the critical path.
+__global__ __launch_bounds__(256) void k_rr_basis32(const double* __restrict__ T, const double* __restrict__ CW,
+                                                    int p, const double* __restrict__ Mc,
+                                                    const double* __restrict__ M2, double* __restrict__ V,
+                                                    double* __restrict__ W, double* __restrict__ part,
+                                                    unsigned* __restrict__ ticket, double* __restrict__ H) {
+  __shared__ double sm2[32][33];
+  __shared__ double smc[32][33];
+  __shared__ double smp[32][33];
+  __shared__ double wpart[4][4][4][64];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  for (int e = tid; e < 32 * 32; e += 256) {
+    sm2[e >> 5][e & 31] = M2[e];
+    smc[e >> 5][e & 31] = Mc[e];
+  }
+  __syncthreads();
+  for (int e = tid; e < 32 * 32; e += 256) {  // Mc·M2
+    const int i = e >> 5, j = e & 31;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) acc = fma(smc[i][k], sm2[k][j], acc);
+    smp[i][j] = acc;
+  }
+  __syncthreads();
+  int lo, hi;
+  cq_blocks(p, lo, hi);
+  f64x4 s[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s[q] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int rb = lo + wave; rb < hi; rb += 4) {
+    f64x4 v0, v1, w0, w1;
+    cq_apply_block(T, p, rb, sm2, g, c, v0, v1);
+    cq_apply_block(CW, p, rb, smp, g, c, w0, w1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * rb + g + 4 * r;
+      if (row < p) {
+        V[(int64_t)row * 32 + c] = v0[r];
+        V[(int64_t)row * 32 + 16 + c] = v1[r];
+        W[(int64_t)row * 32 + c] = w0[r];
+        W[(int64_t)row * 32 + 16 + c] = w1[r];
+      }
+    }
+    // H partial: rows past p are zero in both (cq_apply_block reads them as 0)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0[r], w0[r], s[0], 0, 0, 0);
+      s[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0[r], w1[r], s[1], 0, 0, 0);
+      s[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1[r], w0[r], s[2], 0, 0, 0);
+      s[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1[r], w1[r], s[3], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) wpart[wave][q][r][lane] = s[q][r];
+  __syncthreads();
+  for (int e = tid; e < 1024; e += 256) {
+    const double* w0p = &wpart[0][0][0][0];
+    st_agent(&part[(int64_t)blockIdx.x * 1024 + e], (w0p[e] + w0p[1024 + e]) + (w0p[2048 + e] + w0p[3072 + e]));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    last = (__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) % CQ_G) == CQ_G - 1;
+  __syncthreads();
+  if (!last) return;
+  for (int e = tid; e < 1024; e += 256) {
+    double pv[CQ_G];
+#pragma unroll
+    for (int wg = 0; wg < CQ_G; ++wg) pv[wg] = ld_agent(&part[(int64_t)wg * 1024 + e]);
+    double v = 0.0;
+#pragma unroll
+    for (int wg = 0; wg < CQ_G; ++wg) v += pv[wg];
+    const int q = e >> 8, r = (e >> 6) & 3, l = e & 63;
+    H[(16 * (q >> 1) + (l >> 4) + 4 * r) * 32 + 16 * (q & 1) + (l & 15)] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_rr_resid32(const double* __restrict__ V, const double* __restrict__ W, int p,
                                                     const double* __restrict__ H, double* __restrict__ R,
                                                     double* __restrict__ part, unsigned* __restrict__ ticket,
@@ -2304,15 +2390,32 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
       mslot ^= 1;
       continue;
     }
-    if (fused && Mc) {  // the Rayleigh–Ritz basis: V = CholQR2 of the chain's block (Wc·Mc, then its factor)
-      hipLaunchKernelGGL(k_cq_gram32<true>, dim3(CQ_G), dim3(256), 0, st, Wc, p, Mc, Wc, cq_part, cq_ticket, 0,
+    bool basis_fused = false;
+    if (fused && Mc) {
+      // the Rayleigh–Ritz basis V = CholQR2 of the chain's block: T = Wc·Mc and
+      // its factor M2 (k_cq_gram32<true>) while a side stream forms C·Wc; then
+      // V = T·M2, W = C·V = (C·Wc)·(Mc·M2) and H = VᵀW in one launch
+      rc = eig_side_init(ctx);
+      if (rc) return rc;
+      hipStream_t sc = ctx->eig_side[1];
+      OCM_HIP(hipEventRecord(ctx->eig_ev[0], st));
+      OCM_HIP(hipStreamWaitEvent(sc, ctx->eig_ev[0], 0));
+      hipLaunchKernelGGL(k_cv32, dim3(2 * cv_rb), dim3(512), 0, sc, C, p, Wc, T2, cv_part, cv_ticket);
+      OCM_CHECK_LAUNCH("k_cv32 CWc");
+      OCM_HIP(hipEventRecord(ctx->eig_ev[4], sc));
+      hipLaunchKernelGGL(k_cq_gram32<true>, dim3(CQ_G), dim3(256), 0, st, Wc, p, Mc, T1, cq_part, cq_ticket, 0,
                          (uint64_t)(700 + it), cq_M);
       OCM_CHECK_LAUNCH("k_cq_gram32 rr");
-      hipLaunchKernelGGL(k_cq_apply32, dim3(CQ_G), dim3(256), 0, st, Wc, p, cq_M, V);
-      OCM_CHECK_LAUNCH("k_cq_apply32 rr");
+      OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[4], 0));
+      hipLaunchKernelGGL(k_rr_basis32, dim3(CQ_G), dim3(256), 0, st, T1, T2, p, Mc, cq_M, V, W, cq_part, cq_ticket,
+                         H);
+      OCM_CHECK_LAUNCH("k_rr_basis32");
       Mc = nullptr;
+      basis_fused = true;
     }
-    if (!wide && b == 32) {  // W = C V
+    if (basis_fused) {
+      // V, W and H are formed
+    } else if (!wide && b == 32) {  // W = C V
       hipLaunchKernelGGL(k_cv32, dim3(2 * cv_rb), dim3(512), 0, st, C, p, V, W, cv_part, cv_ticket);
       OCM_CHECK_LAUNCH("k_cv32");
     } else {
@@ -2337,8 +2440,10 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
       // (The eigenproblem of H on the host — implicit QL, ocm_hostla.h —
       // measured slower: ≈ 50–90 µs of QL plus two round trips against the
       // 135 µs Jacobi, profiles/r05m_eig_timeline.txt.)
-      hipLaunchKernelGGL(k_atb32, dim3(CQ_G), dim3(256), 0, st, V, W, p, cq_part, cq_ticket, H);
-      OCM_CHECK_LAUNCH("k_atb32 H");
+      if (!basis_fused) {
+        hipLaunchKernelGGL(k_atb32, dim3(CQ_G), dim3(256), 0, st, V, W, p, cq_part, cq_ticket, H);
+        OCM_CHECK_LAUNCH("k_atb32 H");
+      }
       // two side streams when θ is wanted: A deflates the block and runs
       // θ3; B forms R and S (the test waits for S), then C·R and G2
       hipStream_t sa = st, sb = st;
