@@ -462,7 +462,7 @@ __global__ __launch_bounds__(256) void k_gram_reduce(const float* __restrict__ p
       if (gi < p && gj < p && !(ti == tj && i > j)) {
         const double v = (s[0][q] + s[1][q]) + (s[2][q] + s[3][q]);
         G[(size_t)gi * p + gj] = v;
-        if (gi != gj) G[(size_t)gj * p + gi] = v;
+        if (gi != gj) G[(size_t)gj * p + gi] = v;  // (column-strided; skipping them measured no change, round 5)
       }
     }
   }
