@@ -300,12 +300,24 @@ def make_decision(type_name: str, t2_scale: float, q_scale: float, dlim: float) 
     return OcmDecision(TYPE_CODES[type_name], 0, float(t2_scale), float(q_scale), float(dlim))
 
 
+def score_outputs(X, m: int, k: int, want_T=False, want_T2=True, want_Q=True, want_stats=False) -> dict:
+    """The device tensors ``score`` writes (T and Q in the input dtype,
+    utils/SIMCA.py:65-71); allocated ahead when the launch is latency-critical."""
+    dev = X.device
+    vdt = torch.float64 if X.dtype == torch.float64 else torch.float32
+    return {"T": torch.empty((m, k), dtype=vdt, device=dev) if want_T else None,
+            "T2": torch.empty(m, dtype=torch.float64, device=dev) if want_T2 else None,
+            "Q": torch.empty(m, dtype=vdt, device=dev) if want_Q else None,
+            "stats": torch.empty(4, dtype=torch.float64, device=dev) if want_stats else None}
+
+
 def score(X: torch.Tensor, rows: torch.Tensor | None, m: int, P64: torch.Tensor, mean64: torch.Tensor,
           A: torch.Tensor, want_T=False, want_T2=True, want_Q=True, decision: OcmDecision | None = None,
-          accept_out: torch.Tensor | None = None, accept_stride: int = 1, want_stats=False):
+          accept_out: torch.Tensor | None = None, accept_stride: int = 1, want_stats=False, outs=None):
     """Fused scoring: P64 (k, p) f64 orthonormal rows, mean64 (p,) f64, A the
     (k, k) quadratic form (ocm_score_f32) or its diagonal (k,) (ocm_score_f32_diag,
-    the single-HBM-pass kernel for the SIMCA shapes).  Returns dict of device tensors."""
+    the single-HBM-pass kernel for the SIMCA shapes).  Returns dict of device tensors.
+    ``outs``: the outputs allocated beforehand (``score_outputs``)."""
     X = _plain(X)
     k, p = P64.shape
     dev = X.device
@@ -315,11 +327,9 @@ def score(X: torch.Tensor, rows: torch.Tensor | None, m: int, P64: torch.Tensor,
     f64 = X.dtype == torch.float64
     if f64 and A.dim() != 1:
         raise ValueError("float64 spectra are scored with a diagonal quadratic form (ocm_score_f64_diag)")
-    vdt = torch.float64 if f64 else torch.float32  # T and Q follow the input dtype (utils/SIMCA.py:65-71)
-    T = torch.empty((m, k), dtype=vdt, device=dev) if want_T else None
-    T2 = torch.empty(m, dtype=torch.float64, device=dev) if want_T2 else None
-    Q = torch.empty(m, dtype=vdt, device=dev) if want_Q else None
-    st = torch.empty(4, dtype=torch.float64, device=dev) if want_stats else None
+    if outs is None:
+        outs = score_outputs(X, m, k, want_T, want_T2, want_Q, want_stats)
+    T, T2, Q, st = outs["T"], outs["T2"], outs["Q"], outs["stats"]
     ctx = Context.get(dev.index)
     dec_p = ctypes.byref(decision) if decision is not None else None
     if isinstance(X, PrepView):  # the preprocessing runs on each row tile in registers
@@ -501,11 +511,12 @@ def _pinned(dev: torch.device, n: int) -> torch.Tensor:
     return buf[:n]
 
 
-def inv_evals(evals: torch.Tensor, rcond=1e-15) -> torch.Tensor:
+def inv_evals(evals: torch.Tensor, rcond=1e-15, out: torch.Tensor | None = None) -> torch.Tensor:
     """Diagonal of pinv(cov(T)) for T = centred scores on the eigenbasis:
     cov(T) = diag(λ) (utils/SIMCA.py:69 with np.linalg.pinv's rcond=1e-15 cutoff)."""
     lam = evals.to(torch.float64).contiguous()
-    out = torch.empty_like(lam)
+    if out is None:
+        out = torch.empty_like(lam)
     check(_lib.load().ocm_inv_evals_f64(Context.get(lam.device.index).handle, ptr(lam), lam.numel(), float(rcond),
                                         ptr(out), _stream(lam.device)), "ocm_inv_evals_f64")
     return out
@@ -618,6 +629,13 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
         _mark("cov")
         slice_ = (allreduce.rank, allreduce.world)
         n_total = None
+    # the fit-set outputs are allocated while the GPU still runs the Gram and the
+    # eigensolve: once the eigensolver has read its convergence test back, the
+    # launch queue is nearly empty and every host µs before the scoring launch
+    # is GPU idle time
+    pre = score_outputs(_plain(X), n, k, want_T, True, True, True) if n > 0 else None
+    inv = torch.empty(k, dtype=torch.float64, device=X.device)
+    eig_done = torch.cuda.Event()
     evals, evecs, theta, iters = eig_topk(C, k, theta_mode, theta3_slice=slice_)
     if n_total is None:
         n_total = int(round(float(packed[-1].item())))  # complete: the eigensolver synchronised
@@ -632,11 +650,10 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
     # scoring are launched first (every host µs before that launch is GPU idle
     # time), then λ and θ go to pinned memory on a side stream that waits only
     # for the eigensolve, and the limits overlap the scoring.
-    eig_done = torch.cuda.Event()
     eig_done.record(torch.cuda.current_stream(X.device))
-    inv = inv_evals(evals)
+    inv_evals(evals, out=inv)
     if n > 0:
-        sc = score(X, rows, n, evecs, mean64, inv, want_T=want_T, want_stats=True)
+        sc = score(X, rows, n, evecs, mean64, inv, want_T=want_T, want_stats=True, outs=pre)
     else:  # T and Q in the dtype the other ranks' scoring produces (utils/SIMCA.py:65-71)
         vdt = torch.float64 if X.dtype == torch.float64 else torch.float32
         sc = {"T": torch.empty((0, k), dtype=vdt, device=X.device) if want_T else None,
