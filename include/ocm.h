@@ -161,6 +161,13 @@ int ocm_eig_topk(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol
 int ocm_eig_topk_ex(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
                     int32_t theta_mode, int32_t theta3_slice, int32_t theta3_nslices, double* evals_out,
                     double* evecs_out, double* theta_out, int32_t* iters_out, void* stream);
+/* ocm_eig_topk_ex plus inv_out [dev] k = 1/λ with np.linalg.pinv's cutoff (|λ| ≤ rcond·max|λ| → 0), the
+ * diagonal of pinv(cov(T)) that ocm_inv_evals_f64 forms (utils/SIMCA.py:69), queued inside the call so the
+ * fit-set scoring can follow the eigensolve without another launch from the host. */
+int ocm_eig_topk_ex2(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
+                     int32_t theta_mode, int32_t theta3_slice, int32_t theta3_nslices, double* evals_out,
+                     double* evecs_out, double* theta_out, int32_t* iters_out, double rcond, double* inv_out,
+                     void* stream);
 
 /* ---- row-sharded fit: one all-reduce of packed moments ----
  * ocm_gram_pack turns a rank's shifted Gram (G, colsum about `shift`, n rows,

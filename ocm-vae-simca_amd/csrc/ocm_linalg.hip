@@ -2074,7 +2074,8 @@ int eig_side_init(ocm_ctx* ctx) {
 
 int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
                   int32_t theta_mode, int32_t slice, int32_t nslices, double* evals_out, double* evecs_out,
-                  double* theta_out, int32_t* iters_out, hipStream_t st) {
+                  double* theta_out, int32_t* iters_out, hipStream_t st, double* inv_out = nullptr,
+                  double rcond = 1e-15) {
   if (tol <= 0) tol = 1e-10;
   if (max_iter <= 0) max_iter = 2000;
 
@@ -2089,6 +2090,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     hipLaunchKernelGGL(k_small_finish, dim3(1), dim3(64), 0, st, ev, Z, p, k, evals_out, evecs_out,
                        theta_mode ? theta_out : nullptr);
     OCM_CHECK_LAUNCH("k_small_finish");
+    if (inv_out) hipLaunchKernelGGL(k_inv_evals, dim3(1), dim3(256), 0, st, evals_out, k, rcond, inv_out);
     if (theta_mode && slice != 0) OCM_HIP(hipMemsetAsync(theta_out + 2, 0, sizeof(double), st));
     if (iters_out) *iters_out = 1;
     return OCM_OK;
@@ -2494,6 +2496,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
       OCM_CHECK_LAUNCH("k_cq_apply32 ritz");
       hipLaunchKernelGGL(k_extract_signfix, dim3(k), dim3(256), 0, st, T1, p, b, k, evecs_out, theta, evals_out);
       OCM_CHECK_LAUNCH("k_extract_signfix");
+      if (inv_out) hipLaunchKernelGGL(k_inv_evals, dim3(1), dim3(256), 0, st, evals_out, k, rcond, inv_out);
       if (theta_mode) {  // (the deflation operands and the θ3 arena are reused by the next test too)
         OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[2], 0));
         hipLaunchKernelGGL(k_theta_combine, dim3(1), dim3(256), 0, st, theta, Z, S, L, tr3, b, k, slice == 0 ? 1 : 0,
@@ -2581,6 +2584,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   if (!extracted) {
     hipLaunchKernelGGL(k_extract_signfix, dim3(k), dim3(256), 0, st, V, p, b, k, evecs_out, theta, evals_out);
     OCM_CHECK_LAUNCH("k_extract_signfix");
+    if (inv_out) hipLaunchKernelGGL(k_inv_evals, dim3(1), dim3(256), 0, st, evals_out, k, rcond, inv_out);
   }
 
   if (theta_mode && !fused) {
@@ -2618,6 +2622,19 @@ int ocm_eig_topk_ex(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double 
               "ocm_eig_topk_ex: need 0 <= theta3_slice < theta3_nslices");
   return eig_topk_impl(ctx, C, p, k, tol, max_iter, theta_mode, theta3_slice, theta3_nslices, evals_out, evecs_out,
                        theta_out, iters_out, (hipStream_t)stream);
+}
+
+int ocm_eig_topk_ex2(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double tol, int32_t max_iter,
+                     int32_t theta_mode, int32_t theta3_slice, int32_t theta3_nslices, double* evals_out,
+                     double* evecs_out, double* theta_out, int32_t* iters_out, double rcond, double* inv_out,
+                     void* stream) {
+  OCM_REQUIRE(ctx && C && evals_out && evecs_out && inv_out, "ocm_eig_topk_ex2: NULL argument");
+  OCM_REQUIRE(p >= 1 && k >= 1 && k <= p, "ocm_eig_topk_ex2: need 1 <= k <= p");
+  OCM_REQUIRE(theta_mode == 0 || theta_out, "ocm_eig_topk_ex2: theta_out is NULL");
+  OCM_REQUIRE(theta3_nslices >= 1 && theta3_slice >= 0 && theta3_slice < theta3_nslices,
+              "ocm_eig_topk_ex2: need 0 <= theta3_slice < theta3_nslices");
+  return eig_topk_impl(ctx, C, p, k, tol, max_iter, theta_mode, theta3_slice, theta3_nslices, evals_out, evecs_out,
+                       theta_out, iters_out, (hipStream_t)stream, inv_out, rcond);
 }
 
 int ocm_inv_evals_f64(ocm_ctx* ctx, const double* evals, int32_t k, double rcond, double* out, void* stream) {

@@ -79,6 +79,8 @@ SIGNATURES = {
                              ctypes.POINTER(c_i32), c_void_p]),
     "ocm_eig_topk_ex": (c_i32, [c_void_p, c_void_p, c_i32, c_i32, c_f64, c_i32, c_i32, c_i32, c_i32, c_void_p,
                                 c_void_p, c_void_p, ctypes.POINTER(c_i32), c_void_p]),
+    "ocm_eig_topk_ex2": (c_i32, [c_void_p, c_void_p, c_i32, c_i32, c_f64, c_i32, c_i32, c_i32, c_i32, c_void_p,
+                                 c_void_p, c_void_p, ctypes.POINTER(c_i32), c_f64, c_void_p, c_void_p]),
     "ocm_gram_pack": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_i32, c_void_p, c_void_p]),
     "ocm_cov_from_packed": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_void_p, c_void_p]),
     "ocm_sym_pinv_f64": (c_i32, [c_void_p, c_void_p, c_i32, c_f64, c_void_p, c_void_p]),

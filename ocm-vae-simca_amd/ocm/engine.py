@@ -246,7 +246,7 @@ def eigh_dense(C: torch.Tensor, k: int = 0):
 
 
 def eig_topk(C: torch.Tensor, k: int, theta_mode: int, tol=EIG_TOL, max_iter=EIG_MAX_ITER, theta3_slice=(0, 1),
-             dense_fallback=True):
+             dense_fallback=True, inv_out: torch.Tensor | None = None, rcond=1e-15):
     """Top-k eigenpairs + tail moments of C (ocm_eig_topk_ex).  When the Ritz
     residuals miss ``tol`` within ``max_iter`` iterations (no usable spectral
     gap after component k: a flat noise floor), the loadings of the
@@ -255,7 +255,9 @@ def eig_topk(C: torch.Tensor, k: int, theta_mode: int, tol=EIG_TOL, max_iter=EIG
     reference's full SVD would (utils/SIMCA.py:64-66, 189-191), with a
     warning; ``dense_fallback=False`` raises ``OcmNotConverged`` instead.
     ``theta3_slice = (s, S)``: this call's share of the θ3 trace work (the
-    ranks of a sharded fit sum the partials)."""
+    ranks of a sharded fit sum the partials).  ``inv_out`` (k,): also 1/λ
+    with pinv's cutoff (``inv_evals``), queued inside the call
+    (ocm_eig_topk_ex2)."""
     p = C.shape[0]
     dev = C.device
     evals = torch.empty(k, dtype=torch.float64, device=dev)
@@ -263,9 +265,14 @@ def eig_topk(C: torch.Tensor, k: int, theta_mode: int, tol=EIG_TOL, max_iter=EIG
     theta = torch.zeros(3, dtype=torch.float64, device=dev)
     iters = ctypes.c_int32(0)
     ctx = Context.get(dev.index)
-    rc = _lib.load().ocm_eig_topk_ex(ctx.handle, ptr(C), p, k, tol, max_iter, theta_mode, int(theta3_slice[0]),
-                                     int(theta3_slice[1]), ptr(evals), ptr(evecs), ptr(theta), ctypes.byref(iters),
-                                     _stream(dev))
+    if inv_out is not None:
+        rc = _lib.load().ocm_eig_topk_ex2(ctx.handle, ptr(C), p, k, tol, max_iter, theta_mode, int(theta3_slice[0]),
+                                          int(theta3_slice[1]), ptr(evals), ptr(evecs), ptr(theta),
+                                          ctypes.byref(iters), float(rcond), ptr(inv_out), _stream(dev))
+    else:
+        rc = _lib.load().ocm_eig_topk_ex(ctx.handle, ptr(C), p, k, tol, max_iter, theta_mode, int(theta3_slice[0]),
+                                         int(theta3_slice[1]), ptr(evals), ptr(evecs), ptr(theta),
+                                         ctypes.byref(iters), _stream(dev))
     if rc == _lib.OCM_ERR_NOCONV:
         msg = (f"ocm_eig_topk: the leading {k} eigenpairs of the {p}x{p} covariance did not converge to tol={tol} "
                f"in {max_iter} iterations (no usable spectral gap after component {k})")
@@ -282,7 +289,10 @@ def eig_topk(C: torch.Tensor, k: int, theta_mode: int, tol=EIG_TOL, max_iter=EIG
             th[1] = (tail * tail).sum()
         if theta_mode >= 2 and theta3_slice[0] == 0:  # the whole θ3 on slice 0 (the ranks sum the slices)
             th[2] = (tail * tail * tail).sum()
-        return lam[:k].clone(), vec, th, int(max_iter)
+        top = lam[:k].clone()
+        if inv_out is not None:
+            inv_evals(top, rcond, out=inv_out)
+        return top, vec, th, int(max_iter)
     check(rc, "ocm_eig_topk_ex")
     return evals, evecs, theta, int(iters.value)
 
@@ -636,7 +646,7 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
     pre = score_outputs(_plain(X), n, k, want_T, True, True, True) if n > 0 else None
     inv = torch.empty(k, dtype=torch.float64, device=X.device)
     eig_done = torch.cuda.Event()
-    evals, evecs, theta, iters = eig_topk(C, k, theta_mode, theta3_slice=slice_)
+    evals, evecs, theta, iters = eig_topk(C, k, theta_mode, theta3_slice=slice_, inv_out=inv)
     if n_total is None:
         n_total = int(round(float(packed[-1].item())))  # complete: the eigensolver synchronised
         if n_total < 2:
@@ -650,8 +660,7 @@ def fit_class(X: torch.Tensor, rows: torch.Tensor | None, n: int, k: int, theta_
     # scoring are launched first (every host µs before that launch is GPU idle
     # time), then λ and θ go to pinned memory on a side stream that waits only
     # for the eigensolve, and the limits overlap the scoring.
-    eig_done.record(torch.cuda.current_stream(X.device))
-    inv_evals(evals, out=inv)
+    eig_done.record(torch.cuda.current_stream(X.device))  # (1/λ was queued inside the eigensolve)
     if n > 0:
         sc = score(X, rows, n, evecs, mean64, inv, want_T=want_T, want_stats=True, outs=pre)
     else:  # T and Q in the dtype the other ranks' scoring produces (utils/SIMCA.py:65-71)
