@@ -523,22 +523,58 @@ __global__ __launch_bounds__(64 * WV, 1) void k_score_1p(const float* __restrict
   const int ln = lane & 15, lq = lane >> 4;
 
   // ---- prologue: loadings (f64 → f32) and −μ into LDS, P·μ (fp64), comps
-  // 16..19 and diag(A) into registers
-  for (int e = tid; e < 16 * NCH; e += NT) {
-    const int c = e / NCH, ch = e - c * NCH;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (c < k)
+  // 16..19 and diag(A) into registers.  Every load is unconditional (rows
+  // c ≥ k clamped to row 0, zeroed by a select after the load) and issued in
+  // batches ahead of its use: with per-element branches each load was waited
+  // for before the next issued — ≈220 L2 round trips per workgroup, 40 µs of
+  // every launch (profiles/r05s1_score_prologue_ab.jsonl)
+  {
+    constexpr int PE = 16 * NCH / NT;  // chunks per thread (= NJ)
+    constexpr int UB = PE < 8 ? PE : 8;
+    static_assert(PE % UB == 0, "prologue batches");
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = (float)P[(int64_t)c * PP + 4 * ch + u];
-    P0s[c * NCH + (ch ^ sw(c))] = v;
-  }
-  for (int c = tid; c < PP; c += NT) nmuL[c] = -(float)mu[c];
-  for (int c = w; c < 20; c += W) {  // wave w: comps w, w + 4, ...
-    double s = 0.0;
-    if (c < k)
-      for (int col = lane; col < PP; col += 64) s += P[(int64_t)c * PP + col] * mu[col];
-    s = wave_sum_f64(s);
-    if (lane == 0) pmuL[c] = s;
+    for (int i0 = 0; i0 < PE; i0 += UB) {
+      double v[UB][4];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int e = tid + (i0 + u) * NT, c = e / NCH, ch = e - c * NCH;
+        const double* src = P + (int64_t)(c < k ? c : 0) * PP + 4 * ch;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[u][q] = src[q];
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int e = tid + (i0 + u) * NT, c = e / NCH, ch = e - c * NCH;
+        f32x4 x;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = c < k ? (float)v[u][q] : 0.f;
+        P0s[c * NCH + (ch ^ sw(c))] = x;
+      }
+    }
+    constexpr int ME = PP / NT;  // −μ entries per thread
+    float nm[ME];
+#pragma unroll
+    for (int i = 0; i < ME; ++i) nm[i] = -(float)mu[tid + i * NT];
+#pragma unroll
+    for (int i = 0; i < ME; ++i) nmuL[tid + i * NT] = nm[i];
+    // P·μ: lane l sums columns l, l + 64, ... in that order (fma chain), then
+    // the wave sum; μ's lane columns loaded once for the wave's comps
+    constexpr int CL = PP / 64;
+    double muv[CL];
+#pragma unroll
+    for (int i = 0; i < CL; ++i) muv[i] = mu[lane + 64 * i];
+    for (int c = w; c < 20; c += W) {  // wave w: comps w, w + W, ...
+      double s = 0.0;
+      if (c < k) {
+        double pv[CL];
+#pragma unroll
+        for (int i = 0; i < CL; ++i) pv[i] = P[(int64_t)c * PP + lane + 64 * i];
+#pragma unroll
+        for (int i = 0; i < CL; ++i) s += pv[i] * muv[i];
+      }
+      s = wave_sum_f64(s);
+      if (lane == 0) pmuL[c] = s;
+    }
   }
   float p1a[EX ? NJ : 1];  // comps 16..19: lane (ln, lq) holds P[16 + lq][w·PW + 16j + ln] (sweep 2)
   // the same values with the column of lanes lq ≥ 2 XOR 8 (lane (x, c) holds
@@ -552,13 +588,21 @@ __global__ __launch_bounds__(64 * WV, 1) void k_score_1p(const float* __restrict
   // the 2-way conflicts back — round 3 measured them at no cost in time)
   constexpr bool NOP1B = EX && ((NJ == 32 && HH > 4) || WV == 8);  // WV = 8: no registers to spare either
   float p1b[EX && !NOP1B ? NJ : 1];
-  if constexpr (EX)
+  if constexpr (EX) {
+    const bool p1v = 16 + lq < k;  // rows ≥ k: row 0 loaded, zeroed after
+    const double* p1r = P + (int64_t)(p1v ? 16 + lq : 0) * PP + w * PW;
+    double pa_[NJ], pb_[NOP1B ? 1 : NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int64_t rowp = (int64_t)(16 + lq) * PP + w * PW + 16 * j;
-      p1a[j] = 16 + lq < k ? (float)P[rowp + ln] : 0.f;
-      if constexpr (!NOP1B) p1b[j] = 16 + lq < k ? (float)P[rowp + (ln ^ (8 * (lq >> 1)))] : 0.f;
+      pa_[j] = p1r[16 * j + ln];
+      if constexpr (!NOP1B) pb_[j] = p1r[16 * j + (ln ^ (8 * (lq >> 1)))];
     }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      p1a[j] = p1v ? (float)pa_[j] : 0.f;
+      if constexpr (!NOP1B) p1b[j] = p1v ? (float)pb_[j] : 0.f;
+    }
+  }
   // diag(A) of this lane's comps lq + 4s: registers at WV = 4, LDS at WV = 8
   // (read once per tile, in compute_t; the registers went to the tiles)
   __shared__ double adL[WV == 8 ? 20 : 1];
