@@ -97,6 +97,7 @@ int ocm_ctx_destroy(ocm_ctx* ctx) {
     if (s) (void)hipStreamDestroy(s);
   for (auto e : ctx->eig_ev)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->eig_flag) (void)hipFree(ctx->eig_flag);
   for (auto& v : ctx->ev)
     for (auto& pr : v) ctx->ev_pool.push_back(pr);
   for (auto& pr : ctx->ev_pool) {

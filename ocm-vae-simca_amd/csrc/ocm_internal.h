@@ -35,6 +35,10 @@ struct ocm_ctx {
   hipStream_t eig_side[2] = {nullptr, nullptr};
   hipEvent_t eig_ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   ocm_ctx* eig_sub = nullptr;
+  // the Rayleigh–Ritz test's in-flight hand-off (k_rr_resid32 → k_jacobi_1b):
+  // a device counter raised to eig_epoch when S is stored; it only grows
+  unsigned* eig_flag = nullptr;
+  unsigned eig_epoch = 0;
 };
 
 namespace ocm {

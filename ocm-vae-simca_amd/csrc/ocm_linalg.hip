@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void k_dgemm(const double* __restrict__ A, int
 // thread's 16 elements of E (C) for the epilogue — so one memory latency
 // covers the workgroup instead of one per K-step plus one for E; the K-steps
 // then run from registers through LDS.  Same outputs as k_dgemm<3>.
-__global__ __launch_bounds__(256) void k_deflate64(const double* __restrict__ A, int64_t lda,
+__global__ __launch_bounds__(256, 4) void k_deflate64(const double* __restrict__ A, int64_t lda,
                                                    const double* __restrict__ B, int64_t ldb,
                                                    double* __restrict__ D, int M, int N, int K,
                                                    const double* __restrict__ E, int64_t lde,
@@ -222,17 +222,11 @@ __global__ __launch_bounds__(256) void k_deflate64(const double* __restrict__ A,
   const int m0 = blockIdx.x * DT, n0 = blockIdx.y * DT;
   const int arow = tid >> 2, akc = (tid & 3) * 4;
   const int bk = tid >> 4, bcol = (tid & 15) * 4;
+  // E's 16 elements are loaded after the K-steps: preloaded, they held the
+  // kernel at 2 workgroups per CU (216 registers), two rounds of workgroups
+  // for the 1024 tiles at p = 2048 and no room for the Jacobi workgroup that
+  // runs beside it (r05s5); at ≤ 128 it is 4 per CU, one round
   double ev[2][2][4];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 32 + a * 16 + (lane >> 4) + 4 * r;
-        const int col = n0 + wn * 32 + b * 16 + (lane & 15);
-        ev[a][b][r] = (row < M && col < N) ? E[(int64_t)row * lde + col] : 0.0;
-      }
   double ra[NS][4], rb[NS][4];
 #pragma unroll
   for (int st = 0; st < NS; ++st)
@@ -271,6 +265,16 @@ __global__ __launch_bounds__(256) void k_deflate64(const double* __restrict__ A,
     }
     __syncthreads();
   }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + a * 16 + (lane >> 4) + 4 * r;
+        const int col = n0 + wn * 32 + b * 16 + (lane & 15);
+        ev[a][b][r] = (row < M && col < N) ? E[(int64_t)row * lde + col] : 0.0;
+      }
   double tr = 0.0, fro = 0.0;
   double rs[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
 #pragma unroll
@@ -700,6 +704,176 @@ __global__ __launch_bounds__(256) void k_jacobi_blk(const double* __restrict__ A
     for (int r = 0; r < NF; ++r) Zout[r * NF + rank] = Z[cur][r][i];
   }
   if (tid == 0 && sweeps_out) *sweeps_out = sweep;
+}
+
+// ---------------------------------------------------------------------------
+// The 32×32 block Jacobi with ONE barrier per round (the RR eigensolve's
+// serial step).  k_jacobi_blk's round was: 16 threads compute the rotations →
+// LDS → barrier → block update → barrier.  Here every updating thread computes
+// the (one or two) rotations it applies itself, from the round's 2×2 diagonal
+// blocks (broadcast LDS reads), so the rotations' LDS hand-off and its barrier
+// go; the ping-pong buffers make the remaining barrier the only one.  Threads
+// 0..135: the 136 2×2 blocks (k ≤ l) of A; threads 192..319: Z ← Z J, pair
+// l = t & 15 on rows t/16 + 8i.  The rotation: t = tan φ from the fast
+// (unrefined) v_rsq / v_rcp — t only decides how well a_pq is annihilated —
+// and c = 1/√(1 + t²) refined, s = t·c, so c² + s² = 1 to rounding: every
+// rotation stays orthogonal and A's spectrum is untouched.  The rotated
+// pair's off-diagonal is therefore computed, not set to zero (its remainder,
+// ~1e-7·a_pq, is taken by the later rounds).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void jrot_fast(double app, double aqq, double apq, double& c, double& s) {
+  const double d = aqq - app, e = 2.0 * apq;
+  const double h = fma(d, d, e * e);
+  c = 1.0;
+  s = 0.0;
+  if (apq != 0.0 && h > 0.0) {
+    const double u = fabs(d) + h * __builtin_amdgcn_rsq(h);     // |d| + √(d² + e²), approximately
+    const double t = (d >= 0.0 ? e : -e) * __builtin_amdgcn_rcp(u);  // |t| ≤ 1
+    c = rsqrt(fma(t, t, 1.0));
+    s = t * c;
+  }
+}
+
+// S (optional): the Rayleigh–Ritz test fused at the end — the former k_rr_test32's
+// res[i] = √max(z_iᵀ S z_i, 0) for the first k Ritz pairs, the same sums in
+// the same order — with S taken in flight from k_rr_resid32 on another
+// stream once *sflag reaches epoch (a bounded wait: ≈ 1 s, then NaN
+// residuals, which the host reports as an error instead of hanging)
+template <int NF>
+__global__ __launch_bounds__(320) void k_jacobi_1b(const double* __restrict__ Ain, int max_sweeps,
+                                                   double* __restrict__ evals, double* __restrict__ Zout,
+                                                   int* __restrict__ sweeps_out, const double* __restrict__ S,
+                                                   const unsigned* __restrict__ sflag, unsigned epoch, int ktest,
+                                                   double* __restrict__ res) {
+  static_assert(NF == 32, "thread map for 32×32");
+  constexpr int H = NF / 2, NB = H * (H + 1) / 2, LD = NF + 1, NT = 320, ZT0 = 192;
+  __shared__ double A[2][NF][LD];
+  __shared__ double Z[2][NF][LD];
+  __shared__ double wsum[10];
+  __shared__ int done;
+  const int tid = threadIdx.x;
+  // the top issue priority: this one workgroup shares its CU with the θ3
+  // chain's (deflation, quantiser, Gram) waves, which took ≈ 20 % of its issue
+  // slots (128 against 107 µs alone, r05s4)
+  __builtin_amdgcn_s_setprio(3);
+  for (int e = tid; e < NF * NF; e += NT) {
+    const int i = e / NF, j = e % NF;
+    A[0][i][j] = 0.5 * (Ain[i * NF + j] + Ain[j * NF + i]);
+    Z[0][i][j] = (i == j) ? 1.0 : 0.0;
+  }
+  // this thread's block (k, l), k ≤ l (row-major over the upper triangle), or Z pair
+  int k = 0, l = 0;
+  if (tid < NB) {
+    int b = tid;
+    while (b >= H - k) {
+      b -= H - k;
+      ++k;
+    }
+    l = k + b;
+  } else if (tid >= ZT0) {
+    l = (tid - ZT0) & (H - 1);
+  }
+  const int p = 2 * k, q = p + 1, u = 2 * l, v = u + 1;
+  const int dp = jdest<NF>(p), dq = jdest<NF>(q), du = jdest<NF>(u), dv = jdest<NF>(v);
+  const int zr = (tid - ZT0) >> 4;  // Z rows zr + 8i
+  __syncthreads();
+  int cur = 0, sweep = 0;
+  for (; sweep < max_sweeps; ++sweep) {
+    double off = 0.0, dg = 0.0;
+    for (int e = tid; e < NF * NF; e += NT) {
+      const int i = e / NF, j = e % NF;
+      const double x = A[cur][i][j] * A[cur][i][j];
+      if (i == j) dg += x; else off += x;
+    }
+    off = wave_sum_f64(off);
+    dg = wave_sum_f64(dg);
+    if ((tid & 63) == 0) {
+      wsum[tid >> 6] = off;
+      wsum[5 + (tid >> 6)] = dg;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const double o = ((wsum[0] + wsum[1]) + (wsum[2] + wsum[3])) + wsum[4];
+      const double d = ((wsum[5] + wsum[6]) + (wsum[7] + wsum[8])) + wsum[9];
+      done = (o <= OCM_JACOBI_TOL2 * d) || (o == 0.0);
+    }
+    __syncthreads();
+    if (done) break;
+    for (int round = 0; round < NF - 1; ++round) {
+      const int nx = cur ^ 1;
+      if (tid < NB) {
+        double ck, sk, cl, sl;
+        jrot_fast(A[cur][p][p], A[cur][q][q], A[cur][p][q], ck, sk);
+        jrot_fast(A[cur][u][u], A[cur][v][v], A[cur][u][v], cl, sl);
+        const double a00 = A[cur][p][u], a01 = A[cur][p][v], a10 = A[cur][q][u], a11 = A[cur][q][v];
+        const double b00 = ck * a00 - sk * a10, b01 = ck * a01 - sk * a11;
+        const double b10 = sk * a00 + ck * a10, b11 = sk * a01 + ck * a11;
+        const double o00 = cl * b00 - sl * b01, o01 = sl * b00 + cl * b01;
+        const double o10 = cl * b10 - sl * b11, o11 = sl * b10 + cl * b11;
+        A[nx][dp][du] = o00;
+        A[nx][dp][dv] = o01;
+        A[nx][dq][du] = o10;
+        A[nx][dq][dv] = o11;
+        if (k != l) {
+          A[nx][du][dp] = o00;
+          A[nx][dv][dp] = o01;
+          A[nx][du][dq] = o10;
+          A[nx][dv][dq] = o11;
+        }
+      } else if (tid >= ZT0) {
+        double cl, sl;
+        jrot_fast(A[cur][u][u], A[cur][v][v], A[cur][u][v], cl, sl);
+#pragma unroll
+        for (int i = 0; i < NF / 8; ++i) {
+          const int r = zr + 8 * i;
+          const double zp = Z[cur][r][u], zq = Z[cur][r][v];
+          Z[nx][r][du] = cl * zp - sl * zq;
+          Z[nx][r][dv] = sl * zp + cl * zq;
+        }
+      }
+      __syncthreads();
+      cur = nx;
+    }
+  }
+  int myrank = NF;
+  for (int i = tid; i < NF; i += NT) {
+    const double li = A[cur][i][i];
+    int rank = 0;
+    for (int j = 0; j < NF; ++j) {
+      const double lj = A[cur][j][j];
+      rank += (lj > li) || (lj == li && j < i);
+    }
+    evals[rank] = li;
+    for (int r = 0; r < NF; ++r) Zout[r * NF + rank] = Z[cur][r][i];
+    myrank = rank;
+  }
+  if (tid == 0 && sweeps_out) *sweeps_out = sweep;
+  if (!S) return;
+  const int nx = cur ^ 1;  // free buffers: S into A[nx], S·Z into Z[nx]
+  if (tid == 0) {
+    unsigned n = 0;
+    while ((int)(__hip_atomic_load(const_cast<unsigned*>(sflag), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - epoch) < 0 &&
+           ++n < (1u << 22))
+      __builtin_amdgcn_s_sleep(8);
+    done = n < (1u << 22);
+  }
+  __syncthreads();
+  for (int e = tid; e < NF * NF; e += NT) A[nx][e / NF][e % NF] = ld_agent(S + e);
+  __syncthreads();
+  for (int e = tid; e < NF * NF; e += NT) {
+    const int r = e / NF, i = e % NF;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int j = 0; j < NF; ++j) acc = fma(A[nx][r][j], Z[cur][j][i], acc);
+    Z[nx][r][i] = acc;
+  }
+  __syncthreads();
+  if (tid < NF && myrank < ktest) {
+    double acc = 0.0;
+#pragma unroll 8
+    for (int r = 0; r < NF; ++r) acc = fma(Z[cur][r][tid], Z[nx][r][tid], acc);
+    res[myrank] = done ? sqrt(fmax(acc, 0.0)) : __builtin_nan("");
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1460,10 +1634,12 @@ __global__ __launch_bounds__(256) void k_colnormalize(double* __restrict__ W, in
 //                  workgroups, the last to finish sums the partials in order
 //                  (H = VᵀW, and G2 = Rᵀ(C·R) for θ3);
 //   k_rr_resid32   R = W − V·H (the projection residual, stored) and
-//                  S = RᵀR (same hand-off);
-//   k_rr_test32    the Ritz residuals ‖C v_i − θ_i v_i‖ = ‖R z_i‖ =
-//                  √(z_iᵀ S z_i) of the top-k pairs from the Jacobi output —
-//                  no rotated block is formed for the convergence test;
+//                  S = RᵀR (same hand-off; S stored write-through and a
+//                  counter raised after it);
+//   k_jacobi_1b    the Jacobi on H and, at its end, the Ritz residuals
+//                  ‖C v_i − θ_i v_i‖ = ‖R z_i‖ = √(z_iᵀ S z_i) of the top-k
+//                  pairs (S taken in flight once the counter is up) — no
+//                  rotated block is formed for the convergence test;
 //   k_theta_combine θ1..θ3 of the deflated matrix (I − P_k)C(I − P_k) from the
 //                  b-block deflation Ct_b = (I − P_b)C(I − P_b) (traces,
 //                  computed beside the Jacobi on side streams) plus the
@@ -1617,10 +1793,13 @@ __global__ __launch_bounds__(256) void k_rr_basis32(const double* __restrict__ T
   }
 }
 
+// sflag (optional): S is stored write-through and the counter raised to
+// epoch (release) after it — k_jacobi_1b's test reads S in flight
 __global__ __launch_bounds__(256) void k_rr_resid32(const double* __restrict__ V, const double* __restrict__ W, int p,
                                                     const double* __restrict__ H, double* __restrict__ R,
                                                     double* __restrict__ part, unsigned* __restrict__ ticket,
-                                                    double* __restrict__ S) {
+                                                    double* __restrict__ S, unsigned* __restrict__ sflag = nullptr,
+                                                    unsigned epoch = 0) {
   __shared__ double wpart[4][3][4][64];
   __shared__ double sm[32][33];
   __shared__ int last;
@@ -1681,9 +1860,13 @@ __global__ __launch_bounds__(256) void k_rr_resid32(const double* __restrict__ V
     for (int wg = 0; wg < CQ_G; ++wg) v += pv[wg];
     const int blk = e >> 8, r = (e >> 6) & 3, l = e & 63;
     const int row = 16 * (blk == 2) + (l >> 4) + 4 * r, col = 16 * (blk != 0) + (l & 15);
-    S[row * 32 + col] = v;
-    if (blk == 1) S[col * 32 + row] = v;
+    st_agent(&S[row * 32 + col], v);
+    if (blk == 1) st_agent(&S[col * 32 + row], v);
   }
+  if (!sflag) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(sflag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // q[i] = z_iᵀ M z_i for the 32 columns z_i of Z (32×32, column i = vector i):
@@ -1709,17 +1892,6 @@ __device__ __forceinline__ void quad_forms32(const double* __restrict__ M, doubl
     q[tid] = acc;
   }
   __syncthreads();
-}
-
-// res[i] = √max(z_iᵀ S z_i, 0) for i < k (b = 32, one workgroup)
-__global__ __launch_bounds__(256) void k_rr_test32(const double* __restrict__ S, const double* __restrict__ Z, int b,
-                                                   int k, double* __restrict__ res) {
-  __shared__ double sz[32][33], sy[32][33], smm[32][33];
-  __shared__ double q[32];
-  for (int e = threadIdx.x; e < 1024; e += 256) sz[e >> 5][e & 31] = Z[e];
-  quad_forms32(S, sz, sy, smm, q);
-  if (threadIdx.x < k) res[threadIdx.x] = sqrt(fmax(q[threadIdx.x], 0.0));
-  (void)b;
 }
 
 // tr3[0..2] = tr Ct_b, ‖Ct_b‖², tr Ct_b³ (this slice's part); θ3 corrections
@@ -1771,13 +1943,31 @@ __global__ __launch_bounds__(256) void k_ritz_residual(const double* __restrict_
 
 // evecs[i][j] = s_i · V[j][i] with s_i making the max-|entry| of row i positive
 // (sklearn svd_flip(u_based_decision=False), first index on ties like argmax).
+// inv_out (optional, with theta): workgroup 0 also writes k_inv_evals' 1/λ
+// of the k values (the same cutoff and values; one launch less on the
+// Rayleigh–Ritz tail)
 __global__ __launch_bounds__(256) void k_extract_signfix(const double* __restrict__ V, int p, int b, int k,
                                                          double* __restrict__ evecs,
                                                          const double* __restrict__ theta = nullptr,
-                                                         double* __restrict__ evals = nullptr) {
+                                                         double* __restrict__ evals = nullptr, double rcond = 0.0,
+                                                         double* __restrict__ inv_out = nullptr) {
   if (evals && threadIdx.x == 0) evals[blockIdx.x] = theta[blockIdx.x];  // λ_i (no separate copy)
   __shared__ double bv[256];
   __shared__ int bi[256];
+  if (inv_out && blockIdx.x == 0) {
+    double mx = 0.0;
+    for (int i = threadIdx.x; i < k; i += 256) mx = fmax(mx, fabs(theta[i]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if ((threadIdx.x & 63) == 0) bv[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    const double cut = rcond * fmax(fmax(bv[0], bv[1]), fmax(bv[2], bv[3]));
+    for (int i = threadIdx.x; i < k; i += 256) {
+      const double l = theta[i];
+      inv_out[i] = fabs(l) > cut ? 1.0 / l : 0.0;
+    }
+    __syncthreads();  // bv is reused below
+  }
   const int i = blockIdx.x;
   double best = -1.0;
   int bidx = 0x7fffffff;
@@ -1934,14 +2124,16 @@ int dgemm(const double* A, int64_t lda, const double* B, int64_t ldb, double* D,
   return OCM_OK;
 }
 
-int jacobi(const double* A, int n, int max_sweeps, double* ev, double* Z, hipStream_t st) {
+int jacobi(const double* A, int n, int max_sweeps, double* ev, double* Z, hipStream_t st, const double* S = nullptr,
+           const unsigned* sflag = nullptr, unsigned epoch = 0, int k = 0, double* res = nullptr) {
   // n = 32: the block kernel (0.95 ms per fit against 1.19 with the one-wave k_jacobi<32, 64>, r03z; the
   // same block rounds in one wave without barriers, round 5: 204 against 122–140 µs, r05s_eig_timeline.txt)
 #ifdef OCM_JACOBI_SWEEPS  // make exp diagnostic: print the sweep count of each 32×32 solve
   if (n == 32) {
     static int* dsw = nullptr;
     if (!dsw) (void)hipMalloc(reinterpret_cast<void**>(&dsw), sizeof(int));
-    hipLaunchKernelGGL(k_jacobi_blk<32>, dim3(1), dim3(256), 0, st, A, max_sweeps, ev, Z, dsw);
+    hipLaunchKernelGGL(k_jacobi_1b<32>, dim3(1), dim3(320), 0, st, A, max_sweeps, ev, Z, dsw, S, sflag, epoch, k,
+                       res);
     int hsw = -1;
     (void)hipMemcpyAsync(&hsw, dsw, sizeof(int), hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
@@ -1950,7 +2142,8 @@ int jacobi(const double* A, int n, int max_sweeps, double* ev, double* Z, hipStr
   }
 #endif
   if (n == 32)
-    hipLaunchKernelGGL(k_jacobi_blk<32>, dim3(1), dim3(256), 0, st, A, max_sweeps, ev, Z, nullptr);
+    hipLaunchKernelGGL(k_jacobi_1b<32>, dim3(1), dim3(320), 0, st, A, max_sweeps, ev, Z, nullptr, S, sflag, epoch, k,
+                       res);
   else if (n == 48)
     hipLaunchKernelGGL(k_jacobi_blk<48>, dim3(1), dim3(256), 0, st, A, max_sweeps, ev, Z, nullptr);
   else if (n == 64)
@@ -2065,6 +2258,9 @@ int eig_side_init(ocm_ctx* ctx) {
   if (ctx->eig_sub) return OCM_OK;
   for (auto& s : ctx->eig_side) OCM_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   for (auto& e : ctx->eig_ev) OCM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  OCM_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->eig_flag), sizeof(unsigned)));
+  OCM_HIP(hipMemset(ctx->eig_flag, 0, sizeof(unsigned)));
+  ctx->eig_epoch = 0;
   auto* sub = new ocm_ctx();
   sub->device = ctx->device;
   sub->num_cus = ctx->num_cus;
@@ -2439,7 +2635,7 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
     if (fused) {
       // Rayleigh–Ritz on the unrotated block: H = VᵀW, the projection
       // residual R = W − V·H and S = RᵀR, Jacobi on H; the test reads
-      // ‖R z_i‖ (k_rr_test32).  With θ wanted, R/S, C·R, G2 = Rᵀ(C·R) and the
+      // ‖R z_i‖ (at the Jacobi's end).  With θ wanted, R/S, C·R, G2 = Rᵀ(C·R) and the
       // deflation of the whole block run on side streams beside the Jacobi
       // (they need no Ritz rotation: k_theta_combine adds its terms later).
       // (The eigenproblem of H on the host — implicit QL, ocm_hostla.h —
@@ -2449,24 +2645,29 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
         hipLaunchKernelGGL(k_atb32, dim3(CQ_G), dim3(256), 0, st, V, W, p, cq_part, cq_ticket, H);
         OCM_CHECK_LAUNCH("k_atb32 H");
       }
-      // two side streams when θ is wanted: A deflates the block and runs
-      // θ3; B forms R and S (the test waits for S), then C·R and G2
-      hipStream_t sa = st, sb = st;
+      // two side streams when θ is wanted: J runs the Jacobi, the test and the
+      // speculative outputs; B forms R and S (the test waits for S), then C·R
+      // and G2; the launch stream deflates the block and runs θ3 — the
+      // longest chain (≈ 180 µs against the Jacobi path's ≈ 160), so it
+      // starts without a cross-stream hand-off (≈ 20 µs each, r05s3)
+      hipStream_t sj = st, sb = st;
       rc = eig_side_init(ctx);  // the streams and events (the test's read-back event too)
       if (rc) return rc;
       if (theta_mode) {
-        sa = ctx->eig_side[0];
+        sj = ctx->eig_side[0];
         sb = ctx->eig_side[1];
         OCM_HIP(hipEventRecord(ctx->eig_ev[0], st));
-        OCM_HIP(hipStreamWaitEvent(sa, ctx->eig_ev[0], 0));
+        OCM_HIP(hipStreamWaitEvent(sj, ctx->eig_ev[0], 0));
         OCM_HIP(hipStreamWaitEvent(sb, ctx->eig_ev[0], 0));
       }
       double* R = T1;
       double* CR = T2;
-      hipLaunchKernelGGL(k_rr_resid32, dim3(CQ_G), dim3(256), 0, sb, V, W, p, H, R, cq_part, cq_ticket, S);
+      // S reaches the Jacobi's fused test in flight (ctx->eig_flag)
+      const unsigned epoch = ++ctx->eig_epoch;
+      hipLaunchKernelGGL(k_rr_resid32, dim3(CQ_G), dim3(256), 0, sb, V, W, p, H, R, cq_part, cq_ticket, S,
+                         ctx->eig_flag, epoch);
       OCM_CHECK_LAUNCH("k_rr_resid32");
       if (theta_mode) {
-        OCM_HIP(hipEventRecord(ctx->eig_ev[1], sb));
         hipLaunchKernelGGL(k_cv32, dim3(2 * cv_rb), dim3(512), 0, sb, C, p, R, CR, cv_part, cv_ticket);
         OCM_CHECK_LAUNCH("k_cv32 CR");
         if (theta_mode >= 2) {
@@ -2475,29 +2676,29 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
         }
         OCM_HIP(hipEventRecord(ctx->eig_ev[3], sb));
         // after B's test inputs: theta_into queues its Δ terms on B too
-        rc = theta_into(V, W, H, b, sa, sb, ctx->eig_sub, tr3);
+        rc = theta_into(V, W, H, b, st, sb, ctx->eig_sub, tr3);
         if (rc) return rc;
-        OCM_HIP(hipEventRecord(ctx->eig_ev[2], sa));
       }
-      rc = jacobi(H, b, 40, theta, Z, st);
+      // the Jacobi and the test in one launch (the former k_rr_test32's sums)
+      rc = jacobi(H, b, 40, theta, Z, sj, S, ctx->eig_flag, epoch, k, res);
       if (rc) return rc;
-      if (theta_mode) OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[1], 0));
-      hipLaunchKernelGGL(k_rr_test32, dim3(1), dim3(256), 0, st, S, Z, b, k, res);
-      OCM_CHECK_LAUNCH("k_rr_test32");
-      OCM_HIP(hipMemcpyAsync(hres, theta, 2 * (size_t)b * sizeof(double), hipMemcpyDeviceToHost, st));
-      OCM_HIP(hipEventRecord(ctx->eig_ev[6], st));
+      OCM_HIP(hipMemcpyAsync(hres, theta, 2 * (size_t)b * sizeof(double), hipMemcpyDeviceToHost, sj));
+      OCM_HIP(hipEventRecord(ctx->eig_ev[6], sj));
       // R (= T1) and CR are reused below: side stream B is done with them
-      if (theta_mode) OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[3], 0));
+      if (theta_mode) OCM_HIP(hipStreamWaitEvent(sj, ctx->eig_ev[3], 0));
       // the outputs of a converged test are queued before the host has read
       // it (the GPU would idle through the round trip otherwise): the Ritz
-      // vectors V·Z into T1, λ and the eigenvectors, then θ once side stream
-      // A is done.  A test that fails leaves them to be overwritten.
-      hipLaunchKernelGGL(k_cq_apply32, dim3(CQ_G), dim3(256), 0, st, V, p, Z, T1);  // Ritz vectors
+      // vectors V·Z into T1, λ and the eigenvectors, then θ on the launch
+      // stream once J is done.  A test that fails leaves them to be overwritten.
+      hipLaunchKernelGGL(k_cq_apply32, dim3(CQ_G), dim3(256), 0, sj, V, p, Z, T1);  // Ritz vectors
       OCM_CHECK_LAUNCH("k_cq_apply32 ritz");
-      hipLaunchKernelGGL(k_extract_signfix, dim3(k), dim3(256), 0, st, T1, p, b, k, evecs_out, theta, evals_out);
+      hipLaunchKernelGGL(k_extract_signfix, dim3(k), dim3(256), 0, sj, T1, p, b, k, evecs_out, theta, evals_out, rcond,
+                         inv_out);
       OCM_CHECK_LAUNCH("k_extract_signfix");
-      if (inv_out) hipLaunchKernelGGL(k_inv_evals, dim3(1), dim3(256), 0, st, evals_out, k, rcond, inv_out);
       if (theta_mode) {  // (the deflation operands and the θ3 arena are reused by the next test too)
+        // the launch stream joins J: everything after (the next iteration
+        // too) is ordered after the Jacobi path's outputs
+        OCM_HIP(hipEventRecord(ctx->eig_ev[2], sj));
         OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[2], 0));
         hipLaunchKernelGGL(k_theta_combine, dim3(1), dim3(256), 0, st, theta, Z, S, L, tr3, b, k, slice == 0 ? 1 : 0,
                            theta_mode >= 2 ? 1 : 0, theta_out);
