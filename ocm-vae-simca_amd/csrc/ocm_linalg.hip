@@ -2645,19 +2645,20 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
         hipLaunchKernelGGL(k_atb32, dim3(CQ_G), dim3(256), 0, st, V, W, p, cq_part, cq_ticket, H);
         OCM_CHECK_LAUNCH("k_atb32 H");
       }
-      // two side streams when θ is wanted: J runs the Jacobi, the test and the
-      // speculative outputs; B forms R and S (the test waits for S), then C·R
-      // and G2; the launch stream deflates the block and runs θ3 — the
-      // longest chain (≈ 180 µs against the Jacobi path's ≈ 160), so it
-      // starts without a cross-stream hand-off (≈ 20 µs each, r05s3)
-      hipStream_t sj = st, sb = st;
+      // two side streams when θ is wanted: A deflates the block and runs θ3;
+      // B forms R and S (handed to the Jacobi's test in flight), then C·R and
+      // G2.  The Jacobi stays on the launch stream, queued first: it then
+      // starts at once on an idle chip (107 µs; 128–145 µs when it started
+      // behind the deflation's workgroups with the θ3 chain on the launch
+      // stream, r05s4–r05s7)
+      hipStream_t sa = st, sb = st;
       rc = eig_side_init(ctx);  // the streams and events (the test's read-back event too)
       if (rc) return rc;
       if (theta_mode) {
-        sj = ctx->eig_side[0];
+        sa = ctx->eig_side[0];
         sb = ctx->eig_side[1];
         OCM_HIP(hipEventRecord(ctx->eig_ev[0], st));
-        OCM_HIP(hipStreamWaitEvent(sj, ctx->eig_ev[0], 0));
+        OCM_HIP(hipStreamWaitEvent(sa, ctx->eig_ev[0], 0));
         OCM_HIP(hipStreamWaitEvent(sb, ctx->eig_ev[0], 0));
       }
       double* R = T1;
@@ -2676,29 +2677,27 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
         }
         OCM_HIP(hipEventRecord(ctx->eig_ev[3], sb));
         // after B's test inputs: theta_into queues its Δ terms on B too
-        rc = theta_into(V, W, H, b, st, sb, ctx->eig_sub, tr3);
+        rc = theta_into(V, W, H, b, sa, sb, ctx->eig_sub, tr3);
         if (rc) return rc;
+        OCM_HIP(hipEventRecord(ctx->eig_ev[2], sa));
       }
       // the Jacobi and the test in one launch (the former k_rr_test32's sums)
-      rc = jacobi(H, b, 40, theta, Z, sj, S, ctx->eig_flag, epoch, k, res);
+      rc = jacobi(H, b, 40, theta, Z, st, S, ctx->eig_flag, epoch, k, res);
       if (rc) return rc;
-      OCM_HIP(hipMemcpyAsync(hres, theta, 2 * (size_t)b * sizeof(double), hipMemcpyDeviceToHost, sj));
-      OCM_HIP(hipEventRecord(ctx->eig_ev[6], sj));
+      OCM_HIP(hipMemcpyAsync(hres, theta, 2 * (size_t)b * sizeof(double), hipMemcpyDeviceToHost, st));
+      OCM_HIP(hipEventRecord(ctx->eig_ev[6], st));
       // R (= T1) and CR are reused below: side stream B is done with them
-      if (theta_mode) OCM_HIP(hipStreamWaitEvent(sj, ctx->eig_ev[3], 0));
+      if (theta_mode) OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[3], 0));
       // the outputs of a converged test are queued before the host has read
       // it (the GPU would idle through the round trip otherwise): the Ritz
-      // vectors V·Z into T1, λ and the eigenvectors, then θ on the launch
-      // stream once J is done.  A test that fails leaves them to be overwritten.
-      hipLaunchKernelGGL(k_cq_apply32, dim3(CQ_G), dim3(256), 0, sj, V, p, Z, T1);  // Ritz vectors
+      // vectors V·Z into T1, λ and the eigenvectors, then θ once side stream
+      // A is done.  A test that fails leaves them to be overwritten.
+      hipLaunchKernelGGL(k_cq_apply32, dim3(CQ_G), dim3(256), 0, st, V, p, Z, T1);  // Ritz vectors
       OCM_CHECK_LAUNCH("k_cq_apply32 ritz");
-      hipLaunchKernelGGL(k_extract_signfix, dim3(k), dim3(256), 0, sj, T1, p, b, k, evecs_out, theta, evals_out, rcond,
+      hipLaunchKernelGGL(k_extract_signfix, dim3(k), dim3(256), 0, st, T1, p, b, k, evecs_out, theta, evals_out, rcond,
                          inv_out);
       OCM_CHECK_LAUNCH("k_extract_signfix");
       if (theta_mode) {  // (the deflation operands and the θ3 arena are reused by the next test too)
-        // the launch stream joins J: everything after (the next iteration
-        // too) is ordered after the Jacobi path's outputs
-        OCM_HIP(hipEventRecord(ctx->eig_ev[2], sj));
         OCM_HIP(hipStreamWaitEvent(st, ctx->eig_ev[2], 0));
         hipLaunchKernelGGL(k_theta_combine, dim3(1), dim3(256), 0, st, theta, Z, S, L, tr3, b, k, slice == 0 ? 1 : 0,
                            theta_mode >= 2 ? 1 : 0, theta_out);
