@@ -1813,7 +1813,14 @@ __global__ __launch_bounds__(256, 1) void k_gram8d(Q8Plan q, SegTable st, int nt
 // fragments (4 sub-panels × 3 digits for A and for B) for 96 MFMAs, one load
 // per four MFMAs, one stage ahead into the other of two register sets.
 // ---------------------------------------------------------------------------
-template <bool ALIGNED, int SYNC, bool FRONT = false>
+// SKIP (the θ3 trace Gram's instantiation only): a chunk stops at its last
+// row's stage pair instead of running its last block's zero-padded stages —
+// the trace Gram takes all its rows as ONE chunk (a 2048-row Gram of 136 tiles
+// as two chunks was 272 workgroups: 34 per XCD of 32 CUs, two rounds of 24
+// stages) and so runs 24 + 8 stages in one round.  Not in the headline
+// instantiation: the branch in the unrolled stage loop cost it 3 %
+// (profiles/r05s9_gram_stage_skip_ab.txt).
+template <bool ALIGNED, int SYNC, bool FRONT = false, bool SKIP = false>
 __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt, int ntiles, int total_wg,
                                                    int nwg, int nblocks, float* __restrict__ part, int chunk0) {
   __shared__ __attribute__((aligned(16))) float scl[4][2 * 64];      // wave-private: row, column scales
@@ -1984,6 +1991,7 @@ __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt
     if (SYNC > 0 && stg % SYNC == SYNC - 1) __builtin_amdgcn_s_barrier();
   };
 
+  const int nvs = SKIP ? (int)((r1 - r0 + 63) / 64) : nstage;  // stages holding rows (the rest are zero digits)
   i32x4 F0A[4][3], F0B[4][3], F1A[4][3], F1B[4][3];
 #pragma unroll
   for (int i = 0; i < 24; ++i) load_frag(F0A, F0B, i, 0);
@@ -1991,6 +1999,7 @@ __global__ __launch_bounds__(256, 1) void k_gram8e(Q8Plan q, SegTable st, int nt
     const int s0 = blk * SPB;
 #pragma unroll
     for (int u = 0; u < SPB; u += 2) {
+      if (SKIP && u > 0 && s0 + u >= nvs) break;
       step(F0A, F0B, F1A, F1B, s0 + u, u == 0);
       if (u == 0) {
         SR = srow[(size_t)blk * q.P8];
@@ -2772,7 +2781,10 @@ int gram_impl8(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, i
 #define G8E_LAUNCH3(A_, S_, F_)                                                                                      \
   hipLaunchKernelGGL((k_gram8e<A_, S_, F_>), dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt, ntiles,         \
                      (int)total, nwg, nblocks, pg, (int)c0)
-    if (!k32 && order == 3) G8E_LAUNCH(true, 2);
+    if (tr_O && !k32 && order == 3)
+      hipLaunchKernelGGL((k_gram8e<true, 2, false, true>), dim3((unsigned)total), dim3(256), 0, st, q, tabs[t], nt,
+                         ntiles, (int)total, nwg, nblocks, pg, (int)c0);
+    else if (!k32 && order == 3) G8E_LAUNCH(true, 2);
 #ifdef OCM_EXP_SELECTORS
     else if (!k32 && order == 0) G8E_LAUNCH(false, 0);
     else if (!k32 && order == 1) G8E_LAUNCH(true, 0);
@@ -2943,8 +2955,13 @@ int trace_gram_rows_i8(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t n, int
   *ntr = nt * (nt + 1) / 2 * (Q8T * Q8T / 4 / 256);
   if (p <= SMALL_P) return OCM_ERR_ARG;  // the caller takes the G path
   const int64_t seg[2] = {0, n};
-  return gram_impl8(ctx, X, ldx, nullptr, n, p, nullptr, seg, 1, nullptr, nullptr, st, 0, false, PrepArgs{}, true,
-                    nullptr, 0, O, tr_part);
+  // as few chunks as keep one round of workgroups (chunks × tiles ≤ CUs; one
+  // at p = 2048): the SKIP instantiation stops each chunk at its last row
+  const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(ctx->num_cus / std::max(1, nt * (nt + 1) / 2),
+                                                             (n + Q8BLK - 1) / Q8BLK));
+  const int64_t chunk = (int64_t)ocm::align_up((size_t)((n + nch - 1) / nch), Q8BLK);
+  return gram_impl8(ctx, X, ldx, nullptr, n, p, nullptr, seg, 1, nullptr, nullptr, st, chunk, false, PrepArgs{},
+                    true, nullptr, 0, O, tr_part);
 }
 }  // namespace ocm
 
