@@ -2126,8 +2126,9 @@ int dgemm(const double* A, int64_t lda, const double* B, int64_t ldb, double* D,
 
 int jacobi(const double* A, int n, int max_sweeps, double* ev, double* Z, hipStream_t st, const double* S = nullptr,
            const unsigned* sflag = nullptr, unsigned epoch = 0, int k = 0, double* res = nullptr) {
-  // n = 32: the block kernel (0.95 ms per fit against 1.19 with the one-wave k_jacobi<32, 64>, r03z; the
-  // same block rounds in one wave without barriers, round 5: 204 against 122–140 µs, r05s_eig_timeline.txt)
+  // n = 32: the one-barrier block kernel k_jacobi_1b (107 µs alone against 139 for the two-barrier
+  // k_jacobi_blk, r05s3_jacobi_ab.txt; the block rounds in one wave without barriers measured 204 µs,
+  // r05s_eig_timeline.txt); S: the Rayleigh–Ritz test at its end (S from k_rr_resid32 in flight)
 #ifdef OCM_JACOBI_SWEEPS  // make exp diagnostic: print the sweep count of each 32×32 solve
   if (n == 32) {
     static int* dsw = nullptr;
