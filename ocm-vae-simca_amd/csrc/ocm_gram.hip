@@ -577,24 +577,24 @@ struct CovTerms {
   int nterm;
 };
 
-__global__ void k_cov_mean(CovTerms tm, const float* __restrict__ shift, int p, double n,
-                           double* __restrict__ dvec, double* __restrict__ mean) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p) return;
-  double s = 0.0;
-  for (int t = 0; t < tm.nterm; ++t) s += tm.coef[t] * tm.cs[t][i];
-  const double d = s / n;
-  dvec[i] = d;
-  mean[i] = (double)shift[i] + d;
-}
-
-__global__ void k_cov(CovTerms tm, const double* __restrict__ dvec, int p, double n, double* __restrict__ C) {
+// C = (Σ_t c_t G_t − n d dᵀ)/(n − 1) with d = Σ_t c_t cs_t / n (the mean's
+// offset from the shift), and mean = shift + d from row 0's threads.  Each
+// thread forms its d_i, d_j from the column sums itself (the same sums as the
+// separate mean kernel it replaces: one launch less on the non-sharded path)
+__global__ void k_cov(CovTerms tm, const float* __restrict__ shift, int p, double n, double* __restrict__ C,
+                      double* __restrict__ mean) {
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (size_t)p * p) return;
   const int i = (int)(e / p), j = (int)(e % p);
-  double g = 0.0;
-  for (int t = 0; t < tm.nterm; ++t) g += tm.coef[t] * tm.G[t][e];
-  C[e] = (g - n * dvec[i] * dvec[j]) / (n - 1.0);
+  double si = 0.0, sj = 0.0, g = 0.0;
+  for (int t = 0; t < tm.nterm; ++t) {
+    si += tm.coef[t] * tm.cs[t][i];
+    sj += tm.coef[t] * tm.cs[t][j];
+    g += tm.coef[t] * tm.G[t][e];
+  }
+  const double di = si / n, dj = sj / n;
+  C[e] = (g - n * di * dj) / (n - 1.0);
+  if (i == 0) mean[j] = (double)shift[j] + dj;
 }
 
 // ---------------------------------------------------------------------------
@@ -3100,12 +3100,10 @@ int ocm_cov_from_gram(ocm_ctx* ctx, const double* const* G_list, const double* c
     tm.cs[t] = colsum_list[t];
     tm.coef[t] = coef[t];
   }
-  auto* dvec = static_cast<double*>(ocm::workspace(ctx, (size_t)p * sizeof(double), st));
-  if (!dvec) return OCM_ERR_NOMEM;
-  hipLaunchKernelGGL(k_cov_mean, dim3((p + 255) / 256), dim3(256), 0, st, tm, shift, p, (double)n, dvec, mean_out);
-  OCM_CHECK_LAUNCH("k_cov_mean");
+  (void)ctx;
   const size_t pp = (size_t)p * p;
-  hipLaunchKernelGGL(k_cov, dim3((unsigned)((pp + 255) / 256)), dim3(256), 0, st, tm, dvec, p, (double)n, C_out);
+  hipLaunchKernelGGL(k_cov, dim3((unsigned)((pp + 255) / 256)), dim3(256), 0, st, tm, shift, p, (double)n, C_out,
+                     mean_out);
   OCM_CHECK_LAUNCH("k_cov");
   return OCM_OK;
 }
