@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCM_ABI_VERSION 9
+#define OCM_ABI_VERSION 10
 
 #define OCM_OK 0
 #define OCM_ERR_ARG (-1)         /* invalid argument (maps to ValueError) */
@@ -60,6 +60,11 @@ typedef struct ocm_decision {
 } ocm_decision;
 
 int ocm_abi_version(void);
+/* 16 hex digits: the first 64 bits of the SHA-256 of the library's build
+ * inputs (csrc/*.hip, its headers and Makefile, in the Makefile's ID_INPUTS
+ * order).  The Python binding refuses a library whose id differs from the
+ * hash of the sources beside it (a stale prebuilt libocm.so). */
+const char* ocm_build_id(void);
 const char* ocm_last_error(void);
 int ocm_ctx_create(int device, ocm_ctx** out);
 int ocm_ctx_destroy(ocm_ctx* ctx);
@@ -398,6 +403,11 @@ int ocm_gram_f32_prep_write(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t n
 /* Number of times this context materialised a lazy view (the fallback paths above), for tests and
  * diagnostics: 0 after any call on the fused paths. */
 int ocm_prep_materialised(ocm_ctx* ctx, int64_t* count_out);
+/* How many Rayleigh–Ritz tests of ocm_eig_topk* this context ran twice: the
+ * test fused into the Jacobi takes S from a side stream in flight and gives up
+ * after ≈ 1 s (kernels serialised, or the side stream not scheduled); the host
+ * then runs the Jacobi + test again behind S's event (a diagnostic counter). */
+int ocm_eig_test_reruns(ocm_ctx* ctx, int64_t* count_out);
 int ocm_score_f32_diag_prep(ocm_ctx* ctx, const float* X, int64_t ldx, const int64_t* rows, int64_t m, int32_t p,
                             const ocm_prep* prep, const double* P, const double* mu, const double* a_diag, int32_t k,
                             float* T_out, double* T2_out, float* Q_out, const ocm_decision* dec,

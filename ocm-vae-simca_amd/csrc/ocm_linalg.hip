@@ -737,14 +737,20 @@ __device__ __forceinline__ void jrot_fast(double app, double aqq, double apq, do
 // S (optional): the Rayleigh–Ritz test fused at the end — the former k_rr_test32's
 // res[i] = √max(z_iᵀ S z_i, 0) for the first k Ritz pairs, the same sums in
 // the same order — with S taken in flight from k_rr_resid32 on another
-// stream once *sflag reaches epoch (a bounded wait: ≈ 1 s, then NaN
-// residuals, which the host reports as an error instead of hanging)
+// stream once *sflag reaches epoch.  The wait is bounded (≈ 1 s): on a
+// timeout the residuals are written as −1 (valid ones are ≥ 0), and the host
+// runs the Jacobi and its test again behind the producer's event instead of
+// hanging or mistaking the timeout for bad data
+#define OCM_JACOBI_SPINS_1S (1u << 22)  // ≈ 1 s of s_sleep(8) polls
+#ifndef OCM_JACOBI_WAIT_SPINS           // (make exp: 0 gives up at once, to exercise the re-run)
+#define OCM_JACOBI_WAIT_SPINS OCM_JACOBI_SPINS_1S
+#endif
 template <int NF>
 __global__ __launch_bounds__(320) void k_jacobi_1b(const double* __restrict__ Ain, int max_sweeps,
                                                    double* __restrict__ evals, double* __restrict__ Zout,
                                                    int* __restrict__ sweeps_out, const double* __restrict__ S,
                                                    const unsigned* __restrict__ sflag, unsigned epoch, int ktest,
-                                                   double* __restrict__ res) {
+                                                   double* __restrict__ res, unsigned max_spins) {
   static_assert(NF == 32, "thread map for 32×32");
   constexpr int H = NF / 2, NB = H * (H + 1) / 2, LD = NF + 1, NT = 320, ZT0 = 192;
   __shared__ double A[2][NF][LD];
@@ -853,9 +859,9 @@ __global__ __launch_bounds__(320) void k_jacobi_1b(const double* __restrict__ Ai
   if (tid == 0) {
     unsigned n = 0;
     while ((int)(__hip_atomic_load(const_cast<unsigned*>(sflag), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - epoch) < 0 &&
-           ++n < (1u << 22))
+           ++n < max_spins)
       __builtin_amdgcn_s_sleep(8);
-    done = n < (1u << 22);
+    done = n < max_spins;
   }
   __syncthreads();
   for (int e = tid; e < NF * NF; e += NT) A[nx][e / NF][e % NF] = ld_agent(S + e);
@@ -872,7 +878,7 @@ __global__ __launch_bounds__(320) void k_jacobi_1b(const double* __restrict__ Ai
     double acc = 0.0;
 #pragma unroll 8
     for (int r = 0; r < NF; ++r) acc = fma(Z[cur][r][tid], Z[nx][r][tid], acc);
-    res[myrank] = done ? sqrt(fmax(acc, 0.0)) : __builtin_nan("");
+    res[myrank] = done ? sqrt(fmax(acc, 0.0)) : -1.0;
   }
 }
 
@@ -2125,7 +2131,8 @@ int dgemm(const double* A, int64_t lda, const double* B, int64_t ldb, double* D,
 }
 
 int jacobi(const double* A, int n, int max_sweeps, double* ev, double* Z, hipStream_t st, const double* S = nullptr,
-           const unsigned* sflag = nullptr, unsigned epoch = 0, int k = 0, double* res = nullptr) {
+           const unsigned* sflag = nullptr, unsigned epoch = 0, int k = 0, double* res = nullptr,
+           unsigned spins = OCM_JACOBI_WAIT_SPINS) {
   // n = 32: the one-barrier block kernel k_jacobi_1b (107 µs alone against 139 for the two-barrier
   // k_jacobi_blk, r05s3_jacobi_ab.txt; the block rounds in one wave without barriers measured 204 µs,
   // r05s_eig_timeline.txt); S: the Rayleigh–Ritz test at its end (S from k_rr_resid32 in flight)
@@ -2134,7 +2141,7 @@ int jacobi(const double* A, int n, int max_sweeps, double* ev, double* Z, hipStr
     static int* dsw = nullptr;
     if (!dsw) (void)hipMalloc(reinterpret_cast<void**>(&dsw), sizeof(int));
     hipLaunchKernelGGL(k_jacobi_1b<32>, dim3(1), dim3(320), 0, st, A, max_sweeps, ev, Z, dsw, S, sflag, epoch, k,
-                       res);
+                       res, spins);
     int hsw = -1;
     (void)hipMemcpyAsync(&hsw, dsw, sizeof(int), hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
@@ -2144,7 +2151,7 @@ int jacobi(const double* A, int n, int max_sweeps, double* ev, double* Z, hipStr
 #endif
   if (n == 32)
     hipLaunchKernelGGL(k_jacobi_1b<32>, dim3(1), dim3(320), 0, st, A, max_sweeps, ev, Z, nullptr, S, sflag, epoch, k,
-                       res);
+                       res, spins);
   else if (n == 48)
     hipLaunchKernelGGL(k_jacobi_blk<48>, dim3(1), dim3(256), 0, st, A, max_sweeps, ev, Z, nullptr);
   else if (n == 64)
@@ -2705,6 +2712,22 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
         OCM_CHECK_LAUNCH("k_theta_combine");
       }
       OCM_HIP(hipEventSynchronize(ctx->eig_ev[6]));
+      bool waited_out = false;
+      for (int i = 0; i < k; ++i) waited_out |= hres[b + i] < 0.0;
+      if (waited_out) {
+        // the fused test gave up waiting for S (side stream B not scheduled
+        // within ≈ 1 s): the launch stream has since waited for B's event, so
+        // the same Jacobi + test runs again with S complete (the same Z and λ;
+        // the outputs queued above read them before this rewrites them)
+        ++ctx->eig_test_reruns;
+        rc = jacobi(H, b, 40, theta, Z, st, S, ctx->eig_flag, epoch, k, res, OCM_JACOBI_SPINS_1S);
+        if (rc) return rc;
+        OCM_HIP(hipMemcpyAsync(hres, theta, 2 * (size_t)b * sizeof(double), hipMemcpyDeviceToHost, st));
+        OCM_HIP(hipStreamSynchronize(st));
+        for (int i = 0; i < k; ++i)
+          if (hres[b + i] < 0.0) return ocm::fail(OCM_ERR_HIP, "ocm_eig_topk: the Rayleigh-Ritz test's operand S "
+                                                               "was not ready after its producer finished");
+      }
       double rmax = 0.0;
       for (int i = 0; i < k; ++i) rmax = std::max(rmax, hres[b + i]);
       const double scale = std::fabs(hres[0]);

@@ -384,6 +384,12 @@ int ocm_prep_rowstats_f32(ocm_ctx* ctx, const float* X, int64_t ldx, int64_t m, 
   return OCM_OK;
 }
 
+int ocm_eig_test_reruns(ocm_ctx* ctx, int64_t* count_out) {
+  OCM_REQUIRE(ctx && count_out, "ocm_eig_test_reruns: NULL argument");
+  *count_out = ctx->eig_test_reruns;
+  return OCM_OK;
+}
+
 int ocm_prep_materialised(ocm_ctx* ctx, int64_t* count_out) {
   OCM_REQUIRE(ctx && count_out, "ocm_prep_materialised: NULL argument");
   *count_out = ctx->prep_materialised;

@@ -60,6 +60,7 @@ class OcmNotConverged(OcmError):
 # name -> (restype, argtypes); every symbol include/ocm.h declares
 SIGNATURES = {
     "ocm_abi_version": (c_i32, []),
+    "ocm_build_id": (ctypes.c_char_p, []),
     "ocm_last_error": (ctypes.c_char_p, []),
     "ocm_ctx_create": (c_i32, [c_i32, ctypes.POINTER(c_void_p)]),
     "ocm_ctx_destroy": (c_i32, [c_void_p]),
@@ -147,6 +148,7 @@ SIGNATURES = {
     "ocm_vae_standardise": (c_i32, [c_void_p, c_void_p, c_i32, c_i32, c_void_p, c_void_p, c_i32, c_void_p, c_void_p]),
     "ocm_eigh_f64": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_i32, c_void_p, c_void_p]),
     "ocm_prep_materialised": (c_i32, [c_void_p, ctypes.POINTER(c_i64)]),
+    "ocm_eig_test_reruns": (c_i32, [c_void_p, ctypes.POINTER(c_i64)]),
     "ocm_prep_rowstats_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p]),
     "ocm_prep_apply_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_i64,
                                    c_void_p]),
@@ -162,7 +164,39 @@ SIGNATURES = {
                                         ctypes.POINTER(OcmDecision), c_void_p, c_i64, c_void_p, c_void_p]),
 }
 
-ABI_VERSION = 9  # include/ocm.h OCM_ABI_VERSION
+ABI_VERSION = 10  # include/ocm.h OCM_ABI_VERSION
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+
+
+def source_build_id(csrc: str = CSRC) -> str | None:
+    """The build id the Makefile derives from the library's inputs (the first
+    16 hex digits of the SHA-256 of ID_INPUTS, concatenated in order), or None
+    when the sources are not beside the package."""
+    import hashlib
+    import re
+
+    mk = os.path.join(csrc, "Makefile")
+    if not os.path.exists(mk):
+        return None
+    text = open(mk).read()
+    srcs = re.search(r"^SRCS\s*:=\s*(.+)$", text, re.M).group(1).split()
+    extra = re.search(r"^ID_INPUTS\s*:=\s*\$\(SRCS\)\s*(.+)$", text, re.M).group(1).split()
+    h = hashlib.sha256()
+    for f in srcs + extra:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def file_build_id(path: str = LIB_PATH) -> str | None:
+    """The build id compiled into a libocm.so, read from the file (no load)."""
+    import re
+
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as fh:
+        m = re.search(rb"ocm-build-id:([0-9a-f]{16})", fh.read())
+    return m.group(1).decode() if m else None
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -183,7 +217,12 @@ def load() -> ctypes.CDLL:
             fn.restype = res
             fn.argtypes = args
         if lib.ocm_abi_version() != ABI_VERSION:
-            raise OcmError("libocm ABI version mismatch")
+            raise OcmError(f"libocm ABI version mismatch: {LIB_PATH} has {lib.ocm_abi_version()}, the binding "
+                           f"expects {ABI_VERSION}; rebuild it (`make -C ocm-vae-simca_amd/csrc`)")
+        want, have = source_build_id(), lib.ocm_build_id().decode()
+        if want is not None and have != want:
+            raise OcmError(f"{LIB_PATH} is stale: built from sources with id {have}, the sources beside it hash to "
+                           f"{want}; rebuild it (`make -C ocm-vae-simca_amd/csrc -B`, or __graft_entry__.build())")
         _lib = lib
         return lib
 

@@ -23,7 +23,8 @@ their own fold's prediction and other-class rows the LAST fold's
 (:190, 205-207), eff = √(sens·spec) (:208).
 
 Multi-GPU (``group`` given; the drop-in ``grid`` passes dist.group.WORLD
-when the process runs as one of W > 1 ranks): each rank holds a contiguous row block of X
+when the process runs as one of W > 1 ranks and every rank passed the same X
+and y, ``ocm.replica.replicated_group``): each rank holds a contiguous row block of X
 (``row_offset``) and the full label vector.  Fold f's eigensolve runs on
 its owner rank f mod W: every rank forms its local TRAIN Gram of fold f
 (Σ_g G_g − G_f, fp64 downdating on the device) and one RCCL reduce brings
@@ -43,6 +44,7 @@ import torch
 import torch.distributed as dist
 
 from . import engine, limits
+from .replica import replicated_group
 
 __all__ = ["grid", "cv_grid", "FoldModels"]
 
@@ -107,7 +109,21 @@ def _applicable(base_est, X, y, cv, lv_values, param_grid):
 def grid(base_est, X, y, cv, lv_values, param_grid, class_index, store_predictions):
     """utils/CVSIMCA.py drop-in hook: (records, by_combo), or (None, None)
     when the fold engine does not cover the configuration."""
-    app = _applicable(base_est, X, y, cv, lv_values, param_grid)
+    try:
+        app, err = _applicable(base_est, X, y, cv, lv_values, param_grid), None
+    except Exception as e:  # raised after the exchange, so the other ranks are not left waiting in it
+        app, err = None, e
+    # Under torchrun (an initialised world of W > 1 ranks) the drop-in is
+    # collective only when every rank passed the same X and y, as an unchanged
+    # driver does (ocm/replica.py): rank r then keeps its contiguous row block
+    # and the fold engine runs sharded (C3, SURVEY.md §8e), and every rank
+    # returns the same records and predictions.  Ranks holding different data
+    # run the reference's per-process CV.  Every rank exchanges its
+    # fingerprint before anything rank-dependent decides the path.
+    eligible = app is not None and int(X.shape[0]) == int(np.asarray(y).shape[0])
+    group = replicated_group(X, y, eligible)
+    if err is not None:
+        raise err
     if app is None:
         return None, None
     cls_idx, tl, combos, base = app
@@ -116,30 +132,13 @@ def grid(base_est, X, y, cv, lv_values, param_grid, class_index, store_predictio
         class_index = [tl]
     y = np.asarray(y)
     folds = [cls_idx[test_rel] for _, test_rel in cv.kf.split(cls_idx)]
-    group = _world_group_for(X, y)
     if group is None:
         return cv_grid(X, y, folds, cls_idx, lv_values, combos, base, class_index, store_predictions)
-    # Under torchrun (an initialised world of W > 1 ranks, each holding all
-    # len(y) rows, as an unchanged driver does) the drop-in is collective: rank
-    # r keeps its contiguous row block and the fold engine runs sharded (C3,
-    # SURVEY.md §8e).  Every rank returns the same records and predictions.
     from .synth import shard_bounds
 
     lo, hi = shard_bounds(int(y.shape[0]), dist.get_rank(group), dist.get_world_size(group))
     return cv_grid(X[lo:hi], y, folds, cls_idx, lv_values, combos, base, class_index, store_predictions,
                    row_offset=lo, group=group)
-
-
-def _world_group_for(X, y):
-    """dist.group.WORLD when a process group of more than one rank is
-    initialised and X holds every row of y; otherwise None (single process)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() < 2:
-        return None
-    if int(X.shape[0]) != int(np.asarray(y).shape[0]):
-        raise ValueError(f"cross_validate_simca_grid under a process group of {dist.get_world_size()} ranks: X has "
-                         f"{int(X.shape[0])} rows but y has {int(np.asarray(y).shape[0])}; pass every rank the full "
-                         "X (the drop-in shards it), or call ocm.cv.cv_grid(..., row_offset=, group=) with a block")
-    return dist.group.WORLD
 
 
 class FoldModels:

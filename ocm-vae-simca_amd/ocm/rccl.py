@@ -138,10 +138,30 @@ class Communicator:
             self._comm = ctypes.c_void_p()
 
 
+RECORDER_ENV = ("TORCH_FR_BUFFER_SIZE", "TORCH_NCCL_TRACE_BUFFER_SIZE")  # torch reads the first one set
+
+
+def recorder_enabled() -> bool:
+    """Whether ProcessGroupNCCL keeps a flight recorder (a non-zero buffer
+    size, read by torch when the process group starts; ``ocm`` sets one on
+    import unless the caller chose a value)."""
+    for name in RECORDER_ENV:
+        v = os.environ.get(name)
+        if v is not None:
+            try:
+                return int(v) > 0
+            except ValueError:
+                return False
+    return False
+
+
 def pending_pg_collectives() -> int | None:
     """Eager ProcessGroupNCCL collectives their watchdogs still track (the
     flight recorder's entries the watchdog has not retired yet), or None when
-    the recorder is unavailable.  The dump is this process's own data."""
+    the recorder is unavailable (disabled, or not in this torch build).  The
+    dump is this process's own data."""
+    if not recorder_enabled():
+        return None
     try:
         from torch._C._distributed_c10d import _dump_nccl_trace
     except ImportError:
@@ -153,15 +173,29 @@ def pending_pg_collectives() -> int | None:
     return len(pickle.loads(raw).get("entries", []))
 
 
-def wait_pg_collectives_retired(timeout: float = 30.0) -> int | None:
+def _nccl_group_exists(group=None) -> bool:
+    return (dist.is_available() and dist.is_initialized()
+            and "nccl" in str(dist.get_backend(group)).lower())
+
+
+def wait_pg_collectives_retired(group=None, timeout: float = 30.0) -> int:
     """Block until every eager ProcessGroupNCCL collective issued before has
     been retired by its watchdog (so no watchdog will query an event while a
     graph is being captured); raises after ``timeout`` seconds.  The wait is a
     condition on the watchdogs' own records, not a guess at their poll period.
-    Returns the number that was pending (None: no recorder to consult)."""
+    Returns the number that was pending.  When an NCCL process group exists but
+    its flight recorder is off, nothing tells when the watchdog is done, so
+    this raises instead of proceeding."""
     first = pending_pg_collectives()
+    if first is None:
+        if not _nccl_group_exists(group):
+            return 0
+        raise RuntimeError("a HIP-graph capture beside a ProcessGroupNCCL needs its flight recorder to know when the "
+                           "watchdog has retired the eager collectives (a poll during the capture aborts the process, "
+                           "ocm/rccl.py); set TORCH_FR_BUFFER_SIZE (e.g. 2000) before init_process_group — importing "
+                           "ocm first does — or pass graph=False")
     if not first:
-        return first
+        return 0
     torch.cuda.synchronize()
     t0 = time.monotonic()
     while True:

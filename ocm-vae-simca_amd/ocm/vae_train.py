@@ -257,7 +257,7 @@ class GraphedVAETrainer:
                                  "process group; pass graph=False for a gloo group")
             from .rccl import wait_pg_collectives_retired
 
-            self.pending_at_capture = wait_pg_collectives_retired()
+            self.pending_at_capture = wait_pg_collectives_retired(self.group)
             mode = "thread_local"
         with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.out = self._body()
@@ -276,9 +276,38 @@ class GraphedVAETrainer:
                         if torch.is_tensor(t):
                             t.zero_()
 
+    def close(self):
+        """Release the captured step graph, then the trainer's RCCL communicator
+        — in that order, so no graph that captured the communicator's all-reduce
+        outlives it.  A sweep that builds a trainer per grid point
+        (utils/final_vaesimca.py:312-351) closes each one; the trainer cannot
+        step afterwards.  Idempotent; also the context-manager exit."""
+        if getattr(self, "_closed", False):
+            return
+        dev = self.x.device
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)  # no replay may still be running on the graph or the communicator
+        if self.graph is not None:
+            self.graph.reset()
+            self.graph = None
+            self.out = None
+        if self._comm is not None:
+            self._comm.close()
+            self._comm = None
+        self._closed = True
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
     def step(self, x: torch.Tensor | None = None):
         """Run one training step on ``x`` (copied into the static batch buffer);
         returns device tensors (loss, recon, kl)."""
+        if getattr(self, "_closed", False):
+            raise RuntimeError("GraphedVAETrainer.step() after close()")
         if x is not None:
             self.x.copy_(x, non_blocking=True)
         if self.graph is not None:

@@ -17,6 +17,17 @@ lazy preprocessed view (``ocm.preprocess.snv_savgol(X, ..., lazy=True)``:
 the drivers' SNV / Savitzky–Golay step, applied inside the Gram quantiser and
 the scoring kernel instead of as a pass of its own; results as for tensors).
 
+Multi-GPU: under ``torchrun`` (a process group of W > 1
+ranks) ``fit`` / ``predict`` / ``transform`` first exchange a fingerprint of
+their arguments (``ocm.replica``).  When every rank passed the same X and
+labels — an unchanged driver — the rows are sharded: rank r fits and scores
+its contiguous block, the class moments meet in one all-reduce, and the
+per-row results (``_model`` T / T2 / Q, predict's (m, C) matrix, transform's
+arrays) are all-gathered, so every rank returns the single-process result.
+When the ranks' data differ, each rank runs the reference's per-process
+computation.  Every rank must make the call (``ocm.replica.per_process()``
+for calls on a subset of the ranks).
+
 Documented deviations:
 * predict/transform use the exact top-k loadings of the covariance; the
   reference re-estimates them with a randomized ``PCA(k)`` (utils/SIMCA.py:75)
@@ -43,10 +54,14 @@ from __future__ import annotations
 
 import numpy as np
 import torch
+import torch.distributed as dist
 from sklearn.base import BaseEstimator, ClassifierMixin
 
 from ocm import engine, limits
+from ocm.dist import make_allreduce
 from ocm.prepview import PrepView
+from ocm.replica import gather_rows, replicated_group
+from ocm.synth import shard_bounds
 
 __all__ = ["SIMCA"]
 
@@ -173,23 +188,55 @@ class SIMCA(BaseEstimator, ClassifierMixin):
             self.qlim = "chi2pom"
 
         self._out_dtype = _out_dtype(X)
-        Xd = engine.as_device_x(X)
-        lab = _device_labels(classes, Xd.device)
+        # Under torchrun with the same X and y on every rank (an unchanged
+        # driver, simca_nuts.py:186-189) the fit is row-sharded: rank r fits
+        # its contiguous block with one packed all-reduce of the moments and
+        # the per-row arrays of _model are all-gathered, so every rank holds
+        # the single-process model.  Otherwise the reference's per-process fit.
+        group = replicated_group(X, classes, eligible=_n_rows(classes) == X.shape[0])
+        self._sharded = group is not None
         self._model = {}
         self._fits = {}
-        for i, cls in enumerate(self.model_class):
-            mask = lab == int(cls)
-            n = int(mask.sum().item())
-            rows = None if n == Xd.shape[0] else torch.nonzero(mask).flatten()
-            self._model[cls] = self._fit_one_class(Xd, rows, n, int(self.n_components[i]))
-            self._fits[cls] = self._model[cls]._fit
+        if self._sharded:
+            lab_h = _host_labels(classes)
+            bounds = _bounds(X.shape[0])
+            rank = dist.get_rank()
+            lo, hi = bounds[rank]
+            Xd = engine.as_device_x(X[lo:hi])
+            ar = make_allreduce(group)
+            for i, cls in enumerate(self.model_class):
+                mask = lab_h == cls
+                counts = [int(mask[a:b].sum()) for a, b in bounds]
+                rows = None if counts[rank] == hi - lo else \
+                    torch.from_numpy(np.flatnonzero(mask[lo:hi])).to(Xd.device)
+                self._model[cls] = self._fit_one_class(Xd, rows, counts[rank], int(self.n_components[i]),
+                                                       (counts, ar))
+                self._fits[cls] = self._model[cls]._fit
+        else:
+            Xd = engine.as_device_x(X)
+            lab = _device_labels(classes, Xd.device)
+            for i, cls in enumerate(self.model_class):
+                mask = lab == int(cls)
+                n = int(mask.sum().item())
+                rows = None if n == Xd.shape[0] else torch.nonzero(mask).flatten()
+                self._model[cls] = self._fit_one_class(Xd, rows, n, int(self.n_components[i]))
+                self._fits[cls] = self._model[cls]._fit
         self.n_features_in_ = X.shape[1]
         self.is_fitted_ = True
         return self
 
-    def _fit_one_class(self, Xd, rows, n, k):
-        """utils/SIMCA.py:62-99 on the device."""
-        fit = engine.fit_class(Xd, rows, n, k, limits.theta_mode_for(self), want_T=True, keep_C=True)
+    def _fit_one_class(self, Xd, rows, n, k, shard=None):
+        """utils/SIMCA.py:62-99 on the device.  ``shard`` = (class rows of each
+        rank, all-reduce) marks a row-sharded fit of this rank's block Xd."""
+        if shard is None:
+            fit = engine.fit_class(Xd, rows, n, k, limits.theta_mode_for(self), want_T=True, keep_C=True)
+        else:
+            counts, ar = shard
+            fit = engine.fit_class(Xd, rows, n, k, limits.theta_mode_for(self), want_T=True, keep_C=True,
+                                   allreduce=ar)
+            # every rank holds the single-process per-row arrays (utils/SIMCA.py:65-71, 89-95)
+            fit.T, fit.T2, fit.Q = (gather_rows(t, counts) for t in (fit.T, fit.T2, fit.Q))
+            n = fit.n
         T2m = limits.Moments(n, lambda: fit.T2_stats, None, lambda pct: engine.percentile(fit.T2, pct))
         Qm = limits.Moments(n, lambda: fit.Q_stats, None, lambda pct: engine.percentile(fit.Q, pct))
         T2_limit = limits.t2_limit(self, T2m, k)
@@ -227,6 +274,16 @@ class SIMCA(BaseEstimator, ClassifierMixin):
         })
         return md
 
+    def _score_shard(self, X):
+        """(lo, hi, rows of each rank) when the model was fitted row-sharded and
+        every rank scores the same X (ocm/replica.py): this rank scores rows
+        [lo, hi) and the results are all-gathered.  None: score all rows here."""
+        if not getattr(self, "_sharded", False) or replicated_group(X) is None:
+            return None
+        bounds = _bounds(X.shape[0])
+        lo, hi = bounds[dist.get_rank()]
+        return lo, hi, [b - a for a, b in bounds]
+
     def _decision(self, T2_limit, Q_limit, D_limit):
         if self.type == "dd":
             return engine.make_decision("dd", self._t2dof / self._t2scfact, self._qdof / self._qscfact, D_limit)
@@ -237,11 +294,19 @@ class SIMCA(BaseEstimator, ClassifierMixin):
     # ------------------------------------------------------------ transform
     def transform(self, X):
         """utils/SIMCA.py:101-117 — (T2, T2red, Q, Qred) of the LAST class."""
-        Xd = engine.as_device_x(X)
         cls = self.model_class[-1]
         fit = self._fits[cls]
         m = self._model[cls]
-        out = engine.score(Xd, None, Xd.shape[0], fit.P64, fit.mean64, fit.inv_diag)
+        shard = self._score_shard(X)
+        Xd = engine.as_device_x(X if shard is None else X[shard[0]:shard[1]])
+        if Xd.shape[0]:
+            out = engine.score(Xd, None, Xd.shape[0], fit.P64, fit.mean64, fit.inv_diag)
+        else:  # a rank without rows of a sharded transform
+            vdt = torch.float64 if Xd.dtype == torch.float64 else torch.float32
+            out = {"T2": torch.empty(0, dtype=torch.float64, device=Xd.device),
+                   "Q": torch.empty(0, dtype=vdt, device=Xd.device)}
+        if shard is not None:
+            out = {key: gather_rows(out[key], shard[2]) for key in ("T2", "Q")}
         dec = self._decision(m["T2_limit"], m["Q_limit"], m["D_limit"])
         t2r, qr, _ = engine.decide(out["T2"], out["Q"], dec)
         if _is_dev(X):
@@ -251,7 +316,8 @@ class SIMCA(BaseEstimator, ClassifierMixin):
     # -------------------------------------------------------------- predict
     def predict(self, X, y_true=None):
         """utils/SIMCA.py:120-154 — (m, C) float64 of 0/1, decision fused in the scoring kernel."""
-        Xd = engine.as_device_x(X)
+        shard = self._score_shard(X)
+        Xd = engine.as_device_x(X if shard is None else X[shard[0]:shard[1]])
         m = Xd.shape[0]
         C = len(self.model_class)
         pred = torch.zeros((m, C), dtype=torch.float64, device=Xd.device)
@@ -259,9 +325,14 @@ class SIMCA(BaseEstimator, ClassifierMixin):
             fit = self._fits[cls]
             info = self._model[cls]
             dec = self._decision(info["T2_limit"], info["Q_limit"], info["D_limit"])
+            if m == 0:  # a rank without rows of a sharded predict
+                continue
             acc = pred[:, i:] if C > 1 else pred
             engine.score(Xd, None, m, fit.P64, fit.mean64, fit.inv_diag, want_T2=False, want_Q=False,
                          decision=dec, accept_out=acc, accept_stride=C)
+        if shard is not None:  # every rank returns the (m, C) matrix of all rows
+            pred = gather_rows(pred, shard[2])
+            m = pred.shape[0]
         out = pred if _is_dev(X) else pred.cpu().numpy()
         if y_true is not None:
             yt = _host_labels(y_true)
@@ -377,6 +448,16 @@ def _out_dtype(X):
     if isinstance(X, (torch.Tensor, PrepView)):
         return np.float64 if X.dtype == torch.float64 else np.float32
     return np.float64 if np.asarray(X).dtype == np.float64 else np.float32
+
+
+def _n_rows(y) -> int:
+    return int(y.shape[0]) if hasattr(y, "shape") and len(y.shape) else len(y)
+
+
+def _bounds(n: int):
+    """Every rank's contiguous row block of an n-row matrix."""
+    W = dist.get_world_size()
+    return [shard_bounds(n, r, W) for r in range(W)]
 
 
 def _host_labels(y):

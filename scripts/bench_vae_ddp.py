@@ -11,7 +11,9 @@ HBM (ocm/synth.py: per-chunk Philox seeds, so the matrix does not depend on
 the world size; 10M × 4096 fp32 = 164 GB in all, 20.5 GB per rank at 8).  The
 standardisation statistics are global (one all-reduce of Σx, Σx², n).  The
 C4 network trains through GraphedVAETrainer: one HIP-graph replay per step
-with the flat-gradient RCCL all-reduce captured inside it.  Then every rank
+with the flat-gradient RCCL all-reduce captured inside it; ``--sweep`` grid
+points each build a fresh model and trainer and close it (graph, then its
+RCCL communicator) before the next, as the reference's sweep does.  Then every rank
 encodes its calibration rows and the latent statistics of
 utils/final_vaesimca.py:428-442 (latent Gram, T² / Q percentiles) and the
 f-distance moments of :510-523 are all-reduced, so the thresholds are the
@@ -37,6 +39,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--latent-rows", type=int, default=262144, help="calibration rows encoded per rank")
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--sweep", type=int, default=3,
+                    help="grid points: a fresh model + trainer per point, each closed after its steps "
+                         "(utils/final_vaesimca.py:312-351); the last point's model scores the latents")
     ap.add_argument("--dump", default=None, help="rank 0: save latents, Q and the SIMCA-on-latents outputs (.npz)")
     args = ap.parse_args()
 
@@ -79,32 +84,36 @@ def main():
     torch.cuda.synchronize()
     t_data = time.perf_counter() - t0
 
-    torch.manual_seed(0)
-    m = V.ConvVAE1D(L, 32, mean.float().cpu().numpy(), std.float().cpu().numpy(), conv_blocks=3, n_filters=3,
-                    kernel_size=7, hidden_fc=64).to(dev)
-    tr = GraphedVAETrainer(m, B, lr=1e-3, dtype=torch.bfloat16, group=group)
     nb = max(1, nloc // B)
 
     def batch(i):
         j = i % nb
         return X[j * B:(j + 1) * B]
 
-    for i in range(args.warmup):
-        tr.step(batch(i))
-    loss0 = float(tr.out[0].item()) if args.warmup else float("nan")
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for i in range(args.steps):
-        tr.step(batch(args.warmup + i))
-    torch.cuda.synchronize()
-    dt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    dt = float(dt.item())
-    loss = float(tr.out[0].item())
-    tr.sync_buffers()
+    point_s = []
+    for point in range(max(1, args.sweep)):
+        torch.manual_seed(point)
+        m = V.ConvVAE1D(L, 32, mean.float().cpu().numpy(), std.float().cpu().numpy(), conv_blocks=3, n_filters=3,
+                        kernel_size=7, hidden_fc=64).to(dev)
+        with GraphedVAETrainer(m, B, lr=1e-3, dtype=torch.bfloat16, group=group) as tr:
+            for i in range(args.warmup):
+                tr.step(batch(i))
+            loss0 = float(tr.out[0].item()) if args.warmup else float("nan")
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for i in range(args.steps):
+                tr.step(batch(args.warmup + i))
+            torch.cuda.synchronize()
+            dt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            dt = float(dt.item())
+            loss = float(tr.out[0].item())
+            tr.sync_buffers()
+        point_s.append(dt)
+    dt = sum(point_s) / len(point_s)  # mean over the grid points
 
     # SIMCA-on-latents: calibration latents and reconstruction residuals of
     # this rank's rows, global statistics
@@ -150,6 +159,7 @@ def main():
             "config": {"workload": f"ConvVAE1D cb=3 nf=3 ks=7 hid=64 d=32, B={B}/rank, L={L}, "
                                    f"{args.rows} rows global ({hi - lo} on rank 0), grad all-reduce in the step graph",
                        "params": sum(p.numel() for p in m.parameters())},
+            "sweep_points": len(point_s), "point_ms_per_step": [round(t / args.steps * 1e3, 4) for t in point_s],
             "loss_after_warmup": round(loss0, 5), "final_loss": round(loss, 5), "data_gen_s": round(t_data, 2),
             "params_finite": all(bool(torch.isfinite(p_).all()) for p_ in m.parameters()),
             "latents": {"rows_per_rank": nl, "encode_s": round(t_enc, 3), "stats_s": round(t_stats, 4),
@@ -158,11 +168,9 @@ def main():
         }), flush=True)
     if world > 1:
         dist.barrier()
-    sys.stdout.flush()
-    # leave without tearing the communicator down under the captured step graph
-    # (a live graph still references it; tests/c4_ddp_worker.py does the same)
-    os._exit(0)
+        dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

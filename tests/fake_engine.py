@@ -20,6 +20,12 @@ def as_device_f32(X, device=None):
     return t.to(torch.float32).contiguous()
 
 
+def as_device_x(X, device=None):
+    """ocm.engine.as_device_x: float64 stays float64, anything else float32."""
+    t = X if isinstance(X, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(X))
+    return (t.to(torch.float64) if t.dtype == torch.float64 else t.to(torch.float32)).contiguous()
+
+
 def _rows(X, rows, n):
     Xn = X.numpy()
     if rows is None:
@@ -228,10 +234,29 @@ def score(X, rows, m, P64, mean64, A, want_T=False, want_T2=True, want_Q=True, d
     if decision is not None:
         d = _dred(decision.type, out["T2"].numpy() * decision.t2_scale,
                   out["Q"].numpy().astype(np.float64) * decision.q_scale)
-        accept_out[::accept_stride][:m].copy_(torch.from_numpy((d < decision.dlim).astype(np.float64)))
+        acc = torch.from_numpy((d < decision.dlim).astype(np.float64))
+        if accept_out.dim() == 2:  # a column of the (m, C) prediction matrix
+            accept_out[:m, 0].copy_(acc)
+        else:
+            accept_out[::accept_stride][:m].copy_(acc)
     if not want_T:
         out["T"] = None
     return out
+
+
+def decide(T2, Q, decision, want_red=True, want_dred=False, accept_out=None, accept_stride=1):
+    t = T2.numpy() * decision.t2_scale
+    q = Q.numpy().astype(np.float64) * decision.q_scale
+    d = _dred(decision.type, t, q)
+    return (torch.from_numpy(t) if want_red else None, torch.from_numpy(q) if want_red else None,
+            torch.from_numpy(d) if want_dred else None)
+
+
+def confusion_counts(accept, positive, stride=1):
+    m = positive.numel()
+    a = (accept[:m, 0] if accept.dim() == 2 else accept[::stride][:m]).numpy() == 1
+    pos = positive.numpy().astype(bool)
+    return torch.tensor([np.sum(a & pos), np.sum(~a & ~pos), np.sum(a & ~pos), np.sum(~a & pos)], dtype=torch.int64)
 
 
 class _Fit:

@@ -5,7 +5,7 @@ histograms, the device all-gather of the pooled predictions) over a REAL RCCL
 process group of one rank, against the same engine without a group.  One
 process per GPU is all a one-GPU box allows, so the collectives are RCCL's
 one-rank forms — but every nccl branch of the engine runs.  Prints one JSON
-line and leaves without tearing the communicator down."""
+line, destroys the process group and returns normally."""
 import json
 import os
 import socket
@@ -48,9 +48,9 @@ def main():
                       "sens": [r["sens"] for r in got], "sens_ref": [r["sens"] for r in ref],
                       "pred_diff": int(sum(int((np.asarray(a["prediction"]) != np.asarray(b["prediction"])).sum())
                                            for a, b in zip(gby, rby)))}), flush=True)
-    sys.stdout.flush()
-    os._exit(0)
+    dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

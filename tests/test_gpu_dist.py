@@ -315,12 +315,83 @@ def test_cv_dropin_under_process_group_shards_and_matches(tmp_path, golden_dir):
         np.testing.assert_allclose(got["spec"], ref["spec"], atol=1e-9)
         np.testing.assert_allclose(got["sens"], ref["sens"], atol=1e-9)
         diff = got["pred"] != ref["pred"]
-        assert diff.sum() <= 2 * got["pred"].shape[0], int(diff.sum())  # boundary rows only
+        # the sharded fold Grams sum in another order: at most two boundary
+        # flips over all 24 records' pooled predictions
+        print("pooled prediction flips:", int(diff.sum()), "rows:", np.flatnonzero(diff.any(0)).tolist())
+        assert diff.sum() <= 2, int(diff.sum())
         assert int(got["best_lv"]) == int(ref["best_lv"])
         np.testing.assert_allclose(got["q"], g["q"], rtol=1e-5)
         np.testing.assert_allclose(got["h"], g["h"], rtol=1e-4, atol=1e-6)
         np.testing.assert_allclose(got["f"], g["f"], rtol=1e-4)
         np.testing.assert_allclose(got["crit"], g["crit"], rtol=1e-4)
+
+
+def _dropin_data(seed):
+    from oracle import simca_oracle as O
+
+    X = O.synth_spectra(9000, 256, 8, rank=24, seed=seed, outlier_frac=0.05)
+    y = (np.random.default_rng(seed).random(9000) < 0.2).astype(np.int64)  # other-class rows interleaved
+    return X, y
+
+
+DROPIN_CFGS = [dict(type="alt", t2lim="Fdist", qlim="jm"), dict(type="ci", t2lim="perc", qlim="perc")]
+
+
+def _dropin_simca(X, y, cfg):
+    """An unchanged driver's calls (simca_nuts.py:186-189): fit, predict, transform."""
+    from utils import SIMCA
+
+    m = SIMCA(n_components=8, model_class=0, verbose=False, **cfg).fit(X, y)
+    pred = m.predict(X)
+    t2, t2r, q, qr = m.transform(X)
+    info = m._model[0]
+    return {"lim": np.array([info["T2_limit"], info["Q_limit"], float(info["D_limit"])]), "T2": info["T2"],
+            "Q": info["Q"], "T": info["T"], "pred": np.asarray(pred), "tr_t2": t2, "tr_q": q,
+            "sharded": np.array(getattr(m, "_sharded", False))}
+
+
+def _dropin_simca_worker(rank, world, port, path):
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        out = {}
+        for tag, seed in (("same", 31), ("own", 40 + rank)):  # replicated data, then per-rank data
+            X, y = _dropin_data(seed)
+            for i, cfg in enumerate(DROPIN_CFGS):
+                for key, v in _dropin_simca(X, y, cfg).items():
+                    out[f"{tag}_{key}{i}"] = v
+        np.savez(f"{path}.{rank}.npz", **out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_simca_dropin_under_process_group(tmp_path):
+    """an unchanged ``SIMCA(...).fit(X, y); predict(X);
+    transform(X)`` on both ranks of a world-2 group.  With the same X and y it
+    runs row-sharded (one packed all-reduce, per-row arrays all-gathered) and
+    equals the single-process run (limits rtol 1e-5, T² / Q rtol 1e-4, at most
+    two boundary rows); with different X per rank each rank gets exactly its
+    own single-process result (utils/SIMCA.py:27-154 is per process)."""
+    path = str(tmp_path / "dropin_simca")
+    _spawn(_dropin_simca_worker, path)
+    for r in range(2):
+        got = np.load(f"{path}.{r}.npz")
+        for tag, seed, sharded in (("same", 31, True), ("own", 40 + r, False)):
+            X, y = _dropin_data(seed)
+            for i, cfg in enumerate(DROPIN_CFGS):
+                ref = _dropin_simca(X, y, cfg)
+                assert bool(got[f"{tag}_sharded{i}"]) == sharded, (tag, r)
+                # per-rank data: the same single-process computation in another process
+                tol = dict(rtol=1e-5) if sharded else dict(rtol=1e-9)
+                np.testing.assert_allclose(got[f"{tag}_lim{i}"], ref["lim"], **tol)
+                tol = dict(rtol=1e-4, atol=1e-6) if sharded else dict(rtol=1e-9, atol=1e-12)
+                for key in ("T2", "Q", "tr_t2", "tr_q"):
+                    np.testing.assert_allclose(got[f"{tag}_{key}{i}"], ref[key], **tol, err_msg=f"{tag} {key} {cfg}")
+                np.testing.assert_allclose(np.abs(got[f"{tag}_T{i}"]), np.abs(ref["T"]), rtol=1e-3, atol=1e-3)
+                diff = got[f"{tag}_pred{i}"] != ref["pred"]
+                assert diff.sum() <= (2 if sharded else 0), (tag, cfg, int(diff.sum()))
 
 
 def test_cv_engine_over_rccl_world1():

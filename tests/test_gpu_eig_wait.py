@@ -1,0 +1,55 @@
+"""The eigensolver's in-flight hand-off of S: the Rayleigh–Ritz
+test fused into the Jacobi (k_jacobi_1b, launch stream) waits, bounded, for
+S from k_rr_resid32 on side stream B.  When the wait gives up (the side stream
+not scheduled within ≈ 1 s) the residuals come back as −1 and the host runs
+the Jacobi + test again behind B's event: the fit must converge to the same
+eigenpairs, never report "NaN in covariance", and count the re-runs.
+
+Each case runs in its own child process (tests/eig_wait_worker.py): the
+product library as built, the same under AMD_SERIALIZE_KERNEL=3 (each launch
+waits for the previous one), and a ``make exp`` build whose wait gives up at
+once (OCM_JACOBI_WAIT_SPINS=0: every test takes the re-run path).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+EXP_LIB = os.path.join(REPO, "ocm-vae-simca_amd", "csrc", "build", "exp", "libocm_jwait0.so")
+
+
+def _run(**env):
+    r = subprocess.run([sys.executable, os.path.join(HERE, "eig_wait_worker.py")], capture_output=True, text=True,
+                       timeout=180, cwd=REPO, env=dict(os.environ, **env))
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def _same(a, b):
+    np.testing.assert_allclose(a["evals"], b["evals"], rtol=1e-12)
+    np.testing.assert_allclose(a["thetas"], b["thetas"], rtol=1e-9)
+    np.testing.assert_allclose(a["P"], b["P"], rtol=1e-9)
+
+
+def test_eig_wait_serialised_kernels_and_forced_timeouts():
+    ref = _run()
+    assert ref["reruns"] == 0
+    ser = _run(AMD_SERIALIZE_KERNEL="3")
+    _same(ser, ref)  # S is launched first, so serialised kernels find it ready
+    if not os.path.exists(EXP_LIB):
+        pytest.skip("exp build libocm_jwait0.so absent (make -C ocm-vae-simca_amd/csrc exp EXP_NAME=jwait0 "
+                    "EXP_FLAGS=-DOCM_JACOBI_WAIT_SPINS=0)")
+    forced = _run(OCM_LIB=EXP_LIB, OCM_ALLOW_EXP_LIB="1")
+    assert forced["lib"] == EXP_LIB
+    print("forced-timeout re-runs:", forced["reruns"], "iterations", forced["iters"], "vs", ref["iters"])
+    assert forced["reruns"] >= 1
+    _same(forced, ref)
