@@ -61,8 +61,8 @@ typedef struct ocm_decision {
 
 int ocm_abi_version(void);
 /* 16 hex digits: the first 64 bits of the SHA-256 of the library's build
- * inputs (csrc/*.hip, its headers and Makefile, in the Makefile's ID_INPUTS
- * order).  The Python binding refuses a library whose id differs from the
+ * inputs (the csrc .hip sources, its headers and Makefile, in the Makefile's
+ * ID_INPUTS order).  The Python binding refuses a library whose id differs from the
  * hash of the sources beside it (a stale prebuilt libocm.so). */
 const char* ocm_build_id(void);
 const char* ocm_last_error(void);

@@ -77,6 +77,18 @@ class GraphedVAETrainer:
         dev = next(self.module.parameters()).device
         self.group = group
         distributed = dist.is_available() and dist.is_initialized()
+        # A ProcessGroupNCCL watchdog that polls a collective's end event while
+        # any stream is capturing is refused by HIP and aborts the process
+        # (round 4, DESIGN.md §5 caveat 5).  Eager collectives the CALLER issued
+        # on its process groups are waited out here, on the watchdogs' own
+        # records (flight recorder), before anything else: from here to the
+        # capture the trainer issues none (its own collectives run on its RCCL
+        # communicator, which no watchdog tracks, ocm/rccl.py).
+        self.pending_at_capture = 0
+        if graph and dev.type == "cuda":
+            from .rccl import wait_pg_collectives_retired
+
+            self.pending_at_capture = wait_pg_collectives_retired(group)
         self.world = dist.get_world_size(group) if distributed else 1
         # data-parallel gradient averaging (None: whenever the world has > 1 rank)
         self.allreduce = (self.world > 1) if grad_allreduce is None else bool(grad_allreduce and distributed)
@@ -244,20 +256,13 @@ class GraphedVAETrainer:
                 self._body()
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        # A ProcessGroupNCCL watchdog that polls a collective's end event while
-        # any stream is capturing is refused by HIP and aborts the process
-        # (round 4, DESIGN.md §5 caveat 5).  The trainer's own collectives are
-        # on its RCCL communicator and never tracked (ocm/rccl.py); eager
-        # collectives the CALLER issued on its process group just before are
-        # waited out on the watchdogs' own records (flight recorder).
+        # (the caller's eager ProcessGroupNCCL collectives were waited out when
+        # the trainer started, __init__)
         mode = "global"
         if self.allreduce:
             if self._comm is None:
                 raise ValueError("GraphedVAETrainer(graph=True) with a gradient all-reduce needs an RCCL ('nccl') "
                                  "process group; pass graph=False for a gloo group")
-            from .rccl import wait_pg_collectives_retired
-
-            self.pending_at_capture = wait_pg_collectives_retired(self.group)
             mode = "thread_local"
         with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.out = self._body()

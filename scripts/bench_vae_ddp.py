@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--sweep", type=int, default=3,
                     help="grid points: a fresh model + trainer per point, each closed after its steps "
                          "(utils/final_vaesimca.py:312-351); the last point's model scores the latents")
+    ap.add_argument("--init-seed", type=int, default=0, help="network init seed of point 0")
+    ap.add_argument("--seed-step", type=int, default=0, help="init seed increment per grid point")
     ap.add_argument("--dump", default=None, help="rank 0: save latents, Q and the SIMCA-on-latents outputs (.npz)")
     args = ap.parse_args()
 
@@ -90,9 +92,9 @@ def main():
         j = i % nb
         return X[j * B:(j + 1) * B]
 
-    point_s = []
+    point_s, point_loss = [], []
     for point in range(max(1, args.sweep)):
-        torch.manual_seed(point)
+        torch.manual_seed(args.init_seed + point * args.seed_step)
         m = V.ConvVAE1D(L, 32, mean.float().cpu().numpy(), std.float().cpu().numpy(), conv_blocks=3, n_filters=3,
                         kernel_size=7, hidden_fc=64).to(dev)
         with GraphedVAETrainer(m, B, lr=1e-3, dtype=torch.bfloat16, group=group) as tr:
@@ -113,6 +115,7 @@ def main():
             loss = float(tr.out[0].item())
             tr.sync_buffers()
         point_s.append(dt)
+        point_loss.append((round(loss0, 5), round(loss, 5)))
     dt = sum(point_s) / len(point_s)  # mean over the grid points
 
     # SIMCA-on-latents: calibration latents and reconstruction residuals of
@@ -160,6 +163,7 @@ def main():
                                    f"{args.rows} rows global ({hi - lo} on rank 0), grad all-reduce in the step graph",
                        "params": sum(p.numel() for p in m.parameters())},
             "sweep_points": len(point_s), "point_ms_per_step": [round(t / args.steps * 1e3, 4) for t in point_s],
+            "point_loss": point_loss,
             "loss_after_warmup": round(loss0, 5), "final_loss": round(loss, 5), "data_gen_s": round(t_data, 2),
             "params_finite": all(bool(torch.isfinite(p_).all()) for p_ in m.parameters()),
             "latents": {"rows_per_rank": nl, "encode_s": round(t_enc, 3), "stats_s": round(t_stats, 4),
