@@ -814,6 +814,21 @@ __device__ __forceinline__ void q8_tail(f32x4 (&v)[16], int tid, int cq, int rs,
   auto& pmax = L.u.r.pmax;
   auto& psum = L.u.r.psum;
   float* fmax_ = L.fmax_;
+#ifdef OCM_Q8_DIAG_COPY
+  // timing diagnostic (make exp only; wrong results): no column sums, screen,
+  // scales or digits — the loads, the LDS staging and the digit-plane stores,
+  // i.e. the quantiser's traffic pattern alone
+  (void)wsum; (void)wmax; (void)pmax; (void)psum; (void)fmax_; (void)th; (void)colblk; (void)c0;
+  i32x4 w[3][4];
+#pragma unroll
+  for (int dg = 0; dg < 3; ++dg)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        w[dg][e][k] = (int)(__builtin_bit_cast(uint32_t, v[4 * k][e]) ^ __builtin_bit_cast(uint32_t, v[4 * k + 1][e]) ^
+                            __builtin_bit_cast(uint32_t, v[4 * k + 2][e]) ^ __builtin_bit_cast(uint32_t, v[4 * k + 3][e])) + dg;
+#else
   // column sums over every row (the fix-up does not touch them)
   double cs[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -935,6 +950,7 @@ __device__ __forceinline__ void q8_tail(f32x4 (&v)[16], int tid, int cq, int rs,
       }
     }
   }
+#endif  // OCM_Q8_DIAG_COPY
   // stage image: [group][column 0..31][32 B]; copy-out: 16 B per thread and
   // pass, 1 KiB contiguous per wave instruction (= one group)
   constexpr int GIMG = QC * 32;  // bytes per group image

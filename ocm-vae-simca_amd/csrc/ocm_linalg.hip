@@ -344,9 +344,12 @@ __global__ __launch_bounds__(256, 4) void k_deflate64(const double* __restrict__
 // thread measured 77 µs per launch).
 // ---------------------------------------------------------------------------
 constexpr int CV_W = 8;  // waves per workgroup
-__global__ __launch_bounds__(512) void k_cv32(const double* __restrict__ C, int p, const double* __restrict__ V,
-                                            double* __restrict__ W, double* __restrict__ part,
-                                            unsigned* __restrict__ ticket) {
+// AX (a Chebyshev filter step, below): W = a·(C·V) + bb·V + gc·Vg instead of C·V
+template <bool AX>
+__device__ __forceinline__ void cv32_body(const double* __restrict__ C, int p, const double* __restrict__ V,
+                                          double* __restrict__ W, double* __restrict__ part,
+                                          unsigned* __restrict__ ticket, double a, double bb,
+                                          const double* __restrict__ Vg, double gc) {
   __shared__ double red[CV_W][16 * 33];
   __shared__ int last;
   const int rb = blockIdx.x >> 1, half = blockIdx.x & 1;
@@ -413,7 +416,28 @@ __global__ __launch_bounds__(512) void k_cv32(const double* __restrict__ C, int 
   __syncthreads();
   if (!last) return;
   const double o = part[(int64_t)(blockIdx.x ^ 1) * 512 + tid];
-  if (r0 + orow < p) W[(int64_t)(r0 + orow) * 32 + ocol] = half == 0 ? v + o : o + v;
+  if (r0 + orow < p) {
+    const int64_t e = (int64_t)(r0 + orow) * 32 + ocol;
+    const double cv = half == 0 ? v + o : o + v;
+    if constexpr (AX)
+      W[e] = fma(a, cv, fma(bb, V[e], Vg ? gc * Vg[e] : 0.0));
+    else
+      W[e] = cv;
+  }
+}
+__global__ __launch_bounds__(512) void k_cv32(const double* __restrict__ C, int p, const double* __restrict__ V,
+                                            double* __restrict__ W, double* __restrict__ part,
+                                            unsigned* __restrict__ ticket) {
+  cv32_body<false>(C, p, V, W, part, ticket, 1.0, 0.0, nullptr, 0.0);
+}
+// one step of the three-term Chebyshev recurrence on the block (eig_topk's
+// filtered iterations): W = a·(C·V) + bb·V + g·Vg (Vg nullable), the product as
+// k_cv32's
+__global__ __launch_bounds__(512) void k_cv32x(const double* __restrict__ C, int p, const double* __restrict__ V,
+                                             double* __restrict__ W, double* __restrict__ part,
+                                             unsigned* __restrict__ ticket, double a, double bb,
+                                             const double* __restrict__ Vg, double g) {
+  cv32_body<true>(C, p, V, W, part, ticket, a, bb, Vg, g);
 }
 
 // sum of split-K planes: D[i] = Σ_z P[z][i]
@@ -1593,6 +1617,14 @@ __device__ __forceinline__ double hash_normal(uint64_t a) {
 
 // (+ zeroes nz words at z: the eigensolver's ticket counters, one launch
 // instead of two memsets ahead of it)
+// out = a·x + b·y over n values (the first step of a Chebyshev filter that
+// starts from the Rayleigh–Ritz basis: Y1 = (2/β)·(C·V) − V from W = C·V)
+__global__ void k_axpby(const double* __restrict__ x, const double* __restrict__ y, int64_t n, double a, double b,
+                        double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = fma(a, x[i], b * y[i]);
+}
+
 __global__ void k_randn(double* __restrict__ V, int64_t count, uint64_t seed, unsigned* __restrict__ z0 = nullptr,
                         int nz0 = 0, unsigned* __restrict__ z1 = nullptr, int nz1 = 0) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2563,7 +2595,87 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
   int mslot = 0;
   const double* Sprev = nullptr;  // the Gram the previous plain launch left unfactored (k_cvq32<true>)
   int sslot = 0;
+  // Chebyshev-filtered iterations, from the first failed
+  // Rayleigh–Ritz test on: the test's Ritz values bound the unwanted spectrum
+  // (λ_{b+1} … λ_p ≤ θ_b up to the test's accuracy; C is PSD, so ≥ 0), and a
+  // degree-d Chebyshev polynomial T_d(X), X = 2C/θ_b − I, damps [0, θ_b] to
+  // ≤ 1 while it amplifies λ_k by T_d(2λ_k/θ_b − 1) ≈ e^{d·acosh(2λ_k/θ_b − 1)}
+  // — for a slow gap (λ_k/θ_b = 1 + δ) a rate of e^{−2√δ} per product against
+  // (1 + δ)^{−1} for the plain iteration.  Each product is one three-term step
+  // Y_{j+1} = (4/θ_b)·C·Y_j − 2Y_j − Y_{j−1} (k_cv32x) with no CholQR in
+  // between; a segment ends with one CholQR factor once the block's condition
+  // would pass ≈ 1e6 (T_d(x_1) ≤ 1e6, x_1 = 2θ_1/θ_b − 1), and the next segment
+  // restarts the recurrence from the orthonormalised block.  Before the first
+  // test nothing bounds λ_{b+1} (the bench data converge at that test), so the
+  // plain iterations stay.
+  bool cheb = false;          // filtered continuation active
+  bool cheb_prev = false;     // the interval before the last test was filtered
+  bool y1_from_w = false;     // the segment starts at the Rayleigh–Ritz basis V with C·V = W in hand
+  double cheb_beta = 0.0;
+  int cheb_dmax = 1;
+  auto cheb_degree_cap = [](double x1) {
+    int d = 1;
+    while (d < 8 && std::cosh((d + 1) * std::acosh(x1)) <= 1e6) ++d;
+    return d;
+  };
   for (it = 1; it <= max_iter; ++it) {
+    if (fused && cheb && it < next_rr) {
+      // one filter segment: Y0 (orthonormal) → Y_d, then its CholQR factor
+      const double* Y0 = Wc;
+      if (Mc) {  // Y0 = Wc·Mc
+        hipLaunchKernelGGL(k_cq_apply32, dim3(CQ_G), dim3(256), 0, st, Wc, p, Mc, T1);
+        OCM_CHECK_LAUNCH("k_cq_apply32 cheb");
+        Y0 = T1;
+      }
+      const double a1 = 2.0 / cheb_beta, a2 = 4.0 / cheb_beta;
+      // products in this segment (iterations it .. it + np − 1), degree d
+      const int np = std::max(1, std::min(cheb_dmax - (y1_from_w ? 1 : 0), next_rr - it));
+      const int d = np + (y1_from_w ? 1 : 0);
+      // buffers: intermediates prefer T2, T1, Wa; the last degree lands in a
+      // chain buffer (Wb is never an intermediate, so one is always free)
+      double* pool[4] = {T2, T1, Wa, Wb};
+      const double* ym2 = nullptr;  // Y_{j−2}
+      const double* ym1 = Y0;       // Y_{j−1}
+      for (int j = 1; j <= d; ++j) {
+        double* out = nullptr;
+        if (j == d) {
+          for (double* c2 : {Wa, Wb})
+            if (c2 != ym1 && c2 != ym2 && c2 != Y0) { out = c2; break; }
+        } else {
+          for (double* c2 : pool)
+            if (c2 != ym1 && c2 != ym2 && c2 != Y0) { out = c2; break; }
+        }
+        if (!out) return ocm::fail(OCM_ERR_ARG, "ocm_eig_topk: no free block for the Chebyshev filter");
+        if (j == 1 && y1_from_w) {  // Y1 = X·V = (2/β)·W − V, W = C·V from the test's step
+          hipLaunchKernelGGL(k_axpby, dim3((unsigned)((pb + 255) / 256)), dim3(256), 0, st, W, Y0, (int64_t)pb, a1,
+                             -1.0, out);
+          OCM_CHECK_LAUNCH("k_axpby cheb");
+        } else if (j == 1) {  // Y1 = (2/β)·C·Y0 − Y0
+          hipLaunchKernelGGL(k_cv32x, dim3(2 * cv_rb), dim3(512), 0, st, C, p, Y0, out, cv_part, cv_ticket, a1, -1.0,
+                             nullptr, 0.0);
+          OCM_CHECK_LAUNCH("k_cv32x cheb");
+        } else {  // Y_j = (4/β)·C·Y_{j−1} − 2·Y_{j−1} − Y_{j−2}
+          hipLaunchKernelGGL(k_cv32x, dim3(2 * cv_rb), dim3(512), 0, st, C, p, ym1, out, cv_part, cv_ticket, a2, -2.0,
+                             ym2, -1.0);
+          OCM_CHECK_LAUNCH("k_cv32x cheb");
+        }
+        ym2 = ym1;
+        ym1 = out;
+      }
+      y1_from_w = false;
+      double* Yd = const_cast<double*>(ym1);
+      double* Mn = Mf + 1024 * mslot;
+      hipLaunchKernelGGL(k_cq_gram32<false>, dim3(CQ_G), dim3(256), 0, st, Yd, p, nullptr, nullptr, cq_part, cq_ticket,
+                         1, (uint64_t)(1500 + it), Mn);
+      OCM_CHECK_LAUNCH("k_cq_gram32 cheb");
+      Wc = Yd;
+      Wn = (Yd == Wa) ? Wb : Wa;
+      Mc = Mn;
+      mslot ^= 1;
+      Sprev = nullptr;
+      it += np - 1;  // (the loop adds the last)
+      continue;
+    }
     if (fused && it < next_rr) {  // W ← (C·Wc)·Mc and its factor, one launch
       double* Mn = Mf + 1024 * mslot;
       // the next launch is a plain iteration too: it factors this one's Gram
@@ -2740,14 +2852,44 @@ int eig_topk_impl(ocm_ctx* ctx, const double* C, int32_t p, int32_t k, double to
         break;
       }
       const double tk = std::fabs(hres[k - 1]);
-      double rate = tk > 0 ? std::fabs(hres[b - 1]) / tk : 1.0;
-      if (prev_it > 0 && prev_rmax > 0) rate = std::max(rate, std::pow(rmax / prev_rmax, 1.0 / (it - prev_it)));
+      const double tb = std::fabs(hres[b - 1]), t1 = std::fabs(hres[0]);
+      double rate = tk > 0 ? tb / tk : 1.0;
+      // filtered continuation (above) when θ_b bounds a usable interval
+      const double x1 = tb > 0 ? 2.0 * t1 / tb - 1.0 : 0.0, xk = tb > 0 ? 2.0 * tk / tb - 1.0 : 0.0;
+      int dmax = tb > 0 && x1 > 1.0 && std::isfinite(x1) ? cheb_degree_cap(x1) : 1;
+      // (T_2(x_1) > 1e6: a filter of degree 2 would already pass the condition
+      // budget — the plain iteration stays)
+#ifdef OCM_EIG_NO_CHEB  // make exp A/B: the plain iterations throughout
+      const bool use_cheb = false;
+#else
+      const bool use_cheb = dmax >= 2 && tk > tb * (1.0 + 1e-12);
+#endif
+      if (use_cheb) {
+        // per product: e^{−acosh(x_k)}, less the restarts' factor ½ per segment
+        rate = std::exp(-std::acosh(xk)) * std::pow(2.0, 1.0 / dmax);
+      }
+      const bool measured_same = !use_cheb || cheb_prev;  // the last interval ran the same iteration
+      if (prev_it > 0 && prev_rmax > 0 && measured_same)
+        rate = std::max(rate, std::pow(rmax / prev_rmax, 1.0 / (it - prev_it)));
       int ahead = 1;
       if (rate < 0.999) ahead = (int)std::ceil(std::log(target / rmax) / std::log(std::max(rate, 1e-3)));
       ahead = std::max(1, std::min(ahead, 64));
       next_rr = std::min(it + ahead, max_iter);
       prev_it = it;
       prev_rmax = rmax;
+      cheb_prev = use_cheb;
+      if (use_cheb && next_rr > it + 1) {
+        // the filter starts at the orthonormal basis V, whose C·V = W is in hand
+        cheb = true;
+        cheb_beta = tb;
+        cheb_dmax = dmax;
+        y1_from_w = true;
+        Wc = V;
+        Mc = nullptr;
+        Sprev = nullptr;
+        continue;
+      }
+      cheb = false;
       // the chain continues from W = C·V (span is all it needs) and its factor
       OCM_HIP(hipMemcpyAsync(Wa, W, pb * sizeof(double), hipMemcpyDeviceToDevice, st));
       hipLaunchKernelGGL(k_cq_gram32<false>, dim3(CQ_G), dim3(256), 0, st, Wa, p, nullptr, nullptr, cq_part, cq_ticket,

@@ -45,8 +45,10 @@ def test_eig_wait_serialised_kernels_and_forced_timeouts():
     assert ref["reruns"] == 0
     ser = _run(AMD_SERIALIZE_KERNEL="3")
     _same(ser, ref)  # S is launched first, so serialised kernels find it ready
-    if not os.path.exists(EXP_LIB):
-        pytest.skip("exp build libocm_jwait0.so absent (make -C ocm-vae-simca_amd/csrc exp EXP_NAME=jwait0 "
+    from ocm._lib import file_build_id, source_build_id
+
+    if not os.path.exists(EXP_LIB) or file_build_id(EXP_LIB) != source_build_id():
+        pytest.skip("exp build libocm_jwait0.so absent or built from other sources (make -C ocm-vae-simca_amd/csrc exp EXP_NAME=jwait0 "
                     "EXP_FLAGS=-DOCM_JACOBI_WAIT_SPINS=0)")
     forced = _run(OCM_LIB=EXP_LIB, OCM_ALLOW_EXP_LIB="1")
     assert forced["lib"] == EXP_LIB
