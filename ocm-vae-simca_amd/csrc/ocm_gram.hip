@@ -1077,6 +1077,19 @@ __global__ __launch_bounds__(Q8QS * (QC / 4), 1) void k_q8_quant(const float* __
 // (4 + 2·4HQ)-column window back from the image or the halo table; the row
 // ends use the least-squares edge rows.  The load phase's LDS overlays
 // q8_tail's.
+#ifdef OCM_QP_DPP
+// the quad of the lane CTRL's DPP row shift names (row_shr / row_shl inside 16 lanes)
+// (old = 0, not the source: with old == src hipcc (ROCm 7.2) folded the four
+// components' DPP moves into one and copied its result to all four)
+template <int CTRL>
+__device__ __forceinline__ float q8_dpp1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ f32x4 q8_dpp4(f32x4 x) {
+  return f32x4{q8_dpp1<CTRL>(x.x), q8_dpp1<CTRL>(x.y), q8_dpp1<CTRL>(x.z), q8_dpp1<CTRL>(x.w)};
+}
+#endif
 template <int HH>
 struct Q8PrepLds {
   static constexpr int HQ = (HH + 3) / 4, WN = 2 * HH + 1;
@@ -1216,13 +1229,44 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restri
 #pragma unroll
       for (int e = 0; e < 4; ++e) xs[e] = __fsub_rn(xs[e], mrj);
     }
+    const float srj = __shfl(srl[j & 1], j >> 1, 8);
+    const f32x4* hrow = L.halo + (rs * 16 + j) * 2 * HQ;  // this row's halo: [side][quad]
+    float win[4 + 2 * 4 * HQ];  // columns c0 − 4HQ .. c0 + 3 + 4HQ
+#ifdef OCM_QP_DPP
+    // (make exp A/B; measured: the same digits and X′ bit for
+    // bit, and no faster — cheese write-through quantiser 5.95–5.98 against
+    // 5.86–5.95 ms, profiles/r06k_qp_dpp_ab.txt: the LDS row image is not what
+    // holds the fused quantiser back; its VALU work (3310 instructions, the
+    // taps already on packed f32) and the extra X′ write stream are)
+    // the neighbouring quads of the slice by DPP lane shifts
+    // (row_shr / row_shl by s lanes inside the 16-lane DPP row: lanes whose
+    // source falls outside their own eight-lane slice take the halo instead),
+    // the out-of-slice quads from the halo table, which the load phase filled:
+    // nothing waits on this row's own LDS store; the row image only where the
+    // grid's edge workgroups read it (the least-squares edge rows)
+    if (edge_wg) *reinterpret_cast<f32x4*>(row_img + 4 * cq) = xs;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int e = 0; e < 4; ++e) win[4 * HQ + e] = xs[e];
+#pragma unroll
+    for (int sft = 1; sft <= HQ; ++sft) {
+      static_assert(HQ <= 2, "DPP shifts of one or two lanes");
+      f32x4 l4 = sft == 1 ? q8_dpp4<0x111>(xs) : q8_dpp4<0x112>(xs);  // row_shr: quad cq − sft
+      f32x4 r4 = sft == 1 ? q8_dpp4<0x101>(xs) : q8_dpp4<0x102>(xs);  // row_shl: quad cq + sft
+      const int ql = cq - sft, qr = cq + sft;
+      if (ql < 0) l4 = hrow[HQ + ql];
+      if (qr >= Q8QC / 4) r4 = hrow[HQ + (qr - Q8QC / 4)];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        win[4 * (HQ - sft) + e] = l4[e];
+        win[4 * (HQ + sft) + e] = r4[e];
+      }
+    }
+#else
     // the lanes of one row slice exchange their quads through the row image
     // (wave-private: LDS instructions of a wave execute in order)
     *reinterpret_cast<f32x4*>(row_img + 4 * cq) = xs;
     __builtin_amdgcn_wave_barrier();
-    const float srj = __shfl(srl[j & 1], j >> 1, 8);
-    const f32x4* hrow = L.halo + (rs * 16 + j) * 2 * HQ;  // this row's halo: [side][quad]
-    float win[4 + 2 * 4 * HQ];  // columns c0 − 4HQ .. c0 + 3 + 4HQ
 #pragma unroll
     for (int k = 0; k < 1 + 2 * HQ; ++k) {
       const int qp = cq - HQ + k;  // quad of the row image (−HQ .. 8 + HQ − 1)
@@ -1233,6 +1277,7 @@ __global__ __launch_bounds__(Q8QT, 1) void k_q8_quant_prep(const float* __restri
 #pragma unroll
       for (int e = 0; e < 4; ++e) win[4 * k + e] = t4[e];
     }
+#endif
     f32x4 y;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
