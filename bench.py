@@ -392,11 +392,14 @@ def run_prep(args, rk, n_total):
     for name, (snv, w) in {"nuts_snv_sg5_d1": (True, 5), "cheese_sg15_d1": (False, 15)}.items():
         res = {}
         for mode in ("materialised", "fused", "fused_write"):
+            last = {}
+
             def step():
                 lazy = {"materialised": False, "fused": True, "fused_write": "write"}[mode]
                 Xp = preprocess.snv_savgol(X, w, 2, 1, 1.0, snv=snv, lazy=lazy)
                 model = SIMCA(n_components=k, model_class=0, type="alt", t2lim="Fdist", qlim="jm", verbose=False)
                 model.fit(Xp, y)
+                last["fit"] = model._fits[0]
                 return model.predict(Xp)
 
             step()
@@ -411,7 +414,8 @@ def run_prep(args, rk, n_total):
                          "value": round(n_total * args.steps / dt, 1),
                          "quantise_ms": round(t["quant"][0] / max(t["quant"][1], 1), 4),
                          "score_ms": round(t["score"][0] / max(t["score"][1], 1), 4),
-                         "gram_ms": round(t["gram"][0] / max(t["gram"][1], 1), 4)}
+                         "gram_ms": round(t["gram"][0] / max(t["gram"][1], 1), 4),
+                         "eig_iters": int(last["fit"].eig_iters)}
             if mode != "materialised":
                 res[mode]["materialised_views"] = materialised_count(rk.device.index) - c0
         out[name] = res

@@ -120,7 +120,7 @@ def grid(base_est, X, y, cv, lv_values, param_grid, class_index, store_predictio
     # returns the same records and predictions.  Ranks holding different data
     # run the reference's per-process CV.  Every rank exchanges its
     # fingerprint before anything rank-dependent decides the path.
-    eligible = app is not None and int(X.shape[0]) == int(np.asarray(y).shape[0])
+    eligible = app is not None and y is not None and int(X.shape[0]) == int(np.asarray(y).shape[0])
     group = replicated_group(X, y, eligible)
     if err is not None:
         raise err
