@@ -769,6 +769,16 @@ __device__ __forceinline__ void jrot_fast(double app, double aqq, double apq, do
 #ifndef OCM_JACOBI_WAIT_SPINS           // (make exp: 0 gives up at once, to exercise the re-run)
 #define OCM_JACOBI_WAIT_SPINS OCM_JACOBI_SPINS_1S
 #endif
+#ifdef OCM_JACOBI_STAMPS  // make exp diagnostic: wall-clock stamps of k_jacobi_1b's phases (100 MHz)
+__device__ unsigned long long g_jac_st[16][64];
+// wave 0 stores the stamp at 64 lane addresses (a vector store)
+#define JAC_STAMP(slot_)                                              \
+  do {                                                                \
+    if (tid < 64) g_jac_st[(slot_)][tid] = wall_clock64();           \
+  } while (0)
+#else
+#define JAC_STAMP(slot_)
+#endif
 template <int NF>
 __global__ __launch_bounds__(320) void k_jacobi_1b(const double* __restrict__ Ain, int max_sweeps,
                                                    double* __restrict__ evals, double* __restrict__ Zout,
@@ -786,6 +796,7 @@ __global__ __launch_bounds__(320) void k_jacobi_1b(const double* __restrict__ Ai
   // chain's (deflation, quantiser, Gram) waves, which took ≈ 20 % of its issue
   // slots (128 against 107 µs alone, r05s4)
   __builtin_amdgcn_s_setprio(3);
+  JAC_STAMP(0);
   for (int e = tid; e < NF * NF; e += NT) {
     const int i = e / NF, j = e % NF;
     A[0][i][j] = 0.5 * (Ain[i * NF + j] + Ain[j * NF + i]);
@@ -809,6 +820,7 @@ __global__ __launch_bounds__(320) void k_jacobi_1b(const double* __restrict__ Ai
   __syncthreads();
   int cur = 0, sweep = 0;
   for (; sweep < max_sweeps; ++sweep) {
+    if (sweep < 12) JAC_STAMP(1 + sweep);
     double off = 0.0, dg = 0.0;
     for (int e = tid; e < NF * NF; e += NT) {
       const int i = e / NF, j = e % NF;
@@ -865,6 +877,7 @@ __global__ __launch_bounds__(320) void k_jacobi_1b(const double* __restrict__ Ai
       cur = nx;
     }
   }
+  JAC_STAMP(13);
   int myrank = NF;
   for (int i = tid; i < NF; i += NT) {
     const double li = A[cur][i][i];
@@ -878,6 +891,7 @@ __global__ __launch_bounds__(320) void k_jacobi_1b(const double* __restrict__ Ai
     myrank = rank;
   }
   if (tid == 0 && sweeps_out) *sweeps_out = sweep;
+  JAC_STAMP(14);
   if (!S) return;
   const int nx = cur ^ 1;  // free buffers: S into A[nx], S·Z into Z[nx]
   if (tid == 0) {
@@ -904,6 +918,7 @@ __global__ __launch_bounds__(320) void k_jacobi_1b(const double* __restrict__ Ai
     for (int r = 0; r < NF; ++r) acc = fma(Z[cur][r][tid], Z[nx][r][tid], acc);
     res[myrank] = done ? sqrt(fmax(acc, 0.0)) : -1.0;
   }
+  JAC_STAMP(15);
 }
 
 // ---------------------------------------------------------------------------
@@ -2184,6 +2199,21 @@ int jacobi(const double* A, int n, int max_sweeps, double* ev, double* Z, hipStr
   if (n == 32)
     hipLaunchKernelGGL(k_jacobi_1b<32>, dim3(1), dim3(320), 0, st, A, max_sweeps, ev, Z, nullptr, S, sflag, epoch, k,
                        res, spins);
+#ifdef OCM_JACOBI_STAMPS  // (scripts/jacobi_micro.py, profiles/r06w_jacobi_round_probes.txt)
+  if (n == 32) {
+    static unsigned long long h[16][64];
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_jac_st), sizeof(h));
+    fprintf(stderr, "jacobi32 us: load %.2f", (h[1][0] - h[0][0]) / 100.0);
+    for (int i = 1; i < 13 && h[i + 1][0] > h[i][0] && h[i][0] >= h[1][0]; ++i)
+      fprintf(stderr, " sweep%d %.2f", i - 1, (h[i + 1][0] - h[i][0]) / 100.0);
+    fprintf(stderr, " | rounds %.2f sort+write %.2f", (h[13][0] - h[1][0]) / 100.0, (h[14][0] - h[13][0]) / 100.0);
+    if (S) fprintf(stderr, " test %.2f", (h[15][0] - h[14][0]) / 100.0);
+    fprintf(stderr, "\n");
+    static unsigned long long z[16][64];
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_jac_st), z, sizeof(z));
+  }
+#endif
   else if (n == 48)
     hipLaunchKernelGGL(k_jacobi_blk<48>, dim3(1), dim3(256), 0, st, A, max_sweeps, ev, Z, nullptr);
   else if (n == 64)
