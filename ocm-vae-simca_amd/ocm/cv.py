@@ -200,8 +200,16 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
     K = len(folds)
     lvs = sorted(set(int(v) for v in lv_values))
     lvmax = lvs[-1]
-    if lvmax > p:
-        raise ValueError(f"n_components={lvmax} must be in [1, {p}]")
+    n_target = int(cls_idx.size)
+    # the reference fits each fold's SIMCA on its training rows of the class, LV
+    # by LV in the grid's order, fold by fold (utils/CVSIMCA.py:158-185): the
+    # first LV above min(n_train, p) raises sklearn's ValueError there
+    from utils.SIMCA import check_components
+
+    for lv in lv_values:
+        for f_ in folds:
+            n_tr = n_target - int(f_.size)
+            check_components(int(lv), n_tr, p)
     specs = [_Spec(dict(base_params, **c)) for c in combos]
     theta_mode = max(limits.theta_mode_for(s) for s in specs)
     need_train = any(s.needs_train_stats() for s in specs)
@@ -209,7 +217,6 @@ def cv_grid(X, y, folds, cls_idx, lv_values, combos, base_params, class_index, s
     others = np.setdiff1d(np.arange(n_glob), cls_idx)
     positive_glob = (y == np.asarray(class_index)) if np.ndim(class_index) else (y == class_index)
     positive_glob = np.asarray(positive_glob, dtype=bool).reshape(n_glob)
-    n_target = int(cls_idx.size)
 
     # ---- pass 1: per-fold Grams of the target rows (one HBM pass) ----
     loc_folds = [_local(f, lo, hi) for f in folds]

@@ -151,6 +151,21 @@ def _rates(TP, TN, FP, FN):
     return {"sensitivity": sensitivity, "specificity": specificity, "accuracy": accuracy,
             "efficiency": efficiency, "TP": TP, "TN": TN, "FP": FP, "FN": FN}
 
+def check_components(k: int, n: int, p: int):
+    """The reference fits PCA(n_components=k) on each class (utils/SIMCA.py:73), so
+    k > min(n, p) raises sklearn's ValueError (sklearn/decomposition/_pca.py,
+    ``_fit``); the same message here, before any device work.  The solver it
+    names is the one svd_solver='auto' picks for an n×p class matrix when k
+    cannot fit (a tall, narrow matrix takes 'covariance_eigh', any other 'full')."""
+    if k > min(n, p):
+        solver = "covariance_eigh" if p <= 1000 and n >= 10 * p else "full"
+        raise ValueError(f"n_components={k} must be between 0 and min(n_samples, n_features)={min(n, p)} "
+                         f"with svd_solver='{solver}'")
+
+
+_check_components = check_components
+
+
 class SIMCA(BaseEstimator, ClassifierMixin):
     def __init__(self, n_components=2, model_class=None, type: str = "alt", t2lim="Fdist", t2cl=0.95, qlim="jm",
                  qcl=0.95, dcl=0.95, maxPC=20, criteria="compl", verbose=True):
@@ -207,6 +222,7 @@ class SIMCA(BaseEstimator, ClassifierMixin):
             for i, cls in enumerate(self.model_class):
                 mask = lab_h == cls
                 counts = [int(mask[a:b].sum()) for a, b in bounds]
+                _check_components(int(self.n_components[i]), sum(counts), X.shape[1])
                 rows = None if counts[rank] == hi - lo else \
                     torch.from_numpy(np.flatnonzero(mask[lo:hi])).to(Xd.device)
                 self._model[cls] = self._fit_one_class(Xd, rows, counts[rank], int(self.n_components[i]),
@@ -218,6 +234,7 @@ class SIMCA(BaseEstimator, ClassifierMixin):
             for i, cls in enumerate(self.model_class):
                 mask = lab == int(cls)
                 n = int(mask.sum().item())
+                _check_components(int(self.n_components[i]), n, Xd.shape[1])
                 rows = None if n == Xd.shape[0] else torch.nonzero(mask).flatten()
                 self._model[cls] = self._fit_one_class(Xd, rows, n, int(self.n_components[i]))
                 self._fits[cls] = self._model[cls]._fit
