@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCM_ABI_VERSION 10
+#define OCM_ABI_VERSION 11
 
 #define OCM_OK 0
 #define OCM_ERR_ARG (-1)         /* invalid argument (maps to ValueError) */
@@ -571,6 +571,14 @@ int ocm_cast_multi(ocm_ctx* ctx, int32_t n, const void* const* src, int32_t src_
                    int32_t dst_dtype, const int64_t* numel, void* stream);
 int ocm_vae_standardise(ocm_ctx* ctx, const float* x, int32_t B, int32_t L, const float* mean, const float* std_,
                         int32_t dtype, void* out, void* stream);
+/* ocm_vae_act_bias_bwd (ABI 11): the backward tail of a bf16 Linear layer (vae_model.py:80-84):
+ *   act 1 (Linear → ELU): gy_out = g · elu'(y), y the pre-activation (torch's elu_backward, float32
+ *   arithmetic rounded to bf16), and gbias_out[c] = Σ_r gy[r, c] (float32 over the rounded values,
+ *   rounded to bf16); act 0 (Linear alone): gbias_out = Σ_r g[r, c], y / gy_out unused.
+ *   g, y, gy_out [dev] B×N bf16 row-major, N a multiple of 8, 16-byte aligned; gbias_out [dev] N bf16.
+ *   One launch instead of torch's elu_backward and sum-reduction kernels. */
+int ocm_vae_act_bias_bwd(ocm_ctx* ctx, int32_t act, const void* g, const void* y, int32_t B, int32_t N, void* gy_out,
+                         void* gbias_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -273,9 +273,115 @@ __global__ __launch_bounds__(VT) void k_standardise(const float* __restrict__ x,
   st_act(out, dt, i, (x[i] - mean[j]) / sd[j]);
 }
 
+// A Linear layer's backward tail (vae_model.py:80-84, fc / fc_dec: Linear →
+// ELU, and fc_mu / fc_logvar: Linear alone), bf16: gy = g·elu'(y) (torch's
+// elu_backward on the pre-activation y, in float32, rounded to bf16) and the
+// bias gradient Σ_rows gy (float32 over the rounded gy, fixed order, rounded
+// to bf16) in one pass, instead of torch's elu_backward and sum kernels.
+// Workgroup: 32 columns × 256 row lanes (N = 6144: 192 workgroups); a thread
+// takes 8 contiguous columns (one 16-byte load per row) of rows rl, rl + 256,
+// …; the 16 row lanes of a wave that share a column group are summed by
+// shuffles, the 16 waves in LDS.
+constexpr int AB_T = 1024, AB_CG = 4, AB_RL = AB_T / AB_CG, AB_U = 2;
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ uint32_t bf_rne(float v) {  // the bf16 bits of v, round to nearest even
+  uint32_t u = __float_as_uint(v);
+  if ((u & 0x7f800000u) != 0x7f800000u) u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+template <int ACT>
+__global__ __launch_bounds__(AB_T) void k_act_bias_bwd(const uint16_t* __restrict__ g, const uint16_t* __restrict__ y,
+                                                       int B, int N, uint16_t* __restrict__ gy,
+                                                       uint16_t* __restrict__ gb) {
+  __shared__ float red[AB_T / 64][AB_CG * 8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cg = lane & (AB_CG - 1);
+  const int rl = wave * (64 / AB_CG) + lane / AB_CG;
+  const int c0 = (blockIdx.x * AB_CG + cg) * 8;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < N) {
+    // AB_U rows per pass, their loads issued together (B = 512: one pass)
+    for (int rb = rl; rb < B; rb += AB_U * AB_RL) {
+      uint4 gv[AB_U], yv[AB_U];
+#pragma unroll
+      for (int u = 0; u < AB_U; ++u) {
+        const int r = rb + u * AB_RL;
+        gv[u] = r < B ? *reinterpret_cast<const uint4*>(g + (int64_t)r * N + c0) : make_uint4(0, 0, 0, 0);
+        if (ACT) yv[u] = r < B ? *reinterpret_cast<const uint4*>(y + (int64_t)r * N + c0) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < AB_U; ++u) {
+        const int r = rb + u * AB_RL;
+        const uint32_t gw[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] = bf_lo(gw[k]);
+          v[2 * k + 1] = bf_hi(gw[k]);
+        }
+        if (ACT) {
+          const uint32_t yw[4] = {yv[u].x, yv[u].y, yv[u].z, yv[u].w};
+          uint32_t o[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float y0 = bf_lo(yw[k]), y1 = bf_hi(yw[k]);
+            const uint32_t r0 = bf_rne(y0 > 0.f ? v[2 * k] : v[2 * k] * expf(y0));
+            const uint32_t r1 = bf_rne(y1 > 0.f ? v[2 * k + 1] : v[2 * k + 1] * expf(y1));
+            v[2 * k] = __uint_as_float(r0 << 16);
+            v[2 * k + 1] = __uint_as_float(r1 << 16);
+            o[k] = r0 | (r1 << 16);
+          }
+          if (r < B) *reinterpret_cast<uint4*>(gy + (int64_t)r * N + c0) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] += v[k];  // rows past B loaded as zeros
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+#pragma unroll
+    for (int o = AB_CG; o < 64; o <<= 1) s[k] += __shfl_xor(s[k], o, 64);
+  }
+  if (lane < AB_CG) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[wave][lane * 8 + k] = s[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < AB_CG * 8) {
+    const int c = blockIdx.x * AB_CG * 8 + threadIdx.x;
+    if (c < N) {
+      float t = 0.f;
+      for (int w = 0; w < AB_T / 64; ++w) t += red[w][threadIdx.x];
+      gb[c] = (uint16_t)bf_rne(t);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int ocm_vae_act_bias_bwd(ocm_ctx* ctx, int32_t act, const void* g, const void* y, int32_t B, int32_t N, void* gy_out,
+                         void* gbias_out, void* stream) {
+  OCM_REQUIRE(ctx && g && gbias_out && (act == 0 || (y && gy_out)), "ocm_vae_act_bias_bwd: NULL argument");
+  OCM_REQUIRE(act == 0 || act == 1, "ocm_vae_act_bias_bwd: act 0 (none) or 1 (ELU)");
+  OCM_REQUIRE(B > 0 && N > 0 && N % 8 == 0, "ocm_vae_act_bias_bwd: B > 0, N a positive multiple of 8");
+  OCM_REQUIRE(((uintptr_t)g | (uintptr_t)(act ? y : g) | (uintptr_t)(act ? gy_out : g)) % 16 == 0,
+              "ocm_vae_act_bias_bwd: 16-byte aligned rows");
+  const dim3 grid((unsigned)((N + AB_CG * 8 - 1) / (AB_CG * 8)));
+  const auto* gp = static_cast<const uint16_t*>(g);
+  if (act)
+    hipLaunchKernelGGL(k_act_bias_bwd<1>, grid, dim3(AB_T), 0, (hipStream_t)stream, gp,
+                       static_cast<const uint16_t*>(y), B, N, static_cast<uint16_t*>(gy_out),
+                       static_cast<uint16_t*>(gbias_out));
+  else
+    hipLaunchKernelGGL(k_act_bias_bwd<0>, grid, dim3(AB_T), 0, (hipStream_t)stream, gp, nullptr, B, N, nullptr,
+                       static_cast<uint16_t*>(gbias_out));
+  OCM_CHECK_LAUNCH("k_act_bias_bwd");
+  return OCM_OK;
+}
 
 int ocm_cast_multi(ocm_ctx* ctx, int32_t n, const void* const* src, int32_t src_dtype, void* const* dst,
                    int32_t dst_dtype, const int64_t* numel, void* stream) {

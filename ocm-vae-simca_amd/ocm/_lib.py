@@ -149,6 +149,8 @@ SIGNATURES = {
     "ocm_eigh_f64": (c_i32, [c_void_p, c_void_p, c_i32, c_void_p, c_i32, c_void_p, c_void_p]),
     "ocm_prep_materialised": (c_i32, [c_void_p, ctypes.POINTER(c_i64)]),
     "ocm_eig_test_reruns": (c_i32, [c_void_p, ctypes.POINTER(c_i64)]),
+    "ocm_vae_act_bias_bwd": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_i32, c_void_p, c_void_p,
+                                     c_void_p]),
     "ocm_prep_rowstats_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p]),
     "ocm_prep_apply_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_i64,
                                    c_void_p]),
@@ -164,7 +166,7 @@ SIGNATURES = {
                                         ctypes.POINTER(OcmDecision), c_void_p, c_i64, c_void_p, c_void_p]),
 }
 
-ABI_VERSION = 10  # include/ocm.h OCM_ABI_VERSION
+ABI_VERSION = 11  # include/ocm.h OCM_ABI_VERSION
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 

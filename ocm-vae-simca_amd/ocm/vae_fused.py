@@ -291,6 +291,46 @@ def cast_bf16(*params, into_zeroed_grads: bool = False):
     return _CastBF16.apply(into_zeroed_grads, *params)
 
 
+class _LinearAct(torch.autograd.Function):
+    """y = x·Wᵀ + b (→ ELU when ``act``) on bf16 tensors, for the bottleneck's
+    Linear layers (vae_model.py:80-84: fc, fc_mu, fc_logvar, fc_dec).  The
+    forward is torch's (hipBLASLt with the bias epilogue, torch's ELU); the
+    backward forms gy = g·elu'(y) and the bias gradient in one libocm launch
+    (ocm_vae_act_bias_bwd) instead of torch's elu_backward and column-sum
+    kernels, then the two GEMMs of the weight and input gradients."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, act):
+        y = torch.addmm(b, x, W.t())
+        ctx.act = bool(act)
+        ctx.save_for_backward(x, W, y if act else None)
+        return torch.nn.functional.elu(y) if act else y
+
+    @staticmethod
+    def backward(ctx, ga):
+        x, W, y = ctx.saved_tensors
+        ga = ga.contiguous()
+        B, N = ga.shape
+        if ga.dtype == torch.bfloat16 and N % 8 == 0:
+            gb = torch.empty(N, dtype=ga.dtype, device=ga.device)
+            gy = torch.empty_like(ga) if ctx.act else ga
+            check(_lib.load().ocm_vae_act_bias_bwd(_h(ga.device), 1 if ctx.act else 0, ptr(ga),
+                                                   ptr(y) if ctx.act else None, B, N, ptr(gy) if ctx.act else None,
+                                                   ptr(gb), stream_handle(ga.device)), "ocm_vae_act_bias_bwd")
+        else:  # (other dtypes / widths: torch's kernels, the same arithmetic)
+            gy = torch.ops.aten.elu_backward(ga, 1.0, 1.0, 1.0, False, y) if ctx.act else ga
+            gb = gy.sum(0)
+        gx = gy.mm(W) if ctx.needs_input_grad[0] else None
+        gW = gy.t().mm(x) if ctx.needs_input_grad[1] else None
+        return gx, gW, gb if ctx.needs_input_grad[2] else None, None
+
+
+def linear_act(x: torch.Tensor, lin: torch.nn.Linear, act: bool) -> torch.Tensor:
+    """``lin(x)`` (→ ELU) through _LinearAct, on ``lin``'s (possibly substituted,
+    bf16) weight and bias."""
+    return _LinearAct.apply(x.to(lin.weight.dtype), lin.weight, lin.bias, act)
+
+
 def standardise(x: torch.Tensor, mean: torch.Tensor, std: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
     """(x − mean) / std per column of a B×L float32 batch, in ``dtype``."""
     B, L = x.shape

@@ -37,22 +37,55 @@ import vae_model as V
 
 __all__ = ["GraphedVAETrainer"]
 
+# the bf16 fused step's bottleneck Linear layers through vae_fused.linear_act
+# (False: torch's autocast Linear + ELU, for A/B runs: scripts/vae_linear_ab.py)
+LINEAR_FUSED = True
+
+
+def _elu_dense(seq, pattern) -> bool:
+    """``seq`` is an nn.Sequential of Linear / ELU(α = 1) / Identity laid out as
+    ``pattern`` ("L", "E", "I")."""
+    kinds = {"L": nn.Linear, "E": nn.ELU, "I": nn.Identity}
+    if not isinstance(seq, nn.Sequential) or len(seq) != len(pattern):
+        return False
+    return all(type(mod) is kinds[k] and (k != "E" or float(mod.alpha) == 1.0) for mod, k in zip(seq, pattern))
+
 
 class _FusedForward(nn.Module):
     """encode → z = μ + ε·exp(½logσ²) and the KL (libocm) → decode, as one
     module so torch.func.functional_call can run it on substituted (bf16)
-    Linear parameters (vae_model.py:116-134)."""
+    Linear parameters (vae_model.py:116-134).  With ``linear_fused`` (the bf16
+    step of the stock layout: ELU, no dropout) the bottleneck's Linear layers
+    run through vae_fused.linear_act, whose backward forms the ELU and bias
+    gradients in one launch per layer."""
 
-    def __init__(self, m, vf):
+    def __init__(self, m, vf, linear_fused=False):
         super().__init__()
         self.m = m
         self._vf = vf
+        self._lin_fused = bool(linear_fused) and _elu_dense(getattr(m, "fc", None), "LEI") \
+            and _elu_dense(getattr(m, "fc_dec", None), "LEILE") \
+            and isinstance(getattr(m, "fc_mu", None), nn.Linear) and isinstance(getattr(m, "fc_logvar", None), nn.Linear)
 
     def forward(self, xin):
-        mu, logvar = self.m.encode(xin)
+        m, la = self.m, self._vf.linear_act
+        if self._lin_fused:  # vae_model.py:116-134 with the Linear layers through linear_act
+            h = la(m.encoder_conv(xin.unsqueeze(1)).flatten(1), m.fc[0], True)
+            mu, logvar = la(h, m.fc_mu, False), la(h, m.fc_logvar, False)
+        else:
+            mu, logvar = m.encode(xin)
         eps = torch.randn_like(mu)
         z, kl = self._vf.bottleneck(mu, logvar, eps)
-        return self.m.decode(z), kl
+        if not self._lin_fused:
+            return m.decode(z), kl
+        h = la(la(z, m.fc_dec[0], True), m.fc_dec[3], True)
+        x = m.decoder_conv(h.view(z.shape[0], m._enc_out_channels, m._enc_out_length)).squeeze(1)
+        L = m.input_length
+        if x.shape[-1] > L:
+            x = x[..., :L]
+        elif x.shape[-1] < L:
+            x = torch.nn.functional.pad(x, (0, L - x.shape[-1]))
+        return x, kl
 
 
 class GraphedVAETrainer:
@@ -130,7 +163,7 @@ class GraphedVAETrainer:
             self._rbufs = vae_fused.ReconBuffers(self.module.spec_mean, self.module.spec_std)
             # bf16 steps: the Linear layers run on bf16 copies of their
             # parameters made in one launch per step (vae_fused.cast_bf16)
-            self._fwd = _FusedForward(self.module, vae_fused)
+            self._fwd = _FusedForward(self.module, vae_fused, linear_fused=dtype == torch.bfloat16 and LINEAR_FUSED)
             self._lin = [("m." + n, p) for n, p in self.module.named_parameters()
                          if p.requires_grad and "." in n
                          and isinstance(self.module.get_submodule(n.rsplit(".", 1)[0]), nn.Linear)]

@@ -442,3 +442,39 @@ def test_cast_bf16_accumulates_into_existing_grads():
     opt.step()  # u.grad is None: u is left alone, w takes its step
     torch.testing.assert_close(u.detach(), u_before)
     assert float((w.detach() - w_before).abs().max()) > 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+@pytest.mark.parametrize("k,n,act", [(6144, 64, True), (64, 32, False), (32, 64, True), (64, 6144, True)])
+def test_linear_act_matches_torch(k, n, act):
+    """vae_fused.linear_act (the bf16 step's bottleneck Linear layers, round 6)
+    against F.linear (+ F.elu) under torch autograd on the same bf16 tensors:
+    the forward is the same torch call; the backward's ELU gradient and bias
+    sum (one ocm_vae_act_bias_bwd launch) match torch's elu_backward + sum to
+    a bf16 rounding, and so do the two GEMM gradients built on them."""
+    from torch import nn
+
+    from ocm import vae_fused as vf
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(k + n)
+    lin = nn.Linear(k, n).to(dev).to(torch.bfloat16)
+    x = torch.randn(512, k, generator=g).to(dev).to(torch.bfloat16)
+    go = torch.randn(512, n, generator=g).to(dev).to(torch.bfloat16)
+    xa = x.clone().requires_grad_(True)
+    out = vf.linear_act(xa, lin, act)
+    out.backward(go)
+    ga = (xa.grad, lin.weight.grad.clone(), lin.bias.grad.clone())
+    lin.weight.grad = lin.bias.grad = None
+    xb = x.clone().requires_grad_(True)
+    ref = torch.nn.functional.linear(xb, lin.weight, lin.bias)
+    ref = torch.nn.functional.elu(ref) if act else ref
+    ref.backward(go)
+    gb = (xb.grad, lin.weight.grad, lin.bias.grad)
+    assert torch.equal(out, ref)
+    for name, a, b in zip(("x", "W", "b"), ga, gb):
+        a, b = a.float(), b.float()
+        err = float((a - b).norm() / b.norm())
+        print(name, "rel err", err)
+        assert err < 1e-2, (name, err)
