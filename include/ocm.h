@@ -579,6 +579,15 @@ int ocm_vae_standardise(ocm_ctx* ctx, const float* x, int32_t B, int32_t L, cons
  *   One launch instead of torch's elu_backward and sum-reduction kernels. */
 int ocm_vae_act_bias_bwd(ocm_ctx* ctx, int32_t act, const void* g, const void* y, int32_t B, int32_t N, void* gy_out,
                          void* gbias_out, void* stream);
+/* ocm_gemm_bf16_sk (ABI 11): C = A·B (+ bias) in bf16 with float32 accumulation, for the VAE bottleneck's
+ *   long-K products (vae_model.py:80-84: fc[0]'s forward, fc_dec[3]'s input gradient), split over K in
+ *   256-deep chunks: A [dev] M×K row-major; B [dev] N×K row-major when b_nk (a Linear weight, C = A·Bᵀ),
+ *   else K×N row-major; bias [dev] N bf16 or NULL; C [dev] M×N row-major.  M, N multiples of 64, K of 256,
+ *   16-byte aligned.  scratch [dev] ocm_gemm_bf16_sk_scratch_bytes(M, N, K) bytes (caller-owned, so a
+ *   captured graph keeps it): float32 partial tiles, summed in chunk order by the second launch. */
+size_t ocm_gemm_bf16_sk_scratch_bytes(int32_t M, int32_t N, int32_t K);
+int ocm_gemm_bf16_sk(ocm_ctx* ctx, int32_t b_nk, const void* A, const void* B, const void* bias, int32_t M, int32_t N,
+                     int32_t K, void* C, void* scratch, void* stream);
 
 #ifdef __cplusplus
 }

@@ -359,9 +359,119 @@ __global__ __launch_bounds__(AB_T) void k_act_bias_bwd(const uint16_t* __restric
   }
 }
 
+// Split-K bf16 GEMM for the bottleneck's long-K products (vae_model.py:80-84):
+// C (M×N, bf16) = A (M×K) · B (+ bias), B given as N×K (BT: a Linear weight in
+// the forward, y = x·Wᵀ) or as K×N (BN: the weight in the input gradient,
+// gx = gy·W); M and N multiples of 64, K of 256.  hipBLASLt runs these shapes
+// with a few workgroups that each walk all of K (fc_dec[3]'s input gradient,
+// 512×64 over K = 6144: 20.6 µs; fc[0]'s forward 8.5 µs,
+// profiles/r06zf_vae_gemm_calls.txt).  Here one workgroup takes a 64×64 tile
+// and one 256-deep chunk of K on v_mfma_f32_16x16x32_bf16 (wave w: rows
+// 16w..16w+15, four 16-column tiles; A fragments straight from memory, BN's
+// chunk staged transposed in LDS), the accumulators flushed into f32 running
+// sums every 128 products; the f32 partial tiles go to caller-owned scratch and
+// k_gemm_sk_reduce sums them in chunk order, adds the bias and rounds to bf16.
+constexpr int SK_KC = 256, SK_PAD = 8;
+using sk_bf16x8 = __attribute__((ext_vector_type(8))) short;
+template <bool BT>
+__global__ __launch_bounds__(256) void k_gemm_sk(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, int M,
+                                                 int N, int K, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[BT ? 1 : 64][SK_KC + SK_PAD];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n16 = lane & 15, kg = lane >> 4;
+  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64, k0 = blockIdx.z * SK_KC;
+  if (!BT) {  // B[k0 .. k0 + 255][n0 .. n0 + 63] → Bs[n][k]
+#pragma unroll
+    for (int r = 0; r < SK_KC * 64 / 8 / 256; ++r) {
+      const int e = tid + 256 * r, k = e >> 3, nn = (e & 7) * 8;
+      const uint4 v = *reinterpret_cast<const uint4*>(B + (int64_t)(k0 + k) * N + n0 + nn);
+      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        Bs[nn + 2 * j][k] = (uint16_t)(wv[j] & 0xffffu);
+        Bs[nn + 2 * j + 1][k] = (uint16_t)(wv[j] >> 16);
+      }
+    }
+    __syncthreads();
+  }
+  f32x4 acc[4], run[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) acc[nt] = run[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint16_t* arow = A + (int64_t)(m0 + 16 * w + n16) * K + k0 + 8 * kg;
+#pragma unroll
+  for (int ks = 0; ks < SK_KC / 32; ++ks) {
+    const sk_bf16x8 a = __builtin_bit_cast(sk_bf16x8, *reinterpret_cast<const f32x4*>(arow + 32 * ks));
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int kk = 32 * ks + 8 * kg;
+      const f32x4 bv = BT ? *reinterpret_cast<const f32x4*>(B + (int64_t)(n0 + 16 * nt + n16) * K + k0 + kk)
+                          : *reinterpret_cast<const f32x4*>(&Bs[BT ? 0 : 16 * nt + n16][kk]);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(sk_bf16x8, bv), acc[nt], 0, 0, 0);
+    }
+    if ((ks & 3) == 3) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        run[nt] += acc[nt];
+        acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+  // D layout: column 16·nt + (lane & 15), rows 4·(lane >> 4) + r
+  float* P = part + (int64_t)blockIdx.z * M * N;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) P[(int64_t)(m0 + 16 * w + 4 * kg + r) * N + n0 + 16 * nt + n16] = run[nt][r];
+}
+
+__global__ __launch_bounds__(VT) void k_gemm_sk_reduce(const float* __restrict__ part, int S, int64_t MN, int N,
+                                                       const uint16_t* __restrict__ bias, uint16_t* __restrict__ C) {
+  const int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x;
+  if (i >= MN) return;
+  float t = 0.f;
+  int s = 0;
+  for (; s + 8 <= S; s += 8) {  // eight loads in flight, added in chunk order
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(s + u) * MN + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t += v[u];
+  }
+  for (; s < S; ++s) t += part[(int64_t)s * MN + i];
+  if (bias) t += __uint_as_float((uint32_t)bias[i % N] << 16);
+  C[i] = (uint16_t)bf_rne(t);
+}
+
 }  // namespace
 
 extern "C" {
+
+size_t ocm_gemm_bf16_sk_scratch_bytes(int32_t M, int32_t N, int32_t K) {
+  return (size_t)(K / SK_KC) * (size_t)M * (size_t)N * sizeof(float);
+}
+
+int ocm_gemm_bf16_sk(ocm_ctx* ctx, int32_t b_nk, const void* A, const void* B, const void* bias, int32_t M, int32_t N,
+                     int32_t K, void* C, void* scratch, void* stream) {
+  OCM_REQUIRE(ctx && A && B && C && scratch, "ocm_gemm_bf16_sk: NULL argument");
+  OCM_REQUIRE(M > 0 && N > 0 && K > 0 && M % 64 == 0 && N % 64 == 0 && K % SK_KC == 0,
+              "ocm_gemm_bf16_sk: M, N multiples of 64, K of 256");
+  OCM_REQUIRE(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0, "ocm_gemm_bf16_sk: 16-byte aligned operands");
+  const int S = K / SK_KC;
+  OCM_REQUIRE(S <= 65535, "ocm_gemm_bf16_sk: K ≤ 256·65535");
+  const dim3 grid((unsigned)(M / 64), (unsigned)(N / 64), (unsigned)S);
+  auto* part = static_cast<float*>(scratch);
+  const auto* a = static_cast<const uint16_t*>(A);
+  const auto* bm = static_cast<const uint16_t*>(B);
+  if (b_nk)
+    hipLaunchKernelGGL(k_gemm_sk<true>, grid, dim3(256), 0, (hipStream_t)stream, a, bm, M, N, K, part);
+  else
+    hipLaunchKernelGGL(k_gemm_sk<false>, grid, dim3(256), 0, (hipStream_t)stream, a, bm, M, N, K, part);
+  OCM_CHECK_LAUNCH("k_gemm_sk");
+  const int64_t MN = (int64_t)M * N;
+  hipLaunchKernelGGL(k_gemm_sk_reduce, dim3((unsigned)((MN + VT - 1) / VT)), dim3(VT), 0, (hipStream_t)stream, part, S,
+                     MN, N, static_cast<const uint16_t*>(bias), static_cast<uint16_t*>(C));
+  OCM_CHECK_LAUNCH("k_gemm_sk_reduce");
+  return OCM_OK;
+}
 
 int ocm_vae_act_bias_bwd(ocm_ctx* ctx, int32_t act, const void* g, const void* y, int32_t B, int32_t N, void* gy_out,
                          void* gbias_out, void* stream) {

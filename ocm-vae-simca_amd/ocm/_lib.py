@@ -151,6 +151,9 @@ SIGNATURES = {
     "ocm_eig_test_reruns": (c_i32, [c_void_p, ctypes.POINTER(c_i64)]),
     "ocm_vae_act_bias_bwd": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_i32, c_void_p, c_void_p,
                                      c_void_p]),
+    "ocm_gemm_bf16_sk_scratch_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
+    "ocm_gemm_bf16_sk": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_i32, c_i32, c_i32, c_void_p,
+                                 c_void_p, c_void_p]),
     "ocm_prep_rowstats_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p]),
     "ocm_prep_apply_f32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_i64, c_i32, c_void_p, c_void_p, c_i64,
                                    c_void_p]),

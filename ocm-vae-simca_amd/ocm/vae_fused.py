@@ -291,17 +291,47 @@ def cast_bf16(*params, into_zeroed_grads: bool = False):
     return _CastBF16.apply(into_zeroed_grads, *params)
 
 
+_SKSCRATCH = {}
+SK_MIN_K = 2048  # the split-K GEMM takes products at least this deep (hipBLASLt: the rest)
+
+
+def _sk_ok(M, N, K, *ts) -> bool:
+    return (M % 64 == 0 and N % 64 == 0 and K % 256 == 0 and K >= SK_MIN_K
+            and all(t.dtype == torch.bfloat16 and t.is_contiguous() for t in ts))
+
+
+def gemm_sk(A: torch.Tensor, B: torch.Tensor, b_nk: bool, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """A·Bᵀ (``b_nk``: B is N×K, a Linear weight) or A·B (B is K×N), + bias, in
+    bf16 with float32 accumulation, split over K (ocm_gemm_bf16_sk).  The float32
+    partials live in a per-shape scratch buffer that is never freed (a captured
+    step graph keeps its pointer)."""
+    M, K = A.shape
+    N = B.shape[0] if b_nk else B.shape[1]
+    key = (A.device.index, M, N, K)
+    buf = _SKSCRATCH.get(key)
+    if buf is None:
+        nb = int(_lib.load().ocm_gemm_bf16_sk_scratch_bytes(M, N, K))
+        buf = _SKSCRATCH[key] = torch.empty((nb + 3) // 4, dtype=torch.float32, device=A.device)
+    C = torch.empty((M, N), dtype=torch.bfloat16, device=A.device)
+    check(_lib.load().ocm_gemm_bf16_sk(_h(A.device), 1 if b_nk else 0, ptr(A), ptr(B), ptr(bias), M, N, K, ptr(C),
+                                       ptr(buf), stream_handle(A.device)), "ocm_gemm_bf16_sk")
+    return C
+
+
 class _LinearAct(torch.autograd.Function):
     """y = x·Wᵀ + b (→ ELU when ``act``) on bf16 tensors, for the bottleneck's
     Linear layers (vae_model.py:80-84: fc, fc_mu, fc_logvar, fc_dec).  The
-    forward is torch's (hipBLASLt with the bias epilogue, torch's ELU); the
-    backward forms gy = g·elu'(y) and the bias gradient in one libocm launch
+    forward is hipBLASLt with its bias epilogue and torch's ELU; the backward
+    forms gy = g·elu'(y) and the bias gradient in one libocm launch
     (ocm_vae_act_bias_bwd) instead of torch's elu_backward and column-sum
-    kernels, then the two GEMMs of the weight and input gradients."""
+    kernels, then the weight gradient (hipBLASLt) and the input gradient
+    (gemm_sk for fc_dec[3]'s K = 6144, else hipBLASLt)."""
 
     @staticmethod
     def forward(ctx, x, W, b, act):
-        y = torch.addmm(b, x, W.t())
+        # (fc[0]'s K = 6144 forward through gemm_sk measured 7.7 + 9.1 µs against
+        # hipBLASLt's 8.5: hipBLASLt keeps the forward, profiles/r06zg_vae_step_trace.md)
+        y = torch.addmm(b, x, W.t()) if b is not None else x.mm(W.t())
         ctx.act = bool(act)
         ctx.save_for_backward(x, W, y if act else None)
         return torch.nn.functional.elu(y) if act else y
@@ -320,7 +350,9 @@ class _LinearAct(torch.autograd.Function):
         else:  # (other dtypes / widths: torch's kernels, the same arithmetic)
             gy = torch.ops.aten.elu_backward(ga, 1.0, 1.0, 1.0, False, y) if ctx.act else ga
             gb = gy.sum(0)
-        gx = gy.mm(W) if ctx.needs_input_grad[0] else None
+        gx = None
+        if ctx.needs_input_grad[0]:  # fc_dec[3]: K = 6144 (vae_model.py:83)
+            gx = gemm_sk(gy, W, False) if _sk_ok(B, W.shape[1], N, gy, W) else gy.mm(W)
         gW = gy.t().mm(x) if ctx.needs_input_grad[1] else None
         return gx, gW, gb if ctx.needs_input_grad[2] else None, None
 

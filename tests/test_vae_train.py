@@ -451,8 +451,9 @@ def test_linear_act_matches_torch(k, n, act):
     """vae_fused.linear_act (the bf16 step's bottleneck Linear layers, round 6)
     against F.linear (+ F.elu) under torch autograd on the same bf16 tensors:
     the forward is the same torch call; the backward's ELU gradient and bias
-    sum (one ocm_vae_act_bias_bwd launch) match torch's elu_backward + sum to
-    a bf16 rounding, and so do the two GEMM gradients built on them."""
+    sum (one ocm_vae_act_bias_bwd launch) and the two GEMM gradients built on
+    them (the K = 6144 input gradient through gemm_sk) match torch's to bf16
+    roundings."""
     from torch import nn
 
     from ocm import vae_fused as vf
@@ -472,9 +473,32 @@ def test_linear_act_matches_torch(k, n, act):
     ref = torch.nn.functional.elu(ref) if act else ref
     ref.backward(go)
     gb = (xb.grad, lin.weight.grad, lin.bias.grad)
-    assert torch.equal(out, ref)
+    assert torch.equal(out, ref)  # the forward is torch's call
     for name, a, b in zip(("x", "W", "b"), ga, gb):
         a, b = a.float(), b.float()
         err = float((a - b).norm() / b.norm())
         print(name, "rel err", err)
         assert err < 1e-2, (name, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+@pytest.mark.parametrize("M,N,K,b_nk,bias", [(512, 64, 6144, True, True), (512, 64, 6144, False, False),
+                                             (128, 192, 2048, True, False), (192, 128, 4096, False, True)])
+def test_gemm_sk_matches_float_reference(M, N, K, b_nk, bias):
+    """vae_fused.gemm_sk (ocm_gemm_bf16_sk, round 6: the bottleneck's K = 6144
+    products split over K) against the float64 product of the same bf16
+    operands, rounded to bf16: within two bf16 roundings everywhere."""
+    from ocm import vae_fused as vf
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    B = torch.randn((N, K) if b_nk else (K, N), generator=g).to(torch.bfloat16)
+    b = torch.randn(N, generator=g).to(torch.bfloat16) if bias else None
+    C = vf.gemm_sk(A.to(dev), B.to(dev), b_nk, b.to(dev) if bias else None).cpu().double()
+    ref = A.double() @ (B.double().t() if b_nk else B.double())
+    if bias:
+        ref = ref + b.double()
+    err = (C - ref).abs() / (ref.abs() + 1e-2 * ref.abs().max())
+    assert float(err.max()) < 2 ** -7, float(err.max())
