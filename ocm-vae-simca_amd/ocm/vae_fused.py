@@ -357,6 +357,44 @@ class _LinearAct(torch.autograd.Function):
         return gx, gW, gb if ctx.needs_input_grad[2] else None, None
 
 
+def _bias_grad(g: torch.Tensor) -> torch.Tensor:
+    """Σ_rows g (ocm_vae_act_bias_bwd with act 0) for a bf16 B×N gradient."""
+    g = g.contiguous()
+    B, N = g.shape
+    if g.dtype != torch.bfloat16 or N % 8:
+        return g.sum(0)
+    gb = torch.empty(N, dtype=g.dtype, device=g.device)
+    check(_lib.load().ocm_vae_act_bias_bwd(_h(g.device), 0, ptr(g), None, B, N, None, ptr(gb),
+                                           stream_handle(g.device)), "ocm_vae_act_bias_bwd")
+    return gb
+
+
+class _LinearPair(torch.autograd.Function):
+    """(x·W1ᵀ + b1, x·W2ᵀ + b2) for two Linear layers on one input (fc_mu and
+    fc_logvar on h, vae_model.py:81-82): the input gradient is one GEMM plus
+    one accumulating GEMM (addmm, β = 1) instead of two GEMMs and autograd's
+    add kernel."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2):
+        ctx.save_for_backward(x, W1, W2)
+        return torch.addmm(b1, x, W1.t()), torch.addmm(b2, x, W2.t())
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        x, W1, W2 = ctx.saved_tensors
+        g1 = x.new_zeros((x.shape[0], W1.shape[0])) if g1 is None else g1.contiguous()
+        g2 = x.new_zeros((x.shape[0], W2.shape[0])) if g2 is None else g2.contiguous()
+        gx = g1.mm(W1).addmm_(g2, W2) if ctx.needs_input_grad[0] else None  # (in place: no copy of the first)
+        return gx, g1.t().mm(x), _bias_grad(g1), g2.t().mm(x), _bias_grad(g2)
+
+
+def linear_pair(x: torch.Tensor, lin1: torch.nn.Linear, lin2: torch.nn.Linear):
+    """``(lin1(x), lin2(x))`` through _LinearPair."""
+    x = x.to(lin1.weight.dtype)
+    return _LinearPair.apply(x, lin1.weight, lin1.bias, lin2.weight, lin2.bias)
+
+
 def linear_act(x: torch.Tensor, lin: torch.nn.Linear, act: bool) -> torch.Tensor:
     """``lin(x)`` (→ ELU) through _LinearAct, on ``lin``'s (possibly substituted,
     bf16) weight and bias."""

@@ -71,7 +71,7 @@ class _FusedForward(nn.Module):
         m, la = self.m, self._vf.linear_act
         if self._lin_fused:  # vae_model.py:116-134 with the Linear layers through linear_act
             h = la(m.encoder_conv(xin.unsqueeze(1)).flatten(1), m.fc[0], True)
-            mu, logvar = la(h, m.fc_mu, False), la(h, m.fc_logvar, False)
+            mu, logvar = self._vf.linear_pair(h, m.fc_mu, m.fc_logvar)
         else:
             mu, logvar = m.encode(xin)
         eps = torch.randn_like(mu)

@@ -3,7 +3,7 @@ set -u
 # vae_fused.linear_act — VAE tests, steps/s A/B, kernel trace of the step.
 cd "${GRAFT_REPO_ROOT}"
 export TMPDIR=/tmp
-OUT=gpurun_out/${TAG:-r06zh}
+OUT=gpurun_out/${TAG:-r06zj}
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests/test_vae_train.py tests/test_gpu_vae.py -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -2 $OUT/tests.log

@@ -502,3 +502,34 @@ def test_gemm_sk_matches_float_reference(M, N, K, b_nk, bias):
         ref = ref + b.double()
     err = (C - ref).abs() / (ref.abs() + 1e-2 * ref.abs().max())
     assert float(err.max()) < 2 ** -7, float(err.max())
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+def test_linear_pair_matches_torch():
+    """vae_fused.linear_pair (fc_mu and fc_logvar on one input, round 6: the
+    input gradient as one GEMM + one accumulating GEMM) against two F.linear
+    calls under torch autograd, bf16."""
+    from torch import nn
+
+    from ocm import vae_fused as vf
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    l1, l2 = nn.Linear(64, 32).to(dev).to(torch.bfloat16), nn.Linear(64, 32).to(dev).to(torch.bfloat16)
+    x = torch.randn(512, 64, generator=g).to(dev).to(torch.bfloat16)
+    g1, g2 = (torch.randn(512, 32, generator=g).to(dev).to(torch.bfloat16) for _ in range(2))
+    xa = x.clone().requires_grad_(True)
+    y1, y2 = vf.linear_pair(xa, l1, l2)
+    torch.autograd.backward([y1, y2], [g1, g2])
+    got = [xa.grad] + [p.grad.clone() for p in (l1.weight, l1.bias, l2.weight, l2.bias)]
+    for p in (l1.weight, l1.bias, l2.weight, l2.bias):
+        p.grad = None
+    xb = x.clone().requires_grad_(True)
+    r1, r2 = torch.nn.functional.linear(xb, l1.weight, l1.bias), torch.nn.functional.linear(xb, l2.weight, l2.bias)
+    torch.autograd.backward([r1, r2], [g1, g2])
+    want = [xb.grad] + [p.grad for p in (l1.weight, l1.bias, l2.weight, l2.bias)]
+    assert torch.equal(y1, r1) and torch.equal(y2, r2)
+    for a, b in zip(got, want):
+        a, b = a.float(), b.float()
+        assert float((a - b).norm() / b.norm()) < 1e-2
