@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OCM_ABI_VERSION 11
+#define OCM_ABI_VERSION 12
 
 #define OCM_OK 0
 #define OCM_ERR_ARG (-1)         /* invalid argument (maps to ValueError) */
@@ -501,6 +501,9 @@ int ocm_bn_bwd(ocm_ctx* ctx, int32_t dtype, const void* x, const void* dy, int32
  *   scratch ≥ ocm_conv1d_scratch_bytes(O, I, K), zero-filled before its first use and reused (it
  *   starts with completion counters that every call leaves zero: the last partial workgroup of
  *   an output group sums the partials — one launch); fixed-order two-stage sums (deterministic).
+ * ocm_conv1d_wgrad_qsum (ABI 12): the same G, and qsum_out[i] = Σ_b Σ_j Q[b][i][j] (ConvTranspose1d's bias
+ *   gradient, Q = dy) in the same launch when Lq = s·Lp and pad + s ≤ K (bf16 operands, the matrix-core
+ *   path: a row of ones in P), else by ocm_chan_sum after it.  scratch as ocm_conv1d_wgrad's.
  * ocm_chan_sum: out[c] = Σ_b Σ_l v[b][c][l] (the bias gradient), C ≤ 284; scratch as above with
  *   O·I·K ≥ C (the same zero-filled, reused memory as the layer's wgrad may serve both). */
 #define OCM_CONV_DOWN 0
@@ -512,6 +515,9 @@ int ocm_conv1d(ocm_ctx* ctx, int32_t mode, int32_t dtype_in, const void* x, int3
 int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, int32_t Lp, int32_t dtype_q,
                      const void* Q, int32_t I, int32_t Lq, int32_t B, int32_t K, int32_t stride, int32_t pad,
                      float* G_out, float* psum_out, void* scratch, void* stream);
+int ocm_conv1d_wgrad_qsum(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, int32_t Lp, int32_t dtype_q,
+                          const void* Q, int32_t I, int32_t Lq, int32_t B, int32_t K, int32_t stride, int32_t pad,
+                          float* G_out, float* qsum_out, void* scratch, void* stream);
 int ocm_chan_sum(ocm_ctx* ctx, int32_t dtype, const void* v, int32_t B, int32_t C, int32_t L, float* out,
                  void* scratch, void* stream);
 
@@ -554,6 +560,15 @@ int ocm_vae_bottleneck_fwd(ocm_ctx* ctx, int32_t dtype, const void* mu, const vo
 int ocm_vae_bottleneck_bwd(ocm_ctx* ctx, int32_t dtype, const void* dz, const float* dkl, const void* mu,
                            const void* logvar, const void* eps, int32_t B, int32_t d, void* dmu_out, void* dlogvar_out,
                            void* stream);
+/* ocm_vae_bottleneck_fwd_ld / _bwd_ld (ABI 12): the same with μ, logσ² (and dμ, dlogσ²) as rows of stride
+ * ld ≥ d — ld = 2d, logvar = mu + d: the packed B×2d output of one [fc_mu; fc_logvar] product
+ * (vae_model.py:81-82), read and written in place; ε, z, dz stay B×d. */
+int ocm_vae_bottleneck_fwd_ld(ocm_ctx* ctx, int32_t dtype, const void* mu, const void* logvar, int32_t ld,
+                              const void* eps, int32_t B, int32_t d, void* z_out, float* kl_out, void* scratch,
+                              void* stream);
+int ocm_vae_bottleneck_bwd_ld(ocm_ctx* ctx, int32_t dtype, const void* dz, const float* dkl, const void* mu,
+                              const void* logvar, int32_t ld, const void* eps, int32_t B, int32_t d, void* dmu_out,
+                              void* dlogvar_out, void* stream);
 int ocm_vae_recon_fwd(ocm_ctx* ctx, int32_t kind, const float* x, int32_t dtype, const void* xs, int32_t B, int32_t L,
                       const float* mean, const float* std, float eps, const float* kl, float beta, float* gxs_out,
                       float* out2, void* scratch, void* stream);
@@ -579,6 +594,12 @@ int ocm_vae_standardise(ocm_ctx* ctx, const float* x, int32_t B, int32_t L, cons
  *   One launch instead of torch's elu_backward and sum-reduction kernels. */
 int ocm_vae_act_bias_bwd(ocm_ctx* ctx, int32_t act, const void* g, const void* y, int32_t B, int32_t N, void* gy_out,
                          void* gbias_out, void* stream);
+/* ocm_vae_linear_act (ABI 12): y = x·Wᵀ + b (bf16, float32 accumulation, rounded to bf16) and a = ELU(y) of
+ * the rounded y (torch's expm1 form) in one launch, for the bottleneck's short-K Linear + ELU layers
+ * (vae_model.py:83-84).  x M×K, W N×K, bias N (nullable), y_out / a_out M×N, all bf16 and row-major;
+ * M, N multiples of 64, K ∈ {32, 64, 128, 256}; x and W 16-byte aligned. */
+int ocm_vae_linear_act(ocm_ctx* ctx, const void* x, const void* W, const void* bias, int32_t M, int32_t N, int32_t K,
+                       void* y_out, void* a_out, void* stream);
 /* ocm_gemm_bf16_sk (ABI 11): C = A·B (+ bias) in bf16 with float32 accumulation, for the VAE bottleneck's
  *   long-K products (vae_model.py:80-84: fc[0]'s forward, fc_dec[3]'s input gradient), split over K in
  *   256-deep chunks: A [dev] M×K row-major; B [dev] N×K row-major when b_nk (a Linear weight, C = A·Bᵀ),

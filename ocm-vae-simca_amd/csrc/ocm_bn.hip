@@ -11,6 +11,8 @@
 // Statistics f32 out (save_mean, save_invstd), math in f32/f64.
 // Semantics = torch.nn.functional.batch_norm(training=True): biased variance
 // for the normalisation, unbiased for running_var, momentum update.
+#include <algorithm>
+
 #include "ocm_internal.h"
 
 namespace {
@@ -19,6 +21,16 @@ constexpr int BN_SPLIT = 64;       // workgroups per channel for the reductions,
 constexpr int BN_SPLIT_MAX = 256;  // and at most
 constexpr int BN_U = 8;            // elements per thread per pass of the reduction kernels (loads issued together)
 constexpr int BN_T = 256;
+// the 16-B-load reductions (k_bn_stats8 / k_bn_bwd_stats8) where the layout
+// allows; OCM_BN_VEC_STATS=0 in the environment selects the scalar-load
+// kernels (A/B runs, scripts/vae_ab.py)
+bool bn_vec_stats() {
+  static const bool on = [] {
+    const char* v = getenv("OCM_BN_VEC_STATS");
+    return !v || v[0] != '0';
+  }();
+  return on;
+}
 
 struct bf16_t {  // raw bfloat16 storage (torch.bfloat16 bit layout)
   uint16_t bits;
@@ -116,6 +128,25 @@ __device__ __forceinline__ bool bn_ticket(double s1, double s2, double* part, un
   return last_arrival2(ticket, c, (unsigned)split, (unsigned)sp);
 }
 
+constexpr int BN_U8 = 4;  // 16-B loads per thread and pass of the vectorised reductions
+
+// the 8-element group e of channel c (e < total = N·L/8: row n = e / L8,
+// positions 8·(e mod L8) …), loaded at a clamped index and zeroed past total
+template <typename T>
+__device__ __forceinline__ void bn_ld8_or0(const T* p, int C, int L8, int c, int e, int total, float (&v)[8]) {
+  const bool ok = e < total;
+  const int ec = ok ? e : 0;
+  const int n = ec / L8, l = (ec - n * L8) * 8;
+  bn_ld8(p, ((int64_t)n * C + c) * (int64_t)(8 * L8) + l, v);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = ok ? v[k] : 0.f;
+}
+
+__device__ __forceinline__ void bn_stats_tail(float a1, float a2, double* red, int N, int L, double* part,
+                                              unsigned* ticket, float eps, float momentum, float* save_mean,
+                                              float* save_invstd, float* running_mean, float* running_var,
+                                              int64_t* nbt);
+
 // grid (split, C): partial Σx, Σx² of channel c over its share of the N·L
 // elements; the channel's last workgroup forms mean / invstd and the running
 // statistics (and counts the batch in num_batches_tracked, channel 0)
@@ -139,6 +170,47 @@ __global__ __launch_bounds__(BN_T) void k_bn_stats(const T* __restrict__ x, int 
       a2 = fmaf(v[r], v[r], a2);
     }
   }
+  bn_stats_tail(a1, a2, red, N, L, part, ticket, eps, momentum, save_mean, save_invstd, running_mean, running_var,
+                nbt);
+}
+
+// the same sums from 16-B loads, eight consecutive positions of one row each
+// (L % 8 = 0, x 16-B aligned), BN_U8 of them in flight per thread: grid
+// (bn_split8, C).  The scalar form issued 2-byte loads, one element per lane
+// (8.4 µs per C4 layer, profiles/r06zj_vae_step_trace.md)
+template <typename T>
+__global__ __launch_bounds__(BN_T) void k_bn_stats8(const T* __restrict__ x, int N, int C, int L,
+                                                    double* __restrict__ part, unsigned* __restrict__ ticket,
+                                                    float eps, float momentum, float* __restrict__ save_mean,
+                                                    float* __restrict__ save_invstd, float* __restrict__ running_mean,
+                                                    float* __restrict__ running_var, int64_t* __restrict__ nbt) {
+  __shared__ double red[BN_T / 64];
+  const int c = blockIdx.y, sp = blockIdx.x, split = gridDim.x;
+  const int L8 = L / 8, total = N * L8, step = split * BN_T;
+  float a1 = 0.f, a2 = 0.f;
+  for (int e0 = sp * BN_T + threadIdx.x; e0 < total; e0 += BN_U8 * step) {
+    float v[BN_U8][8];
+#pragma unroll
+    for (int r = 0; r < BN_U8; ++r) bn_ld8_or0(x, C, L8, c, e0 + r * step, total, v[r]);
+#pragma unroll
+    for (int r = 0; r < BN_U8; ++r)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        a1 += v[r][k];
+        a2 = fmaf(v[r][k], v[r][k], a2);
+      }
+  }
+  bn_stats_tail(a1, a2, red, N, L, part, ticket, eps, momentum, save_mean, save_invstd, running_mean, running_var,
+                nbt);
+}
+
+// the workgroup's sums → the channel's last workgroup forms mean / invstd and
+// the running statistics (and counts the batch in num_batches_tracked, channel 0)
+__device__ __forceinline__ void bn_stats_tail(float a1, float a2, double* red, int N, int L, double* part,
+                                              unsigned* ticket, float eps, float momentum, float* save_mean,
+                                              float* save_invstd, float* running_mean, float* running_var,
+                                              int64_t* nbt) {
+  const int c = blockIdx.y, sp = blockIdx.x, split = gridDim.x;
   const double s1 = block_sum_f64(a1, red);
   const double s2 = block_sum_f64(a2, red);
   if (!bn_ticket(s1, s2, part, ticket, c, sp, split) || threadIdx.x >= 64) return;
@@ -244,6 +316,9 @@ __device__ __forceinline__ float bn_grad(const T* dy, const T* ya, int64_t i) {
   return v > 0.f ? g : g * (v + 1.f);
 }
 
+__device__ __forceinline__ void bn_bwd_tail(float a1, float a2, double* red, double* part, unsigned* ticket,
+                                            double* sums, float* dgamma, float* dbeta);
+
 // grid (split, C): partial Σdz, Σdz·x̂; the channel's last workgroup forms
 // the sums (and dβ, dγ)
 template <typename T, bool ELU>
@@ -274,6 +349,49 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_stats(const T* __restrict__ x, 
       a2 = fmaf(g[r], (xv[r] - mu) * is, a2);
     }
   }
+  bn_bwd_tail(a1, a2, red, part, ticket, sums, dgamma, dbeta);
+}
+
+// the same sums from 16-B loads (L % 8 = 0, x / dy / ya 16-B aligned; see
+// k_bn_stats8): grid (bn_split8, C)
+template <typename T, bool ELU>
+__global__ __launch_bounds__(BN_T) void k_bn_bwd_stats8(const T* __restrict__ x, const T* __restrict__ dy,
+                                                        const T* __restrict__ ya, int N, int C, int L,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd, double* __restrict__ part,
+                                                        unsigned* __restrict__ ticket, double* __restrict__ sums,
+                                                        float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ double red[BN_T / 64];
+  const int c = blockIdx.y, sp = blockIdx.x, split = gridDim.x;
+  const float mu = mean[c], is = invstd[c];
+  const int L8 = L / 8, total = N * L8, step = split * BN_T;
+  constexpr int U = BN_U8 / 2;  // three tensors: two groups of each in flight
+  float a1 = 0.f, a2 = 0.f;
+  for (int e0 = sp * BN_T + threadIdx.x; e0 < total; e0 += U * step) {
+    float g[U][8], xv[U][8], yv[ELU ? U : 1][8];
+#pragma unroll
+    for (int r = 0; r < U; ++r) {  // every load of the pass first
+      bn_ld8_or0(dy, C, L8, c, e0 + r * step, total, g[r]);
+      bn_ld8_or0(x, C, L8, c, e0 + r * step, total, xv[r]);
+      if (ELU) bn_ld8_or0(ya, C, L8, c, e0 + r * step, total, yv[ELU ? r : 0]);
+    }
+#pragma unroll
+    for (int r = 0; r < U; ++r)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float gz = g[r][k];
+        if (ELU) gz = yv[ELU ? r : 0][k] > 0.f ? gz : gz * (yv[ELU ? r : 0][k] + 1.f);
+        a1 += gz;
+        // padded groups: g = 0, so the (0 − μ)·invstd term adds nothing
+        a2 = fmaf(gz, (xv[r][k] - mu) * is, a2);
+      }
+  }
+  bn_bwd_tail(a1, a2, red, part, ticket, sums, dgamma, dbeta);
+}
+
+__device__ __forceinline__ void bn_bwd_tail(float a1, float a2, double* red, double* part, unsigned* ticket,
+                                            double* sums, float* dgamma, float* dbeta) {
+  const int c = blockIdx.y, sp = blockIdx.x, split = gridDim.x;
   const double s1 = block_sum_f64(a1, red);
   const double s2 = block_sum_f64(a2, red);
   if (!bn_ticket(s1, s2, part, ticket, c, sp, split) || threadIdx.x >= 64) return;
@@ -335,6 +453,14 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_apply8(const T* __restrict__ x,
 // scratch of the forward / backward calls: per-(channel, split) partials, the
 // backward's channel sums, then one completion counter per channel (zero
 // before the first call; every call leaves them zero)
+// workgroups per channel of the vectorised reductions: BN_U8 16-B groups per
+// thread in one pass (≥ 1, ≤ bn_split(C): the scratch is laid out for that)
+int bn_split8(int N, int C, int L) {
+  const int64_t g8 = (int64_t)N * (L / 8);
+  const int64_t s = (g8 + (int64_t)BN_T * BN_U8 - 1) / ((int64_t)BN_T * BN_U8);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s, bn_split(C)));
+}
+
 size_t bn_part_doubles(int C) { return (size_t)C * bn_split(C) * 2 + 2 * (size_t)C; }
 size_t bn_scratch(int C) {
   return bn_part_doubles(C) * sizeof(double) + (size_t)C * tickets_per_slot(bn_split(C)) * TICKET_STRIDE * sizeof(unsigned);
@@ -346,10 +472,13 @@ int bn_fwd(ocm_ctx* ctx, const void* x, int N, int C, int L, const float* gamma,
            void* scratch, int act, hipStream_t st) {
   auto* part = static_cast<double*>(scratch);
   auto* ticket = reinterpret_cast<unsigned*>(part + bn_part_doubles(C));
-  const int split = bn_split(C);
-  hipLaunchKernelGGL(k_bn_stats<T>, dim3(split, C), dim3(BN_T), 0, st, static_cast<const T*>(x), N, C, L, part,
-                     ticket, eps, momentum, smean, sinv, rmean, rvar, nbt);
   const bool v8 = L % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+  if (v8 && bn_vec_stats())
+    hipLaunchKernelGGL(k_bn_stats8<T>, dim3(bn_split8(N, C, L), C), dim3(BN_T), 0, st, static_cast<const T*>(x), N, C,
+                       L, part, ticket, eps, momentum, smean, sinv, rmean, rvar, nbt);
+  else
+    hipLaunchKernelGGL(k_bn_stats<T>, dim3(bn_split(C), C), dim3(BN_T), 0, st, static_cast<const T*>(x), N, C, L,
+                       part, ticket, eps, momentum, smean, sinv, rmean, rvar, nbt);
   const dim3 ga(v8 ? (L / 8 + BN_T - 1) / BN_T : (L + BN_T - 1) / BN_T, N * C);
 #define OCM_BN_APPLY(K_, E_) \
   hipLaunchKernelGGL((K_<T, E_>), ga, dim3(BN_T), 0, st, static_cast<const T*>(x), C, L, smean, sinv, gamma, beta, \
@@ -372,10 +501,15 @@ int bn_bwd(ocm_ctx* ctx, const void* x, const void* dy, const void* ya, int N, i
   auto* ticket = reinterpret_cast<unsigned*>(part + bn_part_doubles(C));
   const int split = bn_split(C);
   double* sums = part + (size_t)C * split * 2;
-  hipLaunchKernelGGL((k_bn_bwd_stats<T, ELU>), dim3(split, C), dim3(BN_T), 0, st, static_cast<const T*>(x),
-                     static_cast<const T*>(dy), static_cast<const T*>(ya), N, C, L, smean, sinv, part, ticket, sums,
-                     dgamma, dbeta);
   const auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (bn_vec_stats() && L % 8 == 0 && al(x) && al(dy) && (!ELU || al(ya)))
+    hipLaunchKernelGGL((k_bn_bwd_stats8<T, ELU>), dim3(bn_split8(N, C, L), C), dim3(BN_T), 0, st,
+                       static_cast<const T*>(x), static_cast<const T*>(dy), static_cast<const T*>(ya), N, C, L, smean,
+                       sinv, part, ticket, sums, dgamma, dbeta);
+  else
+    hipLaunchKernelGGL((k_bn_bwd_stats<T, ELU>), dim3(split, C), dim3(BN_T), 0, st, static_cast<const T*>(x),
+                       static_cast<const T*>(dy), static_cast<const T*>(ya), N, C, L, smean, sinv, part, ticket, sums,
+                       dgamma, dbeta);
   if (L % 8 == 0 && al(x) && al(dy) && (!ELU || al(ya)) && al(dx))
     hipLaunchKernelGGL((k_bn_bwd_apply8<T, ELU>), dim3((L / 8 + BN_T - 1) / BN_T, N * C), dim3(BN_T), 0, st,
                        static_cast<const T*>(x), static_cast<const T*>(dy), static_cast<const T*>(ya), C, L,

@@ -266,12 +266,18 @@ __host__ __device__ constexpr int wm_qwp() {  // LDS row of one input channel (b
   return ((7 + (WM_CH - 1) * S + CV_KMAX + 7) / 8) * 8;
 }
 
-template <bool WB, int S, int NTT>
+// QB (ConvTranspose1d, P = x, Q = dy): P gains a row of ones (A row O), whose
+// products G[O][i·K + t] = Σ Q[b][i][l·s + t − pad] sum Q over the positions
+// ≡ t − pad (mod s); for Lq = s·Lp and pad + s ≤ K the s taps t = pad …
+// pad + s − 1 cover every position of Q once, so their sum is Σ_b Σ_j Q[b][i][j]
+// (the bias gradient) at no extra MFMA: A had 16 rows and O ≤ 12 used.
+template <bool WB, bool QB, int S, int NTT>
 __global__ __launch_bounds__(256, 4) void k_conv_wgrad_mfma(const bf16_t* __restrict__ P, int O, int Lp,
                                                          const bf16_t* __restrict__ Q, int I, int Lq, int B, int K,
                                                          int pad, float* __restrict__ part,
                                                          unsigned* __restrict__ ticket, float* __restrict__ G,
                                                          float* __restrict__ db) {
+  static_assert(!(WB && QB), "one sum per launch");
   constexpr int QWP = wm_qwp<S>(), N8 = QWP / 8;
   constexpr int QI = (WM_IMAX * N8 + 255) / 256;  // staged 16-B pieces per thread
   __shared__ __attribute__((aligned(16))) uint16_t Qs[WM_IMAX * QWP];
@@ -280,7 +286,8 @@ __global__ __launch_bounds__(256, 4) void k_conv_wgrad_mfma(const bf16_t* __rest
   const int n = lane & 15, kg = lane >> 4;
   const int ncol = I * K + (WB ? 1 : 0);
   const int NT = (ncol + 15) / 16;
-  const int NOUT = O * ncol;
+  const int OR = O + (QB ? 1 : 0);  // G rows (QB: the ones row O last)
+  const int NOUT = OR * ncol;
   const int cpr = Lp / WM_CH, nch = B * cpr;
   // this lane's column of each N tile: LDS offset i·QWP + t (≥ 0), ones (−2), zero (−1)
   int cb[NTT];
@@ -312,7 +319,9 @@ __global__ __launch_bounds__(256, 4) void k_conv_wgrad_mfma(const bf16_t* __rest
     for (int ks = 0; ks < 2; ++ks) {
       const int pos = l0 + 64 * w + 32 * ks + 8 * kg;
       const f32x4 v = *reinterpret_cast<const f32x4*>(P + ((int64_t)b * O + (n < O ? n : O - 1)) * Lp + pos);
-      av[ks] = __builtin_bit_cast(bf16x8, n < O ? v : f32x4{0.f, 0.f, 0.f, 0.f});
+      const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};  // bf16 1.0
+      av[ks] = n < O ? __builtin_bit_cast(bf16x8, v)
+                     : (QB && n == O ? ones : __builtin_bit_cast(bf16x8, f32x4{0.f, 0.f, 0.f, 0.f}));
     }
   };
   f32x4 acc[NTT], run[NTT];
@@ -412,11 +421,23 @@ __global__ __launch_bounds__(256, 4) void k_conv_wgrad_mfma(const bf16_t* __rest
         st_agent(dst + (int64_t)g * NOUT + e, sm);
       } else {
         const int o = e / ncol, c = e - o * ncol;
-        if (c < I * K) G[(int64_t)o * I * K + c] = sm;
+        if (QB && o == O) red[0][0][c] = sm;  // the ones row, staged (the red tiles are read)
+        else if (c < I * K) G[(int64_t)o * I * K + c] = sm;
         else db[o] = sm;
       }
     }
-    if (ng == 1) return;
+    if (ng == 1) {
+      if constexpr (QB) {  // db[i] = Σ_{t = pad}^{pad + S − 1} G[O][i·K + t]
+        __syncthreads();
+        for (int i = tid; i < I; i += 256) {
+          float sm = 0.f;
+#pragma unroll
+          for (int r = 0; r < S; ++r) sm += red[0][0][i * K + pad + r];
+          db[i] = sm;
+        }
+      }
+      return;
+    }
     tk += (int64_t)ng * TICKET_STRIDE;
     src = dst;
     dst += (int64_t)ng * NOUT;
@@ -504,7 +525,8 @@ size_t ocm_conv1d_scratch_bytes(int32_t O, int32_t I, int32_t K) {
   // VALU wgrad: ≤ WG_MAXSPLIT partials of O·I·(K + 1) (+ the channel sums);
   // matrix-core wgrad: WM_WG + 64 + 4 partials of O·(I·K + 1)
   const int64_t valu = ((int64_t)O * I * (K + 1) + (int64_t)(O > I ? O : I)) * WG_MAXSPLIT;
-  const int64_t mfma = (int64_t)O * (I * K + 1) * (WM_WG + 64 + 4);
+  // (the ones column of the Conv1d bias, or the ones row of the ConvTranspose1d bias)
+  const int64_t mfma = std::max((int64_t)O * (I * K + 1), (int64_t)(O + 1) * I * K) * (WM_WG + 64 + 4);
   return CV_TICKETS * sizeof(unsigned) + (size_t)(valu > mfma ? valu : mfma) * sizeof(float) + 256;
 }
 
@@ -524,9 +546,13 @@ int ocm_conv1d(ocm_ctx* ctx, int32_t mode, int32_t dtype_in, const void* x, int3
                                : launch_conv<true>(dtype_in, dtype_out, x, B, I, Lin, w, bias, O, Lout, K, stride, pad, y, st);
 }
 
-int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, int32_t Lp, int32_t dtype_q,
-                     const void* Q, int32_t I, int32_t Lq, int32_t B, int32_t K, int32_t stride, int32_t pad,
-                     float* G_out, float* psum_out, void* scratch, void* stream) {
+}  // extern "C"
+
+namespace {
+// ocm_conv1d_wgrad (qsum_out = nullptr) and ocm_conv1d_wgrad_qsum (psum_out = nullptr)
+int conv_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, int32_t Lp, int32_t dtype_q, const void* Q,
+               int32_t I, int32_t Lq, int32_t B, int32_t K, int32_t stride, int32_t pad, float* G_out,
+               float* psum_out, float* qsum_out, void* scratch, void* stream) {
   OCM_REQUIRE(ctx && P && Q && G_out && scratch, "ocm_conv1d_wgrad: NULL argument");
   OCM_REQUIRE(B > 0 && O > 0 && I > 0 && Lp > 0 && Lq > 0 && (int64_t)I * ((O + CV_OG - 1) / CV_OG) <= 1024,
               "ocm_conv1d_wgrad: bad shape");
@@ -549,6 +575,10 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
   const int split = std::max(1, std::min({WG_MAXSPLIT, std::max(1, 8192 / groups), want}));
   const bool wb = psum_out != nullptr;
   const int ncol = I * K + (wb ? 1 : 0);
+  // Σ Q rides on the matrix-core launch as a ones row of P when Q's positions
+  // are covered once by the taps pad … pad + s − 1 (k_conv_wgrad_mfma QB)
+  const bool qb = qsum_out != nullptr && Lq == stride * Lp && pad + stride <= K && O + 1 <= WM_OMAX &&
+                  (O + 1) * ncol <= WM_NOUT;
   if (dtype_p == OCM_DTYPE_BF16 && dtype_q == OCM_DTYPE_BF16 && O <= WM_OMAX && I <= WM_IMAX && ncol <= 16 * WM_NT &&
       O * ncol <= WM_NOUT &&
       (stride == 1 || stride == 2) && Lp % WM_CH == 0 && Lq % 8 == 0 && pad <= 7 &&
@@ -557,10 +587,17 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
     const int nch = (int)((int64_t)B * Lp / WM_CH);
     const int nwg = std::min(WM_WG, nch);
     const int nt = (ncol + 15) / 16;
-#define OCM_WM3(WB, S, NTT)                                                                                      \
-  hipLaunchKernelGGL((k_conv_wgrad_mfma<WB, S, NTT>), dim3((unsigned)nwg), dim3(256), 0, st,                     \
-                     static_cast<const bf16_t*>(P), O, Lp, static_cast<const bf16_t*>(Q), I, Lq, B, K, pad, part, \
-                     ticket, G_out, psum_out)
+#define OCM_WM3(WB, S, NTT)                                                                                        \
+  do {                                                                                                             \
+    if (qb)                                                                                                        \
+      hipLaunchKernelGGL((k_conv_wgrad_mfma<false, true, S, NTT>), dim3((unsigned)nwg), dim3(256), 0, st,          \
+                         static_cast<const bf16_t*>(P), O, Lp, static_cast<const bf16_t*>(Q), I, Lq, B, K, pad,   \
+                         part, ticket, G_out, qsum_out);                                                           \
+    else                                                                                                           \
+      hipLaunchKernelGGL((k_conv_wgrad_mfma<WB, false, S, NTT>), dim3((unsigned)nwg), dim3(256), 0, st,            \
+                         static_cast<const bf16_t*>(P), O, Lp, static_cast<const bf16_t*>(Q), I, Lq, B, K, pad,   \
+                         part, ticket, G_out, psum_out);                                                           \
+  } while (0)
 #define OCM_WM(WB, S)                    \
   do {                                   \
     if (nt == 1) OCM_WM3(WB, S, 1);      \
@@ -575,6 +612,7 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
 #undef OCM_WM
 #undef OCM_WM3
     OCM_CHECK_LAUNCH("k_conv_wgrad_mfma");
+    if (qsum_out && !qb) return ocm_chan_sum(ctx, dtype_q, Q, B, I, Lq, qsum_out, scratch, stream);
     return OCM_OK;
   }
   dim3 g((unsigned)split, (unsigned)groups);
@@ -595,7 +633,27 @@ int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, in
 #undef OCM_WG_L
 #undef OCM_WG_K
   OCM_CHECK_LAUNCH("k_conv_wgrad");
+  if (qsum_out)  // the layer's scratch again: stream-ordered, its counters left zero
+    return ocm_chan_sum(ctx, dtype_q, Q, B, I, Lq, qsum_out, scratch, stream);
   return OCM_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ocm_conv1d_wgrad(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, int32_t Lp, int32_t dtype_q,
+                     const void* Q, int32_t I, int32_t Lq, int32_t B, int32_t K, int32_t stride, int32_t pad,
+                     float* G_out, float* psum_out, void* scratch, void* stream) {
+  return conv_wgrad(ctx, dtype_p, P, O, Lp, dtype_q, Q, I, Lq, B, K, stride, pad, G_out, psum_out, nullptr, scratch,
+                    stream);
+}
+
+int ocm_conv1d_wgrad_qsum(ocm_ctx* ctx, int32_t dtype_p, const void* P, int32_t O, int32_t Lp, int32_t dtype_q,
+                          const void* Q, int32_t I, int32_t Lq, int32_t B, int32_t K, int32_t stride, int32_t pad,
+                          float* G_out, float* qsum_out, void* scratch, void* stream) {
+  OCM_REQUIRE(qsum_out, "ocm_conv1d_wgrad_qsum: NULL argument");
+  return conv_wgrad(ctx, dtype_p, P, O, Lp, dtype_q, Q, I, Lq, B, K, stride, pad, G_out, nullptr, qsum_out, scratch,
+                    stream);
 }
 
 int ocm_chan_sum(ocm_ctx* ctx, int32_t dtype, const void* v, int32_t B, int32_t C, int32_t L, float* out,

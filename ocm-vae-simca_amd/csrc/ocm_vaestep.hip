@@ -65,14 +65,18 @@ __device__ __forceinline__ float block_minmax(float v, bool is_max, float* red) 
 
 // z and the KL: one element per thread, the workgroups' KL partials summed
 // by the last one (ocm_internal.h last_arrival2)
-__global__ __launch_bounds__(VT) void k_bottleneck_fwd(const void* mu, const void* lv, const void* eps, int dt,
-                                                        int64_t n, int B, void* z, float* kl, double* part,
+// μ / logσ² (and their gradients) are rows of stride ld (ld = d: separate
+// tensors; ld = 2d, logσ² = μ + d: the packed output of one [fc_mu; fc_logvar]
+// product); z, ε, dz are B×d
+__global__ __launch_bounds__(VT) void k_bottleneck_fwd(const void* mu, const void* lv, int ld, const void* eps, int dt,
+                                                        int64_t n, int B, int d, void* z, float* kl, double* part,
                                                         unsigned* ticket) {
   __shared__ double red[VT / 64];
   const int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x;
   double s = 0.0;
   if (i < n) {
-    const float m = ld_act(mu, dt, i), l = ld_act(lv, dt, i), e = ld_act(eps, dt, i);
+    const int64_t r = i / d, j = r * ld + (i - r * d);
+    const float m = ld_act(mu, dt, j), l = ld_act(lv, dt, j), e = ld_act(eps, dt, i);
     st_act(z, dt, i, m + e * expf(0.5f * l));
     s = 1.0 + (double)l - (double)m * m - exp((double)l);
   }
@@ -85,15 +89,16 @@ __global__ __launch_bounds__(VT) void k_bottleneck_fwd(const void* mu, const voi
 }
 
 __global__ __launch_bounds__(VT) void k_bottleneck_bwd(const void* dz, const float* dkl, const void* mu,
-                                                        const void* lv, const void* eps, int dt, int64_t n, int B,
-                                                        void* dmu, void* dlv) {
+                                                        const void* lv, int ld, const void* eps, int dt, int64_t n,
+                                                        int B, int d, void* dmu, void* dlv) {
   const int64_t i = (int64_t)blockIdx.x * VT + threadIdx.x;
   if (i >= n) return;
+  const int64_t r = i / d, j = r * ld + (i - r * d);
   const float g = dz ? ld_act(dz, dt, i) : 0.f;
   const float k = dkl ? *dkl : 0.f;
-  const float m = ld_act(mu, dt, i), l = ld_act(lv, dt, i), e = ld_act(eps, dt, i);
-  st_act(dmu, dt, i, g + k * m / B);
-  st_act(dlv, dt, i, g * e * 0.5f * expf(0.5f * l) - 0.5f * k * (1.f - expf(l)) / B);
+  const float m = ld_act(mu, dt, j), l = ld_act(lv, dt, j), e = ld_act(eps, dt, i);
+  st_act(dmu, dt, j, g + k * m / B);
+  st_act(dlv, dt, j, g * e * 0.5f * expf(0.5f * l) - 0.5f * k * (1.f - expf(l)) / B);
 }
 
 // one workgroup per row: x̂ = xs·std + mean; BCE-with-logits against t =
@@ -441,9 +446,76 @@ __global__ __launch_bounds__(VT) void k_gemm_sk_reduce(const float* __restrict__
   C[i] = (uint16_t)bf_rne(t);
 }
 
+// The bottleneck's short-K Linear layers with their ELU (vae_model.py:83-84,
+// fc_dec: K = 32 and 64): y = x·Wᵀ + b and a = ELU(y) in one launch, where
+// hipBLASLt's GEMM + torch's ELU took two (≈ 5 + 4.5 µs each,
+// profiles/r06zj_vae_step_trace.md).  One 64×64 tile per workgroup on
+// v_mfma_f32_16x16x32_bf16 (wave w: rows 16w..16w+15, four 16-column tiles),
+// the whole K in registers; y is rounded to bf16 (as the GEMM's output) and
+// the ELU — torch's expm1 form — is taken of the rounded value, so a matches
+// torch's elu of the bf16 y.  y (the backward's ELU input) and a are written.
+template <int KS>
+__global__ __launch_bounds__(256) void k_linear_act(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
+                                                    const uint16_t* __restrict__ bias, int N,
+                                                    uint16_t* __restrict__ Y, uint16_t* __restrict__ Aout) {
+  constexpr int K = 32 * KS;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n16 = lane & 15, kg = lane >> 4;
+  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const uint16_t* arow = X + (int64_t)(m0 + 16 * w + n16) * K + 8 * kg;
+  sk_bf16x8 a[KS], b[4][KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) a[ks] = __builtin_bit_cast(sk_bf16x8, *reinterpret_cast<const f32x4*>(arow + 32 * ks));
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      b[nt][ks] = __builtin_bit_cast(
+          sk_bf16x8, *reinterpret_cast<const f32x4*>(W + (int64_t)(n0 + 16 * nt + n16) * K + 32 * ks + 8 * kg));
+  float bv[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) bv[nt] = bias ? __uint_as_float((uint32_t)bias[n0 + 16 * nt + n16] << 16) : 0.f;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], b[nt][ks], acc, 0, 0, 0);
+    // D layout: column 16·nt + (lane & 15), rows 4·(lane >> 4) + r
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t o = (int64_t)(m0 + 16 * w + 4 * kg + r) * N + n0 + 16 * nt + n16;
+      const uint32_t yb = bf_rne(acc[r] + bv[nt]);
+      const float y = __uint_as_float(yb << 16);
+      Y[o] = (uint16_t)yb;
+      Aout[o] = (uint16_t)bf_rne(y > 0.f ? y : expm1f(y));
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int ocm_vae_linear_act(ocm_ctx* ctx, const void* x, const void* W, const void* bias, int32_t M, int32_t N, int32_t K,
+                       void* y_out, void* a_out, void* stream) {
+  OCM_REQUIRE(ctx && x && W && y_out && a_out, "ocm_vae_linear_act: NULL argument");
+  OCM_REQUIRE(M > 0 && N > 0 && M % 64 == 0 && N % 64 == 0 && (K == 32 || K == 64 || K == 128 || K == 256),
+              "ocm_vae_linear_act: M, N multiples of 64, K ∈ {32, 64, 128, 256}");
+  OCM_REQUIRE(((uintptr_t)x | (uintptr_t)W) % 16 == 0, "ocm_vae_linear_act: 16-byte aligned x and W");
+  OCM_REQUIRE(M / 64 <= 65535 && N / 64 <= 65535, "ocm_vae_linear_act: M, N ≤ 64·65535");
+  const dim3 g((unsigned)(M / 64), (unsigned)(N / 64));
+  const auto* xp = static_cast<const uint16_t*>(x);
+  const auto* wp = static_cast<const uint16_t*>(W);
+  const auto* bp = static_cast<const uint16_t*>(bias);
+  auto* yp = static_cast<uint16_t*>(y_out);
+  auto* ap = static_cast<uint16_t*>(a_out);
+  hipStream_t st = (hipStream_t)stream;
+  if (K == 32) hipLaunchKernelGGL(k_linear_act<1>, g, dim3(256), 0, st, xp, wp, bp, N, yp, ap);
+  else if (K == 64) hipLaunchKernelGGL(k_linear_act<2>, g, dim3(256), 0, st, xp, wp, bp, N, yp, ap);
+  else if (K == 128) hipLaunchKernelGGL(k_linear_act<4>, g, dim3(256), 0, st, xp, wp, bp, N, yp, ap);
+  else hipLaunchKernelGGL(k_linear_act<8>, g, dim3(256), 0, st, xp, wp, bp, N, yp, ap);
+  OCM_CHECK_LAUNCH("k_linear_act");
+  return OCM_OK;
+}
 
 size_t ocm_gemm_bf16_sk_scratch_bytes(int32_t M, int32_t N, int32_t K) {
   return (size_t)(K / SK_KC) * (size_t)M * (size_t)N * sizeof(float);
@@ -540,15 +612,22 @@ size_t ocm_vae_bottleneck_scratch_bytes() { return 4096 * sizeof(double) + ticke
 
 int ocm_vae_bottleneck_fwd(ocm_ctx* ctx, int32_t dtype, const void* mu, const void* logvar, const void* eps, int32_t B,
                            int32_t d, void* z_out, float* kl_out, void* scratch, void* stream) {
+  return ocm_vae_bottleneck_fwd_ld(ctx, dtype, mu, logvar, d, eps, B, d, z_out, kl_out, scratch, stream);
+}
+
+int ocm_vae_bottleneck_fwd_ld(ocm_ctx* ctx, int32_t dtype, const void* mu, const void* logvar, int32_t ld,
+                              const void* eps, int32_t B, int32_t d, void* z_out, float* kl_out, void* scratch,
+                              void* stream) {
   OCM_REQUIRE(ctx && mu && logvar && eps && z_out && kl_out && scratch, "ocm_vae_bottleneck_fwd: NULL argument");
-  OCM_REQUIRE(B > 0 && d > 0 && (dtype == OCM_DTYPE_F32 || dtype == OCM_DTYPE_BF16), "ocm_vae_bottleneck_fwd: bad args");
+  OCM_REQUIRE(B > 0 && d > 0 && ld >= d && (dtype == OCM_DTYPE_F32 || dtype == OCM_DTYPE_BF16),
+              "ocm_vae_bottleneck_fwd: bad args");
   const int64_t n = (int64_t)B * d;
   const int64_t nb = (n + VT - 1) / VT;
   OCM_REQUIRE(nb <= 4096, "ocm_vae_bottleneck_fwd: B·d ≤ 2²⁰");
   auto* part = static_cast<double*>(scratch);
   auto* ticket = reinterpret_cast<unsigned*>(part + 4096);
-  hipLaunchKernelGGL(k_bottleneck_fwd, dim3((unsigned)nb), dim3(VT), 0, (hipStream_t)stream, mu, logvar, eps, dtype,
-                     n, B, z_out, kl_out, part, ticket);
+  hipLaunchKernelGGL(k_bottleneck_fwd, dim3((unsigned)nb), dim3(VT), 0, (hipStream_t)stream, mu, logvar, ld, eps,
+                     dtype, n, B, d, z_out, kl_out, part, ticket);
   OCM_CHECK_LAUNCH("k_bottleneck_fwd");
   return OCM_OK;
 }
@@ -556,11 +635,18 @@ int ocm_vae_bottleneck_fwd(ocm_ctx* ctx, int32_t dtype, const void* mu, const vo
 int ocm_vae_bottleneck_bwd(ocm_ctx* ctx, int32_t dtype, const void* dz, const float* dkl, const void* mu,
                            const void* logvar, const void* eps, int32_t B, int32_t d, void* dmu_out, void* dlogvar_out,
                            void* stream) {
+  return ocm_vae_bottleneck_bwd_ld(ctx, dtype, dz, dkl, mu, logvar, d, eps, B, d, dmu_out, dlogvar_out, stream);
+}
+
+int ocm_vae_bottleneck_bwd_ld(ocm_ctx* ctx, int32_t dtype, const void* dz, const float* dkl, const void* mu,
+                              const void* logvar, int32_t ld, const void* eps, int32_t B, int32_t d, void* dmu_out,
+                              void* dlogvar_out, void* stream) {
   OCM_REQUIRE(ctx && mu && logvar && eps && dmu_out && dlogvar_out, "ocm_vae_bottleneck_bwd: NULL argument");
-  OCM_REQUIRE(B > 0 && d > 0 && (dtype == OCM_DTYPE_F32 || dtype == OCM_DTYPE_BF16), "ocm_vae_bottleneck_bwd: bad args");
+  OCM_REQUIRE(B > 0 && d > 0 && ld >= d && (dtype == OCM_DTYPE_F32 || dtype == OCM_DTYPE_BF16),
+              "ocm_vae_bottleneck_bwd: bad args");
   const int64_t n = (int64_t)B * d;
   hipLaunchKernelGGL(k_bottleneck_bwd, dim3((unsigned)((n + VT - 1) / VT)), dim3(VT), 0, (hipStream_t)stream, dz, dkl,
-                     mu, logvar, eps, dtype, n, B, dmu_out, dlogvar_out);
+                     mu, logvar, ld, eps, dtype, n, B, d, dmu_out, dlogvar_out);
   OCM_CHECK_LAUNCH("k_bottleneck_bwd");
   return OCM_OK;
 }

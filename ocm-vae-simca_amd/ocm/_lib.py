@@ -131,6 +131,8 @@ SIGNATURES = {
                            c_i32, c_i32, c_i32, c_i32, c_void_p, c_void_p]),
     "ocm_conv1d_wgrad": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_i32, c_i32, c_i32,
                                  c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ocm_conv1d_wgrad_qsum": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_i32, c_i32, c_i32,
+                                 c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ocm_chan_sum": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
     "ocm_vae_scratch_bytes": (ctypes.c_size_t, [c_i32]),
     "ocm_vae_bottleneck_scratch_bytes": (ctypes.c_size_t, []),
@@ -138,6 +140,12 @@ SIGNATURES = {
                                        c_void_p, c_void_p, c_void_p]),
     "ocm_vae_bottleneck_bwd": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i32,
                                        c_i32, c_void_p, c_void_p, c_void_p]),
+    "ocm_vae_bottleneck_fwd_ld": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_void_p, c_i32, c_i32,
+                                          c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ocm_vae_bottleneck_bwd_ld": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_void_p, c_void_p, c_i32, c_void_p,
+                                          c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
+    "ocm_vae_linear_act": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p,
+                                   c_void_p]),
     "ocm_vae_recon_fwd": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_void_p, c_i32, c_i32, c_void_p, c_void_p,
                                   ctypes.c_float, c_void_p, ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ocm_vae_recon_bwd": (c_i32, [c_void_p, c_void_p, c_void_p, c_i64, c_i32, c_void_p, ctypes.c_float, c_void_p,
@@ -169,7 +177,7 @@ SIGNATURES = {
                                         ctypes.POINTER(OcmDecision), c_void_p, c_i64, c_void_p, c_void_p]),
 }
 
-ABI_VERSION = 11  # include/ocm.h OCM_ABI_VERSION
+ABI_VERSION = 12  # include/ocm.h OCM_ABI_VERSION
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 

@@ -24,6 +24,10 @@ from ._lib import Context, check, ptr, stream_handle
 
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 DOWN, UP = 0, 1  # include/ocm.h OCM_CONV_DOWN / OCM_CONV_UP
+# ConvTranspose1d's bias gradient inside the weight-gradient launch
+# (ocm_conv1d_wgrad_qsum); False: ocm_conv1d_wgrad + ocm_chan_sum (A/B runs,
+# scripts/vae_ab.py)
+QSUM_FUSED = True
 
 
 def _layer_scratch(mod, O: int, I: int, K: int, dev) -> torch.Tensor:
@@ -87,16 +91,21 @@ class _ConvFn(torch.autograd.Function):
             scratch = ctx.scratch
             db = torch.empty(O, dtype=torch.float32, device=dev) if want_db else None
             dw = torch.empty_like(w)
-            if transposed:  # dW[i][o][t] = Σ x[b][i][l] · dy[b][o][l·s + t − pad]; db = Σ dy separately
-                args = (_DT[x.dtype], ptr(x), I, Lin, _DT[dy.dtype], ptr(dy), O, Lout, B, K, stride, pad, ptr(dw),
-                        None)
+            lib = _lib.load()
+            if transposed:  # dW[i][o][t] = Σ x[b][i][l] · dy[b][o][l·s + t − pad]; db = Σ dy (a ones row of P
+                # in the same matrix-core launch when the taps cover dy once, else ocm_chan_sum after it)
+                args = (_DT[x.dtype], ptr(x), I, Lin, _DT[dy.dtype], ptr(dy), O, Lout, B, K, stride, pad, ptr(dw))
+                if want_db and QSUM_FUSED:
+                    check(lib.ocm_conv1d_wgrad_qsum(h, *args, ptr(db), ptr(scratch), st), "ocm_conv1d_wgrad_qsum")
+                else:
+                    check(lib.ocm_conv1d_wgrad(h, *args, None, ptr(scratch), st), "ocm_conv1d_wgrad")
+                    if want_db:
+                        check(lib.ocm_chan_sum(h, _DT[dy.dtype], ptr(dy), B, O, Lout, ptr(db), ptr(scratch), st),
+                              "ocm_chan_sum")
             else:  # dW[o][i][t] = Σ dy[b][o][l] · x[b][i][l·s + t − pad], db = Σ dy in the same pass
                 args = (_DT[dy.dtype], ptr(dy), O, Lout, _DT[x.dtype], ptr(x), I, Lin, B, K, stride, pad, ptr(dw),
                         ptr(db))
-            check(_lib.load().ocm_conv1d_wgrad(h, *args, ptr(scratch), st), "ocm_conv1d_wgrad")
-            if transposed and want_db:
-                check(_lib.load().ocm_chan_sum(h, _DT[dy.dtype], ptr(dy), B, O, Lout, ptr(db), ptr(scratch), st),
-                      "ocm_chan_sum")
+                check(lib.ocm_conv1d_wgrad(h, *args, ptr(scratch), st), "ocm_conv1d_wgrad")
             if not ctx.needs_input_grad[1]:
                 dw = None
         return dx, dw, db, None, None, None, None, None, None

@@ -88,6 +88,43 @@ class _Bottleneck(torch.autograd.Function):
         return dmu, dlv, None
 
 
+class _BottleneckPacked(torch.autograd.Function):
+    """_Bottleneck on the packed B×2d output of one [fc_mu; fc_logvar] product
+    (μ = ml[:, :d], logσ² = ml[:, d:], read in place: no copies), whose
+    gradient is written packed the same way (ocm_vae_bottleneck_*_ld)."""
+
+    @staticmethod
+    def forward(ctx, ml, eps):
+        ml, eps = ml.contiguous(), eps.contiguous()
+        B, d2 = ml.shape
+        d = d2 // 2
+        z = torch.empty((B, d), dtype=ml.dtype, device=ml.device)
+        kl = torch.empty((), dtype=torch.float32, device=ml.device)
+        off = d * ml.element_size()
+        check(_lib.load().ocm_vae_bottleneck_fwd_ld(_h(ml.device), _DT[ml.dtype], ptr(ml), ptr(ml) + off, d2, ptr(eps),
+                                                    B, d, ptr(z), ptr(kl), ptr(_bottleneck_scratch(ml.device)),
+                                                    stream_handle(ml.device)), "ocm_vae_bottleneck_fwd_ld")
+        ctx.save_for_backward(ml, eps)
+        ctx.set_materialize_grads(False)
+        return z, kl
+
+    @staticmethod
+    def backward(ctx, dz, dkl):
+        ml, eps = ctx.saved_tensors
+        B, d2 = ml.shape
+        d = d2 // 2
+        dml = torch.empty_like(ml)
+        if dz is not None:
+            dz = dz.to(ml.dtype).contiguous()
+        if dkl is not None:
+            dkl = dkl.to(torch.float32).contiguous()
+        off = d * ml.element_size()
+        check(_lib.load().ocm_vae_bottleneck_bwd_ld(_h(ml.device), _DT[ml.dtype], ptr(dz), ptr(dkl), ptr(ml),
+                                                    ptr(ml) + off, d2, ptr(eps), B, d, ptr(dml), ptr(dml) + off,
+                                                    stream_handle(ml.device)), "ocm_vae_bottleneck_bwd_ld")
+        return dml, None
+
+
 class _ReconTotal(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, xs, kl, bufs, kind, beta, eps):
@@ -141,6 +178,11 @@ class ReconBuffers:
 
 def bottleneck(mu, logvar, eps):
     return _Bottleneck.apply(mu, logvar, eps)
+
+
+def bottleneck_packed(ml, eps):
+    """(z, kl) from the packed [μ | logσ²] rows of ``ml`` (B×2d)."""
+    return _BottleneckPacked.apply(ml, eps)
 
 
 def recon_total(x, xs, kl, bufs: ReconBuffers, loss: str, beta: float, eps: float = 1e-8):
@@ -255,7 +297,17 @@ class _CastBF16(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, into_zeroed_grads, *params):
-        outs = [torch.empty_like(p, dtype=torch.bfloat16, memory_format=torch.contiguous_format) for p in params]
+        # one flat bf16 buffer: the matrices first, then the vectors, each in
+        # the given order and 16-B aligned, so the weights (and the biases) of
+        # consecutive layers sit back to back (linear_cat reads [fc_mu; fc_logvar]
+        # as one operand without a copy)
+        order = [i for i, p in enumerate(params) if p.dim() > 1] + [i for i, p in enumerate(params) if p.dim() <= 1]
+        offs, o = [0] * len(params), 0
+        for i in order:
+            offs[i] = o
+            o += (params[i].numel() + 7) // 8 * 8
+        flat = torch.empty(max(o, 1), dtype=torch.bfloat16, device=params[0].device)
+        outs = [flat[offs[i]:offs[i] + p.numel()].view(p.shape) for i, p in enumerate(params)]
         _cast_multi([p.detach().contiguous() for p in params], outs, _DT[torch.float32], _DT[torch.bfloat16],
                     params[0].device)
         ctx.params = params
@@ -292,6 +344,9 @@ def cast_bf16(*params, into_zeroed_grads: bool = False):
 
 
 _SKSCRATCH = {}
+# _LinearAct's forward for K ≤ 256 with its ELU through ocm_vae_linear_act
+# (False: hipBLASLt + torch's elu; A/B runs, scripts/vae_ab.py)
+LINEAR_ACT_FUSED = True
 SK_MIN_K = 2048  # the split-K GEMM takes products at least this deep (hipBLASLt: the rest)
 
 
@@ -329,10 +384,23 @@ class _LinearAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, W, b, act):
+        ctx.act = bool(act)
+        M, K = x.shape
+        N = W.shape[0]
+        if (act and LINEAR_ACT_FUSED and x.dtype == W.dtype == torch.bfloat16 and K in (32, 64, 128, 256)
+                and M % 64 == 0 and N % 64 == 0 and x.is_contiguous() and W.is_contiguous()
+                and (b is None or (b.dtype == torch.bfloat16 and b.is_contiguous()))
+                and x.data_ptr() % 16 == 0 and W.data_ptr() % 16 == 0):
+            # fc_dec's short-K layers: GEMM + bias + ELU in one launch (ocm_vae_linear_act)
+            y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+            a = torch.empty_like(y)
+            check(_lib.load().ocm_vae_linear_act(_h(x.device), ptr(x), ptr(W), ptr(b), M, N, K, ptr(y), ptr(a),
+                                                 stream_handle(x.device)), "ocm_vae_linear_act")
+            ctx.save_for_backward(x, W, y)
+            return a
         # (fc[0]'s K = 6144 forward through gemm_sk measured 7.7 + 9.1 µs against
         # hipBLASLt's 8.5: hipBLASLt keeps the forward, profiles/r06zg_vae_step_trace.md)
         y = torch.addmm(b, x, W.t()) if b is not None else x.mm(W.t())
-        ctx.act = bool(act)
         ctx.save_for_backward(x, W, y if act else None)
         return torch.nn.functional.elu(y) if act else y
 
@@ -387,6 +455,45 @@ class _LinearPair(torch.autograd.Function):
         g2 = x.new_zeros((x.shape[0], W2.shape[0])) if g2 is None else g2.contiguous()
         gx = g1.mm(W1).addmm_(g2, W2) if ctx.needs_input_grad[0] else None  # (in place: no copy of the first)
         return gx, g1.t().mm(x), _bias_grad(g1), g2.t().mm(x), _bias_grad(g2)
+
+
+def _adjacent(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """[a; b] along dim 0: a view when b follows a in memory, else torch.cat."""
+    if (a.is_contiguous() and b.is_contiguous() and a.dtype == b.dtype and a.shape[1:] == b.shape[1:]
+            and b.data_ptr() == a.data_ptr() + a.numel() * a.element_size()):
+        return torch.as_strided(a, (a.shape[0] + b.shape[0],) + tuple(a.shape[1:]), a.stride())
+    return torch.cat([a, b])
+
+
+class _LinearCat(torch.autograd.Function):
+    """x·[W1; W2]ᵀ + [b1; b2] as ONE product (fc_mu and fc_logvar on one input,
+    vae_model.py:81-82): one GEMM forward; backward one input-gradient GEMM,
+    one weight-gradient GEMM and one bias sum for both layers (_LinearPair
+    needs 2 + 4 launches).  The output is the packed B×(n1 + n2) [μ | logσ²]
+    that bottleneck_packed reads in place."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2):
+        Wc, bc = _adjacent(W1, W2), _adjacent(b1, b2)
+        ctx.save_for_backward(x, Wc)
+        ctx.n1 = W1.shape[0]
+        return torch.addmm(bc, x, Wc.t())
+
+    @staticmethod
+    def backward(ctx, G):
+        x, Wc = ctx.saved_tensors
+        n1 = ctx.n1
+        G = G.contiguous()
+        gx = G.mm(Wc) if ctx.needs_input_grad[0] else None
+        gW = G.t().mm(x)
+        gb = _bias_grad(G)
+        return gx, gW[:n1], gb[:n1], gW[n1:], gb[n1:]
+
+
+def linear_cat(x: torch.Tensor, lin1: torch.nn.Linear, lin2: torch.nn.Linear) -> torch.Tensor:
+    """``torch.cat([lin1(x), lin2(x)], 1)`` through _LinearCat."""
+    x = x.to(lin1.weight.dtype)
+    return _LinearCat.apply(x, lin1.weight, lin1.bias, lin2.weight, lin2.bias)
 
 
 def linear_pair(x: torch.Tensor, lin1: torch.nn.Linear, lin2: torch.nn.Linear):

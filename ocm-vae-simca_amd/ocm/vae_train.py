@@ -40,6 +40,12 @@ __all__ = ["GraphedVAETrainer"]
 # the bf16 fused step's bottleneck Linear layers through vae_fused.linear_act
 # (False: torch's autocast Linear + ELU, for A/B runs: scripts/vae_linear_ab.py)
 LINEAR_FUSED = True
+# fc_mu and fc_logvar as one packed product read in place by the bottleneck
+# kernel (False: vae_fused.linear_pair + the two-tensor bottleneck; A/B)
+PACKED_MU_LOGVAR = True
+# the fused step's backward seeded from a persistent unit gradient (False:
+# total.backward(), which fills a fresh one each step; A/B, scripts/vae_ab.py)
+PERSISTENT_ONE = True
 
 
 def _elu_dense(seq, pattern) -> bool:
@@ -71,11 +77,19 @@ class _FusedForward(nn.Module):
         m, la = self.m, self._vf.linear_act
         if self._lin_fused:  # vae_model.py:116-134 with the Linear layers through linear_act
             h = la(m.encoder_conv(xin.unsqueeze(1)).flatten(1), m.fc[0], True)
-            mu, logvar = self._vf.linear_pair(h, m.fc_mu, m.fc_logvar)
+            if PACKED_MU_LOGVAR:  # [μ | logσ²] from one product, read in place by the bottleneck
+                ml = self._vf.linear_cat(h, m.fc_mu, m.fc_logvar)
+                d = m.fc_mu.out_features
+                eps = torch.randn((ml.shape[0], d), dtype=ml.dtype, device=ml.device)  # = randn_like(μ)
+                z, kl = self._vf.bottleneck_packed(ml, eps)
+            else:
+                mu, logvar = self._vf.linear_pair(h, m.fc_mu, m.fc_logvar)
+                eps = torch.randn_like(mu)
+                z, kl = self._vf.bottleneck(mu, logvar, eps)
         else:
             mu, logvar = m.encode(xin)
-        eps = torch.randn_like(mu)
-        z, kl = self._vf.bottleneck(mu, logvar, eps)
+            eps = torch.randn_like(mu)
+            z, kl = self._vf.bottleneck(mu, logvar, eps)
         if not self._lin_fused:
             return m.decode(z), kl
         h = la(la(z, m.fc_dec[0], True), m.fc_dec[3], True)
@@ -270,7 +284,14 @@ class GraphedVAETrainer:
             with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32):
                 xs, kl = self._fwd((self.x - m.spec_mean) / m.spec_std)
         total, recon = self._vf.recon_total(self.x, xs, kl, self._rbufs, self.loss, self.beta)
-        total.backward()
+        # d total / d total = 1 from a persistent tensor: backward() would fill a
+        # fresh one (a kernel of its own) every step
+        if not PERSISTENT_ONE:
+            total.backward()
+        else:
+            if getattr(self, "_one", None) is None or self._one.device != total.device:
+                self._one = torch.ones((), dtype=total.dtype, device=total.device)
+            torch.autograd.backward(total, self._one)
         if self.allreduce:
             self._average_grads()
         self.opt.step()

@@ -37,7 +37,7 @@ def test_binding_signatures_cover_header():
 
     assert set(_lib.SIGNATURES) == set(header_symbols())
     lib = _lib.load()
-    assert lib.ocm_abi_version() == _lib.ABI_VERSION == 11
+    assert lib.ocm_abi_version() == _lib.ABI_VERSION == 12
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libocm.so not built")
