@@ -482,6 +482,13 @@ int ocm_bn_fwd_eval(ocm_ctx* ctx, int32_t dtype, const void* x, int32_t N, int32
 int ocm_bn_bwd(ocm_ctx* ctx, int32_t dtype, const void* x, const void* dy, int32_t N, int32_t C, int32_t L,
                const float* gamma, const float* save_mean, const float* save_invstd, int32_t act, const void* y,
                void* dx, float* dgamma, float* dbeta, void* scratch, void* stream);
+/* ocm_bn_fused_timeouts (ABI 12): with OCM_BN_FUSED=1 in the environment (an experiment, off by default:
+ * slower on the C4 step), training-mode ocm_bn_fwd_train / ocm_bn_bwd run as ONE launch where the
+ * layout allows (L % 8 = 0, 16-byte aligned tensors, the grid co-resident on the device): each workgroup
+ * keeps its share of the channel in registers while the channel's last workgroup forms the statistics,
+ * the others waiting on an epoch word in the scratch.  A wait that exceeds ≈ 1 s gives up rather than
+ * hang (its outputs are then wrong) and is counted (count_out: the process total). */
+int ocm_bn_fused_timeouts(int64_t* count_out);
 
 /* ---- VAE narrow convolutions (vae_model.py:37-81: Conv1d / ConvTranspose1d,
  * 1-12 channels, kernel 7, stride 1 or 2; the layers nn.Conv1d /

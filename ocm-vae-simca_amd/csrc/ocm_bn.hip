@@ -24,6 +24,17 @@ constexpr int BN_T = 256;
 // the 16-B-load reductions (k_bn_stats8 / k_bn_bwd_stats8) where the layout
 // allows; OCM_BN_VEC_STATS=0 in the environment selects the scalar-load
 // kernels (A/B runs, scripts/vae_ab.py)
+// OCM_BN_FUSED=1: the one-launch forms below (off by default: they measured
+// 1284-1287 against 1674-1678 steps/s for the two launches, the C4 step in one
+// box, profiles/r06zq_vae_bn_fused_ab.jsonl — the channel's waiting workgroups
+// and its last workgroup's reduction cost more than the launch they save)
+bool bn_fused_on() {
+  static const bool on = [] {
+    const char* v = getenv("OCM_BN_FUSED");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
 bool bn_vec_stats() {
   static const bool on = [] {
     const char* v = getenv("OCM_BN_VEC_STATS");
@@ -450,6 +461,190 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_apply8(const T* __restrict__ x,
   bn_st8(dx, i, xv);
 }
 
+// ---- one-launch forms (round 6): the statistics and the normalisation in
+// one kernel, each thread's share of the channel held in registers between
+// them (read once).  Every workgroup of channel c reads the channel's epoch
+// word before it takes its ticket; the last to arrive forms the statistics,
+// stores them and bumps the epoch; the others wait for the bump (s_sleep
+// polls), then read them.  Opt-in (bn_fused_on).  The host launches this form only when the grid is
+// co-resident (≤ the CUs' occupancy for the kernel, bn_fused_ok) and each
+// thread's share fits one pass; a wait that still exceeds ≈ 1 s gives up (the
+// outputs are then wrong) and counts in g_bn_wait_timeouts
+// (ocm_bn_fused_timeouts) rather than hang the GPU.
+__device__ unsigned long long g_bn_wait_timeouts;
+constexpr unsigned BN_SPINS_1S = 1u << 22;  // ≈ 1 s of s_sleep(8) polls
+
+// thread 0: wait until *epoch differs from e0 (acquire); false on timeout
+__device__ __forceinline__ bool bn_wait_epoch(const unsigned* epoch, unsigned e0) {
+  unsigned n = 0;
+  while (__hip_atomic_load(const_cast<unsigned*>(epoch), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == e0 &&
+         ++n < BN_SPINS_1S)
+    __builtin_amdgcn_s_sleep(8);
+  if (n < BN_SPINS_1S) return true;
+  atomicAdd(&g_bn_wait_timeouts, 1ull);
+  return false;
+}
+__device__ __forceinline__ void bn_bump_epoch(unsigned* epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the statistics' write-through stores have left
+  __hip_atomic_fetch_add(epoch, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// forward: grid (split, C) with N·L/8 ≤ split·BN_T·BN_U8 (one pass)
+template <typename T, bool ELU>
+__global__ __launch_bounds__(BN_T) void k_bn_fused8(const T* __restrict__ x, int N, int C, int L,
+                                                    double* __restrict__ part, unsigned* __restrict__ ticket,
+                                                    unsigned* __restrict__ epoch, float eps, float momentum,
+                                                    float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                                    float* __restrict__ running_mean, float* __restrict__ running_var,
+                                                    int64_t* __restrict__ nbt, const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta, T* __restrict__ y) {
+  __shared__ double red[BN_T / 64];
+  __shared__ unsigned e0s;
+  __shared__ float ab[2];
+  const int c = blockIdx.y, sp = blockIdx.x, split = gridDim.x, tid = threadIdx.x;
+  const int L8 = L / 8, total = N * L8, step = split * BN_T;
+  unsigned* ep = epoch + (size_t)c * TICKET_STRIDE;
+  if (tid == 0) e0s = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // before the ticket
+  float v[BN_U8][8];
+  float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+  for (int r = 0; r < BN_U8; ++r) bn_ld8_or0(x, C, L8, c, sp * BN_T + tid + r * step, total, v[r]);
+#pragma unroll
+  for (int r = 0; r < BN_U8; ++r)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      a1 += v[r][k];
+      a2 = fmaf(v[r][k], v[r][k], a2);
+    }
+  const double s1 = block_sum_f64(a1, red);
+  const double s2 = block_sum_f64(a2, red);
+  const bool last = bn_ticket(s1, s2, part, ticket, c, sp, split);  // (its vmcnt(0) orders the epoch read first)
+  if (last) {
+    if (tid < 64) {
+      double t1, t2;
+      bn_part_sum(part, c, split, t1, t2);
+      if (tid == 0) {
+        const int64_t M = (int64_t)N * L;
+        const double mean = t1 / (double)M;
+        const double var = fmax(t2 / (double)M - mean * mean, 0.0);
+        const float mf = (float)mean, inv = (float)(1.0 / sqrt(var + (double)eps));
+        st_agent(save_mean + c, mf);
+        st_agent(save_invstd + c, inv);
+        if (running_mean) {
+          const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+          running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+          running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+        }
+        if (nbt && c == 0) *nbt += 1;
+        const float a = inv * (gamma ? gamma[c] : 1.f);
+        ab[0] = a;
+        ab[1] = (beta ? beta[c] : 0.f) - mf * a;
+        bn_bump_epoch(ep);
+      }
+    }
+  } else if (tid == 0) {
+    bn_wait_epoch(ep, e0s);
+    const float mf = ld_agent(save_mean + c), inv = ld_agent(save_invstd + c);
+    const float a = inv * (gamma ? gamma[c] : 1.f);
+    ab[0] = a;
+    ab[1] = (beta ? beta[c] : 0.f) - mf * a;
+  }
+  __syncthreads();
+  const float a = ab[0], b = ab[1];
+#pragma unroll
+  for (int r = 0; r < BN_U8; ++r) {
+    const int e = sp * BN_T + tid + r * step;
+    if (e >= total) continue;
+    const int n = e / L8, l = (e - n * L8) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float z = fmaf(v[r][k], a, b);
+      v[r][k] = ELU ? (z > 0.f ? z : expf(z) - 1.f) : z;
+    }
+    bn_st8(y, ((int64_t)n * C + c) * L + l, v[r]);
+  }
+}
+
+// backward: the sums Σdz, Σdz·x̂ and dx = γ·invstd·(dz − Σdz/M − x̂·Σ(dz·x̂)/M) in one launch
+template <typename T, bool ELU>
+__global__ __launch_bounds__(BN_T) void k_bn_bwd_fused8(const T* __restrict__ x, const T* __restrict__ dy,
+                                                        const T* __restrict__ ya, int N, int C, int L,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd,
+                                                        const float* __restrict__ gamma, double* __restrict__ part,
+                                                        unsigned* __restrict__ ticket, unsigned* __restrict__ epoch,
+                                                        double* __restrict__ sums, float* __restrict__ dgamma,
+                                                        float* __restrict__ dbeta, T* __restrict__ dx) {
+  __shared__ double red[BN_T / 64];
+  __shared__ unsigned e0s;
+  __shared__ double m12[2];
+  const int c = blockIdx.y, sp = blockIdx.x, split = gridDim.x, tid = threadIdx.x;
+  const float mu = mean[c], is = invstd[c];
+  const int L8 = L / 8, total = N * L8, step = split * BN_T;
+  unsigned* ep = epoch + (size_t)c * TICKET_STRIDE;
+  if (tid == 0) e0s = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  float g[BN_U8][8], xv[BN_U8][8];
+  {
+    float yv[ELU ? BN_U8 : 1][8];
+#pragma unroll
+    for (int r = 0; r < BN_U8; ++r) {
+      bn_ld8_or0(dy, C, L8, c, sp * BN_T + tid + r * step, total, g[r]);
+      bn_ld8_or0(x, C, L8, c, sp * BN_T + tid + r * step, total, xv[r]);
+      if (ELU) bn_ld8_or0(ya, C, L8, c, sp * BN_T + tid + r * step, total, yv[ELU ? r : 0]);
+    }
+    if (ELU) {
+#pragma unroll
+      for (int r = 0; r < BN_U8; ++r)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[r][k] = yv[ELU ? r : 0][k] > 0.f ? g[r][k] : g[r][k] * (yv[ELU ? r : 0][k] + 1.f);
+    }
+  }
+  float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+  for (int r = 0; r < BN_U8; ++r)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      xv[r][k] = (xv[r][k] - mu) * is;  // x̂ (padded groups: g = 0 adds nothing)
+      a1 += g[r][k];
+      a2 = fmaf(g[r][k], xv[r][k], a2);
+    }
+  const double s1 = block_sum_f64(a1, red);
+  const double s2 = block_sum_f64(a2, red);
+  const bool last = bn_ticket(s1, s2, part, ticket, c, sp, split);
+  if (last) {
+    if (tid < 64) {
+      double t1, t2;
+      bn_part_sum(part, c, split, t1, t2);
+      if (tid == 0) {
+        st_agent(sums + 2 * c, t1);
+        st_agent(sums + 2 * c + 1, t2);
+        if (dbeta) dbeta[c] = (float)t1;
+        if (dgamma) dgamma[c] = (float)t2;
+        m12[0] = t1;
+        m12[1] = t2;
+        bn_bump_epoch(ep);
+      }
+    }
+  } else if (tid == 0) {
+    bn_wait_epoch(ep, e0s);
+    m12[0] = ld_agent(sums + 2 * c);
+    m12[1] = ld_agent(sums + 2 * c + 1);
+  }
+  __syncthreads();
+  const double M = (double)N * L;
+  const float m1 = (float)(m12[0] / M), m2 = (float)(m12[1] / M);
+  const float kk = is * (gamma ? gamma[c] : 1.f);
+#pragma unroll
+  for (int r = 0; r < BN_U8; ++r) {
+    const int e = sp * BN_T + tid + r * step;
+    if (e >= total) continue;
+    const int n = e / L8, l = (e - n * L8) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[r][k] = kk * (g[r][k] - m1 - xv[r][k] * m2);
+    bn_st8(dx, ((int64_t)n * C + c) * L + l, g[r]);
+  }
+}
+
 // scratch of the forward / backward calls: per-(channel, split) partials, the
 // backward's channel sums, then one completion counter per channel (zero
 // before the first call; every call leaves them zero)
@@ -462,8 +657,35 @@ int bn_split8(int N, int C, int L) {
 }
 
 size_t bn_part_doubles(int C) { return (size_t)C * bn_split(C) * 2 + 2 * (size_t)C; }
+size_t bn_ticket_words(int C) { return (size_t)C * tickets_per_slot(bn_split(C)) * TICKET_STRIDE; }
+// + one epoch word per channel (128-B apart) for the one-launch forms
 size_t bn_scratch(int C) {
-  return bn_part_doubles(C) * sizeof(double) + (size_t)C * tickets_per_slot(bn_split(C)) * TICKET_STRIDE * sizeof(unsigned);
+  return bn_part_doubles(C) * sizeof(double) + (bn_ticket_words(C) + (size_t)C * TICKET_STRIDE) * sizeof(unsigned);
+}
+
+// the one-launch form applies (opted in): one pass per thread, the whole grid resident
+// at once (the occupancy of the kernel × the CUs, queried once per kernel)
+template <class K>
+bool bn_fused_ok(ocm_ctx* ctx, K kernel, int N, int C, int L, int split) {
+  if (!bn_fused_on()) return false;
+  if ((int64_t)N * (L / 8) > (int64_t)split * BN_T * BN_U8) return false;
+  static const void* keys[16];  // occupancy per kernel, queried once (benign race: the same value)
+  static int vals[16], used = 0;
+  const void* key = reinterpret_cast<const void*>(kernel);
+  int per_cu = -1;
+  for (int i = 0; i < used; ++i)
+    if (keys[i] == key) per_cu = vals[i];
+  if (per_cu < 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, BN_T, 0) != hipSuccess) nb = 0;
+    per_cu = nb;
+    if (used < 16) {
+      keys[used] = key;
+      vals[used] = nb;
+      ++used;
+    }
+  }
+  return per_cu > 0 && (int64_t)split * C <= (int64_t)per_cu * ctx->num_cus;
 }
 
 template <typename T>
@@ -472,7 +694,24 @@ int bn_fwd(ocm_ctx* ctx, const void* x, int N, int C, int L, const float* gamma,
            void* scratch, int act, hipStream_t st) {
   auto* part = static_cast<double*>(scratch);
   auto* ticket = reinterpret_cast<unsigned*>(part + bn_part_doubles(C));
+  unsigned* epoch = ticket + bn_ticket_words(C);
   const bool v8 = L % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+  if (v8 && bn_vec_stats()) {
+    const int s8 = bn_split8(N, C, L);
+#define OCM_BN_FUSED_L(E_)                                                                                           \
+  if (bn_fused_ok(ctx, k_bn_fused8<T, E_>, N, C, L, s8)) {                                                          \
+    hipLaunchKernelGGL((k_bn_fused8<T, E_>), dim3(s8, C), dim3(BN_T), 0, st, static_cast<const T*>(x), N, C, L, part, \
+                       ticket, epoch, eps, momentum, smean, sinv, rmean, rvar, nbt, gamma, beta, static_cast<T*>(y)); \
+    OCM_CHECK_LAUNCH("k_bn_fused8");                                                                                  \
+    return OCM_OK;                                                                                                    \
+  }
+    if (act == OCM_ACT_ELU) {
+      OCM_BN_FUSED_L(true)
+    } else {
+      OCM_BN_FUSED_L(false)
+    }
+#undef OCM_BN_FUSED_L
+  }
   if (v8 && bn_vec_stats())
     hipLaunchKernelGGL(k_bn_stats8<T>, dim3(bn_split8(N, C, L), C), dim3(BN_T), 0, st, static_cast<const T*>(x), N, C,
                        L, part, ticket, eps, momentum, smean, sinv, rmean, rvar, nbt);
@@ -501,7 +740,16 @@ int bn_bwd(ocm_ctx* ctx, const void* x, const void* dy, const void* ya, int N, i
   auto* ticket = reinterpret_cast<unsigned*>(part + bn_part_doubles(C));
   const int split = bn_split(C);
   double* sums = part + (size_t)C * split * 2;
+  unsigned* epoch = ticket + bn_ticket_words(C);
   const auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (bn_vec_stats() && L % 8 == 0 && al(x) && al(dy) && (!ELU || al(ya)) && al(dx) &&
+      bn_fused_ok(ctx, k_bn_bwd_fused8<T, ELU>, N, C, L, bn_split8(N, C, L))) {
+    hipLaunchKernelGGL((k_bn_bwd_fused8<T, ELU>), dim3(bn_split8(N, C, L), C), dim3(BN_T), 0, st,
+                       static_cast<const T*>(x), static_cast<const T*>(dy), static_cast<const T*>(ya), N, C, L, smean,
+                       sinv, gamma, part, ticket, epoch, sums, dgamma, dbeta, static_cast<T*>(dx));
+    OCM_CHECK_LAUNCH("k_bn_bwd_fused8");
+    return OCM_OK;
+  }
   if (bn_vec_stats() && L % 8 == 0 && al(x) && al(dy) && (!ELU || al(ya)))
     hipLaunchKernelGGL((k_bn_bwd_stats8<T, ELU>), dim3(bn_split8(N, C, L), C), dim3(BN_T), 0, st,
                        static_cast<const T*>(x), static_cast<const T*>(dy), static_cast<const T*>(ya), N, C, L, smean,
@@ -527,6 +775,14 @@ int bn_bwd(ocm_ctx* ctx, const void* x, const void* dy, const void* ya, int N, i
 extern "C" {
 
 size_t ocm_bn_scratch_bytes(int32_t C) { return C > 0 ? bn_scratch(C) : 0; }
+
+int ocm_bn_fused_timeouts(int64_t* count_out) {
+  OCM_REQUIRE(count_out, "ocm_bn_fused_timeouts: NULL argument");
+  unsigned long long v = 0;
+  OCM_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_bn_wait_timeouts), sizeof(v)));
+  *count_out = (int64_t)v;
+  return OCM_OK;
+}
 
 int ocm_bn_fwd_train(ocm_ctx* ctx, int32_t dtype, const void* x, int32_t N, int32_t C, int32_t L,
                      const float* gamma, const float* beta, float eps, float momentum, float* running_mean,

@@ -146,6 +146,7 @@ SIGNATURES = {
                                           c_i32, c_i32, c_void_p, c_void_p, c_void_p]),
     "ocm_vae_linear_act": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p,
                                    c_void_p]),
+    "ocm_bn_fused_timeouts": (c_i32, [ctypes.POINTER(c_i64)]),
     "ocm_vae_recon_fwd": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_void_p, c_i32, c_i32, c_void_p, c_void_p,
                                   ctypes.c_float, c_void_p, ctypes.c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ocm_vae_recon_bwd": (c_i32, [c_void_p, c_void_p, c_void_p, c_i64, c_i32, c_void_p, ctypes.c_float, c_void_p,

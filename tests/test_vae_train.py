@@ -136,6 +136,13 @@ def test_fast_batchnorm_matches_torch(dtype, shape):
     torch.testing.assert_close(fast.running_mean, ref.running_mean, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(fast.running_var, ref.running_var, rtol=1e-3, atol=1e-4)
     assert int(fast.num_batches_tracked) == int(ref.num_batches_tracked) == 1
+    # the one-launch forms (L % 8 = 0 here: the first two shapes) never gave up waiting
+    import ctypes
+
+    from ocm import _lib
+    torch.cuda.synchronize()
+    n = ctypes.c_int64(-1)
+    assert _lib.load().ocm_bn_fused_timeouts(ctypes.byref(n)) == 0 and n.value == 0
 
 
 @pytest.mark.gpu
@@ -216,6 +223,12 @@ def test_fused_batchnorm_elu_matches_torch(dtype, shape):
     fast.eval()
     ref.eval()
     torch.testing.assert_close(fast(x0), torch.nn.functional.elu(ref(x0)))
+    import ctypes
+
+    from ocm import _lib
+    torch.cuda.synchronize()
+    n = ctypes.c_int64(-1)
+    assert _lib.load().ocm_bn_fused_timeouts(ctypes.byref(n)) == 0 and n.value == 0
 
 
 @pytest.mark.gpu
