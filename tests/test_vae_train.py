@@ -487,7 +487,8 @@ def test_linear_act_matches_torch(k, n, act):
     ref.backward(go)
     gb = (xb.grad, lin.weight.grad, lin.bias.grad)
     if act and k <= 256:  # ocm_vae_linear_act: its own f32 sums, within one bf16 rounding of torch's output
-        torch.testing.assert_close(out.float(), ref.float(), rtol=2 ** -7, atol=2 ** -7 * float(ref.abs().max()))
+        torch.testing.assert_close(out.detach().float(), ref.detach().float(), rtol=2 ** -7,
+                                   atol=2 ** -7 * float(ref.detach().abs().max()))
     else:
         assert torch.equal(out, ref)  # the forward is torch's call
     for name, a, b in zip(("x", "W", "b"), ga, gb):
