@@ -77,7 +77,8 @@ class _FusedForward(nn.Module):
         m, la = self.m, self._vf.linear_act
         if self._lin_fused:  # vae_model.py:116-134 with the Linear layers through linear_act
             h = la(m.encoder_conv(xin.unsqueeze(1)).flatten(1), m.fc[0], True)
-            if PACKED_MU_LOGVAR:  # [μ | logσ²] from one product, read in place by the bottleneck
+            if PACKED_MU_LOGVAR and m.fc_mu.out_features == m.fc_logvar.out_features:
+                # [μ | logσ²] from one product, read in place by the bottleneck
                 ml = self._vf.linear_cat(h, m.fc_mu, m.fc_logvar)
                 d = m.fc_mu.out_features
                 eps = torch.randn((ml.shape[0], d), dtype=ml.dtype, device=ml.device)  # = randn_like(μ)
