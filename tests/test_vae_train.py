@@ -459,8 +459,9 @@ def test_cast_bf16_accumulates_into_existing_grads():
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
-@pytest.mark.parametrize("k,n,act", [(6144, 64, True), (64, 32, False), (32, 64, True), (64, 6144, True)])
-def test_linear_act_matches_torch(k, n, act):
+@pytest.mark.parametrize("k,n,act,bias", [(6144, 64, True, True), (64, 32, False, True), (32, 64, True, True),
+                                          (64, 6144, True, True), (128, 64, True, True), (256, 128, True, False)])
+def test_linear_act_matches_torch(k, n, act, bias):
     """vae_fused.linear_act (the bf16 step's bottleneck Linear layers, round 6)
     against F.linear (+ F.elu) under torch autograd on the same bf16 tensors:
     the forward is the same torch call; the backward's ELU gradient and bias
@@ -473,19 +474,21 @@ def test_linear_act_matches_torch(k, n, act):
 
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(k + n)
-    lin = nn.Linear(k, n).to(dev).to(torch.bfloat16)
+    lin = nn.Linear(k, n, bias=bias).to(dev).to(torch.bfloat16)
     x = torch.randn(512, k, generator=g).to(dev).to(torch.bfloat16)
     go = torch.randn(512, n, generator=g).to(dev).to(torch.bfloat16)
     xa = x.clone().requires_grad_(True)
     out = vf.linear_act(xa, lin, act)
     out.backward(go)
-    ga = (xa.grad, lin.weight.grad.clone(), lin.bias.grad.clone())
-    lin.weight.grad = lin.bias.grad = None
+    ga = (xa.grad, lin.weight.grad.clone()) + ((lin.bias.grad.clone(),) if bias else ())
+    lin.weight.grad = None
+    if bias:
+        lin.bias.grad = None
     xb = x.clone().requires_grad_(True)
     ref = torch.nn.functional.linear(xb, lin.weight, lin.bias)
     ref = torch.nn.functional.elu(ref) if act else ref
     ref.backward(go)
-    gb = (xb.grad, lin.weight.grad, lin.bias.grad)
+    gb = (xb.grad, lin.weight.grad) + ((lin.bias.grad,) if bias else ())
     if act and k <= 256:  # ocm_vae_linear_act: its own f32 sums, within one bf16 rounding of torch's output
         torch.testing.assert_close(out.detach().float(), ref.detach().float(), rtol=2 ** -7,
                                    atol=2 ** -7 * float(ref.detach().abs().max()))
