@@ -3,6 +3,7 @@ reference's training step (forward → beta_vae_bce_loss → zero_grad →
 backward → Adam.step, vae_bce_nut.py:178-203) run with the reference-format
 loss on an identical copy of the model."""
 import copy
+import os
 
 import numpy as np
 import pytest
@@ -601,3 +602,49 @@ def test_linear_cat_packed_bottleneck_matches_pair(adjacent):
     for a, b in zip(g1, g2):
         a, b = a.float(), b.float()
         assert float((a - b).norm() / b.norm()) < 1e-2
+
+
+_BN_FUSED_CHILD = r"""
+import ctypes, os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "ocm-vae-simca_amd"))
+import torch
+from ocm import _lib
+from ocm.bn import FastBatchNorm1d
+dev = torch.device("cuda", 0)
+for (N, C, L) in [(512, 3, 2048), (64, 12, 512)]:
+    g = torch.Generator(device="cpu").manual_seed(C * L + 3)
+    x0 = (0.5 + 2.0 * torch.randn(N, C, L, generator=g)).to(dev)
+    ref = torch.nn.BatchNorm1d(C).to(dev)
+    fast = FastBatchNorm1d(C).fuse_elu().to(dev)
+    fast.load_state_dict(ref.state_dict())
+    xr = x0.bfloat16().float().requires_grad_(True)
+    xf = x0.bfloat16().requires_grad_(True)
+    yr, yf = torch.nn.functional.elu(ref(xr)), fast(xf)
+    gy = torch.randn(N, C, L, generator=g).to(dev).bfloat16()
+    (yr * gy.float()).sum().backward()
+    (yf.float() * gy.float()).sum().backward()
+    torch.testing.assert_close(yf.float(), yr, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(xf.grad.float(), xr.grad, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(fast.running_mean, ref.running_mean, rtol=1e-4, atol=1e-4)
+torch.cuda.synchronize()
+n = ctypes.c_int64(-1)
+assert _lib.load().ocm_bn_fused_timeouts(ctypes.byref(n)) == 0 and n.value == 0
+print("bn fused ok")
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+def test_bn_one_launch_opt_in_matches_torch():
+    """The opt-in one-launch BatchNorm (OCM_BN_FUSED=1: statistics and
+    normalisation in one kernel with an in-kernel epoch wait, off by default)
+    against nn.BatchNorm1d + ELU, in a child process (the switch is read once
+    per process); no wait gave up."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OCM_BN_FUSED="1")
+    r = subprocess.run([sys.executable, "-c", _BN_FUSED_CHILD, repo], capture_output=True, text=True, timeout=240,
+                       env=env)
+    assert r.returncode == 0 and "bn fused ok" in r.stdout, r.stderr[-3000:]
